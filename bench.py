@@ -1,0 +1,231 @@
+"""Benchmark: GAT layer forward+backward edges/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syn100k|r15]
+
+One step = one full GAT attention layer forward + backward over the whole graph
+(SURVEY.md §8d, config C4 "synthetic CSR graph 100k nodes / 2M edges, 128-dim
+features, 8 heads"):
+    h = X @ W                     (100k x 128 @ 128 x 128, fp32)
+    el, er = h . a_l, h . a_r     (per head, 8 heads x 16)
+    u = softmax_row(lrelu(el_i + er_j)) @ h      <- msha_edge_attention_fwd (dominant)
+    backward of all of it (msha_edge_attention_bwd_rows + msha_csc_aggregate + GEMMs)
+Inputs are resident in HBM before the timed region.  For N > 1 GPUs the path
+does not shard (SURVEY.md §8e "replicas only"): every rank runs its own replica
+and value = total edges over all ranks / max-over-ranks time ("scaling": "weak").
+
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP
+events around every launch of it inside the timed region) and the CPU baseline
+(the oracle's C restatement, timed on this host's cores, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "edges/sec GAT fwd+bwd @1 GPU; link-score pairs/sec; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def synth_graph(n, e, seed=0):
+    """C4 generator: e unique (row, col) pairs, rows sorted, cols uniform, deg >= 1."""
+    rng = np.random.default_rng(seed)
+    keys = np.arange(n, dtype=np.int64) * n + rng.integers(0, n, n)  # one edge per row
+    while len(keys) < e:
+        need = e - len(keys)
+        extra = rng.integers(0, n, int(need * 1.05) + 16) * n + rng.integers(0, n,
+                                                                            int(need * 1.05) + 16)
+        keys = np.unique(np.concatenate([keys, extra]))
+    if len(keys) > e:  # drop surplus without emptying a row
+        rows = keys // n
+        first = np.ones(len(keys), bool)
+        first[1:] = rows[1:] != rows[:-1]
+        cand = np.nonzero(~first)[0]
+        drop = rng.choice(cand, len(keys) - e, replace=False)
+        keys = np.delete(keys, drop)
+    rows, col = keys // n, keys % n
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(rows, minlength=n), out=rowptr[1:])
+    return rowptr, col
+
+
+def r15_graph():
+    g = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    return g["rowptr"].astype(np.int64), g["col"].astype(np.int64), int(g["n"]), int(g["m"])
+
+
+WORKLOADS = {
+    "syn100k": dict(n=100_000, e=2_000_000, fin=128, heads=8, feat=16),
+    "syn100k_f128": dict(n=100_000, e=2_000_000, fin=128, heads=8, feat=128),
+    "syn2m": dict(n=2_000_000, e=40_000_000, fin=128, heads=8, feat=16),  # cache-busting
+}
+
+
+def fwd_bytes(n, m, e, H, F):
+    """Algorithmic bytes of one msha_edge_attention_fwd launch:
+    rowptr + col + er gather + el + h gather (4HF per edge) + u write + lse write."""
+    return 4 * (n + 1) + 4 * e + 4 * e * H + 4 * n * H + 4 * e * H * F + 4 * n * H * F + 4 * n * H
+
+
+class Layer:
+    """The benchmarked GAT layer (one replica)."""
+
+    def __init__(self, dev, rowptr, col, n, m, fin, H, F, seed):
+        import msha_loader
+
+        msha_loader.load()
+        from msha_gnn_amd import functional as MF
+        from msha_gnn_amd.graph import Graph
+
+        self.MF = MF
+        self.graph = Graph.from_csr(rowptr, col, m, dev)
+        g = torch.Generator().manual_seed(seed)
+        self.n, self.m, self.H, self.F = n, m, H, F
+        self.X = torch.rand(n, fin, generator=g).to(dev)
+        self.W = (torch.randn(fin, H * F, generator=g) * fin ** -0.5).to(dev).requires_grad_(True)
+        self.al = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
+        self.ar = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
+        self.dU = torch.randn(n, H, F, generator=g).to(dev)
+
+    def step(self):
+        for p in (self.W, self.al, self.ar):
+            p.grad = None
+        h = torch.mm(self.X, self.W).view(self.n, self.H, self.F)
+        el = torch.einsum("nhf,hf->nh", h, self.al)
+        er = torch.einsum("nhf,hf->nh", h, self.ar)
+        u = self.MF.edge_attention(self.graph, el, er, h)
+        u.backward(self.dU)
+
+
+def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
+    """Oracle C restatement of the same step (projection via numpy BLAS + edge-softmax
+    aggregate fwd/bwd), whole graph, repeated for ~budget_s."""
+    from oracle import cpu_oracle
+    from oracle import gnn_oracle as O
+
+    rng = np.random.default_rng(0)
+    X = rng.random((n, fin), dtype=np.float32)
+    W = (rng.standard_normal((fin, H * F)) * fin ** -0.5).astype(np.float32)
+    al = rng.standard_normal((H, F)).astype(np.float32)
+    ar = rng.standard_normal((H, F)).astype(np.float32)
+    dU = rng.standard_normal((n, H, F)).astype(np.float32)
+    colptr, perm = O.csr_to_csc(rowptr, col, n)
+    csc_row = O.edge_rows(rowptr)[perm]
+
+    def one():
+        h = (X @ W).reshape(n, H, F)
+        el = np.einsum("nhf,hf->nh", h, al)
+        er = np.einsum("nhf,hf->nh", h, ar)
+        u, lse = cpu_oracle.edge_attention_fwd(rowptr, col, el, er, h)
+        d_el, d_er, d_hc = cpu_oracle.edge_attention_bwd(rowptr, col, colptr, csc_row, perm, el,
+                                                         er, h, lse, u, dU)
+        dh = d_hc + d_el[:, :, None] * al[None] + d_er[:, :, None] * ar[None]
+        dh = dh.reshape(n, H * F)
+        _ = X.T @ dh  # dW
+
+    one()  # warm-up (page-in, thread pool)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        one()
+        reps += 1
+        el_t = time.perf_counter() - t0
+        if el_t >= budget_s or reps >= 50:
+            break
+    return dict(value=len(col) * reps / el_t, unit="edges/s", cores=cpu_oracle.threads(),
+                kind="port",
+                sample=f"whole graph ({n} rows, {len(col)} edges), {reps} fwd+bwd steps in "
+                       f"{el_t:.1f}s: numpy X@W + oracle/edge_attention_cpu.c (OpenMP)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="syn100k", choices=sorted(WORKLOADS) + ["r15"])
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    if args.workload == "r15":
+        rowptr, col, n, m = r15_graph()
+        fin, H, F = 128, 2, 64
+    else:
+        w = WORKLOADS[args.workload]
+        n, fin, H, F = w["n"], w["fin"], w["heads"], w["feat"]
+        m = n
+        rowptr, col = synth_graph(n, w["e"], seed=0)
+    e = len(col)
+    layer = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank)
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        layer.step()
+    barrier()
+    layer.MF.KERNEL_EVENTS = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        layer.step()
+    barrier()
+    dt = time.perf_counter() - t0
+    events = layer.MF.KERNEL_EVENTS.get("edge_attention_fwd", [])
+    layer.MF.KERNEL_EVENTS = None
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+    if dist:
+        t = torch.tensor([dt], device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    if rank != 0:
+        if dist:
+            tdist.destroy_process_group()
+        return
+    ms_per_step = dt / args.steps * 1e3
+    value = world * e * args.steps / dt
+    fb = fwd_bytes(n, m, e, H, F)
+    achieved = fb / (k_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"gat_layer_{args.workload}", "nodes": n, "cols": m, "edges": e,
+                   "in_features": fin, "heads": H, "feat": F, "parallelism": f"replicas{world}"},
+        "roofline": {"kernel": "msha_edge_attention_fwd", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": fb, "avg_launch_us": k_ms * 1e3,
+                     "launches_timed": len(events)},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
+    print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+/*
+ * msha_gnn.h -- C ABI of the MI355X (gfx950) MSHA-GNN attention library.
+ *
+ * The reference (Sienna12321/MSHA--GNN @ 2025-01-17) has no FFI: its hot path is
+ * the Python nn.Module surface that train.py / LLP.py call, computed by dense
+ * ATen ops.  Each entry point below replaces one dense op chain of that surface;
+ * the comment on each cites the reference lines it stands in for.  The Python
+ * host layer (msha--gnn_amd/) binds these with ctypes.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers to caller-owned, contiguous buffers; the
+ *     library never allocates.  Temporary space is passed in as a workspace whose
+ *     size a *_workspace_size() query returns.
+ *   - Every call is stream-ordered and asynchronous on `stream` (a hipStream_t;
+ *     NULL = the legacy default stream).  No host synchronisation, no global
+ *     mutable state: calls are re-entrant and graph-capturable.
+ *   - Return 0 (MSHA_OK) or a negative MSHA_ERR_* code; msha_last_error() gives a
+ *     thread-local message.  No C++ exception crosses the ABI.
+ *   - Floating-point buffers are fp32 unless stated.  Node tables are row-major
+ *     (rows, heads, feat) with the head index outer; per-edge arrays are
+ *     (edges, heads) in CSR edge order.
+ *   - Graph = the mask `adj > 0` of an (n_rows x n_cols) adjacency as CSR
+ *     (row-major edge order == torch.nonzero order).  A row without edges is
+ *     stored as a VIRTUAL FULL ROW (all n_cols columns, rowflag = 1): the
+ *     reference's softmax of an all -9e15 row is uniform over every column
+ *     (Ablation.py:268-270), and so is the GAL's mask/deg (GAT.py:29-31).
+ */
+#ifndef MSHA_GNN_H_
+#define MSHA_GNN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSHA_ABI_VERSION 1
+
+#if defined(__GNUC__) || defined(__clang__)
+#define MSHA_API __attribute__((visibility("default")))
+#else
+#define MSHA_API
+#endif
+
+enum {
+  MSHA_OK = 0,
+  MSHA_ERR_ARG = -1,         /* bad size / null pointer / unsupported shape */
+  MSHA_ERR_UNSUPPORTED = -2, /* shape combination without a compiled kernel */
+  MSHA_ERR_HIP = -3          /* a HIP runtime call failed (see msha_last_error) */
+};
+
+typedef void* msha_stream_t; /* hipStream_t */
+
+/* Graph descriptor.  Built by msha_graph_count / msha_graph_fill from a dense
+ * adjacency, or by the caller from its own CSR.  The CSC view and the column
+ * chunk plan are needed only by msha_csc_aggregate. */
+typedef struct msha_graph {
+  int64_t n_rows, n_cols, n_edges;
+  const int32_t* rowptr;  /* n_rows + 1 */
+  const int32_t* col;     /* n_edges, column of each edge */
+  const uint8_t* rowflag; /* n_rows, 1 = virtual full row (nullable: none) */
+  const int32_t* colptr;  /* n_cols + 1 (CSC) */
+  const int32_t* csc_row; /* n_edges, source row of each CSC slot */
+  const int32_t* csc_eid; /* n_edges, CSR edge id of each CSC slot */
+  /* CSC work split: chunk c covers CSC slots [chunk_start[c], chunk_end[c]) of
+   * column chunk_col[c]; a column with more than one chunk is listed in
+   * multi_col with its first chunk and chunk count (partials summed in order). */
+  int64_t n_chunks;
+  const int32_t* chunk_col;
+  const int32_t* chunk_start;
+  const int32_t* chunk_end;
+  int64_t n_multi;
+  const int32_t* multi_col;
+  const int32_t* multi_first;
+  const int32_t* multi_count;
+} msha_graph;
+
+MSHA_API int msha_abi_version(void);
+MSHA_API const char* msha_last_error(void);
+
+/* ---------------------------------------------------------------- dropout --- */
+/* keep[i] = 1 iff element i survives F.dropout(p) under (seed, offset).  The
+ * kernels below draw exactly these masks (stream-ordered Philox4x32-10), which
+ * is how tests inject the same mask into the CPU oracle. */
+MSHA_API int msha_dropout_keep_mask(uint64_t seed, uint64_t offset, int64_t n, float p, uint8_t* keep,
+                           msha_stream_t stream);
+
+/* ------------------------------------------------------- graph ingestion --- */
+/* dataset.py:279-288 (HigherDataset.inter_adjacent): adj[source[k], recipient[k]] += 1.
+ * Counts are accumulated exactly in int32 (workspace: n_rows*n_cols int32). */
+MSHA_API int msha_inter_adjacency(const int64_t* source, const int64_t* recipient, int64_t n_flows,
+                         int64_t n_rows, int64_t n_cols, float* adj, int32_t* counts_ws,
+                         msha_stream_t stream);
+
+/* model.py:95-100 (normalize_adjacency_matrix): out = (adj * d) * d, d = colsum^-1/2;
+ * a zero column sum spreads NaN to every entry, as the reference's two mm's do.
+ * Workspace: n_cols + 1 floats. */
+MSHA_API int msha_normalize_adjacency(const float* adj, int64_t n_rows, int64_t n_cols, float* out,
+                             float* col_ws, msha_stream_t stream);
+
+/* Ablation.py:268 / GAT.py:30 mask `adj > 0` -> CSR + CSC.  Two phases: count
+ * (row/column degrees incl. virtual rows, rowptr/colptr scans), then the caller
+ * reads rowptr[n_rows] (= n_edges), allocates, and fills.  Deterministic:
+ * CSC slots of a column are in ascending row order. */
+MSHA_API size_t msha_graph_workspace_size(int64_t n_rows, int64_t n_cols);
+MSHA_API int msha_graph_count(const float* adj, int64_t n_rows, int64_t n_cols, int32_t* rowptr,
+                     int32_t* colptr, uint8_t* rowflag, void* ws, size_t ws_bytes,
+                     msha_stream_t stream);
+MSHA_API int msha_graph_fill(const float* adj, int64_t n_rows, int64_t n_cols, const int32_t* rowptr,
+                    const int32_t* colptr, const uint8_t* rowflag, int32_t* col,
+                    int32_t* csc_row, int32_t* csc_eid, void* ws, size_t ws_bytes,
+                    msha_stream_t stream);
+
+/* --------------------------------------------------------- attention core --- */
+/* Fused edge score + per-row segmented softmax + attention-weighted gather.
+ * Replaces Ablation.py:266-271,274 (OursLayer3: e12 = lrelu(cat(h1_j,h2_i) @ a),
+ * where/softmax/dropout, u = att @ h1), per head h:
+ *   s_e   = lrelu(el[i,h] + er[j,h], neg_slope)      (0 on virtual rows)
+ *   att_e = softmax over row i of s
+ *   u[i]  = sum_e dropout(att_e) * hc[j]             hc: (n_cols, heads, feat)
+ * Outputs u (n_rows, heads, feat), lse (n_rows, heads) = log-sum-exp of the row's
+ * scores (the backward recomputes att from it) and, if attd != NULL, the
+ * post-dropout attention (n_edges, heads).
+ * Supported (heads, feat): feat % 4 == 0, heads in {1,2,4,8}, heads*feat in
+ * {8..1024} (see msha_edge_attention_supported). */
+MSHA_API int msha_edge_attention_supported(int32_t heads, int32_t feat);
+MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat, const float* el,
+                            const float* er, const float* hc, float neg_slope, float drop_p,
+                            uint64_t seed, uint64_t offset, float* u, float* lse, float* attd,
+                            msha_stream_t stream);
+
+/* Row half of the backward (autograd of the chain above; Ablation.py:266-274):
+ *   g_e  = dU[i]·hc[j] (+ dV[j]·hs[i] when dV != NULL: the v = att^T @ h2 branch,
+ *          Ablation.py:273)
+ *   ds_e = att_e * (drop(g_e) - sum_row att*drop(g)),  de_e = ds_e * lrelu'(pre_e)
+ * Writes d_el (n_rows, heads) = row sums of de, de (n_edges, heads), attd
+ * (n_edges, heads) = post-dropout attention, and d_hs (n_rows, heads, feat) =
+ * sum_e attd_e dV[j] when dV != NULL.  The column half (d_er, d_hc) is
+ * msha_csc_aggregate over (attd, de). */
+MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
+                                 const float* el, const float* er, const float* hc,
+                                 const float* lse, const float* u, const float* dU,
+                                 const float* hs, const float* dV, float neg_slope,
+                                 float drop_p, uint64_t seed, uint64_t offset, float* d_el,
+                                 float* de, float* attd, float* d_hs, msha_stream_t stream);
+
+/* Column-side (transposed) aggregate over the CSC view:
+ *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
+ *   out_x[j] = sum_{e in col j} x[e]                   (when x != NULL)
+ * Forward v = attd^T @ h2 (Ablation.py:273) and backward d_hc = attd^T @ dU,
+ * d_er = colsum(de).  Long columns are split into chunks whose partial sums are
+ * added in chunk order: deterministic, no atomics. */
+MSHA_API size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);
+MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat, const float* w,
+                       const float* x, const float* table, float* out, float* out_x, void* ws,
+                       size_t ws_bytes, msha_stream_t stream);
+
+/* ----------------------------------------------- GraphAttentionLayer (GAL) --- */
+/* GAT.py:20-35 / Ablation.py:100-115.  The layer's score is constant along a row
+ * (it concatenates h_i with itself), so its attention is mask/deg (uniform on
+ * virtual rows) and the layer is out = elu(dropout(mask/deg) * h), h (n_rows, n_cols).
+ * The bwd returns dh = dout * elu'(z) * dropout(mask/deg). */
+MSHA_API int msha_gal_fwd(const msha_graph* g, const float* h, float drop_p, uint64_t seed,
+                 uint64_t offset, float* out, msha_stream_t stream);
+MSHA_API int msha_gal_bwd(const msha_graph* g, const float* h, const float* dout, float drop_p,
+                 uint64_t seed, uint64_t offset, float* dh, msha_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSHA_GNN_H_ */

@@ -1,0 +1,127 @@
+"""ctypes binding of ``lib/libmsha_gnn.so`` (the C ABI in include/msha_gnn.h).
+
+The library is the product path: there is no CPU or PyTorch fallback.  If it is
+missing or fails to load, every op raises ``MshaLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first: the library binds to it)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
+
+MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
+
+
+class MshaLibraryError(RuntimeError):
+    pass
+
+
+class MshaGraph(C.Structure):
+    """Mirror of ``struct msha_graph`` (include/msha_gnn.h)."""
+
+    _fields_ = [
+        ("n_rows", C.c_int64), ("n_cols", C.c_int64), ("n_edges", C.c_int64),
+        ("rowptr", C.c_void_p), ("col", C.c_void_p), ("rowflag", C.c_void_p),
+        ("colptr", C.c_void_p), ("csc_row", C.c_void_p), ("csc_eid", C.c_void_p),
+        ("n_chunks", C.c_int64), ("chunk_col", C.c_void_p), ("chunk_start", C.c_void_p),
+        ("chunk_end", C.c_void_p),
+        ("n_multi", C.c_int64), ("multi_col", C.c_void_p), ("multi_first", C.c_void_p),
+        ("multi_count", C.c_void_p),
+    ]
+
+
+P = C.c_void_p
+I32, I64, U64, F32, SZ = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_size_t
+GP = C.POINTER(MshaGraph)
+
+# name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
+SIGNATURES = {
+    "msha_abi_version": (C.c_int, []),
+    "msha_last_error": (C.c_char_p, []),
+    "msha_dropout_keep_mask": (C.c_int, [U64, U64, I64, F32, P, P]),
+    "msha_inter_adjacency": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
+    "msha_normalize_adjacency": (C.c_int, [P, I64, I64, P, P, P]),
+    "msha_graph_workspace_size": (SZ, [I64, I64]),
+    "msha_graph_count": (C.c_int, [P, I64, I64, P, P, P, P, SZ, P]),
+    "msha_graph_fill": (C.c_int, [P, I64, I64, P, P, P, P, P, P, P, SZ, P]),
+    "msha_edge_attention_supported": (C.c_int, [I32, I32]),
+    "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, P, P, P, F32, F32, U64, U64, P, P, P,
+                                          P]),
+    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, P, P, F32, F32,
+                                               U64, U64, P, P, P, P, P]),
+    "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
+    "msha_csc_aggregate": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),
+    "msha_gal_bwd": (C.c_int, [GP, P, P, F32, U64, U64, P, P]),
+}
+
+_lib = None
+_load_error = None
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and type the library.  Raises MshaLibraryError if unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        _load_error = (f"HIP library not found at {path}; build it with "
+                       f"`python msha--gnn_amd/build.py` (or __graft_entry__.build())")
+        raise MshaLibraryError(_load_error)
+    try:
+        lib = C.CDLL(path)
+    except OSError as e:  # pragma: no cover - depends on the box
+        _load_error = f"failed to load {path}: {e}"
+        raise MshaLibraryError(_load_error) from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.msha_abi_version() != 1:
+        raise MshaLibraryError("ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except MshaLibraryError:
+        return False
+
+
+def exported_symbols():
+    return sorted(SIGNATURES)
+
+
+def call(name: str, *args):
+    """Invoke an ABI function; raise on a non-zero status with the library message."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != MSHA_OK:
+        msg = lib.msha_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_cuda(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("msha_gnn_amd ops run on the GPU only (got a CPU tensor); "
+                               "move the model and adjacency to the HIP device")

@@ -1,0 +1,80 @@
+"""Build the gfx950 HIP library ``lib/libmsha_gnn.so`` in-tree with hipcc.
+
+    python msha--gnn_amd/build.py [--force]
+
+Each ``csrc/*.hip`` is compiled to an object (cached by mtime against the sources
+and headers), then linked into one shared library whose exported symbols are the
+``extern "C"`` functions of ``include/msha_gnn.h``.  The library links the HIP
+runtime by its soname, so inside a torch process it binds to the runtime torch
+already loaded (one HIP runtime per process, shared streams and allocations).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIBDIR = os.path.join(PKG, "lib")
+OBJDIR = os.path.join(LIBDIR, "obj")
+LIB = os.path.join(LIBDIR, "libmsha_gnn.so")
+ARCH = os.environ.get("MSHA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE,
+          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-parameter",
+          "-fvisibility=hidden", "-munsafe-fp-atomics"]
+
+
+def _headers():
+    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+    if not _stale(obj, [src] + _headers()):
+        return obj, None
+    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    os.replace(obj + ".tmp", obj)
+    return obj, None
+
+
+def build(force: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    if force:
+        for o in glob.glob(os.path.join(OBJDIR, "*.o")):
+            os.remove(o)
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        results = list(ex.map(_compile, srcs))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in results]
+    if force or _stale(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,125 @@
+// Shared device/host helpers for the MSHA-GNN gfx950 library.
+//
+// Everything here is written for CDNA4 (gfx950): 64-lane wavefronts, 64-bit
+// ballots, xor-shuffles lowered to ds_swizzle / DPP by hipcc.  No CUDA shims.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/msha_gnn.h"
+
+namespace msha {
+
+constexpr int kWave = 64;
+
+// ---- error plumbing (thread-local last error, no exceptions across the ABI) ----
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+#define MSHA_ARG_CHECK(cond, msg)                              \
+  do {                                                        \
+    if (!(cond)) return ::msha::fail(MSHA_ERR_ARG, (msg));    \
+  } while (0)
+
+// ---- wave helpers ----
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+template <int FIRST>
+__device__ __forceinline__ float wave_xor_max(float v) {
+#pragma unroll
+  for (int o = FIRST; o < kWave; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+template <int FIRST>
+__device__ __forceinline__ float wave_xor_sum(float v) {
+#pragma unroll
+  for (int o = FIRST; o < kWave; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// sum over an aligned group of G consecutive lanes (G power of two); all lanes get it
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float4 f4_scale(float4 a, float s) {
+  return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
+}
+__device__ __forceinline__ float4 f4_fma(float s, float4 a, float4 c) {
+  return make_float4(fmaf(s, a.x, c.x), fmaf(s, a.y, c.y), fmaf(s, a.z, c.z), fmaf(s, a.w, c.w));
+}
+__device__ __forceinline__ float f4_dot(float4 a, float4 b) {
+  return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+}
+__device__ __forceinline__ float4 f4_xor_add(float4 v, int o) {
+  return make_float4(v.x + __shfl_xor(v.x, o), v.y + __shfl_xor(v.y, o),
+                     v.z + __shfl_xor(v.z, o), v.w + __shfl_xor(v.w, o));
+}
+
+__device__ __forceinline__ float lrelu(float x, float slope) { return x > 0.f ? x : x * slope; }
+
+// ---- counter-based dropout (Philox4x32-10) ----
+// keep(i) = philox(seed; counter = {i, offset}).x >= p * 2^32.  Deterministic per
+// element index, so forward and backward regenerate the same mask without storing it.
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+__host__ __device__ __forceinline__ uint32_t philox_x(uint64_t seed, uint64_t offset,
+                                                      uint64_t idx) {
+  uint32_t c0 = (uint32_t)idx, c1 = (uint32_t)(idx >> 32);
+  uint32_t c2 = (uint32_t)offset, c3 = (uint32_t)(offset >> 32);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+struct Dropout {
+  uint64_t seed, offset;
+  uint32_t threshold;  // drop when philox < threshold
+  float scale;         // 1 / (1 - p)
+  bool active;
+};
+
+inline Dropout make_dropout(float p, uint64_t seed, uint64_t offset) {
+  Dropout d;
+  d.seed = seed;
+  d.offset = offset;
+  d.active = p > 0.f;
+  double t = (double)p * 4294967296.0;
+  d.threshold = p >= 1.f ? 0xFFFFFFFFu : (uint32_t)(t > 4294967295.0 ? 4294967295.0 : t);
+  d.scale = p > 0.f && p < 1.f ? (float)(1.0 / (1.0 - (double)p)) : (p >= 1.f ? 0.f : 1.f);
+  return d;
+}
+
+__device__ __forceinline__ float dropout_factor(const Dropout& d, uint64_t idx) {
+  if (!d.active) return 1.f;
+  return philox_x(d.seed, d.offset, idx) >= d.threshold ? d.scale : 0.f;
+}
+
+inline int grid_for(int64_t work_items, int per_block, int cap = 1 << 20) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace msha

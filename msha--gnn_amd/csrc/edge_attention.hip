@@ -1,0 +1,483 @@
+// Fused edge-softmax + attention-weighted aggregation for gfx950.
+//
+// Reference op chain (dense in the reference, sparse here):
+//   Ablation.py:266-267  e12 = lrelu(cat(h1_j, h2_i) @ a)        -> el_i + er_j per edge
+//   Ablation.py:268-271  where(adj>0, e12, -9e15); softmax; dropout -> segmented softmax
+//   Ablation.py:274      u = att @ h1                             -> CSR gather-aggregate
+//   Ablation.py:273      v = att.t() @ h2                         -> CSC aggregate
+//   + the autograd backward of all of the above.
+//
+// Layout of work on a 64-lane wavefront (one CSR row per wave at a time):
+//   score layout  : lane = e_s * H + h_s   (CE = 64/H edges x H heads per chunk)
+//   gather layout : lane = g_e * NQ + q    (NQ = H*F/4 float4 quads per feature row,
+//                                           EPI = 64/NQ edges per wave-instruction,
+//                                           16 B per lane, whole rows per instruction)
+// Scores/softmax statistics live in the score layout and reach the gather lanes
+// through ds_bpermute (__shfl).  The forward is single-pass (online softmax with
+// per-head rescale of the accumulators) and stores only log-sum-exp per
+// (row, head); the backward recomputes the attention from it and uses
+// sum_e att_e * g_e = dU_i . u_i (FlashAttention's "D" identity), so the row
+// pass needs no second sweep over the gathered rows.
+#include "common.h"
+
+namespace msha {
+
+template <int H, int F>
+struct Geo {
+  static constexpr int D = H * F;
+  static constexpr int NQ = D / 4;
+  static constexpr int QPL = NQ > 64 ? NQ / 64 : 1;
+  static constexpr int EPI = NQ >= 64 ? 1 : 64 / NQ;
+  static constexpr int CE = 64 / H;
+  static constexpr int QH = F / 4;
+  static_assert(F % 4 == 0, "feat must be a multiple of 4");
+  static_assert(H >= 1 && H <= 64 && (64 % H) == 0, "heads must divide 64");
+  static_assert(CE % EPI == 0, "score chunk must cover whole gather groups");
+  static_assert(QH <= 64 && (64 % QH) == 0, "quads per head must divide 64");
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+// quad index (within the feature row) owned by this lane for slot k
+template <class G>
+__device__ __forceinline__ int quad_of(int lane, int k) {
+  return G::QPL == 1 ? (lane % G::NQ) : (lane + 64 * k);
+}
+
+// ------------------------------------------------------------------ forward ---
+template <int H, int F>
+__global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
+    const float* __restrict__ er, const float* __restrict__ hc, float slope, Dropout dp,
+    float* __restrict__ u, float* __restrict__ lse, float* __restrict__ attd) {
+  using G = Geo<H, F>;
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;
+  const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+
+  for (int64_t row = wave; row < n_rows; row += nwaves) {
+    const int32_t start = rowptr[row], end = rowptr[row + 1];
+    const bool virt = rowflag != nullptr && rowflag[row] != 0;
+    const float elh = el[row * H + h_s];
+    float m = -INFINITY, l = 0.f;
+    float4 acc[G::QPL];
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    for (int32_t cs = start; cs < end; cs += G::CE) {
+      const int32_t e = cs + e_s;
+      const bool valid = e < end;
+      const int32_t j = valid ? col[e] : 0;
+      float s = -INFINITY;
+      if (valid) s = virt ? 0.f : lrelu(elh + er[(int64_t)j * H + h_s], slope);
+      const float mn = fmaxf(m, wave_xor_max<H>(s));
+      const float alpha = __expf(m - mn);
+      const float pe = valid ? __expf(s - mn) : 0.f;
+      l = fmaf(l, alpha, wave_xor_sum<H>(pe));
+      m = mn;
+      const float w = valid ? pe * dropout_factor(dp, (uint64_t)e * H + h_s) : 0.f;
+#pragma unroll
+      for (int k = 0; k < G::QPL; ++k) {
+        const int hd = quad_of<G>(lane, k) / G::QH;
+        acc[k] = f4_scale(acc[k], __shfl(alpha, hd));
+      }
+      const int nvalid = min(G::CE, (int)(end - cs));
+#pragma unroll
+      for (int g = 0; g < G::CE; g += G::EPI) {
+        if (g >= nvalid) break;
+        const int ei = g + g_e;
+        const int32_t jq = __shfl(j, ei * H);
+#pragma unroll
+        for (int k = 0; k < G::QPL; ++k) {
+          const int q = quad_of<G>(lane, k);
+          const float wq = __shfl(w, ei * H + q / G::QH);
+          if (ei < nvalid) acc[k] = f4_fma(wq, ld4(hc + (int64_t)jq * G::D + 4 * q), acc[k]);
+        }
+      }
+    }
+    if (G::EPI > 1) {
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = f4_xor_add(acc[0], o);
+    }
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      const int q = quad_of<G>(lane, k);
+      const float lk = __shfl(l, q / G::QH);
+      const float inv = lk > 0.f ? 1.f / lk : 0.f;
+      if (g_e == 0) st4(u + row * G::D + 4 * q, f4_scale(acc[k], inv));
+    }
+    const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
+    if (lane < H) lse[row * H + lane] = lse_h;
+    if (attd != nullptr) {
+      for (int32_t cs = start; cs < end; cs += G::CE) {
+        const int32_t e = cs + e_s;
+        if (e < end) {
+          const float s = virt ? 0.f : lrelu(elh + er[(int64_t)col[e] * H + h_s], slope);
+          attd[(int64_t)e * H + h_s] =
+              __expf(s - lse_h) * dropout_factor(dp, (uint64_t)e * H + h_s);
+        }
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------- backward rows ---
+template <int H, int F, bool DV>
+__global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
+    const float* __restrict__ er, const float* __restrict__ hc, const float* __restrict__ lse,
+    const float* __restrict__ u, const float* __restrict__ dU, const float* __restrict__ hs,
+    const float* __restrict__ dV, float slope, Dropout dp, float* __restrict__ d_el,
+    float* __restrict__ de, float* __restrict__ attd, float* __restrict__ d_hs) {
+  using G = Geo<H, F>;
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;
+  const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  // lane (in the gather layout) holding the first quad of head h_s, and its slot
+  const int dsrc_k = (h_s * G::QH) / 64;
+  const int dsrc_l = (h_s * G::QH) % 64;
+
+  for (int64_t row = wave; row < n_rows; row += nwaves) {
+    const int32_t start = rowptr[row], end = rowptr[row + 1];
+    const bool virt = rowflag != nullptr && rowflag[row] != 0;
+    const float elh = el[row * H + h_s];
+    const float lseh = lse[row * H + h_s];
+    float4 dUq[G::QPL], hsq[G::QPL];
+    float dpart[G::QPL];
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      const int q = quad_of<G>(lane, k);
+      dUq[k] = ld4(dU + row * G::D + 4 * q);
+      dpart[k] = f4_dot(dUq[k], ld4(u + row * G::D + 4 * q));
+      hsq[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (DV) {
+      // w_i = sum_e attd_e dV[j]   (== d hs_i of the v-branch)
+      float4 wacc[G::QPL];
+#pragma unroll
+      for (int k = 0; k < G::QPL; ++k) wacc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int32_t cs = start; cs < end; cs += G::CE) {
+        const int32_t e = cs + e_s;
+        const bool valid = e < end;
+        const int32_t j = valid ? col[e] : 0;
+        float w = 0.f;
+        if (valid) {
+          const float s = virt ? 0.f : lrelu(elh + er[(int64_t)j * H + h_s], slope);
+          w = __expf(s - lseh) * dropout_factor(dp, (uint64_t)e * H + h_s);
+        }
+        const int nvalid = min(G::CE, (int)(end - cs));
+#pragma unroll
+        for (int g = 0; g < G::CE; g += G::EPI) {
+          if (g >= nvalid) break;
+          const int ei = g + g_e;
+          const int32_t jq = __shfl(j, ei * H);
+#pragma unroll
+          for (int k = 0; k < G::QPL; ++k) {
+            const int q = quad_of<G>(lane, k);
+            const float wq = __shfl(w, ei * H + q / G::QH);
+            if (ei < nvalid) wacc[k] = f4_fma(wq, ld4(dV + (int64_t)jq * G::D + 4 * q), wacc[k]);
+          }
+        }
+      }
+      if (G::EPI > 1) {
+#pragma unroll
+        for (int o = G::NQ; o < 64; o <<= 1) wacc[0] = f4_xor_add(wacc[0], o);
+      }
+#pragma unroll
+      for (int k = 0; k < G::QPL; ++k) {
+        const int q = quad_of<G>(lane, k);
+        if (g_e == 0) st4(d_hs + row * G::D + 4 * q, wacc[k]);
+        hsq[k] = ld4(hs + row * G::D + 4 * q);
+        dpart[k] += f4_dot(hsq[k], wacc[k]);
+      }
+    }
+    // D_h = dU_i.u_i (+ hs_i.w_i) per head, delivered to the score layout
+    float Ds = 0.f;
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      const float dk = group_sum<G::QH>(dpart[k]);
+      const float cand = __shfl(dk, dsrc_l);
+      if (k == dsrc_k) Ds = cand;
+    }
+    float del = 0.f;
+    for (int32_t cs = start; cs < end; cs += G::CE) {
+      const int32_t e = cs + e_s;
+      const bool valid = e < end;
+      const int32_t j = valid ? col[e] : 0;
+      float pre = 0.f, att = 0.f, dropf = 0.f;
+      if (valid) {
+        pre = elh + er[(int64_t)j * H + h_s];
+        const float s = virt ? 0.f : lrelu(pre, slope);
+        att = __expf(s - lseh);
+        dropf = dropout_factor(dp, (uint64_t)e * H + h_s);
+      }
+      const int nvalid = min(G::CE, (int)(end - cs));
+      float gsum = 0.f;
+#pragma unroll
+      for (int g = 0; g < G::CE; g += G::EPI) {
+        if (g >= nvalid) break;
+        const int ei = g + g_e;
+        const int32_t jq = __shfl(j, ei * H);
+        const bool mine = e_s >= g && e_s < g + G::EPI;
+        const int srcl = G::QPL == 1 ? ((e_s - g) & (G::EPI - 1)) * G::NQ + h_s * G::QH : dsrc_l;
+#pragma unroll
+        for (int k = 0; k < G::QPL; ++k) {
+          const int q = quad_of<G>(lane, k);
+          float t = 0.f;
+          if (ei < nvalid) {
+            t = f4_dot(dUq[k], ld4(hc + (int64_t)jq * G::D + 4 * q));
+            if (DV) t += f4_dot(hsq[k], ld4(dV + (int64_t)jq * G::D + 4 * q));
+          }
+          t = group_sum<G::QH>(t);
+          const float cand = __shfl(t, srcl);
+          if (mine && (G::QPL == 1 || k == dsrc_k)) gsum = cand;
+        }
+      }
+      if (valid) {
+        const float ds = att * (gsum * dropf - Ds);
+        const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
+        de[(int64_t)e * H + h_s] = dev;
+        attd[(int64_t)e * H + h_s] = att * dropf;
+        del += dev;
+      }
+    }
+    del = wave_xor_sum<H>(del);
+    if (lane < H) d_el[row * H + lane] = del;
+  }
+}
+
+// ------------------------------------------------------- column (CSC) aggregate ---
+template <int H, int F, bool HASX>
+__global__ void __launch_bounds__(256) csc_aggregate_kernel(
+    const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
+    const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
+    const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid,
+    const float* __restrict__ w, const float* __restrict__ x, const float* __restrict__ table,
+    float* __restrict__ out, float* __restrict__ out_x, float* __restrict__ part,
+    float* __restrict__ part_x) {
+  using G = Geo<H, F>;
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;
+  const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+
+  for (int64_t c = wave; c < n_chunks; c += nwaves) {
+    const int32_t jc = chunk_col[c], s0 = chunk_start[c], s1 = chunk_end[c];
+    const bool whole = s0 == colptr[jc] && s1 == colptr[jc + 1];
+    float4 acc[G::QPL];
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float xacc = 0.f;
+    for (int32_t cs = s0; cs < s1; cs += G::CE) {
+      const int32_t slot = cs + e_s;
+      const bool valid = slot < s1;
+      const int32_t i = valid ? csc_row[slot] : 0;
+      const int64_t eid = valid ? (int64_t)csc_eid[slot] : 0;
+      const float wv = valid ? w[eid * H + h_s] : 0.f;
+      if (HASX && valid) xacc += x[eid * H + h_s];
+      const int nvalid = min(G::CE, (int)(s1 - cs));
+#pragma unroll
+      for (int g = 0; g < G::CE; g += G::EPI) {
+        if (g >= nvalid) break;
+        const int ei = g + g_e;
+        const int32_t iq = __shfl(i, ei * H);
+#pragma unroll
+        for (int k = 0; k < G::QPL; ++k) {
+          const int q = quad_of<G>(lane, k);
+          const float wq = __shfl(wv, ei * H + q / G::QH);
+          if (ei < nvalid) acc[k] = f4_fma(wq, ld4(table + (int64_t)iq * G::D + 4 * q), acc[k]);
+        }
+      }
+    }
+    if (G::EPI > 1) {
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = f4_xor_add(acc[0], o);
+    }
+    float* dst = whole ? out + (int64_t)jc * G::D : part + c * G::D;
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      if (g_e == 0) st4(dst + 4 * quad_of<G>(lane, k), acc[k]);
+    }
+    if (HASX) {
+      xacc = wave_xor_sum<H>(xacc);
+      if (lane < H) (whole ? out_x + (int64_t)jc * H : part_x + c * H)[lane] = xacc;
+    }
+  }
+}
+
+// multi-chunk columns: add the chunk partials in chunk order
+__global__ void __launch_bounds__(256) csc_combine_kernel(
+    const int32_t* __restrict__ multi_col, const int32_t* __restrict__ multi_first,
+    const int32_t* __restrict__ multi_count, int64_t n_multi, int D, int H,
+    const float* __restrict__ part, const float* __restrict__ part_x, float* __restrict__ out,
+    float* __restrict__ out_x) {
+  const int W = D + (part_x != nullptr ? H : 0);
+  const int64_t total = n_multi * W;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t mi = t / W;
+    const int f = (int)(t % W);
+    const int32_t jc = multi_col[mi], first = multi_first[mi], cnt = multi_count[mi];
+    float s = 0.f;
+    if (f < D) {
+      for (int k = 0; k < cnt; ++k) s += part[(int64_t)(first + k) * D + f];
+      out[(int64_t)jc * D + f] = s;
+    } else {
+      const int h = f - D;
+      for (int k = 0; k < cnt; ++k) s += part_x[(int64_t)(first + k) * H + h];
+      out_x[(int64_t)jc * H + h] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------- dispatch ---
+// Compiled (heads, feat) set.  Extend here (and in msha_edge_attention_supported).
+#define MSHA_FOR_EACH_SHAPE(X) \
+  X(1, 8) X(1, 16) X(1, 32) X(1, 64) X(1, 128) \
+  X(2, 8) X(2, 16) X(2, 32) X(2, 64) X(2, 128) \
+  X(4, 8) X(4, 16) X(4, 32) X(4, 64) X(4, 128) \
+  X(8, 8) X(8, 16) X(8, 32) X(8, 64) X(8, 128)
+
+static bool shape_supported(int H, int F) {
+#define X(h, f) if (H == h && F == f) return true;
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+  return false;
+}
+
+// one wave per row (or chunk), 4 waves per block; grid-stride beyond the cap
+static dim3 wave_grid(int64_t items) { return dim3(grid_for(items, 4, 1 << 20)); }
+
+static int check_graph(const msha_graph* g, bool need_csc) {
+  MSHA_ARG_CHECK(g != nullptr, "graph descriptor is NULL");
+  MSHA_ARG_CHECK(g->n_rows > 0 && g->n_cols > 0 && g->n_edges >= 0, "graph: bad sizes");
+  MSHA_ARG_CHECK(g->rowptr && (g->n_edges == 0 || g->col), "graph: CSR arrays missing");
+  if (need_csc) {
+    MSHA_ARG_CHECK(g->colptr && (g->n_edges == 0 || (g->csc_row && g->csc_eid)),
+                   "graph: CSC arrays missing");
+    MSHA_ARG_CHECK(g->n_chunks >= g->n_cols && g->chunk_col && g->chunk_start && g->chunk_end,
+                   "graph: CSC chunk plan missing (need >= 1 chunk per column)");
+    MSHA_ARG_CHECK(g->n_multi == 0 || (g->multi_col && g->multi_first && g->multi_count),
+                   "graph: multi-chunk column list missing");
+  }
+  return MSHA_OK;
+}
+
+}  // namespace msha
+
+using namespace msha;
+
+extern "C" int msha_edge_attention_supported(int32_t heads, int32_t feat) {
+  return shape_supported(heads, feat) ? 1 : 0;
+}
+
+extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
+                                       const float* el, const float* er, const float* hc,
+                                       float neg_slope, float drop_p, uint64_t seed,
+                                       uint64_t offset, float* u, float* lse, float* attd,
+                                       msha_stream_t stream) {
+  if (int rc = check_graph(g, false)) return rc;
+  MSHA_ARG_CHECK(el && er && hc && u && lse, "edge_attention_fwd: null pointer");
+  MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_fwd: p must be in [0,1]");
+  if (!shape_supported(heads, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: unsupported (heads, feat)");
+  const Dropout dp = make_dropout(drop_p, seed, offset);
+  hipStream_t s = (hipStream_t)stream;
+#define X(h, f)                                                                             \
+  if (heads == h && feat == f)                                                              \
+    hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f>), wave_grid(g->n_rows), dim3(256), 0, s, \
+                       g->rowptr, g->col, g->rowflag, g->n_rows, el, er, hc, neg_slope, dp, \
+                       u, lse, attd);
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+  return check_launch("edge_attention_fwd");
+}
+
+extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
+                                            const float* el, const float* er, const float* hc,
+                                            const float* lse, const float* u, const float* dU,
+                                            const float* hs, const float* dV, float neg_slope,
+                                            float drop_p, uint64_t seed, uint64_t offset,
+                                            float* d_el, float* de, float* attd, float* d_hs,
+                                            msha_stream_t stream) {
+  if (int rc = check_graph(g, false)) return rc;
+  MSHA_ARG_CHECK(el && er && hc && lse && u && dU && d_el && de && attd,
+                 "edge_attention_bwd_rows: null pointer");
+  MSHA_ARG_CHECK(dV == nullptr || (hs && d_hs), "edge_attention_bwd_rows: dV needs hs and d_hs");
+  MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_bwd_rows: p must be in [0,1]");
+  if (!shape_supported(heads, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_rows: unsupported (heads, feat)");
+  const Dropout dp = make_dropout(drop_p, seed, offset);
+  hipStream_t s = (hipStream_t)stream;
+#define X(h, f)                                                                               \
+  if (heads == h && feat == f) {                                                              \
+    if (dV)                                                                                   \
+      hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, true>), wave_grid(g->n_rows),       \
+                         dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,   \
+                         hc, lse, u, dU, hs, dV, neg_slope, dp, d_el, de, attd, d_hs);        \
+    else                                                                                      \
+      hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, false>), wave_grid(g->n_rows),      \
+                         dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,   \
+                         hc, lse, u, dU, hs, dV, neg_slope, dp, d_el, de, attd, d_hs);        \
+  }
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+  return check_launch("edge_attention_bwd_rows");
+}
+
+extern "C" size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t heads,
+                                                    int32_t feat) {
+  if (g == nullptr || heads <= 0 || feat <= 0) return 0;
+  const size_t per = (size_t)heads * (size_t)feat + (size_t)heads;
+  return (size_t)g->n_chunks * per * sizeof(float) + 256;
+}
+
+extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat,
+                                  const float* w, const float* x, const float* table, float* out,
+                                  float* out_x, void* ws, size_t ws_bytes, msha_stream_t stream) {
+  if (int rc = check_graph(g, true)) return rc;
+  MSHA_ARG_CHECK(w && table && out, "csc_aggregate: null pointer");
+  MSHA_ARG_CHECK(x == nullptr || out_x != nullptr, "csc_aggregate: x needs out_x");
+  if (!shape_supported(heads, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "csc_aggregate: unsupported (heads, feat)");
+  const int64_t D = (int64_t)heads * feat;
+  float* part = nullptr;
+  float* part_x = nullptr;
+  if (g->n_multi > 0) {
+    MSHA_ARG_CHECK(ws != nullptr && ws_bytes >= msha_csc_aggregate_workspace_size(g, heads, feat),
+                   "csc_aggregate: workspace too small");
+    part = (float*)ws;
+    part_x = part + g->n_chunks * D;
+  }
+  hipStream_t s = (hipStream_t)stream;
+#define X(h, f)                                                                                \
+  if (heads == h && feat == f) {                                                               \
+    if (x)                                                                                     \
+      hipLaunchKernelGGL((csc_aggregate_kernel<h, f, true>), wave_grid(g->n_chunks), dim3(256), \
+                         0, s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,        \
+                         g->colptr, g->csc_row, g->csc_eid, w, x, table, out, out_x, part,     \
+                         part_x);                                                              \
+    else                                                                                       \
+      hipLaunchKernelGGL((csc_aggregate_kernel<h, f, false>), wave_grid(g->n_chunks),          \
+                         dim3(256), 0, s, g->chunk_col, g->chunk_start, g->chunk_end,          \
+                         g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x, table, out,     \
+                         out_x, part, part_x);                                                 \
+  }
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+  if (g->n_multi > 0) {
+    const int64_t W = D + (x ? heads : 0);
+    hipLaunchKernelGGL(csc_combine_kernel, dim3(grid_for(g->n_multi * W, 256, 8192)), dim3(256),
+                       0, s, g->multi_col, g->multi_first, g->multi_count, g->n_multi, (int)D,
+                       (int)heads, part, x ? part_x : nullptr, out, out_x);
+  }
+  return check_launch("csc_aggregate");
+}

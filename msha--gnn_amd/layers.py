@@ -1,0 +1,191 @@
+"""Drop-in nn.Modules of the reference hot path, computed by the HIP library.
+
+Same class names, constructor arguments, parameter names/shapes, state_dict keys
+and RNG consumption order as the reference, so a model built after
+``torch.manual_seed(s)`` holds bit-identical initial parameters:
+
+  GraphAttentionLayer   GAT.py:6-35        (also Ablation.py:86-115, LLP.py:117-146)
+  GAT                   GAT.py:38-58
+  LLPGAT                LLP.py:148-168     (GAT whose forward takes external features)
+  OursLayer3            Ablation.py:235-277
+  ablation3             Ablation.py:279-301  (its heads run as ONE multi-head launch)
+
+Adjacency arguments may be dense (N, M) tensors (as in train.py; the CSR/CSC view
+is built once on the GPU and cached) or prebuilt ``Graph`` objects.  Every
+attention op runs on the GPU through include/msha_gnn.h; CPU tensors raise.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import functional as MF
+from .graph import Graph, graph_for
+
+ALPHA = 0.2  # LeakyReLU slope of the reference layers (Ablation.py:241, :267)
+
+
+def _graph(adj) -> Graph:
+    return adj if isinstance(adj, Graph) else graph_for(adj)
+
+
+def _xavier_param(*shape):
+    p = nn.Parameter(torch.zeros(size=shape))
+    nn.init.xavier_uniform_(p.data, gain=1.414)
+    return p
+
+
+def _features_with_gdp(n_rows, n_features, gdp):
+    """``cat(rand([N, d])[:, :-1], gdp)`` -- learnable table whose last column is
+    the county GDP (GAT.py:41-42, Ablation.py:283-284)."""
+    gdp_values = torch.tensor(list(gdp.values())).view(-1, 1)
+    return nn.Parameter(torch.cat((torch.rand([n_rows, n_features])[:, :-1], gdp_values), dim=1))
+
+
+class GraphAttentionLayer(nn.Module):
+    """GAT.py:6-35.  Its score concatenates h_i with itself, so the attention is
+    mask/deg and the layer is ``elu(dropout(mask/deg) * (input @ W))``; the
+    ``a`` parameter is kept (state_dict parity) and receives a zero gradient,
+    which is what the reference's ~1e-7 gradient is up to rounding."""
+
+    def __init__(self, in_features, out_features, dropout):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.dropout = dropout
+        self.W = _xavier_param(in_features, out_features)
+        self.a = _xavier_param(2 * out_features, 1)
+
+    def forward(self, input, adj):
+        g = _graph(adj)
+        h = torch.mm(input, self.W)
+        return MF.gal(g, h, self.dropout, self.training, zero_grad_of=self.a)
+
+
+class GAT(nn.Module):
+    """GAT.py:38-58: heads of GraphAttentionLayer over a learnable feature table."""
+
+    def __init__(self, n_features, n_classes, n_heads, dropout, gdp, N):
+        super().__init__()
+        self.features = _features_with_gdp(N, n_features, gdp)
+        self.n_classes = n_classes
+        self.n_heads = n_heads
+        self.dropout = dropout
+        self.attentions = [GraphAttentionLayer(n_features, n_classes, dropout=dropout)
+                           for _ in range(n_heads)]
+        for i, attention in enumerate(self.attentions):
+            self.add_module(f"attention_{i}", attention)
+        self.out_att = GraphAttentionLayer(n_features * n_heads, n_classes, dropout=dropout)
+
+    def _body(self, x, adj):
+        g = _graph(adj)
+        x = F.dropout(x, self.dropout, training=self.training)
+        x = torch.cat([att(x, g) for att in self.attentions], dim=1)
+        x = F.dropout(x, self.dropout, training=self.training)
+        x = F.elu(self.out_att(x, g))
+        return F.log_softmax(x, dim=1)
+
+    def forward(self, adj):
+        return self._body(self.features, adj)
+
+
+class LLPGAT(GAT):
+    """LLP.py:148-168: the teacher GAT of the link-prediction script -- same layers,
+    no feature table, ``forward(input, adj)``."""
+
+    def __init__(self, n_features, n_classes, n_heads, dropout, gdp=None, N=None):
+        nn.Module.__init__(self)
+        self.n_classes = n_classes
+        self.n_heads = n_heads
+        self.dropout = dropout
+        self.attentions = [GraphAttentionLayer(n_features, n_classes, dropout=dropout)
+                           for _ in range(n_heads)]
+        for i, attention in enumerate(self.attentions):
+            self.add_module(f"attention_{i}", attention)
+        self.out_att = GraphAttentionLayer(n_features * n_heads, n_classes, dropout=dropout)
+
+    def forward(self, input, adj):
+        return self._body(input, adj)
+
+
+class OursLayer3(nn.Module):
+    """Ablation.py:235-277: bipartite source->recipient attention with BN'd u/v
+    aggregates and ``elu(u @ v.T)``.  a3/a4/bn3 exist (state_dict parity) but, as
+    in the reference, take no part in the forward."""
+
+    def __init__(self, in_features, out_features, dropout):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.alpha = ALPHA
+        self.dropout = dropout
+        self.W1 = nn.Parameter(torch.zeros(size=(in_features, out_features)))
+        self.W2 = nn.Parameter(torch.zeros(size=(in_features, out_features)))
+        nn.init.xavier_uniform_(self.W1.data, gain=1.414)
+        nn.init.xavier_uniform_(self.W2.data, gain=1.414)
+        self.a = _xavier_param(2 * out_features, 1)
+        self.a3 = _xavier_param(2 * out_features, 1)
+        self.a4 = _xavier_param(2 * out_features, 1)
+        self.leakyrelu = nn.LeakyReLU(self.alpha)
+        self.bn1 = nn.BatchNorm1d(out_features)
+        self.bn2 = nn.BatchNorm1d(out_features)
+        self.bn3 = nn.BatchNorm1d(out_features)
+
+    def epilogue(self, u, v):
+        """Ablation.py:273-277 on the aggregates: BN + LeakyReLU + u @ v.T + elu."""
+        v_out = self.leakyrelu(self.bn1(v))
+        u_out = self.leakyrelu(self.bn2(u))
+        return F.elu(u_out @ v_out.t())
+
+    def forward(self, Sinput, Rinput, inter_adj, city_adj, province_adj, source_index):
+        return fused_ours_layer3([self], Sinput, Rinput, _graph(inter_adj), self.training)[0]
+
+
+def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
+    """All heads of an ablation3 in one launch: projections stacked along features,
+    one (H-head) edge-attention forward/backward, per-head BN epilogues."""
+    H = len(heads)
+    Fd = heads[0].out_features
+    n, m = s_input.shape[0], r_input.shape[0]
+    if graph.n_cols != m or graph.n_rows != n:
+        raise ValueError(f"inter_adj is {graph.n_rows}x{graph.n_cols}, features are {n} "
+                         f"sources x {m} recipients")
+    W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
+    W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
+    a = torch.stack([h.a.view(-1) for h in heads])  # (H, 2F)
+    h1 = torch.mm(r_input, W1).view(m, H, Fd)  # (M, H, F) recipient side
+    h2 = torch.mm(s_input, W2).view(n, H, Fd)  # (N, H, F) source side
+    er = torch.einsum("mhf,hf->mh", h1, a[:, :Fd])  # a[:F] . h1_j  (Ablation.py:266)
+    el = torch.einsum("nhf,hf->nh", h2, a[:, Fd:])  # a[F:] . h2_i
+    u, v = MF.edge_attention(graph, el, er, h1, hs=h2, p=heads[0].dropout, training=training)
+    return [head.epilogue(u[:, k], v[:, k]) for k, head in enumerate(heads)]
+
+
+class ablation3(nn.Module):  # noqa: N801  (reference class name)
+    """Ablation.py:279-301: n_heads OursLayer3 -> cat -> dropout -> GAL -> elu ->
+    log_softmax over recipients."""
+
+    def __init__(self, in_features, out_features, n_classes, n_heads, dropout, gdp, Scount,
+                 Rcount):
+        super().__init__()
+        self.Sfeatures = _features_with_gdp(Scount, in_features, gdp)
+        self.Rfeatures = nn.Parameter(torch.rand([Rcount, in_features]))
+        self.n_classes = n_classes
+        self.n_heads = n_heads
+        self.dropout = dropout
+        self.attentions = [OursLayer3(in_features, out_features, dropout=dropout)
+                           for _ in range(n_heads)]
+        for i, attention in enumerate(self.attentions):
+            self.add_module(f"attention_{i}", attention)
+        self.out_att = GraphAttentionLayer(n_classes * n_heads, n_classes, dropout=dropout)
+
+    def forward(self, inter_adj, city_adj, province_adj, source_index):
+        g = _graph(inter_adj)
+        s_input = F.dropout(self.Sfeatures, self.dropout, training=self.training)
+        r_input = F.dropout(self.Rfeatures, self.dropout, training=self.training)
+        x = torch.cat(fused_ours_layer3(self.attentions, s_input, r_input, g, self.training),
+                      dim=1)
+        x = F.dropout(x, self.dropout, training=self.training)
+        x = F.elu(self.out_att(x, g))
+        return F.log_softmax(x, dim=1)

@@ -1,0 +1,133 @@
+"""CPU-side checks of the host layer: ABI surface, drop-in constructors, graph plans.
+
+No compute call reaches the GPU here (these run in the CPU-only container)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, golden
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "msha_gnn.h")).read()
+    return sorted(set(re.findall(r"MSHA_API\s+[\w\s\*]+?\b(msha_\w+)\s*\(", text)))
+
+
+def test_header_symbols_bound_by_ctypes(msha):
+    from msha_gnn_amd import _lib
+
+    assert header_symbols() == _lib.exported_symbols()
+
+
+def test_library_exports_every_header_symbol(msha):
+    from msha_gnn_amd import _lib
+
+    lib = _lib.load()  # loads without touching the GPU
+    assert lib.msha_abi_version() == 1
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (msha_\w+)", out))
+    assert set(header_symbols()) <= exported
+    # host-only queries (no kernel launch)
+    assert lib.msha_edge_attention_supported(8, 16) == 1
+    assert lib.msha_edge_attention_supported(3, 16) == 0
+    assert lib.msha_graph_workspace_size(39179, 32) > 0
+
+
+def test_abi_argument_errors_are_reported(msha):
+    from msha_gnn_amd import _lib
+
+    with pytest.raises(RuntimeError, match="graph descriptor is NULL"):
+        _lib.call("msha_edge_attention_fwd", None, 8, 16, None, None, None, 0.2, 0.0, 0, 0, None,
+                  None, None, None)
+    with pytest.raises(RuntimeError, match="p must be in"):
+        _lib.call("msha_dropout_keep_mask", 0, 0, 10, 1.5, 1, None)
+
+
+def _sd_equal(a, b_npz, prefix):
+    for k, v in a.items():
+        ref = b_npz[prefix + k]
+        assert np.array_equal(v.numpy(), ref), k
+
+
+def test_ablation3_init_matches_reference_bitwise(msha):
+    from msha_gnn_amd import layers
+
+    z = golden("sub512.npz")
+    gdp = {i: float(x) for i, x in enumerate(z["gdp"])}
+    torch.manual_seed(0)
+    m = layers.ablation3(in_features=128, out_features=64, n_classes=32, n_heads=2, dropout=0.0,
+                         gdp=gdp, Scount=512, Rcount=32)
+    sd = m.state_dict()
+    assert list(sd.keys()) == [k[len("init."):] for k in z.files if k.startswith("init.")]
+    _sd_equal(sd, z, "init.")
+
+
+def test_gat_init_matches_reference_bitwise(msha):
+    from msha_gnn_amd import layers
+
+    z = golden("gat_sub512.npz")
+    s = golden("sub512.npz")
+    gdp = {i: float(x) for i, x in enumerate(s["gdp"])}
+    torch.manual_seed(1)
+    m = layers.GAT(n_features=32, n_classes=32, n_heads=2, dropout=0.0, gdp=gdp, N=512)
+    sd = m.state_dict()
+    assert list(sd.keys()) == [k[len("init."):] for k in z.files if k.startswith("init.")]
+    _sd_equal(sd, z, "init.")
+
+
+def test_ours_layer3_init_matches_reference(msha):
+    from msha_gnn_amd import layers
+
+    e = golden("edge_cases.npz")
+    torch.manual_seed(6)
+    layer = layers.OursLayer3(16, 8, 0.0)
+    _sd_equal(layer.state_dict(), e, "ol3.init.")
+    torch.manual_seed(8)
+    gal = layers.GraphAttentionLayer(20, 80, 0.0)
+    _sd_equal(gal.state_dict(), e, "gal.init.")
+
+
+def test_csc_chunk_plan(msha):
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(0)
+    n, m = 3000, 7
+    deg = rng.integers(1, 5, n)
+    rowptr = np.concatenate([[0], np.cumsum(deg)])
+    col = np.concatenate([np.sort(rng.choice(m, d, replace=False)) for d in deg])
+    col[rowptr[:-1]] = 0  # column 0 is long: >= 3000 slots -> several chunks
+    col = np.concatenate([np.unique(col[rowptr[i]:rowptr[i + 1]]) for i in range(n)])
+    rowptr = np.concatenate([[0], np.cumsum([len(np.unique(col[rowptr[i]:rowptr[i + 1]]))
+                                             for i in range(n)])])
+    g = Graph.from_csr(rowptr, col, m, device="cpu")
+    p = g._plan
+    colptr = g.colptr.numpy()
+    cc, cs, ce = p["chunk_col"].numpy(), p["chunk_start"].numpy(), p["chunk_end"].numpy()
+    # chunks tile every column's CSC range in order, each <= CSC_CHUNK slots
+    for j in range(m):
+        sel = np.nonzero(cc == j)[0]
+        assert cs[sel[0]] == colptr[j] and ce[sel[-1]] == colptr[j + 1]
+        assert np.all(cs[sel[1:]] == ce[sel[:-1]]) and np.all(ce[sel] - cs[sel] <= 512)
+    mc = p["multi_col"].numpy()
+    assert 0 in mc and np.all(p["multi_count"].numpy() > 1)
+    # CSC slots: ascending rows within a column, eids map back to the same (row, col)
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    cr, ceid = g.csc_row.numpy(), g.csc_eid.numpy()
+    assert np.array_equal(rows[ceid], cr)
+    for j in range(m):
+        seg = cr[colptr[j]:colptr[j + 1]]
+        assert np.all(np.diff(seg) > 0) and np.all(col[ceid[colptr[j]:colptr[j + 1]]] == j)
+
+
+def test_ops_refuse_cpu_tensors(msha):
+    from msha_gnn_amd import layers
+
+    torch.manual_seed(0)
+    gal = layers.GraphAttentionLayer(4, 3, 0.0)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        gal(torch.rand(5, 4), torch.ones(5, 3))

@@ -1,0 +1,196 @@
+"""Pin the CPU oracle (oracle/gnn_oracle.py) against the reference's golden vectors.
+
+The fixtures were produced by running the reference's own modules
+(tests/golden/make_golden.py).  fp64 runs of the reference must be reproduced to
+~1e-10 by the oracle run in fp64; fp32 to the fp32 rounding level.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import gnn_oracle as O
+
+
+def _heads(z, prefix, n_heads, dt):
+    heads = []
+    for h in range(n_heads):
+        p = {}
+        for k in ("W1", "W2", "a"):
+            p[k] = z[f"{prefix}attention_{h}.{k}"].astype(dt)
+        for bn in ("bn1", "bn2"):
+            for k in ("weight", "bias", "running_mean", "running_var"):
+                p[f"{bn}_{k}"] = z[f"{prefix}attention_{h}.{bn}.{k}"].astype(dt)
+        heads.append(p)
+    return heads
+
+
+def _heads_eval(z, heads, tag, dt):
+    """eval() ran after the train forward, so BN running stats had moved once."""
+    for h, p in enumerate(heads):
+        for bn in ("bn1", "bn2"):
+            for k in ("running_mean", "running_var"):
+                p[f"{bn}_{k}"] = z[f"after{tag}.attention_{h}.{bn}.{k}"].astype(dt)
+    return heads
+
+
+def _sub512_inputs(z, dt):
+    rowptr, col = O.dense_to_csr(z["adj_norm"])
+    return rowptr, col, z["init.Sfeatures"].astype(dt), z["init.Rfeatures"].astype(dt)
+
+
+def test_r15_graph_counts_and_normalize():
+    g = golden("r15_graph.npz")
+    n, m = int(g["n"]), int(g["m"])
+    rowptr, col, cnt = g["rowptr"], g["col"].astype(np.int32), g["cnt"].astype(np.float32)
+    assert n == 39179 and m == 32 and len(col) == 91283 and int(g["n_flows"]) == 233887
+    dense = np.zeros((n, m), np.float32)
+    dense[O.edge_rows(rowptr), col] = cnt
+    # oracle CSR == reference mask order (row-major nonzero)
+    r2, c2 = O.dense_to_csr(dense)
+    np.testing.assert_array_equal(r2, rowptr)
+    np.testing.assert_array_equal(c2, col)
+    # reference normalize_adjacency_matrix values, bit-exact
+    norm = O.normalize_adjacency(dense)
+    np.testing.assert_array_equal(norm[dense > 0], g["norm"])
+    assert np.all(norm[dense == 0] == 0)
+    assert np.diff(rowptr).min() >= 1 and np.diff(rowptr).max() == 30
+
+
+def test_inter_adjacency_counts_match_reference():
+    z = golden("sub512.npz")
+    fl = z["flows"]
+    adj = O.inter_adjacency(fl[:, 0], fl[:, 1], 512, 32)
+    np.testing.assert_array_equal(adj, z["counts"])
+
+
+def test_normalize_edge_cases():
+    e = golden("edge_cases.npz")
+    np.testing.assert_array_equal(O.normalize_adjacency(e["norm_rand_in"]), e["norm_rand_out"])
+    out = O.normalize_adjacency(e["norm_zero_col_in"])
+    assert np.isnan(e["norm_zero_col_out"]).all() and np.isnan(out).all()
+    np.testing.assert_array_equal(O.normalize_adjacency(e["counts"]), e["adj_norm32"])
+
+
+@pytest.mark.parametrize("dt,tol", [(np.float64, 1e-10), (np.float32, 2e-5)])
+def test_ours_layer3_intermediates(dt, tol):
+    z = golden("sub512.npz")
+    rowptr, col, S, R = _sub512_inputs(z, dt)
+    tag = "64" if dt == np.float64 else "32"
+    for h, p in enumerate(_heads(z, "init.", 2, dt)):
+        r = O.ours_layer3_fwd(S, R, p, rowptr, col, training=True)
+        np.testing.assert_allclose(r["u_pre"], z[f"bn{tag}.h{h}_u_pre"], rtol=tol, atol=tol)
+        vref = z[f"bn{tag}.h{h}_v_pre"]
+        np.testing.assert_allclose(r["v_pre"], vref, rtol=tol, atol=tol * np.abs(vref).max())
+        if dt == np.float32:
+            att = np.zeros((512, 32), dt)
+            att[O.edge_rows(rowptr), col] = r["att"]
+            np.testing.assert_allclose(att, z[f"sm32.h{h}_att"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt,tol", [(np.float64, 1e-9), (np.float32, 1e-4)])
+def test_ablation3_forward(dt, tol):
+    z = golden("sub512.npz")
+    rowptr, col, S, R = _sub512_inputs(z, dt)
+    heads = _heads(z, "init.", 2, dt)
+    W = z["init.out_att.W"].astype(dt)
+    tag = "64" if dt == np.float64 else "32"
+    out = O.ablation3_fwd(S, R, heads, W, rowptr, col, training=True)
+    np.testing.assert_allclose(out, z[f"out{tag}"], rtol=tol, atol=tol)
+    heads = _heads_eval(z, heads, tag, dt)
+    out_eval = O.ablation3_fwd(S, R, heads, W, rowptr, col, training=False)
+    np.testing.assert_allclose(out_eval, z[f"out_eval{tag}"], rtol=tol, atol=tol)
+
+
+def test_gat_forward():
+    z = golden("gat_sub512.npz")
+    s = golden("sub512.npz")
+    rowptr, col = O.dense_to_csr(s["adj_norm"])
+    out = O.gat_fwd(z["init.features"], [z["init.attention_0.W"], z["init.attention_1.W"]],
+                    z["init.out_att.W"], rowptr, col)
+    np.testing.assert_allclose(out, z["out"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("tag", ["32", "64"])
+def test_edge_cases_layer(tag):
+    e = golden("edge_cases.npz")
+    dt = np.float64 if tag == "64" else np.float32
+    tol = 1e-9 if tag == "64" else 2e-4
+    adj = e[f"adj_norm{tag}"]
+    rowptr, col = O.dense_to_csr(adj)
+    deg = np.diff(rowptr)
+    assert deg[0] == 0 and deg[1] == 1 and deg[2] == 80 and deg[3] == 65
+    p = {k: e[f"ol3.init.{k}"].astype(dt) for k in ("W1", "W2", "a")}
+    for bn in ("bn1", "bn2"):
+        for k in ("weight", "bias", "running_mean", "running_var"):
+            p[f"{bn}_{k}"] = e[f"ol3.init.{bn}.{k}"].astype(dt)
+    S, R = e[f"ol3.S{tag}"], e[f"ol3.R{tag}"]
+    r = O.ours_layer3_fwd(S, R, p, rowptr, col, training=True)
+    att = np.zeros(adj.shape, dt)
+    att[O.edge_rows(rowptr), col] = r["att"]
+    att[deg == 0] = 1.0 / adj.shape[1]
+    np.testing.assert_allclose(att, e[f"ol3.att{tag}"], rtol=1e-6, atol=1e-7)
+    ref = e[f"ol3.out{tag}"]
+    np.testing.assert_allclose(r["out"], ref, rtol=tol, atol=tol * np.abs(ref).max())
+    r = O.ours_layer3_fwd(S, R, p, rowptr, col, training=False)
+    ref = e[f"ol3.out_eval{tag}"]
+    np.testing.assert_allclose(r["out"], ref, rtol=tol, atol=tol * np.abs(ref).max())
+    # GAL over the same 80-column adjacency (degree 0 / 1 / 80 / 65 rows)
+    x = e[f"gal.x{tag}"]
+    W = e["gal.init.W"].astype(dt)
+    out, h, attd = O.gal_fwd(x, W, rowptr, col)
+    np.testing.assert_allclose(out, e[f"gal.out{tag}"], rtol=tol, atol=tol)
+    g = O.gal_bwd(x, W, h, attd, e[f"gal.dout{tag}"].astype(dt))
+    np.testing.assert_allclose(g["dx"], e[f"gal.grad{tag}.x"], rtol=tol, atol=tol)
+    np.testing.assert_allclose(g["dW"], e[f"gal.grad{tag}.W"], rtol=tol, atol=tol)
+    assert np.abs(e[f"gal.grad{tag}.a"]).max() < 1e-5  # reference grad of GAL.a is ~0
+
+
+def test_link_predictor():
+    z = golden("link.npz")
+    xi, xj = z["x_i"], z["x_j"]
+    for mode in ("mlp", "inner"):
+        lins = [(z[f"{mode}.init.lins.0.weight"], z[f"{mode}.init.lins.0.bias"]),
+                (z[f"{mode}.init.lins.1.weight"], z[f"{mode}.init.lins.1.bias"])]
+        y = O.link_predict(xi, xj, mode, lins)
+        np.testing.assert_allclose(y, z[f"{mode}.out"], rtol=1e-6, atol=1e-6)
+        g = O.link_predict_bwd(xi, xj, mode, lins, z[f"{mode}.dout"])
+        np.testing.assert_allclose(g["dx_i"], z[f"{mode}.grad.x_i"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g["dx_j"], z[f"{mode}.grad.x_j"], rtol=1e-5, atol=1e-6)
+        if mode == "mlp":
+            np.testing.assert_allclose(g["dW"], z["mlp.grad.lins.0.weight"], rtol=1e-5,
+                                       atol=1e-6)
+            np.testing.assert_allclose(g["db"], z["mlp.grad.lins.0.bias"], rtol=1e-5,
+                                       atol=1e-6)
+
+
+def _dense_core_torch(rowptr, col, el, er, hc, hs, n_cols):
+    """Dense torch restatement of the masked-softmax core for autograd (fp64)."""
+    n = len(rowptr) - 1
+    mask = torch.zeros(n, n_cols, dtype=torch.bool)
+    mask[torch.as_tensor(O.edge_rows(rowptr)), torch.as_tensor(col, dtype=torch.long)] = True
+    e = torch.nn.functional.leaky_relu(el[:, None, :] + er[None, :, :], 0.2)  # (N,M,H)
+    e = torch.where(mask[:, :, None], e, torch.full_like(e, -9e15))
+    att = torch.softmax(e, dim=1)
+    u = torch.einsum("nmh,mhf->nhf", att, hc)
+    v = torch.einsum("nmh,nhf->mhf", att, hs)
+    return u, v
+
+
+def test_edge_aggregate_bwd_matches_autograd():
+    rng = np.random.default_rng(0)
+    e = golden("edge_cases.npz")
+    rowptr, col = O.dense_to_csr(e["counts"])
+    n, m, H, F = 40, 80, 2, 3
+    el, er = rng.standard_normal((n, H)), rng.standard_normal((m, H))
+    hc, hs = rng.standard_normal((m, H, F)), rng.standard_normal((n, H, F))
+    dU, dV = rng.standard_normal((n, H, F)), rng.standard_normal((m, H, F))
+    fw = O.edge_aggregate_fwd(rowptr, col, el, er, hc, hs=hs)
+    bw = O.edge_aggregate_bwd(rowptr, col, fw, hc, dU, hs=hs, dV=dV)
+    t = [torch.tensor(x, requires_grad=True) for x in (el, er, hc, hs)]
+    u, v = _dense_core_torch(rowptr, col, *t, m)
+    np.testing.assert_allclose(fw["u"], u.detach().numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(fw["v"], v.detach().numpy(), rtol=1e-12, atol=1e-12)
+    ((u * torch.tensor(dU)).sum() + (v * torch.tensor(dV)).sum()).backward()
+    for name, ref in zip(("d_el", "d_er", "d_hc", "d_hs"), t):
+        np.testing.assert_allclose(bw[name], ref.grad.numpy(), rtol=1e-10, atol=1e-10)
