@@ -98,11 +98,83 @@ class Layer:
     def step(self):
         for p in (self.W, self.al, self.ar):
             p.grad = None
-        h = torch.mm(self.X, self.W).view(self.n, self.H, self.F)
-        el = torch.einsum("nhf,hf->nh", h, self.al)
-        er = torch.einsum("nhf,hf->nh", h, self.ar)
-        u = self.MF.edge_attention(self.graph, el, er, h)
+        # h = X @ W with the per-head score halves fused into the MFMA epilogue
+        h, el, er = self.MF.project_scores(self.X, self.W, self.al, self.ar, heads=self.H)
+        u = self.MF.edge_attention(self.graph, el, er, h.view(self.n, self.H, self.F))
         u.backward(self.dU)
+
+
+def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup=3,
+                     hidden=128, n_pairs=4_000_000):
+    """score P = 4M pairs (2M graph edges + 2M uniform negatives,
+    seed 1) against h (n x F) with LinkPredictor 'mlp' (hidden 128) and 'inner'.
+    Rank r owns rows [r n/W, (r+1) n/W) of h; one RCCL all_gather_into_tensor per
+    batch rebuilds the full table (timed, included), then each rank scores its
+    contiguous P/W slice of the batch.  Returns pairs/s over all ranks."""
+    from msha_gnn_amd import functional as MF
+
+    g = torch.Generator().manual_seed(1)
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    pick = np.random.default_rng(1).choice(len(col), n_pairs // 2, replace=False)
+    src = np.concatenate([rows[pick], torch.randint(0, n, (n_pairs // 2,), generator=g).numpy()])
+    dst = np.concatenate([col[pick], torch.randint(0, n, (n_pairs // 2,), generator=g).numpy()])
+    per = n_pairs // world
+    lo = rank * per
+    t_src = torch.as_tensor(src[lo:lo + per], device=dev)
+    t_dst = torch.as_tensor(dst[lo:lo + per], device=dev)
+    rows_per = (n + world - 1) // world
+    h_local = torch.rand(rows_per, F, generator=torch.Generator().manual_seed(10 + rank)).to(dev)
+    h_full = torch.empty(rows_per * world, F, device=dev)
+    W = (torch.randn(hidden, F, generator=g) * F ** -0.5).to(dev)
+    b = torch.randn(hidden, generator=g).to(dev)
+    out_mlp = torch.empty(per, hidden, device=dev)
+    out_inner = torch.empty(per, device=dev)
+    if dist:
+        import torch.distributed as tdist
+
+    def gather():
+        if dist:
+            tdist.all_gather_into_tensor(h_full, h_local)
+        else:
+            h_full.copy_(h_local)
+
+    res = {}
+    for mode in ("mlp", "inner"):
+        def one():
+            gather()
+            if mode == "mlp":
+                MF.score_pairs(h_full, t_src, t_dst, "mlp", W, b, out=out_mlp)
+            else:
+                MF.score_pairs(h_full, t_src, t_dst, "inner", out=out_inner)
+        for _ in range(warmup):
+            one()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        if dist:
+            tt = torch.tensor([dt], device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            dt = float(tt.item())
+        res[f"pairs_per_sec_{mode}"] = per * world * steps / dt
+        res[f"ms_per_batch_{mode}"] = dt / steps * 1e3
+    # all-gather alone
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gather()
+    torch.cuda.synchronize(dev)
+    res["allgather_ms"] = (time.perf_counter() - t0) / steps * 1e3
+    res.update(pairs_per_batch=per * world, feat=F, hidden=hidden, world=world, dtype="f32",
+               sharding="h rows all-gathered over RCCL, pairs split contiguously per rank"
+               if dist else "single GPU (no collective)")
+    return res
 
 
 def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
@@ -154,6 +226,7 @@ def main():
     ap.add_argument("--workload", default="syn100k", choices=sorted(WORKLOADS) + ["r15"])
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-link-score", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,6 +272,9 @@ def main():
         t = torch.tensor([dt], device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         dt = float(t.item())
+    link = None
+    if not args.no_link_score and args.workload != "r15":
+        link = link_score_bench(dev, rowptr, col, n, H * F, world, rank, dist)
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -220,6 +296,8 @@ def main():
                      "algorithmic_bytes_per_launch": fb, "avg_launch_us": k_ms * 1e3,
                      "launches_timed": len(events)},
     }
+    if link is not None:
+        out["link_score"] = link
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
     print(json.dumps(out), flush=True)

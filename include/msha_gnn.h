@@ -166,6 +166,65 @@ MSHA_API int msha_gal_fwd(const msha_graph* g, const float* h, float drop_p, uin
 MSHA_API int msha_gal_bwd(const msha_graph* g, const float* h, const float* dout, float drop_p,
                  uint64_t seed, uint64_t offset, float* dh, msha_stream_t stream);
 
+/* ------------------------------------------------ projections (MFMA, fp32) --- */
+/* Ablation.py:262-263 (h1 = R @ W1, h2 = S @ W2), GAT.py:21 (h = input @ W) and the
+ * gradients of those products.  C = A @ B with arbitrary element strides
+ * (A[m,k] = A[m*sAm + k*sAk], B[k,n] = B[k*sBk + n*sBn]), C row-major with ldc.
+ * v_mfma_f32_16x16x4_f32: exact fp32 FMA chains.  splits > 1 splits K over
+ * workgroups (for long reductions such as dW = X^T dH over all rows); partial
+ * slabs are added in split order (deterministic) and beta (0 or 1) selects
+ * C = sum or C += sum.  Workspace: msha_gemm_workspace_size(M, N, splits). */
+MSHA_API size_t msha_gemm_workspace_size(int64_t M, int64_t N, int32_t splits);
+MSHA_API int msha_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm,
+                           int64_t sAk, const float* B, int64_t sBk, int64_t sBn, float* C,
+                           int64_t ldc, float beta, int32_t splits, void* ws, size_t ws_bytes,
+                           msha_stream_t stream);
+
+/* Projection with the attention-score halves fused into its epilogue:
+ *   h = X @ W  (M x heads*feat),  el[m,h] = h[m,h,:] . al[h,:],  er[m,h] = h[m,h,:] . ar[h,:]
+ * Replaces Ablation.py:262-267's projection + the (N, M, 2F) score tensor: the
+ * score of edge (i, j) is lrelu(el_i + er_j).  al/el and ar/er are optional pairs;
+ * feat must be 4, 8, 16, 32, 64 or 128 when a score vector is given. */
+MSHA_API int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t feat,
+                                 const float* X, const float* W, const float* al,
+                                 const float* ar, float* h, float* el, float* er,
+                                 msha_stream_t stream);
+
+/* out = dh + de (x) a [+ de2 (x) a2]  (rows x heads*feat; de (rows, heads), a (heads, feat)):
+ * the gradient reaching h through el = h . a (the backward of msha_project_scores). */
+MSHA_API int msha_add_head_outer(int64_t rows, int32_t heads, int32_t feat, const float* dh,
+                                 const float* de, const float* a, const float* de2,
+                                 const float* a2, float* out, msha_stream_t stream);
+
+/* ----------------------------------------------------------- link scoring --- */
+/* LLP.py:104-115 LinkPredictor with the caller's gather (LLP.py:233) fused:
+ * x_i = G[gi[b]], x_j = G2[gj[b]] (gi / gj NULL: row b).
+ * 'mlp' layer: out = act((x_i * x_j) @ W^T + bias), W an nn.Linear weight (N x K);
+ * with G2 == NULL and gj == NULL the input is x_i alone (deeper predictor layers);
+ * act bits: 1 bias, 2 relu, 4 dropout(drop_p, seed, offset), 8 sigmoid. */
+MSHA_API int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const float* G, int64_t ldg,
+                              const int64_t* gi, const float* G2, int64_t ldg2,
+                              const int64_t* gj, const float* W, const float* bias, int32_t act,
+                              float drop_p, uint64_t seed, uint64_t offset, float* out,
+                              msha_stream_t stream);
+/* 'inner': out[b] = sigmoid(sum_f x_i[b,f] x_j[b,f]); feat a power of two in [4, 256]. */
+MSHA_API int msha_pair_inner_fwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
+                                 const int64_t* gi, const float* G2, int64_t ldg2,
+                                 const int64_t* gj, float* out, msha_stream_t stream);
+/* backward of 'inner' given its output s: dx_i = dout*s*(1-s)*x_j, dx_j = ...*x_i */
+MSHA_API int msha_pair_inner_bwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
+                                 const int64_t* gi, const float* G2, int64_t ldg2,
+                                 const int64_t* gj, const float* s, const float* dout,
+                                 float* dxi, float* dxj, msha_stream_t stream);
+/* backward through y = [sigmoid](dropout(relu(z))) given its output y: dz */
+MSHA_API int msha_pair_mlp_dz(int64_t n, const float* s, const float* dout, float drop_p,
+                              int32_t sigmoid, float* dz, msha_stream_t stream);
+/* x = x_i * x_j (dx == NULL), or dx_i = dx * x_j, dx_j = dx * x_i */
+MSHA_API int msha_pair_hadamard(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
+                                const int64_t* gi, const float* G2, int64_t ldg2,
+                                const int64_t* gj, const float* dx, float* x_or_dxi, float* dxj,
+                                msha_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,17 @@ SIGNATURES = {
     "msha_csc_aggregate": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),
     "msha_gal_bwd": (C.c_int, [GP, P, P, F32, U64, U64, P, P]),
+    "msha_gemm_workspace_size": (SZ, [I64, I64, I32]),
+    "msha_gemm_f32": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, F32, I32, P, SZ,
+                                P]),
+    "msha_project_scores": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
+    "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
+    "msha_pair_linear": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64, U64,
+                                   P, P]),
+    "msha_pair_inner_fwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
+    "msha_pair_inner_bwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P, P]),
+    "msha_pair_mlp_dz": (C.c_int, [I64, P, P, F32, I32, P, P]),
+    "msha_pair_hadamard": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P]),
 }
 
 _lib = None

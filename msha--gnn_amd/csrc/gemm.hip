@@ -1,0 +1,586 @@
+// Feature x W projections on the matrix cores (gfx950 v_mfma_f32_16x16x4_f32).
+//
+// Reference: every layer projects its features densely before attending --
+// Ablation.py:262-263 (h1 = R @ W1, h2 = S @ W2), GAT.py:21 (h = input @ W),
+// LLP.py:105-110 (Linear of x_i * x_j).  This is the only MFMA user of the library.
+//
+// C[m, n] = sum_k A[m, k] * B[k, n], fp32 in / fp32 accumulate: the f32 MFMA is a
+// k-ordered fp32 FMA chain (exact f32, no TF32 on gfx950), at the fp32 vector rate.
+//
+// Tile: 128 x 128 x 32, 256 threads = 4 waves; wave w owns rows [32w, 32w+32) x 128
+// columns as 2 x 8 accumulators of 16 x 16.  A is staged m-major ([m][k], rows of
+// 34 floats: the 16 rows x 2 k a ds_read_b32 half touches map to banks 2m + k, all
+// distinct) and B k-major ([k][n], rows of 144 floats: the two k-rows of a half fall
+// in disjoint bank halves), so operand reads and staging writes are conflict free.
+//
+// A-operand loaders:   strided (any (sAm, sAk): row-major, transposed views)
+//                      gather-hadamard A[m, k] = G[gi[m], k] * G[gj[m], k]  (pair scorer)
+// Epilogues:           store / split-K slab, bias+relu+dropout+sigmoid (Linear of the
+//                      link predictor), and attention-score heads
+//                      el[m, h] = sum_f C[m, h*F+f] * al[h, f]  (+ er with ar)
+#include <cstring>
+
+#include "common.h"
+
+namespace msha {
+
+constexpr int BM = 128, BN = 128, BK = 32, LDA = BK + 2, LDP = 144;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum : int { A_STRIDED = 0, A_GATHER_HADAMARD = 1 };
+enum : int { EPI_STORE = 0, EPI_ACT = 1, EPI_SCORE = 2 };
+enum : int { ACT_BIAS = 1, ACT_RELU = 2, ACT_DROPOUT = 4, ACT_SIGMOID = 8 };
+
+struct GemmArgs {
+  int64_t M, N, K;
+  const float* A;
+  int64_t sAm, sAk;
+  const int64_t* gi;  // gather-hadamard rows (A_GATHER_HADAMARD)
+  const int64_t* gj;  // nullable: plain gather of gi
+  const float* G;
+  const float* G2;  // table of the second gather (nullable: G)
+  int64_t ldg, ldg2;
+  const float* B;
+  int64_t sBk, sBn;
+  float* C;
+  int64_t ldc;
+  int64_t k_chunk;  // split-K: K range of blockIdx.z
+  float* slab;      // split-K partial output (M x N per split), nullable
+  // EPI_ACT
+  int act;
+  const float* bias;
+  Dropout dp;
+  // EPI_SCORE
+  const float* al;
+  const float* ar;
+  float* el;
+  float* er;
+  int H;
+};
+
+template <int AMODE>
+__device__ __forceinline__ float load_a(const GemmArgs& p, int64_t m, int64_t k) {
+  if (m >= p.M || k >= p.K) return 0.f;
+  if (AMODE == A_STRIDED) return p.A[m * p.sAm + k * p.sAk];
+  const int64_t i = p.gi ? p.gi[m] : m;
+  const float x = p.G[i * p.ldg + k];
+  if (p.G2 == nullptr && p.gj == nullptr) return x;  // single input (deeper layers)
+  const int64_t j = p.gj ? p.gj[m] : m;
+  return x * (p.G2 ? p.G2 : p.G)[j * p.ldg2 + k];
+}
+
+// Vectorised staging (16-byte loads, prefetched into registers one K-stage ahead)
+// for the layouts the library uses: A with k contiguous (row-major X, gathered
+// rows) or m contiguous (X^T of a weight gradient); B with n contiguous (W) or
+// k contiguous (W^T, nn.Linear weights).  Anything else takes the scalar path.
+enum : int { LD_SCALAR = 0, LD_VEC = 1 };
+
+struct Stage {
+  float4 a[4];
+  float4 b[4];
+  uint32_t okmask;  // bit it: a[it] in range, bit 4+it: b[it] in range
+};
+
+// Branch-free 16-byte loads: an out-of-range element reads a clamped in-range
+// address and is zeroed by a select, so the compiler can issue a stage's loads
+// back to back and wait for them once (at the LDS store of the next stage).
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// The zeroing select of out-of-range elements is applied in stage_store (after the
+// barrier): placed next to the loads, it forces the wait for them before the MFMAs.
+template <int AMODE>
+__device__ __forceinline__ float4 load_a4_kfast(const GemmArgs& p, int64_t m, int64_t k,
+                                                bool& ok) {
+  // 4 consecutive k of row m (K % 4 == 0)
+  ok = m < p.M && k < p.K;
+  const int64_t mc = ok ? m : 0, kc = ok ? k : 0;
+  if (AMODE == A_STRIDED) return *reinterpret_cast<const float4*>(p.A + mc * p.sAm + kc);
+  const int64_t i = p.gi ? p.gi[mc] : mc;
+  const float4 x = *reinterpret_cast<const float4*>(p.G + i * p.ldg + kc);
+  if (p.G2 == nullptr && p.gj == nullptr) return x;
+  const int64_t j = p.gj ? p.gj[mc] : mc;
+  const float4 y = *reinterpret_cast<const float4*>((p.G2 ? p.G2 : p.G) + j * p.ldg2 + kc);
+  return make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
+}
+
+// AK: A's k is contiguous (else m is); BNF: B's n is contiguous (else k is)
+template <int AMODE, int AK, int BNF>
+__device__ __forceinline__ void stage_load(const GemmArgs& p, Stage& st, int64_t m0, int64_t n0,
+                                           int64_t k0, int64_t ke, int tid) {
+  uint32_t okm = 0u;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = tid + 256 * it;
+    bool oka, okb;
+    if (AK) {  // 128 rows x 8 float4 along k
+      const int mm = idx >> 3, kq = idx & 7;
+      const int64_t k = k0 + 4 * kq;
+      st.a[it] = load_a4_kfast<AMODE>(p, m0 + mm, k < ke ? k : p.K, oka);
+    } else {  // 32 k x 32 float4 along m (A[m, k] = A[k * sAk + m])
+      const int kk = idx >> 5, mq = idx & 31;
+      const int64_t k = k0 + kk, m = m0 + 4 * mq;
+      oka = k < ke && m < p.M;
+      st.a[it] = *reinterpret_cast<const float4*>(p.A + (oka ? k * p.sAk + m : 0));
+    }
+    if (BNF) {  // 32 k x 32 float4 along n
+      const int kk = idx >> 5, nq = idx & 31;
+      const int64_t k = k0 + kk, n = n0 + 4 * nq;
+      okb = k < ke && n < p.N;
+      st.b[it] = *reinterpret_cast<const float4*>(p.B + (okb ? k * p.sBk + n : 0));
+    } else {  // 128 n x 8 float4 along k (B[k, n] = B[n * sBn + k])
+      const int nn = idx >> 3, kq = idx & 7;
+      const int64_t k = k0 + 4 * kq, n = n0 + nn;
+      okb = k < ke && n < p.N;
+      st.b[it] = *reinterpret_cast<const float4*>(p.B + (okb ? n * p.sBn + k : 0));
+    }
+    okm |= (oka ? 1u : 0u) << it;
+    okm |= (okb ? 1u : 0u) << (4 + it);
+  }
+  st.okmask = okm;
+}
+
+template <int AK, int BNF>
+__device__ __forceinline__ void stage_store(const Stage& st0, float* As, float* Bs, int tid) {
+  Stage st;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    st.a[it] = sel4((st0.okmask >> it) & 1u, st0.a[it]);
+    st.b[it] = sel4((st0.okmask >> (4 + it)) & 1u, st0.b[it]);
+  }
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = tid + 256 * it;
+    if (AK) {
+      const int mm = idx >> 3, kq = idx & 7;
+      float* d = As + mm * LDA + 4 * kq;  // 8-byte aligned (LDA even)
+      *reinterpret_cast<float2*>(d) = make_float2(st.a[it].x, st.a[it].y);
+      *reinterpret_cast<float2*>(d + 2) = make_float2(st.a[it].z, st.a[it].w);
+    } else {
+      const int kk = idx >> 5, mq = idx & 31;
+      As[(4 * mq + 0) * LDA + kk] = st.a[it].x;
+      As[(4 * mq + 1) * LDA + kk] = st.a[it].y;
+      As[(4 * mq + 2) * LDA + kk] = st.a[it].z;
+      As[(4 * mq + 3) * LDA + kk] = st.a[it].w;
+    }
+    if (BNF) {
+      const int kk = idx >> 5, nq = idx & 31;
+      *reinterpret_cast<float4*>(Bs + kk * LDP + 4 * nq) = st.b[it];
+    } else {
+      const int nn = idx >> 3, kq = idx & 7;
+      Bs[(4 * kq + 0) * LDP + nn] = st.b[it].x;
+      Bs[(4 * kq + 1) * LDP + nn] = st.b[it].y;
+      Bs[(4 * kq + 2) * LDP + nn] = st.b[it].z;
+      Bs[(4 * kq + 3) * LDP + nn] = st.b[it].w;
+    }
+  }
+}
+
+template <int AMODE>
+__device__ __forceinline__ void stage_scalar(const GemmArgs& p, float* As, float* Bs, int64_t m0,
+                                             int64_t n0, int64_t k0, int64_t ke, bool a_kfast,
+                                             bool b_nfast, int tid) {
+#pragma unroll 4
+  for (int it = 0; it < (BM * BK) / 256; ++it) {
+    const int idx = tid + 256 * it;
+    int mm, kk;
+    if (a_kfast) { kk = idx % BK; mm = idx / BK; } else { mm = idx % BM; kk = idx / BM; }
+    const int64_t k = k0 + kk;
+    As[mm * LDA + kk] = k < ke ? load_a<AMODE>(p, m0 + mm, k) : 0.f;
+  }
+#pragma unroll 4
+  for (int it = 0; it < (BK * BN) / 256; ++it) {
+    const int idx = tid + 256 * it;
+    int nn, kk;
+    if (b_nfast) { nn = idx % BN; kk = idx / BN; } else { kk = idx % BK; nn = idx / BK; }
+    const int64_t k = k0 + kk, n = n0 + nn;
+    Bs[kk * LDP + nn] = (k < ke && n < p.N) ? p.B[k * p.sBk + n * p.sBn] : 0.f;
+  }
+}
+
+constexpr int TP = BN + 4;  // epilogue staging row pitch (floats)
+
+// VEC = LD_VEC: 16-byte staging with compile-time layouts (AK, BNF); LD_SCALAR:
+// element-wise staging for any strides (layouts decided at run time).
+template <int AMODE, int EPI, int FEPI, int VEC, int AK, int BNF>
+__global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
+  // one LDS object (operand tiles; reused as the epilogue's C staging)
+  __shared__ __attribute__((aligned(16))) float smem[BM * LDA + BK * LDP];
+  float* As = smem;
+  float* Bs = smem + BM * LDA;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  int64_t kb = 0, ke = p.K;
+  if (p.k_chunk > 0) {
+    kb = (int64_t)blockIdx.z * p.k_chunk;
+    ke = min(p.K, kb + p.k_chunk);
+  }
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool a_kfast = AMODE != A_STRIDED || p.sAk == 1 || p.sAm != 1;
+  const bool b_nfast = p.sBn == 1 || p.sBk != 1;
+  Stage st;
+  if (VEC == LD_VEC && kb < ke) stage_load<AMODE, AK, BNF>(p, st, m0, n0, kb, ke, tid);
+  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+    __syncthreads();
+    if (VEC == LD_VEC) {
+      stage_store<AK, BNF>(st, As, Bs, tid);
+    } else {
+      stage_scalar<AMODE>(p, As, Bs, m0, n0, k0, ke, a_kfast, b_nfast, tid);
+    }
+    __syncthreads();
+    // prefetch the next stage into registers while the MFMAs run
+    if (VEC == LD_VEC && k0 + BK < ke) stage_load<AMODE, AK, BNF>(p, st, m0, n0, k0 + BK, ke, tid);
+    // ---- 8 k-steps of 4: 2 A reads + 8 B reads feed 16 MFMAs
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      const float a0 = As[(w * 32 + (lane & 15)) * LDA + kr];
+      const float a1 = As[(w * 32 + 16 + (lane & 15)) * LDA + kr];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float b = Bs[kr * LDP + c * 16 + (lane & 15)];
+        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][c], 0, 0, 0);
+        acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][c], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue.  MFMA C/D layout: col = lane & 15, row = (lane >> 4) * 4 + reg.
+  // Each wave stages its 16-row halves through LDS, then every lane finishes a
+  // 32-column segment of one row: activation, per-head score dots, 16-B stores.
+  static_assert(4 * 16 * TP <= BM * LDA + BK * LDP, "epilogue staging exceeds LDS");
+  __syncthreads();  // all waves are done reading the operand tiles
+  float* T = smem + w * (16 * TP);
+  float* out = p.C;
+  int64_t ldo = p.ldc;
+  if (p.slab != nullptr) {
+    out = p.slab + (int64_t)blockIdx.z * p.M * p.N;
+    ldo = p.N;
+  }
+  const int rl = lane >> 2;   // row within the 16-row half
+  const int seg = lane & 3;   // 32-column segment
+  const int64_t cbase = n0 + seg * 32;
+  // per-lane constants of its segment
+  float4 bia[8], alv[8], arv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int64_t col = cbase + 4 * q;
+    const bool ok = col < p.N;
+    bia[q] = alv[q] = arv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (EPI == EPI_ACT && (p.act & ACT_BIAS) && ok) bia[q] = *reinterpret_cast<const float4*>(p.bias + col);
+    if (EPI == EPI_SCORE && p.al && ok) alv[q] = *reinterpret_cast<const float4*>(p.al + col);
+    if (EPI == EPI_SCORE && p.ar && ok) arv[q] = *reinterpret_cast<const float4*>(p.ar + col);
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) T[((lane >> 4) * 4 + i) * TP + c * 16 + (lane & 15)] = acc[r][c][i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+    __builtin_amdgcn_wave_barrier();
+    const int64_t row = m0 + w * 32 + r * 16 + rl;
+    float4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(T + rl * TP + seg * 32 + 4 * q);
+    if (EPI == EPI_ACT) {
+      // keep bits of this lane's 32 outputs, drawn in a rolled loop (an inlined
+      // Philox per unrolled element spills to scratch)
+      uint32_t kb = 0xffffffffu;
+      if (p.act & ACT_DROPOUT) {
+        kb = 0u;
+#pragma unroll 1
+        for (int u = 0; u < 32; ++u)
+          if (philox_x(p.dp.seed, p.dp.offset, (uint64_t)(row * p.N + cbase + u)) >= p.dp.threshold)
+            kb |= 1u << u;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+        const float bb[4] = {bia[q].x, bia[q].y, bia[q].z, bia[q].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float x = e[u] + bb[u];
+          if (p.act & ACT_RELU) x = fmaxf(x, 0.f);
+          if (p.act & ACT_DROPOUT) x *= ((kb >> (4 * q + u)) & 1u) ? p.dp.scale : 0.f;
+          if (p.act & ACT_SIGMOID) x = 1.f / (1.f + __expf(-x));
+          e[u] = x;
+        }
+        v[q] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+    if (row < p.M) {
+      const bool vec = ((ldo & 3) == 0) && ((((uintptr_t)out) & 15) == 0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t col = cbase + 4 * q;
+        if (vec && col + 3 < p.N) {
+          *reinterpret_cast<float4*>(out + row * ldo + col) = v[q];
+        } else {
+          const float e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (col + u < p.N) out[row * ldo + col + u] = e[u];
+        }
+      }
+    }
+    if (EPI == EPI_SCORE) {
+      // FEPI <= 32: 32 / FEPI whole heads inside the segment; FEPI > 32: the head
+      // spans FEPI / 32 segments (lanes seg, seg^1, ...) -> reduce across them.
+      constexpr int FE = FEPI > 0 ? FEPI : 16;
+      constexpr int HS = FE <= 32 ? 32 / FE : 1;
+      constexpr int QPH = FE <= 32 ? FE / 4 : 8;  // float4 per head inside the segment
+      float sl[HS], sr[HS];
+#pragma unroll
+      for (int hh = 0; hh < HS; ++hh) {
+        sl[hh] = sr[hh] = 0.f;
+#pragma unroll
+        for (int q = hh * QPH; q < (hh + 1) * QPH; ++q) {
+          sl[hh] += f4_dot(v[q], alv[q]);
+          sr[hh] += f4_dot(v[q], arv[q]);
+        }
+      }
+      if (FE > 32) {
+#pragma unroll
+        for (int o = 1; o < FE / 32; o <<= 1) {
+          sl[0] += __shfl_xor(sl[0], o);
+          sr[0] += __shfl_xor(sr[0], o);
+        }
+      }
+#pragma unroll
+      for (int hh = 0; hh < HS; ++hh) {
+        const int64_t hg = FE <= 32 ? (cbase / FE) + hh : cbase / FE;
+        const bool writer = FE <= 32 ? true : (seg % (FE / 32)) == 0;
+        if (writer && row < p.M && hg < p.H && cbase < p.N) {
+          if (p.el) p.el[row * p.H + hg] = sl[hh];
+          if (p.er) p.er[row * p.H + hg] = sr[hh];
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // reads done before the next half overwrites T
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// split-K: C = sum_z slab[z] (in z order: deterministic)
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab,
+                                                          int splits, int64_t M, int64_t N,
+                                                          float* __restrict__ C, int64_t ldc,
+                                                          float beta) {
+  const int64_t total = M * N;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {  // 4 independent chains keep 4 loads in flight
+      s0 += slab[(int64_t)(z + 0) * total + t];
+      s1 += slab[(int64_t)(z + 1) * total + t];
+      s2 += slab[(int64_t)(z + 2) * total + t];
+      s3 += slab[(int64_t)(z + 3) * total + t];
+    }
+    for (; z < splits; ++z) s0 += slab[(int64_t)z * total + t];
+    const float s = (s0 + s1) + (s2 + s3);
+    const int64_t r = t / N, c = t % N;
+    C[r * ldc + c] = beta != 0.f ? beta * C[r * ldc + c] + s : s;
+  }
+}
+
+// out = dh + de (x) a : dh (rows, H*F), de (rows, H), a (H, F)
+__global__ void __launch_bounds__(256) add_head_outer_kernel(const float* __restrict__ dh,
+                                                             const float* __restrict__ de,
+                                                             const float* __restrict__ a,
+                                                             const float* __restrict__ de2,
+                                                             const float* __restrict__ a2,
+                                                             int64_t rows, int H, int F,
+                                                             float* __restrict__ out) {
+  const int64_t D = (int64_t)H * F;
+  const int64_t total = rows * D;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / D;
+    const int c = (int)(t % D);
+    const int h = c / F;
+    float v = dh[t] + de[r * H + h] * a[c];
+    if (de2) v += de2[r * H + h] * a2[c];
+    out[t] = v;
+  }
+}
+
+static bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+// 16-byte staging applies when the contiguous dimension of each operand has unit
+// stride, its other stride and extent are multiples of 4, and bases are aligned.
+template <int AMODE>
+static bool vec_ok(const GemmArgs& p) {
+  if (p.K % 4 != 0) return false;
+  bool a_ok;
+  if (AMODE == A_GATHER_HADAMARD) {
+    a_ok = aligned16(p.G) && p.ldg % 4 == 0 && (p.G2 == nullptr || (aligned16(p.G2) && p.ldg2 % 4 == 0));
+  } else if (p.sAk == 1) {
+    a_ok = aligned16(p.A) && p.sAm % 4 == 0;
+  } else if (p.sAm == 1) {
+    a_ok = aligned16(p.A) && p.sAk % 4 == 0 && p.M % 4 == 0;
+  } else {
+    a_ok = false;
+  }
+  bool b_ok;
+  if (p.sBn == 1) b_ok = aligned16(p.B) && p.sBk % 4 == 0 && p.N % 4 == 0;
+  else if (p.sBk == 1) b_ok = aligned16(p.B) && p.sBn % 4 == 0;
+  else b_ok = false;
+  return a_ok && b_ok;
+}
+
+template <int AMODE, int EPI, int FEPI>
+static void launch(const GemmArgs& p, int splits, hipStream_t s) {
+  dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)splits);
+  if (!vec_ok<AMODE>(p)) {
+    hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_SCALAR, 1, 1>), grid, dim3(256), 0, s,
+                       p);
+    return;
+  }
+  const bool ak = AMODE != A_STRIDED || p.sAk == 1;
+  const bool bn = p.sBn == 1;
+  if (AMODE != A_STRIDED || EPI != EPI_STORE) {  // projections / pair scorer: fixed layouts
+    if (bn)
+      hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_VEC, 1, 1>), grid, dim3(256), 0, s,
+                         p);
+    else
+      hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_VEC, 1, 0>), grid, dim3(256), 0, s,
+                         p);
+    return;
+  }
+  if (ak && bn)
+    hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_VEC, 1, 1>), grid, dim3(256), 0, s, p);
+  else if (ak)
+    hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_VEC, 1, 0>), grid, dim3(256), 0, s, p);
+  else if (bn)
+    hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_VEC, 0, 1>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<AMODE, EPI, FEPI, LD_VEC, 0, 0>), grid, dim3(256), 0, s, p);
+}
+
+static GemmArgs base_args(int64_t M, int64_t N, int64_t K) {
+  GemmArgs p;
+  memset(&p, 0, sizeof(p));
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.dp = make_dropout(0.f, 0, 0);
+  return p;
+}
+
+}  // namespace msha
+
+using namespace msha;
+
+extern "C" size_t msha_gemm_workspace_size(int64_t M, int64_t N, int32_t splits) {
+  if (splits <= 1) return 0;
+  return (size_t)splits * (size_t)M * (size_t)N * sizeof(float);
+}
+
+extern "C" int msha_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm,
+                             int64_t sAk, const float* B, int64_t sBk, int64_t sBn, float* C,
+                             int64_t ldc, float beta, int32_t splits, void* ws, size_t ws_bytes,
+                             msha_stream_t stream) {
+  MSHA_ARG_CHECK(M > 0 && N > 0 && K > 0, "gemm_f32: bad sizes");
+  MSHA_ARG_CHECK(A && B && C, "gemm_f32: null pointer");
+  MSHA_ARG_CHECK(splits >= 1 && splits <= 65535, "gemm_f32: splits out of range");
+  MSHA_ARG_CHECK(splits == 1 || beta == 0.f || beta == 1.f, "gemm_f32: beta must be 0 or 1");
+  MSHA_ARG_CHECK(splits > 1 || beta == 0.f, "gemm_f32: beta needs splits > 1");
+  GemmArgs p = base_args(M, N, K);
+  p.A = A; p.sAm = sAm; p.sAk = sAk;
+  p.B = B; p.sBk = sBk; p.sBn = sBn;
+  p.C = C; p.ldc = ldc;
+  hipStream_t s = (hipStream_t)stream;
+  if (splits > 1) {
+    MSHA_ARG_CHECK(ws && ws_bytes >= msha_gemm_workspace_size(M, N, splits),
+                   "gemm_f32: split-K workspace too small");
+    int64_t kc = (K + splits - 1) / splits;
+    kc = ((kc + BK - 1) / BK) * BK;
+    const int used = (int)((K + kc - 1) / kc);
+    p.k_chunk = kc;
+    p.slab = (float*)ws;
+    launch<A_STRIDED, EPI_STORE, 0>(p, used, s);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(M * N, 256, 8192)), dim3(256), 0, s,
+                       (const float*)ws, used, M, N, C, ldc, beta);
+  } else {
+    launch<A_STRIDED, EPI_STORE, 0>(p, 1, s);
+  }
+  return check_launch("gemm_f32");
+}
+
+extern "C" int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t feat,
+                                   const float* X, const float* W, const float* al,
+                                   const float* ar, float* h, float* el, float* er,
+                                   msha_stream_t stream) {
+  MSHA_ARG_CHECK(M > 0 && K > 0 && heads > 0 && feat > 0, "project_scores: bad sizes");
+  MSHA_ARG_CHECK(X && W && h, "project_scores: null pointer");
+  MSHA_ARG_CHECK((al == nullptr) == (el == nullptr) && (ar == nullptr) == (er == nullptr),
+                 "project_scores: score vectors and outputs must be paired");
+  const int64_t N = (int64_t)heads * feat;
+  GemmArgs p = base_args(M, N, K);
+  p.A = X; p.sAm = K; p.sAk = 1;
+  p.B = W; p.sBk = N; p.sBn = 1;
+  p.C = h; p.ldc = N;
+  p.al = al; p.ar = ar; p.el = el; p.er = er; p.H = heads;
+  hipStream_t s = (hipStream_t)stream;
+  if (al == nullptr && ar == nullptr) {
+    launch<A_STRIDED, EPI_STORE, 0>(p, 1, s);
+  } else if (feat == 4) {
+    launch<A_STRIDED, EPI_SCORE, 4>(p, 1, s);
+  } else if (feat == 8) {
+    launch<A_STRIDED, EPI_SCORE, 8>(p, 1, s);
+  } else if (feat == 16) {
+    launch<A_STRIDED, EPI_SCORE, 16>(p, 1, s);
+  } else if (feat == 32) {
+    launch<A_STRIDED, EPI_SCORE, 32>(p, 1, s);
+  } else if (feat == 64) {
+    launch<A_STRIDED, EPI_SCORE, 64>(p, 1, s);
+  } else if (feat == 128) {
+    launch<A_STRIDED, EPI_SCORE, 128>(p, 1, s);
+  } else {
+    return fail(MSHA_ERR_UNSUPPORTED, "project_scores: feat must be 4, 8, 16, 32, 64 or 128 "
+                                      "when score vectors are given");
+  }
+  return check_launch("project_scores");
+}
+
+extern "C" int msha_add_head_outer(int64_t rows, int32_t heads, int32_t feat, const float* dh,
+                                   const float* de, const float* a, const float* de2,
+                                   const float* a2, float* out, msha_stream_t stream) {
+  MSHA_ARG_CHECK(rows > 0 && heads > 0 && feat > 0, "add_head_outer: bad sizes");
+  MSHA_ARG_CHECK(dh && de && a && out && ((de2 == nullptr) == (a2 == nullptr)),
+                 "add_head_outer: null pointer");
+  const int64_t total = rows * heads * feat;
+  hipLaunchKernelGGL(add_head_outer_kernel, dim3(grid_for(total, 256, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, dh, de, a, de2, a2, rows, heads, feat, out);
+  return check_launch("add_head_outer");
+}
+
+extern "C" int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const float* G,
+                                int64_t ldg, const int64_t* gi, const float* G2, int64_t ldg2,
+                                const int64_t* gj, const float* W, const float* bias,
+                                int32_t act, float drop_p, uint64_t seed, uint64_t offset,
+                                float* out, msha_stream_t stream) {
+  MSHA_ARG_CHECK(n_pairs > 0 && K > 0 && N > 0, "pair_linear: bad sizes");
+  MSHA_ARG_CHECK(G && W && out, "pair_linear: null pointer");
+  MSHA_ARG_CHECK(!(act & ACT_BIAS) || bias, "pair_linear: bias missing");
+  GemmArgs p = base_args(n_pairs, N, K);
+  p.G = G; p.ldg = ldg; p.gi = gi; p.gj = gj; p.G2 = G2; p.ldg2 = G2 ? ldg2 : ldg;
+  p.B = W; p.sBk = 1; p.sBn = K;  // nn.Linear weight (N x K): B[k, n] = W[n, k]
+  p.C = out; p.ldc = N;
+  p.act = act; p.bias = bias;
+  p.dp = make_dropout(drop_p, seed, offset);
+  if (!p.dp.active) p.act &= ~ACT_DROPOUT;
+  launch<A_GATHER_HADAMARD, EPI_ACT, 0>(p, 1, (hipStream_t)stream);
+  return check_launch("pair_linear");
+}

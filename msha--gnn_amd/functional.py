@@ -185,3 +185,219 @@ def dropout_keep_mask(n: int, p: float, seed: int, device, offset: int = 0) -> t
     _lib.call("msha_dropout_keep_mask", seed, offset, n, p, keep.data_ptr(),
               _lib.stream_handle(device))
     return keep
+
+
+# ------------------------------------------------------------------ projections ---
+def _splits_for(rows: int) -> int:
+    """split-K factor for reductions over `rows`: ~256 workgroups of >= 256 rows."""
+    return max(1, min(256, rows // 256))
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
+         accumulate: bool = False, splits: int | None = None) -> torch.Tensor:
+    """C = A @ B (or C += A @ B) on the MFMA GEMM; A and B may be strided views
+    (transposes included).  Long reductions use deterministic split-K."""
+    M, K = A.shape
+    K2, N = B.shape
+    assert K == K2
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    assert out.stride(1) == 1
+    if splits is None:
+        splits = _splits_for(K) if K >= 4096 else 1
+    if accumulate and splits == 1:
+        splits = 2
+    ws = None
+    if splits > 1:
+        wsb = _lib.load().msha_gemm_workspace_size(M, N, splits)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=A.device)
+    _lib.call("msha_gemm_f32", M, N, K, A.data_ptr(), A.stride(0), A.stride(1), B.data_ptr(),
+              B.stride(0), B.stride(1), out.data_ptr(), out.stride(0),
+              1.0 if accumulate else 0.0, splits, _lib.ptr(ws), 0 if ws is None else ws.numel(),
+              _stream(A))
+    return out
+
+
+class _ProjectScores(torch.autograd.Function):
+    """h = X @ W, el = h . al, er = h . ar (per head) in one MFMA launch."""
+
+    @staticmethod
+    def forward(ctx, X, W, al, ar, heads: int, feat: int):
+        X, W = _f32c(X), _f32c(W)
+        al, ar = _f32c(al), _f32c(ar)
+        M, K = X.shape
+        dev = X.device
+        h = torch.empty(M, heads * feat, device=dev, dtype=torch.float32)
+        el = torch.empty(M, heads, device=dev, dtype=torch.float32) if al is not None else None
+        er = torch.empty(M, heads, device=dev, dtype=torch.float32) if ar is not None else None
+        _lib.call("msha_project_scores", M, K, heads, feat, X.data_ptr(), W.data_ptr(),
+                  _lib.ptr(al), _lib.ptr(ar), h.data_ptr(), _lib.ptr(el), _lib.ptr(er),
+                  _stream(X))
+        ctx.heads, ctx.feat = heads, feat
+        ctx.save_for_backward(X, W, al, ar, h)
+        outs = [h]
+        if el is not None:
+            outs.append(el)
+        if er is not None:
+            outs.append(er)
+        return tuple(outs) if len(outs) > 1 else h
+
+    @staticmethod
+    def backward(ctx, dh, *dscores):
+        X, W, al, ar, h = ctx.saved_tensors
+        H, Fd = ctx.heads, ctx.feat
+        M = X.shape[0]
+        dev = X.device
+        s = _stream(X)
+        it = iter(dscores)
+        d_el = next(it) if al is not None else None
+        d_er = next(it) if ar is not None else None
+        dh = torch.zeros_like(h) if dh is None else _f32c(dh)
+        terms = [(d, a) for d, a in ((d_el, al), (d_er, ar)) if d is not None]
+        if terms:
+            tot = torch.empty_like(dh)
+            (d1, a1) = terms[0]
+            d2, a2 = terms[1] if len(terms) > 1 else (None, None)
+            _lib.call("msha_add_head_outer", M, H, Fd, dh.data_ptr(), _f32c(d1).data_ptr(),
+                      a1.data_ptr(), _lib.ptr(_f32c(d2)), _lib.ptr(a2), tot.data_ptr(), s)
+            dh = tot
+        dX = dW = dal = dar = None
+        if ctx.needs_input_grad[0]:
+            dX = gemm(dh, W.t())
+        if ctx.needs_input_grad[1]:
+            dW = gemm(X.t(), dh)
+        if terms and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
+            # dal[h,f] = sum_m d_el[m,h] h[m,h,f]: rows of ([d_el | d_er]^T @ h), diagonal blocks
+            D = torch.cat([_f32c(d) for d in (d_el, d_er) if d is not None], dim=1)  # (M, k*H)
+            R = gemm(D.t(), h)  # (k*H, H*F)
+            idx = torch.arange(H, device=dev)
+            blocks = R.view(-1, H, H, Fd)[:, idx, idx]  # (k, H, F)
+            k = 0
+            if d_el is not None:
+                dal = blocks[k].reshape(al.shape)
+                k += 1
+            if d_er is not None:
+                dar = blocks[k].reshape(ar.shape)
+        return dX, dW, dal, dar, None, None
+
+
+def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = None):
+    """``h = X @ W`` on the MFMA GEMM, with optional fused per-head score halves
+    ``el = h . al``, ``er = h . ar`` (al/ar: (heads, feat)).  Returns h or
+    (h, el[, er])."""
+    _lib.require_cuda(X, W)
+    feat = W.shape[1] // heads if feat is None else feat
+    if al is not None:
+        al = al.reshape(heads, feat)
+    if ar is not None:
+        ar = ar.reshape(heads, feat)
+    return _ProjectScores.apply(X, W, al, ar, heads, feat)
+
+
+# ------------------------------------------------------------------ link scoring ---
+ACT_BIAS, ACT_RELU, ACT_DROPOUT, ACT_SIGMOID = 1, 2, 4, 8
+
+
+class _PairInner(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_i, x_j):
+        x_i, x_j = _f32c(x_i), _f32c(x_j)
+        B, Fd = x_i.shape
+        out = torch.empty(B, device=x_i.device, dtype=torch.float32)
+        _lib.call("msha_pair_inner_fwd", B, Fd, x_i.data_ptr(), Fd, None, x_j.data_ptr(), Fd,
+                  None, out.data_ptr(), _stream(x_i))
+        ctx.save_for_backward(x_i, x_j, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x_i, x_j, out = ctx.saved_tensors
+        B, Fd = x_i.shape
+        dxi, dxj = torch.empty_like(x_i), torch.empty_like(x_j)
+        _lib.call("msha_pair_inner_bwd", B, Fd, x_i.data_ptr(), Fd, None, x_j.data_ptr(), Fd,
+                  None, out.data_ptr(), _f32c(dout).data_ptr(), dxi.data_ptr(), dxj.data_ptr(),
+                  _stream(x_i))
+        return dxi, dxj
+
+
+class _PairLayer(torch.autograd.Function):
+    """y = [sigmoid](dropout(relu(x @ W^T + b))) with x = x_i * x_j (first layer,
+    fused) or x = x_i (deeper layers, x_j None)."""
+
+    @staticmethod
+    def forward(ctx, x_i, x_j, W, b, p: float, seed: int, sigmoid: bool):
+        x_i, x_j, W, b = _f32c(x_i), _f32c(x_j), _f32c(W), _f32c(b)
+        B, K = x_i.shape
+        N = W.shape[0]
+        act = ACT_BIAS | ACT_RELU | (ACT_DROPOUT if p > 0 else 0) | (ACT_SIGMOID if sigmoid else 0)
+        out = torch.empty(B, N, device=x_i.device, dtype=torch.float32)
+        _lib.call("msha_pair_linear", B, K, N, x_i.data_ptr(), K, None, _lib.ptr(x_j), K, None,
+                  W.data_ptr(), b.data_ptr(), act, p, seed, 0, out.data_ptr(), _stream(x_i))
+        ctx.p, ctx.sigmoid = p, sigmoid
+        ctx.has_xj = x_j is not None
+        ctx.save_for_backward(x_i, x_j if x_j is not None else x_i.new_empty(0), W, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x_i, x_j, W, out = ctx.saved_tensors
+        B, K = x_i.shape
+        N = W.shape[0]
+        s = _stream(x_i)
+        dz = torch.empty_like(out)
+        _lib.call("msha_pair_mlp_dz", B * N, out.data_ptr(), _f32c(dout).data_ptr(), ctx.p,
+                  1 if ctx.sigmoid else 0, dz.data_ptr(), s)
+        if ctx.has_xj:
+            x = torch.empty_like(x_i)
+            _lib.call("msha_pair_hadamard", B, K, x_i.data_ptr(), K, None, x_j.data_ptr(), K, None,
+                      None, x.data_ptr(), None, s)
+        else:
+            x = x_i
+        dW = gemm(dz.t(), x)                      # (N, K) = dz^T x
+        one = torch.ones(1, device=x_i.device, dtype=torch.float32)
+        db = gemm(one.as_strided((1, B), (0, 0)), dz).view(N)  # column sums of dz
+        dx = gemm(dz, W)                          # (B, K)
+        if ctx.has_xj:
+            dxi, dxj = torch.empty_like(x_i), torch.empty_like(x_j)
+            _lib.call("msha_pair_hadamard", B, K, x_i.data_ptr(), K, None, x_j.data_ptr(), K, None,
+                      dx.data_ptr(), dxi.data_ptr(), dxj.data_ptr(), s)
+            return dxi, dxj, dW, db, None, None, None
+        return dx, None, dW, db, None, None, None
+
+
+def pair_inner(x_i, x_j):
+    """'inner' LinkPredictor head: sigmoid(sum(x_i * x_j, -1))  (LLP.py:112-115)."""
+    _lib.require_cuda(x_i, x_j)
+    return _PairInner.apply(x_i, x_j)
+
+
+def pair_layer(x_i, x_j, W, b, p=0.0, training=False, sigmoid=False, seed=None):
+    _lib.require_cuda(x_i, x_j, W, b)
+    p = float(p) if training else 0.0
+    if seed is None:
+        seed = new_seed() if p > 0 else 0
+    return _PairLayer.apply(x_i, x_j, W, b, p, seed, sigmoid)
+
+
+def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None):
+    """Fused caller gather + predictor (LLP.py:233 + LLP.py:104-115), inference:
+    ``predictor(h[src], h[dst])`` without materialising the gathered rows.
+    'inner' -> (P,), 'mlp' (one used Linear W (hidden, F), b) -> (P, hidden)."""
+    _lib.require_cuda(h, src, dst)
+    h = _f32c(h)
+    src = src.to(torch.int64).contiguous()
+    dst = dst.to(torch.int64).contiguous()
+    P, Fd = src.numel(), h.shape[1]
+    s = _stream(h)
+    if mode == "inner":
+        out = torch.empty(P, device=h.device, dtype=torch.float32) if out is None else out
+        _lib.call("msha_pair_inner_fwd", P, Fd, h.data_ptr(), h.stride(0), src.data_ptr(),
+                  h.data_ptr(), h.stride(0), dst.data_ptr(), out.data_ptr(), s)
+        return out
+    W, b = _f32c(W), _f32c(b)
+    N = W.shape[0]
+    out = torch.empty(P, N, device=h.device, dtype=torch.float32) if out is None else out
+    _lib.call("msha_pair_linear", P, Fd, N, h.data_ptr(), h.stride(0), src.data_ptr(),
+              h.data_ptr(), h.stride(0), dst.data_ptr(), W.data_ptr(), b.data_ptr(),
+              ACT_BIAS | ACT_RELU | ACT_SIGMOID, 0.0, 0, 0, out.data_ptr(), s)
+    return out

@@ -9,6 +9,7 @@ and RNG consumption order as the reference, so a model built after
   LLPGAT                LLP.py:148-168     (GAT whose forward takes external features)
   OursLayer3            Ablation.py:235-277
   ablation3             Ablation.py:279-301  (its heads run as ONE multi-head launch)
+  LinkPredictor         LLP.py:86-115
 
 Adjacency arguments may be dense (N, M) tensors (as in train.py; the CSR/CSC view
 is built once on the GPU and cached) or prebuilt ``Graph`` objects.  Every
@@ -59,7 +60,7 @@ class GraphAttentionLayer(nn.Module):
 
     def forward(self, input, adj):
         g = _graph(adj)
-        h = torch.mm(input, self.W)
+        h = MF.project_scores(input, self.W)  # GAT.py:21 on the MFMA GEMM
         return MF.gal(g, h, self.dropout, self.training, zero_grad_of=self.a)
 
 
@@ -154,11 +155,11 @@ def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
     W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
     W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
     a = torch.stack([h.a.view(-1) for h in heads])  # (H, 2F)
-    h1 = torch.mm(r_input, W1).view(m, H, Fd)  # (M, H, F) recipient side
-    h2 = torch.mm(s_input, W2).view(n, H, Fd)  # (N, H, F) source side
-    er = torch.einsum("mhf,hf->mh", h1, a[:, :Fd])  # a[:F] . h1_j  (Ablation.py:266)
-    el = torch.einsum("nhf,hf->nh", h2, a[:, Fd:])  # a[F:] . h2_i
-    u, v = MF.edge_attention(graph, el, er, h1, hs=h2, p=heads[0].dropout, training=training)
+    # Ablation.py:262-267: a[:F] scores the recipient (column) side h1, a[F:] the source h2
+    h1, er = MF.project_scores(r_input, W1, ar=a[:, :Fd], heads=H)  # (M, H*F), (M, H)
+    h2, el = MF.project_scores(s_input, W2, al=a[:, Fd:], heads=H)  # (N, H*F), (N, H)
+    u, v = MF.edge_attention(graph, el, er, h1.view(m, H, Fd), hs=h2.view(n, H, Fd),
+                             p=heads[0].dropout, training=training)
     return [head.epilogue(u[:, k], v[:, k]) for k, head in enumerate(heads)]
 
 
@@ -189,3 +190,52 @@ class ablation3(nn.Module):  # noqa: N801  (reference class name)
         x = F.dropout(x, self.dropout, training=self.training)
         x = F.elu(self.out_att(x, g))
         return F.log_softmax(x, dim=1)
+
+
+class LinkPredictor(torch.nn.Module):
+    """LLP.py:86-115.  'mlp': the used layers lins[:-1] each run as ONE fused
+    (hadamard) Linear + ReLU + dropout [+ sigmoid] MFMA launch; as in the reference
+    the last Linear is built but never applied, so the output is (B, hidden).
+    'inner': sigmoid(sum(x_i * x_j, -1)), one fused gather-free reduction launch."""
+
+    def __init__(self, predictor, in_channels, hidden_channels, out_channels, num_layers,
+                 dropout):
+        super().__init__()
+        self.predictor = predictor
+        self.lins = torch.nn.ModuleList()
+        self.lins.append(torch.nn.Linear(in_channels, hidden_channels))
+        for _ in range(num_layers - 2):
+            self.lins.append(torch.nn.Linear(hidden_channels, hidden_channels))
+        self.lins.append(torch.nn.Linear(hidden_channels, out_channels))
+        self.dropout = dropout
+
+    def reset_parameters(self):
+        for lin in self.lins:
+            lin.reset_parameters()
+
+    def forward(self, x_i, x_j):
+        if self.predictor == "inner":
+            return MF.pair_inner(x_i, x_j)
+        if self.predictor != "mlp":
+            raise NotImplementedError(f"predictor {self.predictor!r}: only 'mlp' and 'inner'")
+        used = self.lins[:-1]
+        if len(used) == 0:
+            raise NotImplementedError("LinkPredictor with num_layers < 2 (no used Linear)")
+        x = None
+        for k, lin in enumerate(used):
+            last = k == len(used) - 1
+            if k == 0:
+                x = MF.pair_layer(x_i, x_j, lin.weight, lin.bias, self.dropout, self.training,
+                                  sigmoid=last)
+            else:
+                x = MF.pair_layer(x, None, lin.weight, lin.bias, self.dropout, self.training,
+                                  sigmoid=last)
+        return x
+
+    def score_pairs(self, h, src, dst):
+        """Inference with the caller's gather fused (LLP.py:233): predictor(h[src], h[dst])."""
+        if self.predictor == "inner":
+            return MF.score_pairs(h, src, dst, "inner")
+        if len(self.lins) != 2:
+            return self.forward(h[src], h[dst])
+        return MF.score_pairs(h, src, dst, "mlp", self.lins[0].weight, self.lins[0].bias)

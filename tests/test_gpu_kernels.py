@@ -227,3 +227,124 @@ def test_gal_fwd_bwd(cuda, p):
     y.backward(t(dout, cuda))
     ref_dh = O.gal_bwd(h, x, h, att, dout)["dh"]
     tol_close(th.grad.cpu().numpy(), ref_dh, 1e-5, 1e-6)
+
+
+# --------------------------------------------------------------- MFMA projection
+@pytest.mark.parametrize("M,N,K,trans_a,trans_b,splits", [
+    (1000, 128, 128, False, False, 1), (257, 64, 64, False, False, 1),
+    (64, 200, 96, False, True, 1), (128, 128, 20000, True, False, 64),
+    (33, 40, 5000, False, False, 8),
+])
+def test_gemm_f32(cuda, M, N, K, trans_a, trans_b, splits):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((K, M) if trans_a else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if trans_b else (K, N)).astype(np.float32)
+    tA, tB = t(A, cuda), t(B, cuda)
+    tA = tA.t() if trans_a else tA
+    tB = tB.t() if trans_b else tB
+    C = MF.gemm(tA, tB, splits=splits).cpu().numpy()
+    ref = (A.T if trans_a else A).astype(np.float64) @ (B.T if trans_b else B).astype(np.float64)
+    tol_close(C, ref, 1e-5, 2e-6 * np.sqrt(K))
+    C2 = MF.gemm(tA, tB, out=torch.as_tensor(C, device=cuda), accumulate=True,
+                 splits=max(splits, 2)).cpu().numpy()
+    tol_close(C2, 2 * ref, 1e-5, 2e-6 * np.sqrt(K))
+
+
+@pytest.mark.parametrize("M,K,H,F", [(3000, 128, 8, 16), (517, 128, 2, 64), (80, 16, 1, 8),
+                                     (300, 64, 4, 32), (200, 32, 1, 128)])
+def test_project_scores_fwd_bwd(cuda, M, K, H, F):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M)
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((K, H * F)).astype(np.float32) / np.sqrt(K)
+    al = rng.standard_normal((H, F)).astype(np.float32)
+    ar = rng.standard_normal((H, F)).astype(np.float32)
+    dh = rng.standard_normal((M, H * F)).astype(np.float32)
+    dl = rng.standard_normal((M, H)).astype(np.float32)
+    dr = rng.standard_normal((M, H)).astype(np.float32)
+    ts = [t(x, cuda).requires_grad_(True) for x in (X, W, al, ar)]
+    h, el, er = MF.project_scores(*ts, heads=H)
+    # torch fp64 reference of the same op
+    rs = [torch.tensor(x, dtype=torch.float64, requires_grad=True) for x in (X, W, al, ar)]
+    rh = rs[0] @ rs[1]
+    rel = (rh.view(M, H, F) * rs[2]).sum(-1)
+    rer = (rh.view(M, H, F) * rs[3]).sum(-1)
+    for got, want in ((h, rh), (el, rel), (er, rer)):
+        tol_close(got.detach().cpu().numpy(), want.detach().numpy(), 1e-5, 1e-5)
+    (h * t(dh, cuda)).sum().add_((el * t(dl, cuda)).sum()).add_((er * t(dr, cuda)).sum()) \
+        .backward()
+    ((rh * torch.tensor(dh, dtype=torch.float64)).sum() + (rel * torch.tensor(dl, dtype=torch.float64)).sum()
+     + (rer * torch.tensor(dr, dtype=torch.float64)).sum()).backward()
+    for got, want in zip(ts, rs):
+        tol_close(got.grad.cpu().numpy(), want.grad.numpy(), 1e-4, 1e-5)
+
+
+# ------------------------------------------------------------------ link scoring
+def test_link_predictor_matches_reference(cuda, msha):
+    from msha_gnn_amd import layers
+
+    z = golden("link.npz")
+    for mode in ("mlp", "inner"):
+        torch.manual_seed(4)
+        lp = layers.LinkPredictor(mode, 32, 32, 1, 2, 0.0)
+        for k, v in lp.state_dict().items():  # same init as the reference (bitwise)
+            assert np.array_equal(v.numpy(), z[f"{mode}.init.{k}"]), k
+        lp = lp.to(cuda).train()
+        xi = t(z["x_i"], cuda).requires_grad_(True)
+        xj = t(z["x_j"], cuda).requires_grad_(True)
+        y = lp(xi, xj)
+        tol_close(y.detach().cpu().numpy(), z[f"{mode}.out"], 1e-5, 1e-6)
+        y.backward(t(z[f"{mode}.dout"], cuda))
+        tol_close(xi.grad.cpu().numpy(), z[f"{mode}.grad.x_i"], 1e-4, 1e-5)
+        tol_close(xj.grad.cpu().numpy(), z[f"{mode}.grad.x_j"], 1e-4, 1e-5)
+        if mode == "mlp":
+            tol_close(lp.lins[0].weight.grad.cpu().numpy(), z["mlp.grad.lins.0.weight"], 1e-4,
+                      1e-5)
+            tol_close(lp.lins[0].bias.grad.cpu().numpy(), z["mlp.grad.lins.0.bias"], 1e-4, 1e-5)
+            assert lp.lins[1].weight.grad is None
+
+
+def test_link_predictor_deep_and_dropout(cuda, msha):
+    """num_layers=3 (two used Linears) and dropout: vs oracle with the kernel's mask."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd import layers
+
+    torch.manual_seed(0)
+    lp = layers.LinkPredictor("mlp", 16, 24, 1, 3, 0.0).to(cuda).eval()
+    rng = np.random.default_rng(2)
+    xi, xj = (rng.standard_normal((300, 16)).astype(np.float32) for _ in range(2))
+    y = lp(t(xi, cuda), t(xj, cuda)).detach().cpu().numpy()
+    W0, b0 = lp.lins[0].weight.detach().cpu().numpy(), lp.lins[0].bias.detach().cpu().numpy()
+    W1, b1 = lp.lins[1].weight.detach().cpu().numpy(), lp.lins[1].bias.detach().cpu().numpy()
+    x = np.maximum((xi * xj) @ W0.T + b0, 0)
+    x = np.maximum(x @ W1.T + b1, 0)
+    tol_close(y, 1 / (1 + np.exp(-x)), 1e-5, 1e-6)
+    # dropout on the fused layer: mask index = row * N + col
+    W = t(W0, cuda)
+    b = t(b0, cuda)
+    out = MF.pair_layer(t(xi, cuda), t(xj, cuda), W, b, p=0.5, training=True, sigmoid=True,
+                        seed=77).cpu().numpy()
+    keep = MF.dropout_keep_mask(300 * 24, 0.5, 77, cuda).cpu().numpy().reshape(300, 24)
+    z = np.maximum((xi * xj) @ W0.T + b0, 0) * keep * 2.0
+    tol_close(out, 1 / (1 + np.exp(-z)), 1e-5, 1e-6)
+
+
+@pytest.mark.parametrize("F", [32, 128])
+def test_score_pairs_fused_gather(cuda, F):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(F)
+    n, P, hid = 5000, 20000, 64
+    h = rng.standard_normal((n, F)).astype(np.float32)
+    src = rng.integers(0, n, P)
+    dst = rng.integers(0, n, P)
+    W = (rng.standard_normal((hid, F)) / np.sqrt(F)).astype(np.float32)
+    b = rng.standard_normal(hid).astype(np.float32)
+    th, ts, td = t(h, cuda), t(src, cuda, torch.int64), t(dst, cuda, torch.int64)
+    inner = MF.score_pairs(th, ts, td, "inner").cpu().numpy()
+    tol_close(inner, O.score_pairs(h, src, dst, "inner"), 1e-5, 1e-6)
+    mlp = MF.score_pairs(th, ts, td, "mlp", t(W, cuda), t(b, cuda)).cpu().numpy()
+    tol_close(mlp, O.score_pairs(h, src, dst, "mlp", [(W, b), (None, None)]), 1e-5, 1e-6)
