@@ -108,44 +108,36 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
                      hidden=128, n_pairs=4_000_000):
     """score P = 4M pairs (2M graph edges + 2M uniform negatives,
     seed 1) against h (n x F) with LinkPredictor 'mlp' (hidden 128) and 'inner'.
-    Rank r owns rows [r n/W, (r+1) n/W) of h; one RCCL all_gather_into_tensor per
-    batch rebuilds the full table (timed, included), then each rank scores its
-    contiguous P/W slice of the batch.  Returns pairs/s over all ranks."""
+    Rank r owns rows [r R, (r+1) R) of h (sharding.ShardedTable); one RCCL
+    all_gather_into_tensor per batch rebuilds the full table (inside the timed
+    loop), then each rank scores its contiguous P/W slice.  pairs/s over all ranks."""
     from msha_gnn_amd import functional as MF
+    from msha_gnn_amd import sharding
 
     g = torch.Generator().manual_seed(1)
     rows = np.repeat(np.arange(n), np.diff(rowptr))
     pick = np.random.default_rng(1).choice(len(col), n_pairs // 2, replace=False)
     src = np.concatenate([rows[pick], torch.randint(0, n, (n_pairs // 2,), generator=g).numpy()])
     dst = np.concatenate([col[pick], torch.randint(0, n, (n_pairs // 2,), generator=g).numpy()])
-    per = n_pairs // world
-    lo = rank * per
-    t_src = torch.as_tensor(src[lo:lo + per], device=dev)
-    t_dst = torch.as_tensor(dst[lo:lo + per], device=dev)
-    rows_per = (n + world - 1) // world
-    h_local = torch.rand(rows_per, F, generator=torch.Generator().manual_seed(10 + rank)).to(dev)
-    h_full = torch.empty(rows_per * world, F, device=dev)
+    t_src = torch.as_tensor(src, device=dev)
+    t_dst = torch.as_tensor(dst, device=dev)
+    table = sharding.ShardedTable(n, F, world, rank, dev)
+    lo, hi = sharding.row_range(n, world, rank)
+    table.set_local(torch.rand(hi - lo, F, generator=torch.Generator().manual_seed(10 + rank))
+                    .to(dev))
     W = (torch.randn(hidden, F, generator=g) * F ** -0.5).to(dev)
     b = torch.randn(hidden, generator=g).to(dev)
-    out_mlp = torch.empty(per, hidden, device=dev)
-    out_inner = torch.empty(per, device=dev)
+    plo, phi = sharding.pair_range(n_pairs, world, rank)
+    out_mlp = torch.empty(phi - plo, hidden, device=dev)
+    out_inner = torch.empty(phi - plo, device=dev)
     if dist:
         import torch.distributed as tdist
-
-    def gather():
-        if dist:
-            tdist.all_gather_into_tensor(h_full, h_local)
-        else:
-            h_full.copy_(h_local)
-
+    fns = {"mlp": lambda h, s_, d_: MF.score_pairs(h, s_, d_, "mlp", W, b, out=out_mlp),
+           "inner": lambda h, s_, d_: MF.score_pairs(h, s_, d_, "inner", out=out_inner)}
     res = {}
     for mode in ("mlp", "inner"):
         def one():
-            gather()
-            if mode == "mlp":
-                MF.score_pairs(h_full, t_src, t_dst, "mlp", W, b, out=out_mlp)
-            else:
-                MF.score_pairs(h_full, t_src, t_dst, "inner", out=out_inner)
+            sharding.score_sharded(table, t_src, t_dst, fns[mode])
         for _ in range(warmup):
             one()
         if dist:
@@ -162,19 +154,69 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
             tt = torch.tensor([dt], device=dev)
             tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
             dt = float(tt.item())
-        res[f"pairs_per_sec_{mode}"] = per * world * steps / dt
+        res[f"pairs_per_sec_{mode}"] = n_pairs * steps / dt
         res[f"ms_per_batch_{mode}"] = dt / steps * 1e3
-    # all-gather alone
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        gather()
+        table.gather()
     torch.cuda.synchronize(dev)
     res["allgather_ms"] = (time.perf_counter() - t0) / steps * 1e3
-    res.update(pairs_per_batch=per * world, feat=F, hidden=hidden, world=world, dtype="f32",
-               sharding="h rows all-gathered over RCCL, pairs split contiguously per rank"
-               if dist else "single GPU (no collective)")
+    res.update(pairs_per_batch=n_pairs, feat=F, hidden=hidden, world=world, dtype="f32",
+               sharding="h rows all-gathered over RCCL (all_gather_into_tensor), pairs split "
+               "contiguously per rank" if dist else "single GPU (no collective)")
     return res
+
+
+def r15_train_step(dev, steps=20, warmup=5):
+    """configs[1] at the shipped 2015 graph: one train.py iteration (train.py:221-232)
+    of ablation3(in 128, F 64, 2 heads, dropout 0.5) with Adam(lr 1e-3, wd 5e-4):
+    full-graph forward, nll on a 64-flow batch, backward, optimizer step."""
+    import msha_loader
+
+    msha = msha_loader.load()
+    from msha_gnn_amd import layers
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    n, m = int(z["n"]), int(z["m"])
+    rows = np.repeat(np.arange(n), np.diff(z["rowptr"]))
+    counts = torch.zeros(n, m)
+    counts[torch.as_tensor(rows), torch.as_tensor(z["col"].astype(np.int64))] = torch.as_tensor(
+        z["cnt"].astype(np.float32))
+    adj = msha.normalize_adjacency_matrix(counts.to(dev))
+    gdp = {i: float(x) for i, x in enumerate(z["gdp"])}
+    torch.manual_seed(0)
+    model = layers.ablation3(128, 64, m, 2, 0.5, gdp, n, m).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
+    g = torch.Generator().manual_seed(0)
+    flows_src = torch.as_tensor(np.repeat(rows, z["cnt"].astype(np.int64)))
+    flows_dst = torch.as_tensor(np.repeat(z["col"].astype(np.int64), z["cnt"].astype(np.int64)))
+    batches = [torch.randint(0, len(flows_src), (64,), generator=g) for _ in range(8)]
+    batches = [(flows_src[b].to(dev), flows_dst[b].to(dev)) for b in batches]
+    model.train()
+
+    def one(k):
+        si, ri = batches[k % len(batches)]
+        opt.zero_grad()
+        out = model(adj, None, None, si)
+        loss = torch.nn.functional.nll_loss(out[si], ri)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for k in range(warmup):
+        one(k)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        loss = one(k)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / steps
+    e = int(z["rowptr"][-1])
+    return dict(workload="ablation3 train step, 2015 graph (N 39179, M 32, E 91283), in 128, "
+                         "F 64, 2 heads, dropout 0.5, Adam", ms_per_step=dt * 1e3,
+                edges_per_sec=e / dt, loss=float(loss),
+                reference_cpu_s_per_step="1.01-1.27 (BASELINE.md, 8-core container, not this box)")
 
 
 def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
@@ -227,6 +269,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-link-score", action="store_true")
+    ap.add_argument("--no-r15", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -298,6 +341,8 @@ def main():
     }
     if link is not None:
         out["link_score"] = link
+    if world == 1 and not args.no_r15:
+        out["r15_train_step"] = r15_train_step(dev)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
     print(json.dumps(out), flush=True)

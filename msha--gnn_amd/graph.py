@@ -179,7 +179,11 @@ def inter_adjacency(source: torch.Tensor, recipient: torch.Tensor, n_rows: int,
 
 def normalize_adjacency_matrix(adjacency_matrix: torch.Tensor) -> torch.Tensor:
     """model.py:95-100: ``adj @ diag(d) @ diag(d)``, ``d = colsum ** -0.5``, computed as
-    ``(adj * d) * d`` (bit-identical for finite d; a zero column gives NaN everywhere)."""
+    ``(adj * d) * d`` (bit-identical for finite d; a zero column gives NaN everywhere).
+    Group adjacencies (data.GroupAdjacency) pass through: every column of a
+    same-group mask has a non-zero sum, so normalising keeps the mask."""
+    if not torch.is_tensor(adjacency_matrix) and hasattr(adjacency_matrix, "ids"):
+        return adjacency_matrix
     _lib.require_cuda(adjacency_matrix)
     a = adjacency_matrix.detach()
     if a.dtype != torch.float32:
