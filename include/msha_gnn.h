@@ -76,6 +76,19 @@ typedef struct msha_graph {
   const int32_t* multi_count;
 } msha_graph;
 
+/* Same-group adjacency of the full MSHA layer (city and province, dataset.py:260-277
+ * builds them as dense N x N masks): group id per node, and per group the sorted
+ * member list (CSR: gptr over gmem). */
+typedef struct msha_groups {
+  int64_t n_nodes;
+  const int32_t* gid3;  /* n_nodes: city group of each node */
+  const int32_t* gptr3; /* n_city_groups + 1 */
+  const int32_t* gmem3; /* n_nodes: members, grouped, ascending */
+  const int32_t* gid4;  /* province */
+  const int32_t* gptr4;
+  const int32_t* gmem4;
+} msha_groups;
+
 MSHA_API int msha_abi_version(void);
 MSHA_API const char* msha_last_error(void);
 
@@ -137,11 +150,14 @@ MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t
  * Writes d_el (n_rows, heads) = row sums of de, de (n_edges, heads), attd
  * (n_edges, heads) = post-dropout attention, and d_hs (n_rows, heads, feat) =
  * sum_e attd_e dV[j] when dV != NULL.  The column half (d_er, d_hc) is
- * msha_csc_aggregate over (attd, de). */
+ * msha_csc_aggregate over (attd, de).  row_coef (n_rows, heads), nullable: an extra
+ * gradient row_coef[i] * exp(attd_e) on the attention of row i -- the full MSHA
+ * layer's normaliser sums exp(attention_inter) of its batch rows (Ours.py:84-86). */
 MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
                                  const float* el, const float* er, const float* hc,
                                  const float* lse, const float* u, const float* dU,
-                                 const float* hs, const float* dV, float neg_slope,
+                                 const float* hs, const float* dV, const float* row_coef,
+                                 float neg_slope,
                                  float drop_p, uint64_t seed, uint64_t offset, float* d_el,
                                  float* de, float* attd, float* d_hs, msha_stream_t stream);
 
@@ -224,6 +240,36 @@ MSHA_API int msha_pair_hadamard(int64_t n_pairs, int32_t feat, const float* G, i
                                 const int64_t* gi, const float* G2, int64_t ldg2,
                                 const int64_t* gj, const float* dx, float* x_or_dxi, float* dxj,
                                 msha_stream_t stream);
+
+/* ----------------------------------------------- full MSHA layer (Ours.py) --- */
+/* Intra-source attention of a batch (Ours.py:71-101) on top of the inter forward:
+ *   e3_b = lrelu(h2[src_b] . a3s), E3 = exp(e3_b); e4/E4 with a4s (a3s = a3[:F] + a3[F:])
+ *   SUM_b = |city(src_b)| E3 + |prov(src_b)| E4 + sum_j exp(attd[src_b, j]) (all M columns)
+ *   u_out[n] = u_inter[n] + sum_{b: same city} drop E3/SUM h2[src_b]
+ *                         + sum_{b: same province} drop E4/SUM h2[src_b]
+ * (per head; heads*feat <= 512).  el/er/lse are the inter forward's.  bstat (B, heads, 8)
+ * keeps the per-batch statistics for the backward.  Dropout of att3/att4 uses Philox
+ * offsets offset+1+2h / offset+2+2h on the dense (B, N) index. */
+MSHA_API int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, int64_t B,
+                                 const int64_t* src, int32_t heads, int32_t feat,
+                                 const float* h2, const float* a3s, const float* a4s,
+                                 const float* el, const float* er, const float* lse,
+                                 const float* u_inter, float neg_slope, float drop_p,
+                                 uint64_t seed, uint64_t offset, float* bstat, float* u_out,
+                                 msha_stream_t stream);
+/* Backward, two stages around msha_edge_attention_bwd_rows:
+ *   stage 0: G (B, 2, heads*feat) = group sums of dropout * dU; bgrad (B, heads, 4);
+ *            row_coef (n_rows, heads; zero-filled by the caller) = dL/dSUM per batch row;
+ *            da3s, da4s (heads, feat).
+ *   stage 1: d_hs[src_b] += the intra gradient of h2's batch rows.
+ * Per-row sums follow batch order (deterministic). */
+MSHA_API int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, int64_t B,
+                                 const int64_t* src, int32_t heads, int32_t feat,
+                                 const float* h2, const float* a3s, const float* a4s,
+                                 const float* bstat, const float* dU, int32_t stage,
+                                 float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
+                                 float* G, float* bgrad, float* row_coef, float* da3s,
+                                 float* da4s, float* d_hs, msha_stream_t stream);
 
 #ifdef __cplusplus
 }

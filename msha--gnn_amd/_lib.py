@@ -38,6 +38,17 @@ P = C.c_void_p
 I32, I64, U64, F32, SZ = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_size_t
 GP = C.POINTER(MshaGraph)
 
+
+class MshaGroups(C.Structure):
+    """Mirror of ``struct msha_groups`` (include/msha_gnn.h)."""
+
+    _fields_ = [("n_nodes", C.c_int64),
+                ("gid3", C.c_void_p), ("gptr3", C.c_void_p), ("gmem3", C.c_void_p),
+                ("gid4", C.c_void_p), ("gptr4", C.c_void_p), ("gmem4", C.c_void_p)]
+
+
+GRP = C.POINTER(MshaGroups)
+
 # name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
 SIGNATURES = {
     "msha_abi_version": (C.c_int, []),
@@ -51,8 +62,8 @@ SIGNATURES = {
     "msha_edge_attention_supported": (C.c_int, [I32, I32]),
     "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, P, P, P, F32, F32, U64, U64, P, P, P,
                                           P]),
-    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, P, P, F32, F32,
-                                               U64, U64, P, P, P, P, P]),
+    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, P, P, P, F32,
+                                               F32, U64, U64, P, P, P, P, P]),
     "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
     "msha_csc_aggregate": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),
@@ -68,6 +79,10 @@ SIGNATURES = {
     "msha_pair_inner_bwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P, P]),
     "msha_pair_mlp_dz": (C.c_int, [I64, P, P, F32, I32, P, P]),
     "msha_pair_hadamard": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P]),
+    "msha_ours_intra_fwd": (C.c_int, [GP, GRP, I64, P, I32, I32, P, P, P, P, P, P, P, F32, F32,
+                                      U64, U64, P, P, P]),
+    "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, P, P, P, P, P, I32, F32, F32,
+                                      U64, U64, P, P, P, P, P, P, P]),
 }
 
 _lib = None

@@ -132,8 +132,9 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
     const float* __restrict__ er, const float* __restrict__ hc, const float* __restrict__ lse,
     const float* __restrict__ u, const float* __restrict__ dU, const float* __restrict__ hs,
-    const float* __restrict__ dV, float slope, Dropout dp, float* __restrict__ d_el,
-    float* __restrict__ de, float* __restrict__ attd, float* __restrict__ d_hs) {
+    const float* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
+    float* __restrict__ d_el, float* __restrict__ de, float* __restrict__ attd,
+    float* __restrict__ d_hs) {
   using G = Geo<H, F>;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
@@ -206,6 +207,21 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
       const float cand = __shfl(dk, dsrc_l);
       if (k == dsrc_k) Ds = cand;
     }
+    // Ours.py:84-86: SUM_county adds sum_j exp(attd_ij) for batch rows, so those rows'
+    // attention gets the extra gradient coef * exp(attd) (row_coef = dL/dSUM terms)
+    const float coef = row_coef != nullptr ? row_coef[row * H + h_s] : 0.f;
+    if (__ballot(coef != 0.f)) {
+      float t = 0.f;
+      for (int32_t cs = start; cs < end; cs += G::CE) {
+        const int32_t e = cs + e_s;
+        if (e < end) {
+          const float s = virt ? 0.f : lrelu(elh + er[(int64_t)col[e] * H + h_s], slope);
+          const float ad = __expf(s - lseh) * dropout_factor(dp, (uint64_t)e * H + h_s);
+          t += ad * expf(ad);
+        }
+      }
+      Ds += coef * wave_xor_sum<H>(t);
+    }
     float del = 0.f;
     for (int32_t cs = start; cs < end; cs += G::CE) {
       const int32_t e = cs + e_s;
@@ -241,6 +257,7 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
         }
       }
       if (valid) {
+        if (coef != 0.f) gsum += coef * expf(att * dropf);
         const float ds = att * (gsum * dropf - Ds);
         const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
         de[(int64_t)e * H + h_s] = dev;
@@ -404,7 +421,8 @@ extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32
 extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
                                             const float* el, const float* er, const float* hc,
                                             const float* lse, const float* u, const float* dU,
-                                            const float* hs, const float* dV, float neg_slope,
+                                            const float* hs, const float* dV,
+                                            const float* row_coef, float neg_slope,
                                             float drop_p, uint64_t seed, uint64_t offset,
                                             float* d_el, float* de, float* attd, float* d_hs,
                                             msha_stream_t stream) {
@@ -422,11 +440,13 @@ extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, 
     if (dV)                                                                                   \
       hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, true>), wave_grid(g->n_rows),       \
                          dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,   \
-                         hc, lse, u, dU, hs, dV, neg_slope, dp, d_el, de, attd, d_hs);        \
+                         hc, lse, u, dU, hs, dV, row_coef, neg_slope, dp, d_el, de, attd,     \
+                         d_hs);                                                               \
     else                                                                                      \
       hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, false>), wave_grid(g->n_rows),      \
                          dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,   \
-                         hc, lse, u, dU, hs, dV, neg_slope, dp, d_el, de, attd, d_hs);        \
+                         hc, lse, u, dU, hs, dV, row_coef, neg_slope, dp, d_el, de, attd,     \
+                         d_hs);                                                               \
   }
   MSHA_FOR_EACH_SHAPE(X)
 #undef X

@@ -1,0 +1,352 @@
+// Full MSHA layer (Ours.OursLayer, Ours.py:54-109): the intra-source attention of a
+// batch of sources over their city / province groups, coupled to the inter
+// attention through the joint normaliser SUM_county (Ours.py:84-90).
+//
+// Reference (dense): for a batch of B sources (source_index),
+//   e3_b  = lrelu(h2_b . (a3[:F] + a3[F:]))           constant along n (Ours.py:74-75)
+//   att3  = where(city_adj[src] > 0, e3, -9e15)        (B, N)          (Ours.py:81)
+//   SUM_b = sum_n exp(att3) + sum_n exp(att4) + sum_j exp(attd_inter[src_b, j])
+//         (no max subtraction; the last term runs over ALL M columns, post-dropout)
+//   att3  = dropout(exp(att3) / SUM), att4 likewise    (Ours.py:87-90)
+//   IntraNC = att3^T @ h2[src] + att4^T @ h2[src]      (N, F)          (Ours.py:99)
+//   u = lrelu(bn2(att_inter @ h1 + IntraNC))           (Ours.py:101)
+// Here the masks are group ids (same city <=> same id): the (B, N) tensors are
+// never built.  Per batch entry b: c3 = |city group|, so sum_n exp(att3) = c3 E3.
+//
+// Kernels:  prep (wave per b): e3/e4, the inter term I_b, SUM_b, weights w3/w4
+//           fwd  (wave per node n): ballot-match the batch against n's groups and
+//                gather-aggregate the matching h2 rows (dropout per (b, n))
+//           bwd_gather (wave per (b, kind)): G_b = sum_{n in group} drop * dU_n
+//           bwd_finish (one workgroup): scalar chain, deterministic per-row sums
+#include "common.h"
+
+namespace msha {
+
+constexpr int kMaxD = 512;  // heads * feat
+
+struct OursArgs {
+  int64_t B, N, M;
+  int H, F;
+  const int64_t* src;
+  const int32_t* gid3;
+  const int32_t* gptr3;
+  const int32_t* gmem3;
+  const int32_t* gid4;
+  const int32_t* gptr4;
+  const int32_t* gmem4;
+  const float* h2;   // (N, H, F)
+  const float* a3s;  // (H, F) = a3[:F] + a3[F:]
+  const float* a4s;
+  float slope;
+  Dropout dp;  // edge dropout: offset; intra att3/att4 use offset + 1 + 2h / + 2 + 2h
+};
+
+enum { BS_PRE3 = 0, BS_PRE4, BS_E3, BS_E4, BS_SUM, BS_W3, BS_W4, BS_I, BS_N };
+
+__device__ __forceinline__ float intra_drop(const Dropout& d, int kind, int h, uint64_t idx) {
+  if (!d.active) return 1.f;
+  return philox_x(d.seed, d.offset + 1 + 2 * (uint64_t)h + (uint64_t)kind, idx) >= d.threshold
+             ? d.scale : 0.f;
+}
+
+// ---------------------------------------------------------------------- prep ---
+__global__ void __launch_bounds__(256) ours_prep_kernel(
+    OursArgs a, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const uint8_t* __restrict__ rowflag, const float* __restrict__ el,
+    const float* __restrict__ er, const float* __restrict__ lse, float* __restrict__ bstat) {
+  const int lane = lane_id();
+  const int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (b >= a.B) return;
+  const int64_t i = a.src[b];
+  const int H = a.H, F = a.F;
+  const int32_t start = rowptr[i], end = rowptr[i + 1];
+  const bool virt = rowflag != nullptr && rowflag[i] != 0;
+  const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
+  const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
+  for (int h = 0; h < H; ++h) {
+    float p3 = 0.f, p4 = 0.f;
+    for (int f = lane; f < F; f += 64) {
+      const float x = a.h2[(i * H + h) * F + f];
+      p3 = fmaf(x, a.a3s[h * F + f], p3);
+      p4 = fmaf(x, a.a4s[h * F + f], p4);
+    }
+    p3 = wave_xor_sum<1>(p3);
+    p4 = wave_xor_sum<1>(p4);
+    // I_b = sum over ALL M columns of exp(post-dropout inter attention): non-edges
+    // hold attention 0 -> exp(0) = 1 each
+    float I = 0.f;
+    for (int32_t e = start + lane; e < end; e += 64) {
+      const float s = virt ? 0.f : lrelu(el[i * H + h] + er[(int64_t)col[e] * H + h], a.slope);
+      const float att = __expf(s - lse[i * H + h]) * dropout_factor(a.dp, (uint64_t)e * H + h);
+      I += expf(att);
+    }
+    I = wave_xor_sum<1>(I) + (float)(a.M - (end - start));
+    const float E3 = expf(lrelu(p3, a.slope)), E4 = expf(lrelu(p4, a.slope));
+    const float sum = (c3 * E3 + c4 * E4) + I;
+    if (lane == 0) {
+      float* o = bstat + (b * H + h) * BS_N;
+      o[BS_PRE3] = p3; o[BS_PRE4] = p4; o[BS_E3] = E3; o[BS_E4] = E4;
+      o[BS_SUM] = sum; o[BS_W3] = E3 / sum; o[BS_W4] = E4 / sum; o[BS_I] = I;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward ---
+// u_out[n] = u_in[n] + sum_{b: city(src_b) = city(n)} drop * w3_b h2[src_b]
+//                    + sum_{b: prov(src_b) = prov(n)} drop * w4_b h2[src_b]
+__global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* __restrict__ bstat,
+                                                       const float* __restrict__ u_in,
+                                                       float* __restrict__ u_out) {
+  const int lane = lane_id();
+  const int D = a.H * a.F;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  constexpr int KD = kMaxD / 64;
+  for (int64_t n = wave; n < a.N; n += nwaves) {
+    const int32_t g3 = a.gid3[n], g4 = a.gid4[n];
+    float acc3[KD], acc4[KD];
+#pragma unroll
+    for (int k = 0; k < KD; ++k) acc3[k] = acc4[k] = 0.f;
+    for (int64_t base = 0; base < a.B; base += 64) {
+      const int64_t b = base + lane;
+      const bool valid = b < a.B;
+      const int64_t ib = valid ? a.src[b] : 0;
+      uint64_t bal3 = __ballot(valid && a.gid3[ib] == g3);
+      uint64_t bal4 = __ballot(valid && a.gid4[ib] == g4);
+      for (int kind = 0; kind < 2; ++kind) {
+        uint64_t bal = kind == 0 ? bal3 : bal4;
+        while (bal) {
+          const int bit = __ffsll((long long)bal) - 1;
+          bal &= bal - 1;
+          const int64_t bb = base + bit;
+          const int64_t ibb = __shfl(ib, bit);
+#pragma unroll
+          for (int k = 0; k < KD; ++k) {
+            const int d = lane + 64 * k;
+            if (d < D) {
+              const int h = d / a.F;
+              const float w = bstat[(bb * a.H + h) * BS_N + (kind == 0 ? BS_W3 : BS_W4)] *
+                              intra_drop(a.dp, kind, h, (uint64_t)bb * a.N + n);
+              const float x = a.h2[ibb * D + d];
+              if (kind == 0) acc3[k] = fmaf(w, x, acc3[k]); else acc4[k] = fmaf(w, x, acc4[k]);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = lane + 64 * k;
+      if (d < D) u_out[n * D + d] = u_in[n * D + d] + (acc3[k] + acc4[k]);
+    }
+  }
+}
+
+// ----------------------------------------------------------- backward: gather ---
+// G[b, kind] = sum_{n in group(kind, src_b)} drop(kind, b, n) * dU[n]   (members ascending)
+__global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
+                                                              const float* __restrict__ dU,
+                                                              float* __restrict__ G) {
+  const int lane = lane_id();
+  const int D = a.H * a.F;
+  const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (wv >= 2 * a.B) return;
+  const int64_t b = wv >> 1;
+  const int kind = (int)(wv & 1);
+  const int64_t i = a.src[b];
+  const int32_t* gptr = kind == 0 ? a.gptr3 : a.gptr4;
+  const int32_t* gmem = kind == 0 ? a.gmem3 : a.gmem4;
+  const int32_t grp = kind == 0 ? a.gid3[i] : a.gid4[i];
+  const int32_t m0 = gptr[grp], m1 = gptr[grp + 1];
+  constexpr int KD = kMaxD / 64;
+  float acc[KD];
+#pragma unroll
+  for (int k = 0; k < KD; ++k) acc[k] = 0.f;
+  for (int32_t t = m0; t < m1; ++t) {
+    const int64_t n = gmem[t];
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = lane + 64 * k;
+      if (d < D) {
+        const int h = d / a.F;
+        acc[k] = fmaf(intra_drop(a.dp, kind, h, (uint64_t)b * a.N + n), dU[n * D + d], acc[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KD; ++k) {
+    const int d = lane + 64 * k;
+    if (d < D) G[(b * 2 + kind) * D + d] = acc[k];
+  }
+}
+
+// ------------------------------------------------------------ backward: finish ---
+// mode 0 (before the inter row backward):
+//   per (b, h): dw3 = G3 . h2_b, dw4 = G4 . h2_b; through w = E/SUM, SUM = c3E3 + c4E4 + I,
+//   E = exp(lrelu(pre)): bgrad = {dpre3, dpre4, dI}; row_coef[src, h] = sum_b dI (per row,
+//   batch order) -- the extra gradient sum_j exp(attd_ij) puts on the inter attention;
+//   da3s[h, f] = sum_b dpre3 h2_b, da4s likewise.
+// mode 1 (after it): d_hs[src_b] += w3 G3 + w4 G4 + dpre3 a3s + dpre4 a4s (per row,
+//   batch order).  One workgroup: B is a mini-batch (train.py:33, 64 flows).
+__global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
+    OursArgs a, int mode, const float* __restrict__ bstat, const float* __restrict__ G,
+    float* __restrict__ bgrad, float* __restrict__ row_coef, float* __restrict__ da3s,
+    float* __restrict__ da4s, float* __restrict__ d_hs) {
+  const int H = a.H, F = a.F, D = H * F;
+  const int64_t B = a.B;
+  if (mode == 0) {
+    for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
+      const int64_t b = t / H;
+      const int h = (int)(t % H);
+      const int64_t i = a.src[b];
+      const float* st = bstat + (b * H + h) * BS_N;
+      float dw3 = 0.f, dw4 = 0.f;
+      for (int f = 0; f < F; ++f) {
+        const float x = a.h2[i * D + h * F + f];
+        dw3 = fmaf(G[(b * 2 + 0) * D + h * F + f], x, dw3);
+        dw4 = fmaf(G[(b * 2 + 1) * D + h * F + f], x, dw4);
+      }
+      const float sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
+      const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
+      const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
+      const float dsum = -(dw3 * E3 + dw4 * E4) / (sum * sum);
+      const float dE3 = dw3 / sum + dsum * c3;
+      const float dE4 = dw4 / sum + dsum * c4;
+      const float p3 = st[BS_PRE3], p4 = st[BS_PRE4];
+      float* o = bgrad + t * 4;
+      o[0] = dE3 * E3 * (p3 > 0.f ? 1.f : a.slope);
+      o[1] = dE4 * E4 * (p4 > 0.f ? 1.f : a.slope);
+      o[2] = dsum;
+    }
+    __syncthreads();
+    for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
+      const int64_t b = t / H;
+      const int h = (int)(t % H);
+      const int64_t i = a.src[b];
+      bool first = true;
+      for (int64_t q = 0; q < b && first; ++q) first = a.src[q] != i;
+      if (!first) continue;
+      float s = 0.f;
+      for (int64_t q = b; q < B; ++q)
+        if (a.src[q] == i) s += bgrad[(q * H + h) * 4 + 2];
+      row_coef[i * H + h] = s;
+    }
+    for (int64_t t = threadIdx.x; t < (int64_t)H * F; t += blockDim.x) {
+      const int h = (int)(t / F);
+      float s3 = 0.f, s4 = 0.f;
+      for (int64_t b = 0; b < B; ++b) {
+        const float x = a.h2[a.src[b] * D + t];
+        s3 = fmaf(bgrad[(b * H + h) * 4 + 0], x, s3);
+        s4 = fmaf(bgrad[(b * H + h) * 4 + 1], x, s4);
+      }
+      da3s[t] = s3;
+      da4s[t] = s4;
+    }
+  } else {
+    for (int64_t t = threadIdx.x; t < B * D; t += blockDim.x) {
+      const int64_t b = t / D;
+      const int d = (int)(t % D);
+      const int h = d / F;
+      const int64_t i = a.src[b];
+      bool first = true;
+      for (int64_t q = 0; q < b && first; ++q) first = a.src[q] != i;
+      if (!first) continue;
+      float s = 0.f;
+      for (int64_t q = b; q < B; ++q) {
+        if (a.src[q] != i) continue;
+        const float* st = bstat + (q * H + h) * BS_N;
+        const float* gq = bgrad + (q * H + h) * 4;
+        s += st[BS_W3] * G[(q * 2 + 0) * D + d] + st[BS_W4] * G[(q * 2 + 1) * D + d] +
+             gq[0] * a.a3s[d] + gq[1] * a.a4s[d];
+      }
+      d_hs[i * D + d] += s;
+    }
+  }
+}
+
+static int check(const msha_graph* g, const msha_groups* grp, int64_t B, const int64_t* src,
+                 int32_t heads, int32_t feat) {
+  MSHA_ARG_CHECK(g && g->rowptr && g->col && g->n_rows > 0 && g->n_cols > 0,
+                 "ours: graph CSR missing");
+  MSHA_ARG_CHECK(grp && grp->gid3 && grp->gptr3 && grp->gmem3 && grp->gid4 && grp->gptr4 &&
+                     grp->gmem4 && grp->n_nodes == g->n_rows,
+                 "ours: group CSR missing or not over the graph's rows");
+  MSHA_ARG_CHECK(B >= 0 && (B == 0 || src), "ours: batch missing");
+  MSHA_ARG_CHECK(heads > 0 && feat > 0 && heads * feat <= kMaxD, "ours: heads*feat must be <= 512");
+  return MSHA_OK;
+}
+
+static OursArgs make_args(const msha_graph* g, const msha_groups* grp, int64_t B,
+                          const int64_t* src, int32_t heads, int32_t feat, const float* h2,
+                          const float* a3s, const float* a4s, float slope, float drop_p,
+                          uint64_t seed, uint64_t offset) {
+  OursArgs a;
+  a.B = B; a.N = g->n_rows; a.M = g->n_cols; a.H = heads; a.F = feat; a.src = src;
+  a.gid3 = grp->gid3; a.gptr3 = grp->gptr3; a.gmem3 = grp->gmem3;
+  a.gid4 = grp->gid4; a.gptr4 = grp->gptr4; a.gmem4 = grp->gmem4;
+  a.h2 = h2; a.a3s = a3s; a.a4s = a4s; a.slope = slope;
+  a.dp = make_dropout(drop_p, seed, offset);
+  return a;
+}
+
+}  // namespace msha
+
+using namespace msha;
+
+extern "C" int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, int64_t B,
+                                   const int64_t* src, int32_t heads, int32_t feat,
+                                   const float* h2, const float* a3s, const float* a4s,
+                                   const float* el, const float* er, const float* lse,
+                                   const float* u_inter, float neg_slope, float drop_p,
+                                   uint64_t seed, uint64_t offset, float* bstat, float* u_out,
+                                   msha_stream_t stream) {
+  if (int rc = check(g, grp, B, src, heads, feat)) return rc;
+  MSHA_ARG_CHECK(h2 && a3s && a4s && el && er && lse && u_inter && bstat && u_out,
+                 "ours_intra_fwd: null pointer");
+  const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
+                               seed, offset);
+  hipStream_t s = (hipStream_t)stream;
+  if (B > 0)
+    hipLaunchKernelGGL(ours_prep_kernel, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
+                       g->col, g->rowflag, el, er, lse, bstat);
+  hipLaunchKernelGGL(ours_fwd_kernel, dim3(grid_for(g->n_rows, 4, 1 << 16)), dim3(256), 0, s, a,
+                     (const float*)bstat, u_inter, u_out);
+  return check_launch("ours_intra_fwd");
+}
+
+extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, int64_t B,
+                                   const int64_t* src, int32_t heads, int32_t feat,
+                                   const float* h2, const float* a3s, const float* a4s,
+                                   const float* bstat, const float* dU, int32_t stage,
+                                   float neg_slope, float drop_p, uint64_t seed,
+                                   uint64_t offset, float* G, float* bgrad, float* row_coef,
+                                   float* da3s, float* da4s, float* d_hs,
+                                   msha_stream_t stream) {
+  if (int rc = check(g, grp, B, src, heads, feat)) return rc;
+  MSHA_ARG_CHECK(stage == 0 || stage == 1, "ours_intra_bwd: stage must be 0 or 1");
+  MSHA_ARG_CHECK(h2 && a3s && a4s && bstat && G && bgrad, "ours_intra_bwd: null pointer");
+  MSHA_ARG_CHECK(stage == 1 || (dU && row_coef && da3s && da4s), "ours_intra_bwd: stage 0 outputs");
+  MSHA_ARG_CHECK(stage == 0 || d_hs, "ours_intra_bwd: stage 1 needs d_hs");
+  const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
+                               seed, offset);
+  hipStream_t s = (hipStream_t)stream;
+  if (B == 0) {
+    if (stage == 0) {
+      if (hipMemsetAsync(da3s, 0, sizeof(float) * heads * feat, s) != hipSuccess ||
+          hipMemsetAsync(da4s, 0, sizeof(float) * heads * feat, s) != hipSuccess)
+        return check_launch("ours_intra_bwd memset");
+    }
+    return MSHA_OK;
+  }
+  if (stage == 0) {
+    hipLaunchKernelGGL(ours_bwd_gather_kernel, dim3(grid_for(2 * B, 4)), dim3(256), 0, s, a, dU,
+                       G);
+    hipLaunchKernelGGL(ours_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, a, 0, bstat,
+                       (const float*)G, bgrad, row_coef, da3s, da4s, (float*)nullptr);
+  } else {
+    hipLaunchKernelGGL(ours_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, a, 1, bstat,
+                       (const float*)G, bgrad, (float*)nullptr, (float*)nullptr,
+                       (float*)nullptr, d_hs);
+  }
+  return check_launch("ours_intra_bwd");
+}

@@ -95,7 +95,8 @@ class _EdgeAttention(torch.autograd.Function):
         d_hs = torch.empty(n, H, F, device=dev, dtype=torch.float32) if use_dv else None
         _lib.call("msha_edge_attention_bwd_rows", g, H, F, el.data_ptr(), er.data_ptr(),
                   hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
-                  hs.data_ptr() if use_dv else None, _lib.ptr(dV), ctx.slope, ctx.p, ctx.seed, 0,
+                  hs.data_ptr() if use_dv else None, _lib.ptr(dV), None, ctx.slope, ctx.p,
+                  ctx.seed, 0,
                   d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), _lib.ptr(d_hs), s)
         d_hc = torch.empty(m, H, F, device=dev, dtype=torch.float32)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
@@ -401,3 +402,96 @@ def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None):
               h.data_ptr(), h.stride(0), dst.data_ptr(), W.data_ptr(), b.data_ptr(),
               ACT_BIAS | ACT_RELU | ACT_SIGMOID, 0.0, 0, 0, out.data_ptr(), s)
     return out
+
+
+# --------------------------------------------------------- full MSHA layer (Ours) ---
+class _OursAttention(torch.autograd.Function):
+    """Ours.py:54-101 core: inter attention (u, v) + batch intra attention added to u."""
+
+    @staticmethod
+    def forward(ctx, el, er, h1, h2, a3s, a4s, graph: Graph, groups, src, p: float, seed: int,
+                slope: float):
+        n, H = el.shape
+        m, _, Fd = h1.shape
+        el, er, h1, h2 = _f32c(el), _f32c(er), _f32c(h1), _f32c(h2)
+        a3s, a4s = _f32c(a3s), _f32c(a4s)
+        src = src.to(torch.int64).contiguous()
+        B = src.numel()
+        dev = el.device
+        s = _stream(el)
+        g = graph.desc
+        u_inter = torch.empty(n, H, Fd, device=dev, dtype=torch.float32)
+        lse = torch.empty(n, H, device=dev, dtype=torch.float32)
+        attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
+        _lib.call("msha_edge_attention_fwd", g, H, Fd, el.data_ptr(), er.data_ptr(),
+                  h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(), lse.data_ptr(),
+                  attd.data_ptr(), s)
+        v = torch.empty(m, H, Fd, device=dev, dtype=torch.float32)
+        _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
+        bstat = torch.empty(max(B, 1), H, 8, device=dev, dtype=torch.float32)
+        u = torch.empty_like(u_inter)
+        _lib.call("msha_ours_intra_fwd", g, groups.desc, B, src.data_ptr(), H, Fd, h2.data_ptr(),
+                  a3s.data_ptr(), a4s.data_ptr(), el.data_ptr(), er.data_ptr(), lse.data_ptr(),
+                  u_inter.data_ptr(), slope, p, seed, 0, bstat.data_ptr(), u.data_ptr(), s)
+        ctx.graph, ctx.groups, ctx.p, ctx.seed, ctx.slope = graph, groups, p, seed, slope
+        ctx.save_for_backward(el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src)
+        # post-dropout inter attention and batch statistics: outputs for record mode
+        ctx.mark_non_differentiable(attd, bstat)
+        return u, v, attd, bstat
+
+    @staticmethod
+    def backward(ctx, dU, dV, _attd=None, _bstat=None):
+        el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src = ctx.saved_tensors
+        graph, groups = ctx.graph, ctx.groups
+        n, H = el.shape
+        m, _, Fd = h1.shape
+        B = src.numel()
+        dev = el.device
+        s = _stream(el)
+        g, gr = graph.desc, groups.desc
+        dU = torch.zeros_like(u_inter) if dU is None else _f32c(dU)
+        dV = torch.zeros(m, H, Fd, device=dev) if dV is None else _f32c(dV)
+        G = torch.empty(max(B, 1), 2, H * Fd, device=dev, dtype=torch.float32)
+        bgrad = torch.empty(max(B, 1), H, 4, device=dev, dtype=torch.float32)
+        row_coef = torch.zeros(n, H, device=dev, dtype=torch.float32)
+        da3s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
+        da4s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
+        args = (g, gr, B, src.data_ptr(), H, Fd, h2.data_ptr(), a3s.data_ptr(), a4s.data_ptr(),
+                bstat.data_ptr(), dU.data_ptr())
+        _lib.call("msha_ours_intra_bwd", *args, 0, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
+                  bgrad.data_ptr(), row_coef.data_ptr(), da3s.data_ptr(), da4s.data_ptr(), None,
+                  s)
+        E = max(graph.n_edges, 1)
+        d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
+        de = torch.empty(E, H, device=dev, dtype=torch.float32)
+        attd = torch.empty(E, H, device=dev, dtype=torch.float32)
+        d_hs = torch.empty(n, H, Fd, device=dev, dtype=torch.float32)
+        _lib.call("msha_edge_attention_bwd_rows", g, H, Fd, el.data_ptr(), er.data_ptr(),
+                  h1.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), dU.data_ptr(),
+                  h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p, ctx.seed,
+                  0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), d_hs.data_ptr(), s)
+        _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
+                  bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), s)
+        d_hc = torch.empty(m, H, Fd, device=dev, dtype=torch.float32)
+        d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
+        _csc_aggregate(graph, H, Fd, attd, de, dU, d_hc, d_er, s)
+        return d_el, d_er, d_hc, d_hs, da3s, da4s, None, None, None, None, None, None
+
+
+def ours_attention(graph: Graph, groups, src, el, er, h1, h2, a3s, a4s, p: float = 0.0,
+                   training: bool = False, slope: float = NEG_SLOPE, seed: int | None = None,
+                   return_aux: bool = False):
+    """Full MSHA attention core (Ours.py:54-101): returns (u, v), u = inter + intra;
+    with return_aux also (attd (E, H) post-dropout inter attention, bstat (B, H, 8))."""
+    _lib.require_cuda(el, er, h1, h2, a3s, a4s, src)
+    H, Fd = el.shape[1], h1.shape[-1]
+    if not _lib.load().msha_edge_attention_supported(H, Fd):
+        raise NotImplementedError(f"ours_attention: (heads={H}, feat={Fd}) not compiled")
+    if H * Fd > 512:
+        raise NotImplementedError("ours_attention: heads*feat must be <= 512")
+    p = float(p) if training else 0.0
+    if seed is None:
+        seed = new_seed() if p > 0 else 0
+    u, v, attd, bstat = _OursAttention.apply(el, er, h1, h2, a3s, a4s, graph, groups, src, p,
+                                             seed, slope)
+    return (u, v, attd, bstat) if return_aux else (u, v)

@@ -195,3 +195,64 @@ def normalize_adjacency_matrix(adjacency_matrix: torch.Tensor) -> torch.Tensor:
     _lib.call("msha_normalize_adjacency", a.data_ptr(), n, m, out.data_ptr(), ws.data_ptr(),
               _lib.stream_handle(a.device))
     return out
+
+
+# ----------------------------------------------------------- group adjacency ---
+class Groups:
+    """City + province membership of the N source nodes as CSR (struct msha_groups).
+
+    The reference passes same-group masks as dense N x N matrices
+    (dataset.py:260-277); here a node's group is an id and each group a sorted
+    member list, built once (host) and kept on the device."""
+
+    def __init__(self, city_ids, prov_ids, device):
+        self.n = int(len(city_ids))
+        self.device = torch.device(device)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=self.device)  # noqa
+        self._keep = []
+        for ids in (city_ids, prov_ids):
+            ids = np.asarray(ids.cpu() if torch.is_tensor(ids) else ids, np.int64)
+            _, gid = np.unique(ids, return_inverse=True)
+            order = np.argsort(gid, kind="stable")
+            gptr = np.zeros(gid.max() + 2 if len(gid) else 1, np.int64)
+            np.cumsum(np.bincount(gid, minlength=len(gptr) - 1), out=gptr[1:])
+            self._keep.append((t(gid), t(gptr), t(order)))
+        self._desc = None
+
+    @property
+    def desc(self) -> _lib.MshaGroups:
+        if self._desc is None:
+            d = _lib.MshaGroups()
+            d.n_nodes = self.n
+            (g3, p3, m3), (g4, p4, m4) = self._keep
+            d.gid3, d.gptr3, d.gmem3 = g3.data_ptr(), p3.data_ptr(), m3.data_ptr()
+            d.gid4, d.gptr4, d.gmem4 = g4.data_ptr(), p4.data_ptr(), m4.data_ptr()
+            self._desc = d
+        return self._desc
+
+
+def _group_ids(adj):
+    """Group id per node from a GroupAdjacency or a dense same-group mask (the id of a
+    node is the first member of its row: rows of one group are identical)."""
+    if hasattr(adj, "ids"):
+        return adj.ids
+    a = adj.detach()
+    if a.dim() != 2 or a.shape[0] != a.shape[1]:
+        raise ValueError("group adjacency must be square (N, N) or a GroupAdjacency")
+    return (a > 0).to(torch.int8).argmax(dim=1)
+
+
+_GROUP_CACHE: dict = {}
+
+
+def groups_for(city_adj, province_adj, device) -> Groups:
+    key = (id(city_adj), id(province_adj), str(device))
+    hit = _GROUP_CACHE.get(key)
+    if hit is not None and hit[0]() is city_adj and hit[1]() is province_adj:
+        return hit[2]
+    g = Groups(_group_ids(city_adj), _group_ids(province_adj), device)
+    try:
+        _GROUP_CACHE[key] = (weakref.ref(city_adj), weakref.ref(province_adj), g)
+    except TypeError:  # objects without weakref support: no caching
+        pass
+    return g

@@ -10,6 +10,7 @@ and RNG consumption order as the reference, so a model built after
   OursLayer3            Ablation.py:235-277
   ablation3             Ablation.py:279-301  (its heads run as ONE multi-head launch)
   LinkPredictor         LLP.py:86-115
+  OursLayer, Ours       Ours.py:29-167 (full MSHA: inter + city/province attention)
 
 Adjacency arguments may be dense (N, M) tensors (as in train.py; the CSR/CSC view
 is built once on the GPU and cached) or prebuilt ``Graph`` objects.  Every
@@ -22,7 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as MF
-from .graph import Graph, graph_for
+from .graph import Graph, graph_for, groups_for
 
 ALPHA = 0.2  # LeakyReLU slope of the reference layers (Ablation.py:241, :267)
 
@@ -239,3 +240,97 @@ class LinkPredictor(torch.nn.Module):
         if len(self.lins) != 2:
             return self.forward(h[src], h[dst])
         return MF.score_pairs(h, src, dst, "mlp", self.lins[0].weight, self.lins[0].bias)
+
+
+class OursLayer(OursLayer3):
+    """Ours.py:29-109: OursLayer3's inter attention plus the intra-source attention
+    of the batch ``source_index`` over its city / province groups (joint normaliser
+    SUM_county).  city_adj / province_adj: dense same-group masks (as the reference)
+    or ``data.GroupAdjacency``."""
+
+    def forward(self, Sinput, Rinput, inter_adj, city_adj, province_adj, source_index,
+                record=False, Coeff12=None, Coeff3=None, Coeff4=None):
+        return fused_ours_layer([self], Sinput, Rinput, _graph(inter_adj), city_adj,
+                                province_adj, source_index, self.training, record, Coeff12,
+                                Coeff3, Coeff4)[0]
+
+
+def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_adj,
+                     source_index, training, record=False, Coeff12=None, Coeff3=None,
+                     Coeff4=None):
+    H = len(heads)
+    Fd = heads[0].out_features
+    n, m = s_input.shape[0], r_input.shape[0]
+    if graph.n_cols != m or graph.n_rows != n:
+        raise ValueError(f"inter_adj is {graph.n_rows}x{graph.n_cols}, features are {n} "
+                         f"sources x {m} recipients")
+    groups = groups_for(city_adj, province_adj, s_input.device)
+    W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
+    W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
+    a = torch.stack([h.a.view(-1) for h in heads])
+    a3 = torch.stack([h.a3.view(-1) for h in heads])
+    a4 = torch.stack([h.a4.view(-1) for h in heads])
+    h1, er = MF.project_scores(r_input, W1, ar=a[:, :Fd], heads=H)
+    h2, el = MF.project_scores(s_input, W2, al=a[:, Fd:], heads=H)
+    # e3 = lrelu(cat(h2_b, h2_b) @ a3) = lrelu(h2_b . (a3[:F] + a3[F:]))  (Ours.py:74-75)
+    a3s = a3[:, :Fd] + a3[:, Fd:]
+    a4s = a4[:, :Fd] + a4[:, Fd:]
+    src = torch.as_tensor(source_index, device=s_input.device)
+    u, v, attd, bstat = MF.ours_attention(graph, groups, src, el, er, h1.view(m, H, Fd),
+                                          h2.view(n, H, Fd), a3s, a4s, p=heads[0].dropout,
+                                          training=training, return_aux=True)
+    if record:
+        _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4)
+    return [head.epilogue(u[:, k], v[:, k]) for k, head in enumerate(heads)]
+
+
+def _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4):
+    """Ours.py:92-96 attention dump for Explainer (record=True): the last head's
+    post-dropout inter attention (dense N x M) into Coeff12 and its intra rows into
+    Coeff3[source_index] / Coeff4[source_index] (each head overwrites, as in the
+    reference).  Off the hot path (torch scatter); dropout-free values (Record()
+    runs in eval mode, train.py:284-291)."""
+    H = len(heads)
+    dev = attd.device
+    rows = torch.repeat_interleave(torch.arange(graph.n_rows, device=dev), graph.deg().long())
+    dense = torch.zeros(graph.n_rows, graph.n_cols, device=dev)
+    dense[rows, graph.col.long()] = attd[: graph.n_edges, H - 1]
+    if Coeff12 is not None:
+        Coeff12.copy_(dense.to(Coeff12.dtype))
+    (g3, _, _), (g4, _, _) = groups._keep
+    for Cf, gid, col in ((Coeff3, g3, 5), (Coeff4, g4, 6)):
+        if Cf is None:
+            continue
+        same = (gid[src.long()][:, None] == gid[None, :]).to(Cf.dtype)
+        Cf[src.long()] = same * bstat[: src.numel(), H - 1, col][:, None].to(Cf.dtype)
+
+
+class Ours(nn.Module):
+    """Ours.py:144-167: n_heads OursLayer (one fused launch set) -> cat -> dropout ->
+    GAL -> elu -> log_softmax."""
+
+    def __init__(self, in_features, out_features, n_classes, n_heads, dropout, gdp, Scount,
+                 Rcount):
+        super().__init__()
+        self.Sfeatures = _features_with_gdp(Scount, in_features, gdp)
+        self.Rfeatures = nn.Parameter(torch.rand([Rcount, in_features]))
+        self.n_classes = n_classes
+        self.n_heads = n_heads
+        self.dropout = dropout
+        self.attentions = [OursLayer(in_features, out_features, dropout=dropout)
+                           for _ in range(n_heads)]
+        for i, attention in enumerate(self.attentions):
+            self.add_module(f"attention_{i}", attention)
+        self.out_att = GraphAttentionLayer(n_classes * n_heads, n_classes, dropout=dropout)
+
+    def forward(self, inter_adj, city_adj, province_adj, source_index, record=False,
+                Coeff12=None, Coeff3=None, Coeff4=None):
+        g = _graph(inter_adj)
+        s_input = F.dropout(self.Sfeatures, self.dropout, training=self.training)
+        r_input = F.dropout(self.Rfeatures, self.dropout, training=self.training)
+        x = torch.cat(fused_ours_layer(self.attentions, s_input, r_input, g, city_adj,
+                                       province_adj, source_index, self.training, record,
+                                       Coeff12, Coeff3, Coeff4), dim=1)
+        x = F.dropout(x, self.dropout, training=self.training)
+        x = F.elu(self.out_att(x, g))
+        return F.log_softmax(x, dim=1)

@@ -359,3 +359,69 @@ def link_predict_bwd(x_i, x_j, mode, lins, dout):
     dz = dr * (z > 0)
     dx = dz @ W
     return dict(dx_i=dx * x_j, dx_j=dx * x_i, dW=dz.T @ x, db=dz.sum(axis=0))
+
+
+# ----------------------------------------------------------------------------------
+# Ours.OursLayer (full MSHA: inter + city/province intra attention), Ours.py:54-109
+# ----------------------------------------------------------------------------------
+def ours_intra(h2, a3, a4, src, city, prov, attd_rows, n_cols, keep3=None, keep4=None, p=0.0,
+               slope=NEG_SLOPE):
+    """Intra-source attention of a batch (Ours.py:71-99), one head.
+
+    e3_b = lrelu(h2_b . (a3[:F] + a3[F:])) is constant along n (Ours.py:74-75 concatenate
+    h2_b with itself); the mask is "same city" (Ours.py:81).  SUM_b (Ours.py:84-86) adds,
+    WITHOUT max subtraction, exp of the masked scores and exp of the batch row's
+    post-dropout inter attention over ALL n_cols columns (non-edges give exp(0) = 1).
+    attd_rows: (B, n_cols) dense post-dropout inter attention of rows src.
+    Returns dict(intra (N,F), w3, w4, SUM, pre3, pre4)."""
+    dt = h2.dtype
+    F = h2.shape[1]
+    a3 = a3.reshape(-1)
+    a4 = a4.reshape(-1)
+    hb = h2[np.asarray(src, np.int64)]
+    pre3 = hb @ (a3[:F] + a3[F:]) if False else hb @ a3[:F] + hb @ a3[F:]
+    pre4 = hb @ a4[:F] + hb @ a4[F:]
+    E3, E4 = np.exp(lrelu(pre3, slope)), np.exp(lrelu(pre4, slope))
+    m3 = (np.asarray(city)[np.asarray(src)][:, None] == np.asarray(city)[None, :]).astype(dt)
+    m4 = (np.asarray(prov)[np.asarray(src)][:, None] == np.asarray(prov)[None, :]).astype(dt)
+    SUM = m3.sum(1) * E3 + m4.sum(1) * E4 + np.exp(attd_rows).sum(1)
+    att3 = m3 * (E3 / SUM)[:, None]
+    att4 = m4 * (E4 / SUM)[:, None]
+    if keep3 is not None:
+        s = np.asarray(1.0 / (1.0 - p), dt)
+        att3 = att3 * keep3 * s
+        att4 = att4 * keep4 * s
+    intra = att3.T @ hb + att4.T @ hb
+    return dict(intra=intra, w3=E3 / SUM, w4=E4 / SUM, SUM=SUM, pre3=pre3, pre4=pre4,
+                att3=att3, att4=att4)
+
+
+def ours_layer_fwd(S, R, p, rowptr, col, city, prov, src, training, rowflag=None,
+                   slope=NEG_SLOPE):
+    """OursLayer.forward restated (Ours.py:54-109) with dropout off."""
+    h1 = R @ p["W1"]
+    h2 = S @ p["W2"]
+    F = h1.shape[1]
+    a = p["a"].reshape(-1)
+    er = (h1 @ a[:F])[:, None]
+    el = (h2 @ a[F:])[:, None]
+    m_cols = h1.shape[0]
+    fw = edge_aggregate_fwd(rowptr, col, el, er, h1[:, None, :], hs=h2[:, None, :],
+                            slope=slope, rowflag=rowflag)
+    rows = edge_rows(rowptr)
+    dense = np.zeros((len(rowptr) - 1, m_cols), h1.dtype)
+    dense[rows, np.asarray(col, np.int64)] = fw["attd"][:, 0]
+    it = ours_intra(h2, p["a3"], p["a4"], src, city, prov, dense[np.asarray(src)], m_cols,
+                    slope=slope)
+    u_pre = fw["u"][:, 0, :] + it["intra"]
+    v_pre = fw["v"][:, 0, :]
+    if training:
+        v = batchnorm_train(v_pre, p["bn1_weight"], p["bn1_bias"])
+        u = batchnorm_train(u_pre, p["bn2_weight"], p["bn2_bias"])
+    else:
+        v = batchnorm_eval(v_pre, p["bn1_weight"], p["bn1_bias"], p["bn1_running_mean"],
+                           p["bn1_running_var"])
+        u = batchnorm_eval(u_pre, p["bn2_weight"], p["bn2_bias"], p["bn2_running_mean"],
+                           p["bn2_running_var"])
+    out = elu(lrelu(u, slope) @ lrelu(v, slope).T)
+    return dict(out=out, u_pre=u_pre, v_pre=v_pre, intra=it)

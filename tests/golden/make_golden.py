@@ -389,41 +389,52 @@ def make_edge_cases():
 
 
 def make_ours_small(g):
-    """Ours.OursLayer on 64 sources of 2015 (city/province groups restricted)."""
+    """Ours.OursLayer on 64 sources of 2015 (city/province groups restricted):
+    case A fp32 as the reference runs it; case B fp64 with a repeated source in the
+    batch and one source row without flows (uniform inter attention)."""
     O = extract(os.path.join(REF, "Ours.py"), {"OursLayer"})["OursLayer"]
     rows = np.arange(64)
-    counts = g["counts"][torch.as_tensor(rows)]
+    counts = g["counts"][torch.as_tensor(rows)].clone()
     keepc = (counts > 0).sum(0) > 0
     counts = counts[:, keepc]
     city = g["city"][rows]
     prov = g["prov"][rows]
-    city_adj = torch.as_tensor((city[:, None] == city[None, :]).astype(np.float32))
-    prov_adj = torch.as_tensor((prov[:, None] == prov[None, :]).astype(np.float32))
-    inter = refmodel.normalize_adjacency_matrix(counts)
-    city_n = refmodel.normalize_adjacency_matrix(city_adj)
-    prov_n = refmodel.normalize_adjacency_matrix(prov_adj)
-    torch.manual_seed(10)
-    layer = O(16, 8, 0.0)
     res = dict(counts=counts.numpy(), city=city, prov=prov)
-    for k, v in layer.state_dict().items():
-        res[f"init.{k}"] = v.numpy()
-    gg = torch.Generator().manual_seed(11)
-    S = torch.rand(64, 16, generator=gg).requires_grad_(True)
-    R = torch.rand(counts.shape[1], 16, generator=gg).requires_grad_(True)
-    si = torch.randperm(64, generator=gg)[:16]
-    res["S"], res["R"], res["source_index"] = S.detach().numpy(), R.detach().numpy(), si.numpy()
-    layer.train()
-    y = layer(S, R, inter, city_n, prov_n, si, False)
-    w = torch.randn(y.shape, generator=gg)
-    (y * w).sum().backward()
-    res["out"], res["dout"] = np32(y), w.numpy()
-    res["grad.S"], res["grad.R"] = np32(S.grad), np32(R.grad)
-    for k, p in layer.named_parameters():
-        if p.grad is not None:
-            res[f"grad.{k}"] = np32(p.grad)
-    layer.eval()
-    with torch.no_grad():
-        res["out_eval"] = np32(layer(S, R, inter, city_n, prov_n, si, False))
+    for tag, dt, si_fix, empty_row in (("", torch.float32, None, None),
+                                       ("B.", torch.float64, [5, 17, 5, 40, 33, 5, 60, 12], 33)):
+        c = counts.clone()
+        if empty_row is not None:
+            c[empty_row] = 0
+            res[tag + "counts"] = c.numpy()
+        city_adj = torch.as_tensor((city[:, None] == city[None, :]).astype(np.float32))
+        prov_adj = torch.as_tensor((prov[:, None] == prov[None, :]).astype(np.float32))
+        inter = refmodel.normalize_adjacency_matrix(c).to(dt)
+        city_n = refmodel.normalize_adjacency_matrix(city_adj).to(dt)
+        prov_n = refmodel.normalize_adjacency_matrix(prov_adj).to(dt)
+        torch.manual_seed(10)
+        layer = O(16, 8, 0.0)
+        if tag == "":
+            for k, v in layer.state_dict().items():
+                res[f"init.{k}"] = v.numpy().copy()
+        layer = layer.to(dt)
+        gg = torch.Generator().manual_seed(11)
+        S = torch.rand(64, 16, generator=gg, dtype=torch.float64).to(dt).requires_grad_(True)
+        R = torch.rand(c.shape[1], 16, generator=gg, dtype=torch.float64).to(dt).requires_grad_(True)
+        si = torch.randperm(64, generator=gg)[:16] if si_fix is None else torch.as_tensor(si_fix)
+        res[tag + "S"], res[tag + "R"] = S.detach().numpy(), R.detach().numpy()
+        res[tag + "source_index"] = si.numpy()
+        layer.eval()  # before the train forward: BN running stats still at init
+        with torch.no_grad():
+            res[tag + "out_eval"] = layer(S, R, inter, city_n, prov_n, si, False).numpy()
+        layer.train()
+        y = layer(S, R, inter, city_n, prov_n, si, False)
+        w = torch.randn(y.shape, generator=gg, dtype=torch.float64).to(dt)
+        (y * w).sum().backward()
+        res[tag + "out"], res[tag + "dout"] = y.detach().numpy(), w.numpy()
+        res[tag + "grad.S"], res[tag + "grad.R"] = S.grad.numpy(), R.grad.numpy()
+        for k, p in layer.named_parameters():
+            if p.grad is not None:
+                res[f"{tag}grad.{k}"] = p.grad.numpy()
     np.savez_compressed(os.path.join(OUT, "ours_small.npz"), **res)
 
 

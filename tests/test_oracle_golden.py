@@ -194,3 +194,25 @@ def test_edge_aggregate_bwd_matches_autograd():
     ((u * torch.tensor(dU)).sum() + (v * torch.tensor(dV)).sum()).backward()
     for name, ref in zip(("d_el", "d_er", "d_hc", "d_hs"), t):
         np.testing.assert_allclose(bw[name], ref.grad.numpy(), rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("tag,tol", [("", 2e-4), ("B.", 1e-9)])
+def test_ours_layer_forward(tag, tol):
+    """Full MSHA layer (Ours.py:54-109): inter + same-city / same-province attention."""
+    z = golden("ours_small.npz")
+    dt = np.float64 if tag else np.float32
+    counts = z[tag + "counts"] if tag + "counts" in z.files else z["counts"]
+    mask = counts > 0
+    empty = ~mask.any(1)
+    mask[empty] = True
+    rowptr, col = O.dense_to_csr(mask.astype(np.float32))
+    p = {k: z[f"init.{k}"].astype(dt) for k in ("W1", "W2", "a", "a3", "a4")}
+    for bn in ("bn1", "bn2"):
+        for k in ("weight", "bias", "running_mean", "running_var"):
+            p[f"{bn}_{k}"] = z[f"init.{bn}.{k}"].astype(dt)
+    S, R, src = z[tag + "S"].astype(dt), z[tag + "R"].astype(dt), z[tag + "source_index"]
+    for training, key in ((True, "out"), (False, "out_eval")):
+        r = O.ours_layer_fwd(S, R, p, rowptr, col, z["city"], z["prov"], src, training,
+                             rowflag=empty)
+        ref = z[tag + key]
+        np.testing.assert_allclose(r["out"], ref, rtol=tol, atol=tol * np.abs(ref).max())
