@@ -168,37 +168,61 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
     return res
 
 
-def r15_train_step(dev, steps=20, warmup=5):
-    """configs[1] at the shipped 2015 graph: one train.py iteration (train.py:221-232)
-    of ablation3(in 128, F 64, 2 heads, dropout 0.5) with Adam(lr 1e-3, wd 5e-4):
-    full-graph forward, nll on a 64-flow batch, backward, optimizer step."""
+def _year_graph(year):
+    """(N, M, flows (F, 2), city ids, prov ids, gdp) of a shipped year; 2016-2018 flows
+    are synthesised with the 2015 degree law (seed = year)."""
+    import msha_loader
+
+    msha_loader.load()
+    from msha_gnn_amd.data import synthetic_flows
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    yz = np.load(os.path.join(ROOT, "tests", "golden", "years.npz"))
+    n, m = int(yz[f"{year}.n"]), int(yz[f"{year}.m"])
+    rows15 = np.repeat(np.arange(int(z["n"])), np.diff(z["rowptr"]))
+    col15 = z["col"].astype(np.int64)
+    if year == "2015":
+        cnt = z["cnt"].astype(np.int64)
+        flows = np.stack([np.repeat(rows15, cnt), np.repeat(col15, cnt)], 1)
+    else:
+        deg_hist = np.bincount(np.diff(z["rowptr"]))
+        col_w = np.bincount(col15, minlength=m).astype(np.float64)
+        flows = synthetic_flows(n, m, deg_hist, col_w, seed=int(year))
+    return n, m, flows, yz[f"{year}.city"].astype(np.int64), yz[f"{year}.prov"].astype(
+        np.int64), yz[f"{year}.gdp"]
+
+
+def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5):
+    """configs[1]: one train.py iteration (train.py:221-232) on a shipped year's graph:
+    full-graph forward of the model (in 128, F 64, 2 heads, dropout 0.5), nll on a
+    64-flow batch, backward, Adam(lr 1e-3, wd 5e-4) step.  model_kind: 'Ours' (full
+    MSHA, Ours.py) or 'ablation3' (the model train.py:206 builds)."""
     import msha_loader
 
     msha = msha_loader.load()
     from msha_gnn_amd import layers
+    from msha_gnn_amd.data import GroupAdjacency
 
-    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
-    n, m = int(z["n"]), int(z["m"])
-    rows = np.repeat(np.arange(n), np.diff(z["rowptr"]))
-    counts = torch.zeros(n, m)
-    counts[torch.as_tensor(rows), torch.as_tensor(z["col"].astype(np.int64))] = torch.as_tensor(
-        z["cnt"].astype(np.float32))
-    adj = msha.normalize_adjacency_matrix(counts.to(dev))
-    gdp = {i: float(x) for i, x in enumerate(z["gdp"])}
+    n, m, flows, city, prov, gdp_arr = _year_graph(year)
+    src_t = torch.as_tensor(flows[:, 0], device=dev)
+    dst_t = torch.as_tensor(flows[:, 1], device=dev)
+    adj = msha.normalize_adjacency_matrix(msha.inter_adjacency(src_t, dst_t, n, m))
+    cadj = GroupAdjacency(torch.as_tensor(city, device=dev))
+    padj = GroupAdjacency(torch.as_tensor(prov, device=dev))
+    gdp = {i: float(x) for i, x in enumerate(gdp_arr)}
     torch.manual_seed(0)
-    model = layers.ablation3(128, 64, m, 2, 0.5, gdp, n, m).to(dev)
+    cls = layers.Ours if model_kind == "Ours" else layers.ablation3
+    model = cls(128, 64, m, 2, 0.5, gdp, n, m).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
     g = torch.Generator().manual_seed(0)
-    flows_src = torch.as_tensor(np.repeat(rows, z["cnt"].astype(np.int64)))
-    flows_dst = torch.as_tensor(np.repeat(z["col"].astype(np.int64), z["cnt"].astype(np.int64)))
-    batches = [torch.randint(0, len(flows_src), (64,), generator=g) for _ in range(8)]
-    batches = [(flows_src[b].to(dev), flows_dst[b].to(dev)) for b in batches]
+    picks = [torch.randint(0, len(flows), (64,), generator=g).to(dev) for _ in range(8)]
+    batches = [(src_t[b], dst_t[b]) for b in picks]
     model.train()
 
     def one(k):
         si, ri = batches[k % len(batches)]
         opt.zero_grad()
-        out = model(adj, None, None, si)
+        out = model(adj, cadj, padj, si)
         loss = torch.nn.functional.nll_loss(out[si], ri)
         loss.backward()
         opt.step()
@@ -212,11 +236,12 @@ def r15_train_step(dev, steps=20, warmup=5):
         loss = one(k)
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
-    e = int(z["rowptr"][-1])
-    return dict(workload="ablation3 train step, 2015 graph (N 39179, M 32, E 91283), in 128, "
-                         "F 64, 2 heads, dropout 0.5, Adam", ms_per_step=dt * 1e3,
-                edges_per_sec=e / dt, loss=float(loss),
-                reference_cpu_s_per_step="1.01-1.27 (BASELINE.md, 8-core container, not this box)")
+    from msha_gnn_amd.graph import graph_for
+
+    e = graph_for(adj).n_edges
+    return dict(model=model_kind, year=year, nodes=n, recipients=m, edges=e,
+                flows="shipped" if year == "2015" else "synthetic (2015 degree law)",
+                ms_per_step=dt * 1e3, edges_per_sec=e / dt, loss=float(loss.detach()))
 
 
 def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
@@ -342,7 +367,13 @@ def main():
     if link is not None:
         out["link_score"] = link
     if world == 1 and not args.no_r15:
-        out["r15_train_step"] = r15_train_step(dev)
+        out["train_step_configs1"] = {
+            "workload": "train.py iteration: full-graph fwd + nll(64 flows) + bwd + Adam; "
+                        "in 128, F 64, 2 heads, dropout 0.5, fp32",
+            "reference_cpu_s_per_step": "ablation3 @2015: 1.01-1.27 (BASELINE.md, 8-core "
+                                        "container CPU; not this box)",
+            "runs": [train_step_leg(dev, y, "Ours") for y in ("2015", "2016", "2017", "2018")]
+            + [train_step_leg(dev, "2015", "ablation3")]}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
     print(json.dumps(out), flush=True)

@@ -87,6 +87,7 @@ typedef struct msha_groups {
   const int32_t* gid4;  /* province */
   const int32_t* gptr4;
   const int32_t* gmem4;
+  int64_t max_group; /* largest group (either kind): sizes the backward's chunking */
 } msha_groups;
 
 MSHA_API int msha_abi_version(void);
@@ -212,6 +213,14 @@ MSHA_API int msha_add_head_outer(int64_t rows, int32_t heads, int32_t feat, cons
                                  const float* de, const float* a, const float* de2,
                                  const float* a2, float* out, msha_stream_t stream);
 
+/* Gradient of the score vectors of msha_project_scores (el = h . al):
+ * out1[h, f] = sum_r s1[r, h] h[r, h, f] (and out2 with s2); deterministic row-block
+ * partials.  Workspace: msha_head_colsum_workspace_size(rows, heads, feat). */
+MSHA_API size_t msha_head_colsum_workspace_size(int64_t rows, int32_t heads, int32_t feat);
+MSHA_API int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, const float* s1,
+                              const float* s2, const float* T, float* out1, float* out2,
+                              void* ws, size_t ws_bytes, msha_stream_t stream);
+
 /* ----------------------------------------------------------- link scoring --- */
 /* LLP.py:104-115 LinkPredictor with the caller's gather (LLP.py:233) fused:
  * x_i = G[gi[b]], x_j = G2[gj[b]] (gi / gj NULL: row b).
@@ -262,14 +271,18 @@ MSHA_API int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, in
  *            row_coef (n_rows, heads; zero-filled by the caller) = dL/dSUM per batch row;
  *            da3s, da4s (heads, feat).
  *   stage 1: d_hs[src_b] += the intra gradient of h2's batch rows.
- * Per-row sums follow batch order (deterministic). */
+ * Per-row sums follow batch order (deterministic).  Stage 0 needs a workspace of
+ * msha_ours_workspace_size(grp, B, heads, feat) bytes (chunked group sums). */
+MSHA_API size_t msha_ours_workspace_size(const msha_groups* grp, int64_t B, int32_t heads,
+                                         int32_t feat);
 MSHA_API int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, int64_t B,
                                  const int64_t* src, int32_t heads, int32_t feat,
                                  const float* h2, const float* a3s, const float* a4s,
                                  const float* bstat, const float* dU, int32_t stage,
                                  float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
                                  float* G, float* bgrad, float* row_coef, float* da3s,
-                                 float* da4s, float* d_hs, msha_stream_t stream);
+                                 float* da4s, float* d_hs, void* ws, size_t ws_bytes,
+                                 msha_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,8 @@ class MshaGroups(C.Structure):
 
     _fields_ = [("n_nodes", C.c_int64),
                 ("gid3", C.c_void_p), ("gptr3", C.c_void_p), ("gmem3", C.c_void_p),
-                ("gid4", C.c_void_p), ("gptr4", C.c_void_p), ("gmem4", C.c_void_p)]
+                ("gid4", C.c_void_p), ("gptr4", C.c_void_p), ("gmem4", C.c_void_p),
+                ("max_group", C.c_int64)]
 
 
 GRP = C.POINTER(MshaGroups)
@@ -73,6 +74,8 @@ SIGNATURES = {
                                 P]),
     "msha_project_scores": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
     "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
+    "msha_head_colsum_workspace_size": (SZ, [I64, I32, I32]),
+    "msha_head_colsum": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, SZ, P]),
     "msha_pair_linear": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64, U64,
                                    P, P]),
     "msha_pair_inner_fwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
@@ -81,8 +84,9 @@ SIGNATURES = {
     "msha_pair_hadamard": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P]),
     "msha_ours_intra_fwd": (C.c_int, [GP, GRP, I64, P, I32, I32, P, P, P, P, P, P, P, F32, F32,
                                       U64, U64, P, P, P]),
+    "msha_ours_workspace_size": (SZ, [GRP, I64, I32, I32]),
     "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, P, P, P, P, P, I32, F32, F32,
-                                      U64, U64, P, P, P, P, P, P, P]),
+                                      U64, U64, P, P, P, P, P, P, P, SZ, P]),
 }
 
 _lib = None

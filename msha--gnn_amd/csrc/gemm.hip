@@ -439,6 +439,97 @@ static bool vec_ok(const GemmArgs& p) {
   return a_ok && b_ok;
 }
 
+// Gradient of the score vectors of msha_project_scores:
+//   out1[h, f] = sum_r s1[r, h] * T[r, h*F + f]   (and out2 with s2)
+// A block covers kColsumRows rows: its threads are (row group, float4 column quad),
+// each row group strides the block's rows with 16-byte loads; the row groups are
+// added in a fixed LDS tree, and a second pass adds the block partials in block
+// order (deterministic).
+constexpr int kColsumRows = 512;
+
+template <int VEC>
+struct ColVec;
+template <>
+struct ColVec<4> {
+  using T = float4;
+  static __device__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ T fma(float a, T x, T c) { return f4_fma(a, x, c); }
+  static __device__ T add(T a, T b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+};
+template <>
+struct ColVec<1> {
+  using T = float;
+  static __device__ T zero() { return 0.f; }
+  static __device__ T fma(float a, T x, T c) { return fmaf(a, x, c); }
+  static __device__ T add(T a, T b) { return a + b; }
+};
+
+// grid (row blocks, column tiles of <= 256 vectors); D % VEC == 0
+template <int VEC>
+__global__ void __launch_bounds__(256) head_colsum_partial_kernel(
+    int64_t rows, int H, int F, const float* __restrict__ s1, const float* __restrict__ s2,
+    const float* __restrict__ T, float* __restrict__ part) {
+  using V = ColVec<VEC>;
+  using VT = typename V::T;
+  __shared__ VT red[2 * 256];
+  const int D = H * F, QD = D / VEC;
+  const int QT = QD < 256 ? QD : 256;  // vectors per column tile
+  const int RG = 256 / QT;             // row groups
+  const int qi = threadIdx.x % QT, rg = threadIdx.x / QT;
+  const int q = blockIdx.y * QT + qi;
+  const bool live = rg < RG && q < QD;
+  const int h = live ? (VEC * q) / F : 0;
+  const int64_t r0 = (int64_t)blockIdx.x * kColsumRows;
+  const int64_t r1 = min(rows, r0 + kColsumRows);
+  VT a1 = V::zero(), a2 = V::zero();
+  if (live) {
+#pragma unroll 4
+    for (int64_t r = r0 + rg; r < r1; r += RG) {
+      const VT x = reinterpret_cast<const VT*>(T + r * D)[q];
+      a1 = V::fma(s1[r * H + h], x, a1);
+      if (s2) a2 = V::fma(s2[r * H + h], x, a2);
+    }
+  }
+  red[threadIdx.x] = a1;
+  red[256 + threadIdx.x] = a2;
+  __syncthreads();
+  int w = 1;
+  while (w < RG) w <<= 1;
+  for (w >>= 1; w >= 1; w >>= 1) {  // fixed-order tree over the row groups
+    if (rg < w && rg + w < RG) {
+      const int i = rg * QT + qi, j = (rg + w) * QT + qi;
+      red[i] = V::add(red[i], red[j]);
+      red[256 + i] = V::add(red[256 + i], red[256 + j]);
+    }
+    __syncthreads();
+  }
+  if (rg == 0 && q < QD) {
+    reinterpret_cast<VT*>(part + ((int64_t)blockIdx.x * 2 + 0) * D)[q] = red[qi];
+    reinterpret_cast<VT*>(part + ((int64_t)blockIdx.x * 2 + 1) * D)[q] = red[256 + qi];
+  }
+}
+
+__global__ void __launch_bounds__(256) head_colsum_reduce_kernel(int nblk, int D,
+                                                                 const float* __restrict__ part,
+                                                                 float* __restrict__ out1,
+                                                                 float* __restrict__ out2) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * D) return;
+  const int which = t / D, d = t % D;
+  float* out = which == 0 ? out1 : out2;
+  if (out == nullptr) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = 0;
+  for (; b + 4 <= nblk; b += 4) {
+    s0 += part[((int64_t)(b + 0) * 2 + which) * D + d];
+    s1 += part[((int64_t)(b + 1) * 2 + which) * D + d];
+    s2 += part[((int64_t)(b + 2) * 2 + which) * D + d];
+    s3 += part[((int64_t)(b + 3) * 2 + which) * D + d];
+  }
+  for (; b < nblk; ++b) s0 += part[((int64_t)b * 2 + which) * D + d];
+  out[d] = (s0 + s1) + (s2 + s3);
+}
+
 template <int AMODE, int EPI, int FEPI>
 static void launch(const GemmArgs& p, int splits, hipStream_t s) {
   dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)splits);
@@ -583,4 +674,35 @@ extern "C" int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const flo
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
   launch<A_GATHER_HADAMARD, EPI_ACT, 0>(p, 1, (hipStream_t)stream);
   return check_launch("pair_linear");
+}
+
+extern "C" size_t msha_head_colsum_workspace_size(int64_t rows, int32_t heads, int32_t feat) {
+  if (rows <= 0 || heads <= 0 || feat <= 0) return 0;
+  const int64_t nblk = (rows + kColsumRows - 1) / kColsumRows;
+  return (size_t)nblk * 2 * (size_t)heads * (size_t)feat * sizeof(float);
+}
+
+extern "C" int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, const float* s1,
+                                const float* s2, const float* T, float* out1, float* out2,
+                                void* ws, size_t ws_bytes, msha_stream_t stream) {
+  MSHA_ARG_CHECK(rows > 0 && heads > 0 && feat > 0, "head_colsum: bad sizes");
+  MSHA_ARG_CHECK(s1 && T && out1 && ((s2 == nullptr) == (out2 == nullptr)),
+                 "head_colsum: null pointer");
+  MSHA_ARG_CHECK(ws && ws_bytes >= msha_head_colsum_workspace_size(rows, heads, feat),
+                 "head_colsum: workspace too small");
+  const int D = heads * feat;
+  const int nblk = (int)((rows + kColsumRows - 1) / kColsumRows);
+  hipStream_t s = (hipStream_t)stream;
+  const bool v4 = feat % 4 == 0 && ((uintptr_t)T & 15) == 0;
+  const int QD = v4 ? D / 4 : D;
+  const dim3 grid(nblk, (QD + 255) / 256);
+  if (v4)
+    hipLaunchKernelGGL(head_colsum_partial_kernel<4>, grid, dim3(256), 0, s, rows, (int)heads,
+                       (int)feat, s1, s2, T, (float*)ws);
+  else
+    hipLaunchKernelGGL(head_colsum_partial_kernel<1>, grid, dim3(256), 0, s, rows, (int)heads,
+                       (int)feat, s1, s2, T, (float*)ws);
+  hipLaunchKernelGGL(head_colsum_reduce_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, nblk,
+                     D, (const float*)ws, out1, out2);
+  return check_launch("head_colsum");
 }

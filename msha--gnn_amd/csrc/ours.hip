@@ -143,21 +143,28 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 }
 
 // ----------------------------------------------------------- backward: gather ---
-// G[b, kind] = sum_{n in group(kind, src_b)} drop(kind, b, n) * dU[n]   (members ascending)
+// Gp[b, kind, c] = sum_{n in chunk c of group(kind, src_b)} drop(kind, b, n) * dU[n]
+// (chunks of kGatherChunk members, ascending), then G[b, kind] = sum_c Gp[b, kind, c]
+// in chunk order: one wave per (b, kind, chunk) keeps thousands of members in flight.
+constexpr int kGatherChunk = 64;
+
 __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
                                                               const float* __restrict__ dU,
-                                                              float* __restrict__ G) {
+                                                              int nck, float* __restrict__ Gp) {
   const int lane = lane_id();
   const int D = a.H * a.F;
   const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (wv >= 2 * a.B) return;
-  const int64_t b = wv >> 1;
-  const int kind = (int)(wv & 1);
+  if (wv >= 2 * a.B * nck) return;
+  const int c = (int)(wv % nck);
+  const int64_t bk = wv / nck;
+  const int64_t b = bk >> 1;
+  const int kind = (int)(bk & 1);
   const int64_t i = a.src[b];
   const int32_t* gptr = kind == 0 ? a.gptr3 : a.gptr4;
   const int32_t* gmem = kind == 0 ? a.gmem3 : a.gmem4;
   const int32_t grp = kind == 0 ? a.gid3[i] : a.gid4[i];
-  const int32_t m0 = gptr[grp], m1 = gptr[grp + 1];
+  const int32_t m0 = gptr[grp] + c * kGatherChunk;
+  const int32_t m1 = min(gptr[grp + 1], m0 + kGatherChunk);
   constexpr int KD = kMaxD / 64;
   float acc[KD];
 #pragma unroll
@@ -176,7 +183,21 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
 #pragma unroll
   for (int k = 0; k < KD; ++k) {
     const int d = lane + 64 * k;
-    if (d < D) G[(b * 2 + kind) * D + d] = acc[k];
+    if (d < D) Gp[(bk * nck + c) * D + d] = acc[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, int D, int nck,
+                                                                     const float* __restrict__ Gp,
+                                                                     float* __restrict__ G) {
+  const int64_t total = 2 * B * D;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bk = t / D;
+    const int d = (int)(t % D);
+    float s = 0.f;
+    for (int c = 0; c < nck; ++c) s += Gp[(bk * nck + c) * D + d];
+    G[t] = s;
   }
 }
 
@@ -314,14 +335,22 @@ extern "C" int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, 
   return check_launch("ours_intra_fwd");
 }
 
+extern "C" size_t msha_ours_workspace_size(const msha_groups* grp, int64_t B, int32_t heads,
+                                           int32_t feat) {
+  if (grp == nullptr || B <= 0) return 0;
+  const int64_t maxg = grp->max_group > 0 ? grp->max_group : grp->n_nodes;
+  const int64_t nck = (maxg + kGatherChunk - 1) / kGatherChunk;
+  return (size_t)(2 * B * nck) * (size_t)heads * (size_t)feat * sizeof(float);
+}
+
 extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, int64_t B,
                                    const int64_t* src, int32_t heads, int32_t feat,
                                    const float* h2, const float* a3s, const float* a4s,
                                    const float* bstat, const float* dU, int32_t stage,
                                    float neg_slope, float drop_p, uint64_t seed,
                                    uint64_t offset, float* G, float* bgrad, float* row_coef,
-                                   float* da3s, float* da4s, float* d_hs,
-                                   msha_stream_t stream) {
+                                   float* da3s, float* da4s, float* d_hs, void* ws,
+                                   size_t ws_bytes, msha_stream_t stream) {
   if (int rc = check(g, grp, B, src, heads, feat)) return rc;
   MSHA_ARG_CHECK(stage == 0 || stage == 1, "ours_intra_bwd: stage must be 0 or 1");
   MSHA_ARG_CHECK(h2 && a3s && a4s && bstat && G && bgrad, "ours_intra_bwd: null pointer");
@@ -339,8 +368,16 @@ extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, 
     return MSHA_OK;
   }
   if (stage == 0) {
-    hipLaunchKernelGGL(ours_bwd_gather_kernel, dim3(grid_for(2 * B, 4)), dim3(256), 0, s, a, dU,
-                       G);
+    const int maxg = grp->max_group > 0 ? grp->max_group : (int)g->n_rows;
+    const int nck = (maxg + kGatherChunk - 1) / kGatherChunk;
+    MSHA_ARG_CHECK(ws && ws_bytes >= msha_ours_workspace_size(grp, B, heads, feat),
+                   "ours_intra_bwd: workspace too small");
+    float* Gp = (float*)ws;
+    hipLaunchKernelGGL(ours_bwd_gather_kernel, dim3(grid_for(2 * B * nck, 4)), dim3(256), 0, s,
+                       a, dU, nck, Gp);
+    hipLaunchKernelGGL(ours_bwd_gather_reduce_kernel,
+                       dim3(grid_for(2 * B * heads * feat, 256, 4096)), dim3(256), 0, s, B,
+                       heads * feat, nck, (const float*)Gp, G);
     hipLaunchKernelGGL(ours_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, a, 0, bstat,
                        (const float*)G, bgrad, row_coef, da3s, da4s, (float*)nullptr);
   } else {

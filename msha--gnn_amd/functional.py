@@ -268,17 +268,22 @@ class _ProjectScores(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dW = gemm(X.t(), dh)
         if terms and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
-            # dal[h,f] = sum_m d_el[m,h] h[m,h,f]: rows of ([d_el | d_er]^T @ h), diagonal blocks
-            D = torch.cat([_f32c(d) for d in (d_el, d_er) if d is not None], dim=1)  # (M, k*H)
-            R = gemm(D.t(), h)  # (k*H, H*F)
-            idx = torch.arange(H, device=dev)
-            blocks = R.view(-1, H, H, Fd)[:, idx, idx]  # (k, H, F)
+            # dal[h,f] = sum_m d_el[m,h] h[m,h,f] (and dar): one pass over h
+            (d1, a1) = terms[0]
+            d2 = terms[1][0] if len(terms) > 1 else None
+            o1 = torch.empty(H, Fd, device=dev, dtype=torch.float32)
+            o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
+            wsb = int(_lib.load().msha_head_colsum_workspace_size(M, H, Fd))
+            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+            _lib.call("msha_head_colsum", M, H, Fd, _f32c(d1).data_ptr(), _lib.ptr(_f32c(d2)),
+                      h.data_ptr(), o1.data_ptr(), _lib.ptr(o2), ws.data_ptr(), ws.numel(), s)
+            outs = [o1] + ([o2] if o2 is not None else [])
             k = 0
             if d_el is not None:
-                dal = blocks[k].reshape(al.shape)
+                dal = outs[k].reshape(al.shape)
                 k += 1
             if d_er is not None:
-                dar = blocks[k].reshape(ar.shape)
+                dar = outs[k].reshape(ar.shape)
         return dX, dW, dal, dar, None, None
 
 
@@ -458,9 +463,11 @@ class _OursAttention(torch.autograd.Function):
         da4s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
         args = (g, gr, B, src.data_ptr(), H, Fd, h2.data_ptr(), a3s.data_ptr(), a4s.data_ptr(),
                 bstat.data_ptr(), dU.data_ptr())
+        wsb = int(_lib.load().msha_ours_workspace_size(gr, B, H, Fd))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
         _lib.call("msha_ours_intra_bwd", *args, 0, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
                   bgrad.data_ptr(), row_coef.data_ptr(), da3s.data_ptr(), da4s.data_ptr(), None,
-                  s)
+                  ws.data_ptr(), ws.numel(), s)
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
         de = torch.empty(E, H, device=dev, dtype=torch.float32)
@@ -471,7 +478,7 @@ class _OursAttention(torch.autograd.Function):
                   h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p, ctx.seed,
                   0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), d_hs.data_ptr(), s)
         _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
-                  bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), s)
+                  bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), None, 0, s)
         d_hc = torch.empty(m, H, Fd, device=dev, dtype=torch.float32)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
         _csc_aggregate(graph, H, Fd, attd, de, dU, d_hc, d_er, s)

@@ -210,12 +210,15 @@ class Groups:
         self.device = torch.device(device)
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=self.device)  # noqa
         self._keep = []
+        self.max_group = 0
         for ids in (city_ids, prov_ids):
             ids = np.asarray(ids.cpu() if torch.is_tensor(ids) else ids, np.int64)
             _, gid = np.unique(ids, return_inverse=True)
             order = np.argsort(gid, kind="stable")
             gptr = np.zeros(gid.max() + 2 if len(gid) else 1, np.int64)
-            np.cumsum(np.bincount(gid, minlength=len(gptr) - 1), out=gptr[1:])
+            sizes = np.bincount(gid, minlength=len(gptr) - 1)
+            np.cumsum(sizes, out=gptr[1:])
+            self.max_group = max(self.max_group, int(sizes.max()) if len(sizes) else 0)
             self._keep.append((t(gid), t(gptr), t(order)))
         self._desc = None
 
@@ -227,6 +230,7 @@ class Groups:
             (g3, p3, m3), (g4, p4, m4) = self._keep
             d.gid3, d.gptr3, d.gmem3 = g3.data_ptr(), p3.data_ptr(), m3.data_ptr()
             d.gid4, d.gptr4, d.gmem4 = g4.data_ptr(), p4.data_ptr(), m4.data_ptr()
+            d.max_group = self.max_group
             self._desc = d
         return self._desc
 

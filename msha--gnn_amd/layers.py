@@ -135,9 +135,11 @@ class OursLayer3(nn.Module):
         self.bn3 = nn.BatchNorm1d(out_features)
 
     def epilogue(self, u, v):
-        """Ablation.py:273-277 on the aggregates: BN + LeakyReLU + u @ v.T + elu."""
-        v_out = self.leakyrelu(self.bn1(v))
-        u_out = self.leakyrelu(self.bn2(u))
+        """Ablation.py:273-277 on the aggregates: BN + LeakyReLU + u @ v.T + elu.
+        (u, v arrive as head slices of the fused (rows, H, F) outputs; BatchNorm1d's
+        backward is ~30x slower on the strided view, so they are made contiguous.)"""
+        v_out = self.leakyrelu(self.bn1(v.contiguous()))
+        u_out = self.leakyrelu(self.bn2(u.contiguous()))
         return F.elu(u_out @ v_out.t())
 
     def forward(self, Sinput, Rinput, inter_adj, city_adj, province_adj, source_index):

@@ -438,6 +438,26 @@ def make_ours_small(g):
     np.savez_compressed(os.path.join(OUT, "ours_small.npz"), **res)
 
 
+def make_years():
+    """Per-year node tables of the shipped 2015-2018 graphs (Adjacent{Y}.json,
+    GDP{Y}.json): N, city / province group ids, GDP.  Flows of 2016-2018 are not
+    shipped (.MISSING_LARGE_BLOBS); bench.py synthesises them with the 2015 degree
+    law (msha_gnn_amd.data.synthetic_flows, seed = year)."""
+    res = {}
+    for year in ("2015", "2016", "2017", "2018"):
+        adj = json.load(open(os.path.join(DATA, f"Adjacent{year}.json"), encoding="utf-8"))
+        src = adj["source_index"]
+        n = len(src)
+        groups = np.array([src[str(i)] for i in range(n)], np.int64)
+        gdp = json.load(open(os.path.join(DATA, f"GDP{year}.json")))["GDP_embedding"]
+        res[f"{year}.n"] = n
+        res[f"{year}.m"] = len(adj["recipient_index"])
+        res[f"{year}.city"] = groups[:, 0].astype(np.int16)
+        res[f"{year}.prov"] = groups[:, 1].astype(np.int8)
+        res[f"{year}.gdp"] = np.array([gdp[str(i)] for i in range(n)], np.float32)
+    np.savez_compressed(os.path.join(OUT, "years.npz"), **res)
+
+
 def main():
     torch.set_num_threads(8)
     g = load_2015()
@@ -447,6 +467,7 @@ def main():
     make_link()
     make_edge_cases()
     make_ours_small(g)
+    make_years()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -282,6 +282,39 @@ def test_project_scores_fwd_bwd(cuda, M, K, H, F):
         tol_close(got.grad.cpu().numpy(), want.grad.numpy(), 1e-4, 1e-5)
 
 
+@pytest.mark.parametrize("M,H,F,two", [(100000, 8, 16, True), (1025, 3, 4, True),
+                                       (700, 1, 3, False), (513, 4, 512, True), (1, 2, 8, True)])
+def test_head_colsum(cuda, M, H, F, two):
+    """out[h,f] = sum_r s[r,h] T[r,h*F+f]: float4 path, scalar path (F % 4 != 0),
+    column tiles (H*F > 1024), ragged row blocks; deterministic across calls."""
+    from msha_gnn_amd import _lib
+
+    rng = np.random.default_rng(M + F)
+    T = rng.standard_normal((M, H * F)).astype(np.float32)
+    s1 = rng.standard_normal((M, H)).astype(np.float32)
+    s2 = rng.standard_normal((M, H)).astype(np.float32) if two else None
+    tT, t1 = t(T, cuda), t(s1, cuda)
+    t2 = t(s2, cuda) if two else None
+    o1 = torch.empty(H, F, device=cuda)
+    o2 = torch.empty(H, F, device=cuda) if two else None
+    ws = torch.empty(int(_lib.load().msha_head_colsum_workspace_size(M, H, F)) + 16,
+                     dtype=torch.uint8, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for _ in range(2):
+        _lib.call("msha_head_colsum", M, H, F, t1.data_ptr(), _lib.ptr(t2), tT.data_ptr(),
+                  o1.data_ptr(), _lib.ptr(o2), ws.data_ptr(), ws.numel(), st)
+        outs.append([o1.cpu().numpy().copy()] + ([o2.cpu().numpy().copy()] if two else []))
+    T3 = T.astype(np.float64).reshape(M, H, F)
+    refs = [np.einsum("mh,mhf->hf", s1.astype(np.float64), T3)]
+    if two:
+        refs.append(np.einsum("mh,mhf->hf", s2.astype(np.float64), T3))
+    for got, ref in zip(outs[0], refs):
+        tol_close(got, ref, 1e-5, 1e-5)
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+
+
 # ------------------------------------------------------------------ link scoring
 def test_link_predictor_matches_reference(cuda, msha):
     from msha_gnn_amd import layers
