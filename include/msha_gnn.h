@@ -197,6 +197,20 @@ MSHA_API int msha_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int6
                            int64_t ldc, float beta, int32_t splits, void* ws, size_t ws_bytes,
                            msha_stream_t stream);
 
+/* msha_gemm_f32 with the backward of msha_project_scores folded into one operand's
+ * loads: operand 0 (A, M x K, K = heads*feat, sAk = 1) or 1 (B, K x N, N = heads*feat,
+ * sBn = 1) is read as X + de (x) a [+ de2 (x) a2], i.e. X[r, c] + de[r, c/feat] a[c].
+ * dX = (dh + de (x) a) W^T and dW = X^T (dh + de (x) a) without materialising the sum
+ * (replaces msha_add_head_outer + msha_gemm_f32).  MSHA_ERR_UNSUPPORTED when the
+ * operands cannot take the 16-byte path (then use those two calls). */
+MSHA_API int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const float* A,
+                                      int64_t sAm, int64_t sAk, const float* B, int64_t sBk,
+                                      int64_t sBn, float* C, int64_t ldc, float beta,
+                                      int32_t splits, void* ws, size_t ws_bytes, int32_t operand,
+                                      int32_t heads, int32_t feat, const float* de,
+                                      const float* a, const float* de2, const float* a2,
+                                      msha_stream_t stream);
+
 /* Projection with the attention-score halves fused into its epilogue:
  *   h = X @ W  (M x heads*feat),  el[m,h] = h[m,h,:] . al[h,:],  er[m,h] = h[m,h,:] . ar[h,:]
  * Replaces Ablation.py:262-267's projection + the (N, M, 2F) score tensor: the

@@ -73,6 +73,8 @@ SIGNATURES = {
     "msha_gemm_f32": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, F32, I32, P, SZ,
                                 P]),
     "msha_project_scores": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
+    "msha_gemm_f32_head_outer": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, F32,
+                                           I32, P, SZ, I32, I32, I32, P, P, P, P, P]),
     "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
     "msha_head_colsum_workspace_size": (SZ, [I64, I32, I32]),
     "msha_head_colsum": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, SZ, P]),
@@ -129,13 +131,17 @@ def exported_symbols():
     return sorted(SIGNATURES)
 
 
+def raise_for(rc: int, name: str):
+    """Raise the library's thread-local message for a failed call."""
+    msg = load().msha_last_error().decode(errors="replace")
+    raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
 def call(name: str, *args):
     """Invoke an ABI function; raise on a non-zero status with the library message."""
-    lib = load()
-    rc = getattr(lib, name)(*args)
+    rc = getattr(load(), name)(*args)
     if rc != MSHA_OK:
-        msg = lib.msha_last_error().decode(errors="replace")
-        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+        raise_for(rc, name)
     return rc
 
 

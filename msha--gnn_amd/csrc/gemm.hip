@@ -57,7 +57,16 @@ struct GemmArgs {
   float* el;
   float* er;
   int H;
+  // head-outer operand update (HO_A / HO_B): X[r, c] += de[r, c / hF] * ha[c]
+  // (+ de2 * ha2), X the A (r = m, c = k) or B (r = k, c = n) operand
+  const float* de;
+  const float* ha;
+  const float* de2;
+  const float* ha2;
+  int hH, hF;
 };
+
+enum : int { HO_NONE = 0, HO_A = 1, HO_B = 2 };
 
 template <int AMODE>
 __device__ __forceinline__ float load_a(const GemmArgs& p, int64_t m, int64_t k) {
@@ -80,11 +89,17 @@ struct Stage {
   float4 a[4];
   float4 b[4];
   uint32_t okmask;  // bit it: a[it] in range, bit 4+it: b[it] in range
+  float d1[4], d2[4];  // head-outer update (HO_A / HO_B)
+  float4 ha1, ha2;
 };
 
 // Branch-free 16-byte loads: an out-of-range element reads a clamped in-range
 // address and is zeroed by a select, so the compiler can issue a stage's loads
 // back to back and wait for them once (at the LDS store of the next stage).
+__device__ __forceinline__ float f4_get(float4 v, int i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
 __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
   return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
@@ -106,8 +121,23 @@ __device__ __forceinline__ float4 load_a4_kfast(const GemmArgs& p, int64_t m, in
   return make_float4(x.x * y.x, x.y * y.y, x.z * y.z, x.w * y.w);
 }
 
+// Head-outer operand update: the loads of de / ha go out with the operand loads
+// and the fma is applied in stage_store (after the barrier), so the prefetch stays
+// asynchronous.  ha of a thread's 4 columns is the same for all 4 slots `it`.
+__device__ __forceinline__ void head_outer_load(const GemmArgs& p, int64_t r, int64_t c,
+                                                Stage& st, int it) {
+  const int64_t h = c / p.hF;
+  st.d1[it] = p.de[r * p.hH + h];
+  st.d2[it] = p.de2 != nullptr ? p.de2[r * p.hH + h] : 0.f;
+  if (it == 0) {
+    st.ha1 = *reinterpret_cast<const float4*>(p.ha + c);
+    st.ha2 = p.ha2 != nullptr ? *reinterpret_cast<const float4*>(p.ha2 + c)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 // AK: A's k is contiguous (else m is); BNF: B's n is contiguous (else k is)
-template <int AMODE, int AK, int BNF>
+template <int AMODE, int AK, int BNF, int HO = HO_NONE>
 __device__ __forceinline__ void stage_load(const GemmArgs& p, Stage& st, int64_t m0, int64_t n0,
                                            int64_t k0, int64_t ke, int tid) {
   uint32_t okm = 0u;
@@ -119,6 +149,7 @@ __device__ __forceinline__ void stage_load(const GemmArgs& p, Stage& st, int64_t
       const int mm = idx >> 3, kq = idx & 7;
       const int64_t k = k0 + 4 * kq;
       st.a[it] = load_a4_kfast<AMODE>(p, m0 + mm, k < ke ? k : p.K, oka);
+      if (HO == HO_A) head_outer_load(p, oka ? m0 + mm : 0, oka ? k : 0, st, it);
     } else {  // 32 k x 32 float4 along m (A[m, k] = A[k * sAk + m])
       const int kk = idx >> 5, mq = idx & 31;
       const int64_t k = k0 + kk, m = m0 + 4 * mq;
@@ -130,6 +161,7 @@ __device__ __forceinline__ void stage_load(const GemmArgs& p, Stage& st, int64_t
       const int64_t k = k0 + kk, n = n0 + 4 * nq;
       okb = k < ke && n < p.N;
       st.b[it] = *reinterpret_cast<const float4*>(p.B + (okb ? k * p.sBk + n : 0));
+      if (HO == HO_B) head_outer_load(p, okb ? k : 0, okb ? n : 0, st, it);
     } else {  // 128 n x 8 float4 along k (B[k, n] = B[n * sBn + k])
       const int nn = idx >> 3, kq = idx & 7;
       const int64_t k = k0 + 4 * kq, n = n0 + nn;
@@ -142,13 +174,16 @@ __device__ __forceinline__ void stage_load(const GemmArgs& p, Stage& st, int64_t
   st.okmask = okm;
 }
 
-template <int AK, int BNF>
+template <int AK, int BNF, int HO = HO_NONE>
 __device__ __forceinline__ void stage_store(const Stage& st0, float* As, float* Bs, int tid) {
   Stage st;
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
-    st.a[it] = sel4((st0.okmask >> it) & 1u, st0.a[it]);
-    st.b[it] = sel4((st0.okmask >> (4 + it)) & 1u, st0.b[it]);
+    float4 a = st0.a[it], b = st0.b[it];
+    if (HO == HO_A) a = f4_fma(st0.d2[it], st0.ha2, f4_fma(st0.d1[it], st0.ha1, a));
+    if (HO == HO_B) b = f4_fma(st0.d2[it], st0.ha2, f4_fma(st0.d1[it], st0.ha1, b));
+    st.a[it] = sel4((st0.okmask >> it) & 1u, a);
+    st.b[it] = sel4((st0.okmask >> (4 + it)) & 1u, b);
   }
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
@@ -204,7 +239,7 @@ constexpr int TP = BN + 4;  // epilogue staging row pitch (floats)
 
 // VEC = LD_VEC: 16-byte staging with compile-time layouts (AK, BNF); LD_SCALAR:
 // element-wise staging for any strides (layouts decided at run time).
-template <int AMODE, int EPI, int FEPI, int VEC, int AK, int BNF>
+template <int AMODE, int EPI, int FEPI, int VEC, int AK, int BNF, int HO = HO_NONE>
 __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
   // one LDS object (operand tiles; reused as the epilogue's C staging)
   __shared__ __attribute__((aligned(16))) float smem[BM * LDA + BK * LDP];
@@ -228,17 +263,17 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
   const bool a_kfast = AMODE != A_STRIDED || p.sAk == 1 || p.sAm != 1;
   const bool b_nfast = p.sBn == 1 || p.sBk != 1;
   Stage st;
-  if (VEC == LD_VEC && kb < ke) stage_load<AMODE, AK, BNF>(p, st, m0, n0, kb, ke, tid);
+  if (VEC == LD_VEC && kb < ke) stage_load<AMODE, AK, BNF, HO>(p, st, m0, n0, kb, ke, tid);
   for (int64_t k0 = kb; k0 < ke; k0 += BK) {
     __syncthreads();
     if (VEC == LD_VEC) {
-      stage_store<AK, BNF>(st, As, Bs, tid);
+      stage_store<AK, BNF, HO>(st, As, Bs, tid);
     } else {
       stage_scalar<AMODE>(p, As, Bs, m0, n0, k0, ke, a_kfast, b_nfast, tid);
     }
     __syncthreads();
     // prefetch the next stage into registers while the MFMAs run
-    if (VEC == LD_VEC && k0 + BK < ke) stage_load<AMODE, AK, BNF>(p, st, m0, n0, k0 + BK, ke, tid);
+    if (VEC == LD_VEC && k0 + BK < ke) stage_load<AMODE, AK, BNF, HO>(p, st, m0, n0, k0 + BK, ke, tid);
     // ---- 8 k-steps of 4: 2 A reads + 8 B reads feed 16 MFMAs
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
@@ -371,26 +406,35 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
   }
 }
 
-// split-K: C = sum_z slab[z] (in z order: deterministic)
+// split-K: C = sum_z slab[z].  A block owns 64 consecutive outputs; its 4 waves add
+// the interleaved z-subsets {zg, zg+4, ...} and the 4 partials are added in zg order
+// (a fixed order: deterministic).
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab,
                                                           int splits, int64_t M, int64_t N,
                                                           float* __restrict__ C, int64_t ldc,
                                                           float beta) {
+  __shared__ float red[256];
   const int64_t total = M * N;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int z = 0;
-    for (; z + 4 <= splits; z += 4) {  // 4 independent chains keep 4 loads in flight
-      s0 += slab[(int64_t)(z + 0) * total + t];
-      s1 += slab[(int64_t)(z + 1) * total + t];
-      s2 += slab[(int64_t)(z + 2) * total + t];
-      s3 += slab[(int64_t)(z + 3) * total + t];
+  const int lane = threadIdx.x & 63, zg = threadIdx.x >> 6;
+  for (int64_t g = blockIdx.x; g * 64 < total; g += gridDim.x) {
+    const int64_t t = g * 64 + lane;
+    float s0 = 0.f, s1 = 0.f;
+    if (t < total) {
+      int z = zg;
+      for (; z + 4 < splits; z += 8) {
+        s0 += slab[(int64_t)z * total + t];
+        s1 += slab[(int64_t)(z + 4) * total + t];
+      }
+      if (z < splits) s0 += slab[(int64_t)z * total + t];
     }
-    for (; z < splits; ++z) s0 += slab[(int64_t)z * total + t];
-    const float s = (s0 + s1) + (s2 + s3);
-    const int64_t r = t / N, c = t % N;
-    C[r * ldc + c] = beta != 0.f ? beta * C[r * ldc + c] + s : s;
+    red[threadIdx.x] = s0 + s1;
+    __syncthreads();
+    if (zg == 0 && t < total) {
+      const float s = (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]);
+      const int64_t r = t / N, c = t % N;
+      C[r * ldc + c] = beta != 0.f ? beta * C[r * ldc + c] + s : s;
+    }
+    __syncthreads();
   }
 }
 
@@ -445,7 +489,7 @@ static bool vec_ok(const GemmArgs& p) {
 // each row group strides the block's rows with 16-byte loads; the row groups are
 // added in a fixed LDS tree, and a second pass adds the block partials in block
 // order (deterministic).
-constexpr int kColsumRows = 512;
+constexpr int kColsumRows = 64;
 
 template <int VEC>
 struct ColVec;
@@ -509,25 +553,29 @@ __global__ void __launch_bounds__(256) head_colsum_partial_kernel(
   }
 }
 
+// one wave per output element: lane l adds blocks l, l+64, ... in order, then a
+// fixed xor tree across the lanes (deterministic)
 __global__ void __launch_bounds__(256) head_colsum_reduce_kernel(int nblk, int D,
                                                                  const float* __restrict__ part,
                                                                  float* __restrict__ out1,
                                                                  float* __restrict__ out2) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
   if (t >= 2 * D) return;
   const int which = t / D, d = t % D;
   float* out = which == 0 ? out1 : out2;
   if (out == nullptr) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int b = 0;
-  for (; b + 4 <= nblk; b += 4) {
-    s0 += part[((int64_t)(b + 0) * 2 + which) * D + d];
-    s1 += part[((int64_t)(b + 1) * 2 + which) * D + d];
-    s2 += part[((int64_t)(b + 2) * 2 + which) * D + d];
-    s3 += part[((int64_t)(b + 3) * 2 + which) * D + d];
+  float s0 = 0.f, s1 = 0.f;
+  int b = lane;
+  for (; b + 64 < nblk; b += 128) {
+    s0 += part[((int64_t)b * 2 + which) * D + d];
+    s1 += part[((int64_t)(b + 64) * 2 + which) * D + d];
   }
-  for (; b < nblk; ++b) s0 += part[((int64_t)b * 2 + which) * D + d];
-  out[d] = (s0 + s1) + (s2 + s3);
+  if (b < nblk) s0 += part[((int64_t)b * 2 + which) * D + d];
+  float v = s0 + s1;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if (lane == 0) out[d] = v;
 }
 
 template <int AMODE, int EPI, int FEPI>
@@ -578,6 +626,54 @@ extern "C" size_t msha_gemm_workspace_size(int64_t M, int64_t N, int32_t splits)
   return (size_t)splits * (size_t)M * (size_t)N * sizeof(float);
 }
 
+template <int HO>
+static void launch_ho(const GemmArgs& p, int splits, hipStream_t s) {
+  dim3 grid((unsigned)((p.M + BM - 1) / BM), (unsigned)((p.N + BN - 1) / BN), (unsigned)splits);
+  const bool ak = p.sAk == 1, bn = p.sBn == 1;
+  if (HO == HO_A) {  // A has k contiguous
+    if (bn)
+      hipLaunchKernelGGL((gemm_f32_kernel<A_STRIDED, EPI_STORE, 0, LD_VEC, 1, 1, HO>), grid,
+                         dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_f32_kernel<A_STRIDED, EPI_STORE, 0, LD_VEC, 1, 0, HO>), grid,
+                         dim3(256), 0, s, p);
+  } else {  // B has n contiguous
+    if (ak)
+      hipLaunchKernelGGL((gemm_f32_kernel<A_STRIDED, EPI_STORE, 0, LD_VEC, 1, 1, HO>), grid,
+                         dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_f32_kernel<A_STRIDED, EPI_STORE, 0, LD_VEC, 0, 1, HO>), grid,
+                         dim3(256), 0, s, p);
+  }
+}
+
+// shared body of msha_gemm_f32 / msha_gemm_f32_head_outer
+static int gemm_run(GemmArgs& p, int ho, float beta, int32_t splits, void* ws, size_t ws_bytes,
+                    hipStream_t s) {
+  const int64_t M = p.M, N = p.N, K = p.K;
+  auto go = [&](int used) {
+    if (ho == HO_A) launch_ho<HO_A>(p, used, s);
+    else if (ho == HO_B) launch_ho<HO_B>(p, used, s);
+    else launch<A_STRIDED, EPI_STORE, 0>(p, used, s);
+  };
+  if (splits > 1) {
+    MSHA_ARG_CHECK(ws && ws_bytes >= msha_gemm_workspace_size(M, N, splits),
+                   "gemm_f32: split-K workspace too small");
+    int64_t kc = (K + splits - 1) / splits;
+    kc = ((kc + BK - 1) / BK) * BK;
+    const int used = (int)((K + kc - 1) / kc);
+    p.k_chunk = kc;
+    p.slab = (float*)ws;
+    go(used);
+    const int64_t groups = (M * N + 63) / 64;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(groups, 1, 65535)), dim3(256), 0, s,
+                       (const float*)ws, used, M, N, p.C, p.ldc, beta);
+  } else {
+    go(1);
+  }
+  return check_launch("gemm_f32");
+}
+
 extern "C" int msha_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm,
                              int64_t sAk, const float* B, int64_t sBk, int64_t sBn, float* C,
                              int64_t ldc, float beta, int32_t splits, void* ws, size_t ws_bytes,
@@ -591,22 +687,38 @@ extern "C" int msha_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, in
   p.A = A; p.sAm = sAm; p.sAk = sAk;
   p.B = B; p.sBk = sBk; p.sBn = sBn;
   p.C = C; p.ldc = ldc;
-  hipStream_t s = (hipStream_t)stream;
-  if (splits > 1) {
-    MSHA_ARG_CHECK(ws && ws_bytes >= msha_gemm_workspace_size(M, N, splits),
-                   "gemm_f32: split-K workspace too small");
-    int64_t kc = (K + splits - 1) / splits;
-    kc = ((kc + BK - 1) / BK) * BK;
-    const int used = (int)((K + kc - 1) / kc);
-    p.k_chunk = kc;
-    p.slab = (float*)ws;
-    launch<A_STRIDED, EPI_STORE, 0>(p, used, s);
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(M * N, 256, 8192)), dim3(256), 0, s,
-                       (const float*)ws, used, M, N, C, ldc, beta);
-  } else {
-    launch<A_STRIDED, EPI_STORE, 0>(p, 1, s);
-  }
-  return check_launch("gemm_f32");
+  return gemm_run(p, HO_NONE, beta, splits, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const float* A,
+                                        int64_t sAm, int64_t sAk, const float* B, int64_t sBk,
+                                        int64_t sBn, float* C, int64_t ldc, float beta,
+                                        int32_t splits, void* ws, size_t ws_bytes,
+                                        int32_t operand, int32_t heads, int32_t feat,
+                                        const float* de, const float* a, const float* de2,
+                                        const float* a2, msha_stream_t stream) {
+  MSHA_ARG_CHECK(M > 0 && N > 0 && K > 0, "gemm_f32_head_outer: bad sizes");
+  MSHA_ARG_CHECK(A && B && C && de && a && ((de2 == nullptr) == (a2 == nullptr)),
+                 "gemm_f32_head_outer: null pointer");
+  MSHA_ARG_CHECK(operand == 0 || operand == 1, "gemm_f32_head_outer: operand must be 0 (A) or 1 (B)");
+  MSHA_ARG_CHECK(heads > 0 && feat > 0 && feat % 4 == 0,
+                 "gemm_f32_head_outer: feat must be a positive multiple of 4");
+  MSHA_ARG_CHECK((operand == 0 ? K : N) == (int64_t)heads * feat,
+                 "gemm_f32_head_outer: the updated operand's column count must be heads*feat");
+  MSHA_ARG_CHECK(splits >= 1 && splits <= 65535, "gemm_f32_head_outer: splits out of range");
+  MSHA_ARG_CHECK(splits == 1 || beta == 0.f || beta == 1.f, "gemm_f32_head_outer: beta must be 0 or 1");
+  MSHA_ARG_CHECK(splits > 1 || beta == 0.f, "gemm_f32_head_outer: beta needs splits > 1");
+  GemmArgs p = base_args(M, N, K);
+  p.A = A; p.sAm = sAm; p.sAk = sAk;
+  p.B = B; p.sBk = sBk; p.sBn = sBn;
+  p.C = C; p.ldc = ldc;
+  p.de = de; p.ha = a; p.de2 = de2; p.ha2 = a2; p.hH = heads; p.hF = feat;
+  const bool lay = operand == 0 ? sAk == 1 : sBn == 1;
+  const bool al = aligned16(a) && (a2 == nullptr || aligned16(a2));
+  if (!lay || !al || !vec_ok<A_STRIDED>(p))
+    return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer: the updated operand needs unit stride "
+                                      "along heads*feat and 16-byte aligned, vectorizable operands");
+  return gemm_run(p, operand == 0 ? HO_A : HO_B, beta, splits, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t feat,
@@ -702,7 +814,7 @@ extern "C" int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, const
   else
     hipLaunchKernelGGL(head_colsum_partial_kernel<1>, grid, dim3(256), 0, s, rows, (int)heads,
                        (int)feat, s1, s2, T, (float*)ws);
-  hipLaunchKernelGGL(head_colsum_reduce_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, s, nblk,
+  hipLaunchKernelGGL(head_colsum_reduce_kernel, dim3((2 * D + 3) / 4), dim3(256), 0, s, nblk,
                      D, (const float*)ws, out1, out2);
   return check_launch("head_colsum");
 }

@@ -219,6 +219,34 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
     return out
 
 
+def gemm_head_outer(A: torch.Tensor, B: torch.Tensor, operand: int, outer) -> torch.Tensor:
+    """A @ B with operand 0 (A) or 1 (B) read as X + de (x) a [+ de2 (x) a2]
+    (outer = (heads, feat, de, a, de2, a2)); falls back to materialising the sum with
+    msha_add_head_outer only when the operand layout cannot take the fused loads."""
+    H, Fd, d1, a1, d2, a2 = outer
+    M, K = A.shape
+    N = B.shape[1]
+    out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    splits = _splits_for(K) if K >= 4096 else 1
+    ws = None
+    if splits > 1:
+        ws = torch.empty(int(_lib.load().msha_gemm_workspace_size(M, N, splits)),
+                         dtype=torch.uint8, device=A.device)
+    rc = _lib.load().msha_gemm_f32_head_outer(
+        M, N, K, A.data_ptr(), A.stride(0), A.stride(1), B.data_ptr(), B.stride(0), B.stride(1),
+        out.data_ptr(), out.stride(0), 0.0, splits, _lib.ptr(ws), 0 if ws is None else ws.numel(),
+        operand, H, Fd, d1.data_ptr(), a1.data_ptr(), _lib.ptr(d2), _lib.ptr(a2), _stream(A))
+    if rc == 0:
+        return out
+    if rc != _lib.MSHA_ERR_UNSUPPORTED:
+        _lib.raise_for(rc, "msha_gemm_f32_head_outer")
+    X = A if operand == 0 else B
+    tot = torch.empty(X.shape, device=X.device, dtype=torch.float32)
+    _lib.call("msha_add_head_outer", X.shape[0], H, Fd, _f32c(X).data_ptr(), d1.data_ptr(),
+              a1.data_ptr(), _lib.ptr(d2), _lib.ptr(a2), tot.data_ptr(), _stream(X))
+    return gemm(tot, B) if operand == 0 else gemm(A, tot)
+
+
 class _ProjectScores(torch.autograd.Function):
     """h = X @ W, el = h . al, er = h . ar (per head) in one MFMA launch."""
 
@@ -255,18 +283,22 @@ class _ProjectScores(torch.autograd.Function):
         d_er = next(it) if ar is not None else None
         dh = torch.zeros_like(h) if dh is None else _f32c(dh)
         terms = [(d, a) for d, a in ((d_el, al), (d_er, ar)) if d is not None]
+        dX = dW = dal = dar = None
         if terms:
-            tot = torch.empty_like(dh)
+            # dh + d_el (x) al (+ d_er (x) ar) is folded into the GEMM operand loads
             (d1, a1) = terms[0]
             d2, a2 = terms[1] if len(terms) > 1 else (None, None)
-            _lib.call("msha_add_head_outer", M, H, Fd, dh.data_ptr(), _f32c(d1).data_ptr(),
-                      a1.data_ptr(), _lib.ptr(_f32c(d2)), _lib.ptr(a2), tot.data_ptr(), s)
-            dh = tot
-        dX = dW = dal = dar = None
-        if ctx.needs_input_grad[0]:
-            dX = gemm(dh, W.t())
-        if ctx.needs_input_grad[1]:
-            dW = gemm(X.t(), dh)
+            d1, d2 = _f32c(d1), _f32c(d2)
+            outer = (H, Fd, d1, a1, d2, a2)
+            if ctx.needs_input_grad[0]:
+                dX = gemm_head_outer(dh, W.t(), 0, outer)
+            if ctx.needs_input_grad[1]:
+                dW = gemm_head_outer(X.t(), dh, 1, outer)
+        else:
+            if ctx.needs_input_grad[0]:
+                dX = gemm(dh, W.t())
+            if ctx.needs_input_grad[1]:
+                dW = gemm(X.t(), dh)
         if terms and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
             # dal[h,f] = sum_m d_el[m,h] h[m,h,f] (and dar): one pass over h
             (d1, a1) = terms[0]

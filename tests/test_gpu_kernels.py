@@ -282,6 +282,38 @@ def test_project_scores_fwd_bwd(cuda, M, K, H, F):
         tol_close(got.grad.cpu().numpy(), want.grad.numpy(), 1e-4, 1e-5)
 
 
+@pytest.mark.parametrize("operand,M,H,F,K,two", [(1, 100000, 8, 16, 128, True),
+                                                 (1, 5000, 2, 64, 96, False),
+                                                 (0, 3000, 8, 16, 128, True),
+                                                 (0, 517, 1, 8, 40, False)])
+def test_gemm_head_outer(cuda, operand, M, H, F, K, two):
+    """dX = (dh + de (x) a) W^T (operand 0) and dW = X^T (dh + de (x) a) (operand 1)
+    with the sum folded into the operand loads, vs torch fp64."""
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M + operand)
+    D = H * F
+    dh = rng.standard_normal((M, D)).astype(np.float32)
+    de = rng.standard_normal((M, H)).astype(np.float32)
+    a = rng.standard_normal((H, F)).astype(np.float32)
+    de2 = rng.standard_normal((M, H)).astype(np.float32) if two else None
+    a2 = rng.standard_normal((H, F)).astype(np.float32) if two else None
+    tot = dh.astype(np.float64) + np.repeat(de, F, 1) * a.reshape(-1)
+    if two:
+        tot += np.repeat(de2, F, 1) * a2.reshape(-1)
+    outer = (H, F, t(de, cuda), t(a, cuda), t(de2, cuda) if two else None,
+             t(a2, cuda) if two else None)
+    if operand == 0:
+        W = rng.standard_normal((K, D)).astype(np.float32)
+        got = MF.gemm_head_outer(t(dh, cuda), t(W, cuda).t(), 0, outer).cpu().numpy()
+        ref = tot @ W.T.astype(np.float64)
+    else:
+        X = rng.standard_normal((M, K)).astype(np.float32)
+        got = MF.gemm_head_outer(t(X, cuda).t(), t(dh, cuda), 1, outer).cpu().numpy()
+        ref = X.T.astype(np.float64) @ tot
+    tol_close(got, ref, 1e-5, 1e-5)
+
+
 @pytest.mark.parametrize("M,H,F,two", [(100000, 8, 16, True), (1025, 3, 4, True),
                                        (700, 1, 3, False), (513, 4, 512, True), (1, 2, 8, True)])
 def test_head_colsum(cuda, M, H, F, two):
