@@ -69,16 +69,17 @@ WORKLOADS = {
 }
 
 
-def fwd_bytes(n, m, e, H, F):
+def fwd_bytes(n, m, e, H, F, s=4):
     """Algorithmic bytes of one msha_edge_attention_fwd launch:
-    rowptr + col + er gather + el + h gather (4HF per edge) + u write + lse write."""
-    return 4 * (n + 1) + 4 * e + 4 * e * H + 4 * n * H + 4 * e * H * F + 4 * n * H * F + 4 * n * H
+    rowptr + col + er gather + el + h gather (s*HF per edge) + u write + lse write;
+    s = bytes per table element (4 fp32, 2 bf16)."""
+    return 4 * (n + 1) + 4 * e + 4 * e * H + 4 * n * H + s * e * H * F + s * n * H * F + 4 * n * H
 
 
 class Layer:
     """The benchmarked GAT layer (one replica)."""
 
-    def __init__(self, dev, rowptr, col, n, m, fin, H, F, seed):
+    def __init__(self, dev, rowptr, col, n, m, fin, H, F, seed, dtype=torch.float32, graph=None):
         import msha_loader
 
         msha_loader.load()
@@ -86,14 +87,16 @@ class Layer:
         from msha_gnn_amd.graph import Graph
 
         self.MF = MF
-        self.graph = Graph.from_csr(rowptr, col, m, dev)
+        self.graph = graph if graph is not None else Graph.from_csr(rowptr, col, m, dev)
         g = torch.Generator().manual_seed(seed)
         self.n, self.m, self.H, self.F = n, m, H, F
-        self.X = torch.rand(n, fin, generator=g).to(dev)
-        self.W = (torch.randn(fin, H * F, generator=g) * fin ** -0.5).to(dev).requires_grad_(True)
+        # dtype = storage of the feature table, W and the node tables (bf16: config C3)
+        self.X = torch.rand(n, fin, generator=g).to(dev, dtype)
+        self.W = (torch.randn(fin, H * F, generator=g) * fin ** -0.5).to(dev, dtype) \
+            .requires_grad_(True)
         self.al = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
         self.ar = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
-        self.dU = torch.randn(n, H, F, generator=g).to(dev)
+        self.dU = torch.randn(n, H, F, generator=g).to(dev, dtype)
 
     def step(self):
         for p in (self.W, self.al, self.ar):
@@ -192,7 +195,8 @@ def _year_graph(year):
         np.int64), yz[f"{year}.gdp"]
 
 
-def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5):
+def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
+                   dtype=torch.float32):
     """configs[1]: one train.py iteration (train.py:221-232) on a shipped year's graph:
     full-graph forward of the model (in 128, F 64, 2 heads, dropout 0.5), nll on a
     64-flow batch, backward, Adam(lr 1e-3, wd 5e-4) step.  model_kind: 'Ours' (full
@@ -212,7 +216,7 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5):
     gdp = {i: float(x) for i, x in enumerate(gdp_arr)}
     torch.manual_seed(0)
     cls = layers.Ours if model_kind == "Ours" else layers.ablation3
-    model = cls(128, 64, m, 2, 0.5, gdp, n, m).to(dev)
+    model = cls(128, 64, m, 2, 0.5, gdp, n, m).to(dev, dtype)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
     g = torch.Generator().manual_seed(0)
     picks = [torch.randint(0, len(flows), (64,), generator=g).to(dev) for _ in range(8)]
@@ -223,7 +227,7 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5):
         si, ri = batches[k % len(batches)]
         opt.zero_grad()
         out = model(adj, cadj, padj, si)
-        loss = torch.nn.functional.nll_loss(out[si], ri)
+        loss = torch.nn.functional.nll_loss(out[si].float(), ri)
         loss.backward()
         opt.step()
         return loss
@@ -239,7 +243,8 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5):
     from msha_gnn_amd.graph import graph_for
 
     e = graph_for(adj).n_edges
-    return dict(model=model_kind, year=year, nodes=n, recipients=m, edges=e,
+    return dict(model=model_kind, year=year, dtype=str(dtype).replace("torch.", ""), nodes=n,
+                recipients=m, edges=e,
                 flows="shipped" if year == "2015" else "synthetic (2015 degree law)",
                 ms_per_step=dt * 1e3, edges_per_sec=e / dt, loss=float(loss.detach()))
 
@@ -295,6 +300,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-link-score", action="store_true")
     ap.add_argument("--no-r15", action="store_true")
+    ap.add_argument("--no-bf16", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -324,22 +330,44 @@ def main():
             tdist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
-        layer.step()
-    barrier()
-    layer.MF.KERNEL_EVENTS = {}
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        layer.step()
-    barrier()
-    dt = time.perf_counter() - t0
-    events = layer.MF.KERNEL_EVENTS.get("edge_attention_fwd", [])
-    layer.MF.KERNEL_EVENTS = None
-    k_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
-    if dist:
-        t = torch.tensor([dt], device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        dt = float(t.item())
+    def timed(lay, steps, warmup):
+        """(max-over-ranks seconds for `steps` steps, mean fwd-kernel ms, launches)"""
+        for _ in range(warmup):
+            lay.step()
+        barrier()
+        lay.MF.KERNEL_EVENTS = {}
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            lay.step()
+        barrier()
+        dt_ = time.perf_counter() - t0
+        events = lay.MF.KERNEL_EVENTS.get("edge_attention_fwd", [])
+        lay.MF.KERNEL_EVENTS = None
+        k = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+        if dist:
+            tt = torch.tensor([dt_], device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            dt_ = float(tt.item())
+        return dt_, k, len(events)
+
+    dt, k_ms, n_launch = timed(layer, args.steps, args.warmup)
+    bf16_leg = None
+    if not args.no_bf16:
+        # config C3: the same layer with bf16 tables / projection (bf16 MFMA)
+        lay16 = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank, dtype=torch.bfloat16,
+                      graph=layer.graph)
+        dt16, k16, n16 = timed(lay16, args.steps, args.warmup)
+        fb16 = fwd_bytes(n, m, e, H, F, s=2)
+        a16 = fb16 / (k16 * 1e-3) / 1e9
+        bf16_leg = {"workload": f"gat_layer_{args.workload} (config C3: bf16 tables, bf16 MFMA "
+                                "projection, fp32 scores/softmax)",
+                    "value": world * e * args.steps / dt16, "unit": "edges/s",
+                    "ms_per_step": dt16 / args.steps * 1e3, "dtype": "bf16",
+                    "roofline": {"kernel": "msha_edge_attention_fwd<bf16>", "bound": "hbm",
+                                 "achieved": a16, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": a16 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": fb16,
+                                 "avg_launch_us": k16 * 1e3, "launches_timed": n16}}
+        del lay16
     link = None
     if not args.no_link_score and args.workload != "r15":
         link = link_score_bench(dev, rowptr, col, n, H * F, world, rank, dist)
@@ -362,8 +390,10 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": fb, "avg_launch_us": k_ms * 1e3,
-                     "launches_timed": len(events)},
+                     "launches_timed": n_launch},
     }
+    if bf16_leg is not None:
+        out["bf16"] = bf16_leg
     if link is not None:
         out["link_score"] = link
     if world == 1 and not args.no_r15:
@@ -374,6 +404,13 @@ def main():
                                         "container CPU; not this box)",
             "runs": [train_step_leg(dev, y, "Ours") for y in ("2015", "2016", "2017", "2018")]
             + [train_step_leg(dev, "2015", "ablation3")]}
+        if not args.no_bf16:
+            out["train_step_configs2"] = {
+                "workload": "configs[2]: the same Ours model in bf16 (model.to(bfloat16): bf16 "
+                            "parameters and node tables, bf16 MFMA projections, fp32 scores, "
+                            "softmax and statistics), same step as configs[1]",
+                "runs": [train_step_leg(dev, y, "Ours", dtype=torch.bfloat16)
+                         for y in ("2015", "2016", "2017", "2018")]}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
     print(json.dumps(out), flush=True)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 1
+#define MSHA_ABI_VERSION 2
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -51,6 +51,11 @@ enum {
 };
 
 typedef void* msha_stream_t; /* hipStream_t */
+
+/* Storage type of node-feature tables (h, u, v, dU, dV, dh): fp32, or bf16 with
+ * fp32 arithmetic (loads widen, stores round to nearest even).  Scores, softmax
+ * statistics, per-edge values and their gradients are always fp32. */
+enum { MSHA_DTYPE_F32 = 0, MSHA_DTYPE_BF16 = 1 };
 
 /* Graph descriptor.  Built by msha_graph_count / msha_graph_fill from a dense
  * adjacency, or by the caller from its own CSR.  The CSC view and the column
@@ -136,13 +141,15 @@ MSHA_API int msha_graph_fill(const float* adj, int64_t n_rows, int64_t n_cols, c
  * Outputs u (n_rows, heads, feat), lse (n_rows, heads) = log-sum-exp of the row's
  * scores (the backward recomputes att from it) and, if attd != NULL, the
  * post-dropout attention (n_edges, heads).
- * Supported (heads, feat): feat % 4 == 0, heads in {1,2,4,8}, heads*feat in
- * {8..1024} (see msha_edge_attention_supported). */
+ * Supported (heads, feat): heads in {1,2,4,8}, feat in {8,16,32,64,128} (see
+ * msha_edge_attention_supported).  dtype (MSHA_DTYPE_*) is the storage type of the
+ * tables hc / u (and hs, dU, dV, d_hs, table, out below); fp32 arithmetic either way. */
 MSHA_API int msha_edge_attention_supported(int32_t heads, int32_t feat);
-MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat, const float* el,
-                            const float* er, const float* hc, float neg_slope, float drop_p,
-                            uint64_t seed, uint64_t offset, float* u, float* lse, float* attd,
-                            msha_stream_t stream);
+MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
+                                     int32_t dtype, const float* el, const float* er,
+                                     const void* hc, float neg_slope, float drop_p,
+                                     uint64_t seed, uint64_t offset, void* u, float* lse,
+                                     float* attd, msha_stream_t stream);
 
 /* Row half of the backward (autograd of the chain above; Ablation.py:266-274):
  *   g_e  = dU[i]·hc[j] (+ dV[j]·hs[i] when dV != NULL: the v = att^T @ h2 branch,
@@ -155,12 +162,12 @@ MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t
  * gradient row_coef[i] * exp(attd_e) on the attention of row i -- the full MSHA
  * layer's normaliser sums exp(attention_inter) of its batch rows (Ours.py:84-86). */
 MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
-                                 const float* el, const float* er, const float* hc,
-                                 const float* lse, const float* u, const float* dU,
-                                 const float* hs, const float* dV, const float* row_coef,
-                                 float neg_slope,
-                                 float drop_p, uint64_t seed, uint64_t offset, float* d_el,
-                                 float* de, float* attd, float* d_hs, msha_stream_t stream);
+                                          int32_t dtype, const float* el, const float* er,
+                                          const void* hc, const float* lse, const void* u,
+                                          const void* dU, const void* hs, const void* dV,
+                                          const float* row_coef, float neg_slope, float drop_p,
+                                          uint64_t seed, uint64_t offset, float* d_el, float* de,
+                                          float* attd, void* d_hs, msha_stream_t stream);
 
 /* Column-side (transposed) aggregate over the CSC view:
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
@@ -169,9 +176,9 @@ MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, in
  * d_er = colsum(de).  Long columns are split into chunks whose partial sums are
  * added in chunk order: deterministic, no atomics. */
 MSHA_API size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);
-MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat, const float* w,
-                       const float* x, const float* table, float* out, float* out_x, void* ws,
-                       size_t ws_bytes, msha_stream_t stream);
+MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype,
+                                const float* w, const float* x, const void* table, void* out,
+                                float* out_x, void* ws, size_t ws_bytes, msha_stream_t stream);
 
 /* ----------------------------------------------- GraphAttentionLayer (GAL) --- */
 /* GAT.py:20-35 / Ablation.py:100-115.  The layer's score is constant along a row
@@ -221,6 +228,28 @@ MSHA_API int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t fe
                                  const float* ar, float* h, float* el, float* er,
                                  msha_stream_t stream);
 
+/* bf16 projections (config C3: the same model in bf16), v_mfma_f32_16x16x32_bf16 with
+ * fp32 accumulation.  A, B bf16 with element strides as msha_gemm_f32; each operand
+ * needs one unit stride (its extent along it a multiple of 8; the other stride a
+ * multiple of 8; 16-byte aligned base), else MSHA_ERR_UNSUPPORTED.  C (ldc, N
+ * multiples of 8) is fp32 or bf16 (c_dtype).  ho_operand 0 / 1 reads A / B as
+ * X + de (x) a [+ de2 (x) a2] (as msha_gemm_f32_head_outer; feat % 8 == 0, A
+ * k-contiguous / B n-contiguous), -1 = none.  splits > 1: deterministic split-K with
+ * an fp32 slab workspace of msha_gemm_bf16_workspace_size(M, N, splits) bytes. */
+MSHA_API size_t msha_gemm_bf16_workspace_size(int64_t M, int64_t N, int32_t splits);
+MSHA_API int msha_gemm_bf16(int64_t M, int64_t N, int64_t K, const void* A, int64_t sAm,
+                            int64_t sAk, const void* B, int64_t sBk, int64_t sBn, void* C,
+                            int64_t ldc, int32_t c_dtype, int32_t splits, void* ws,
+                            size_t ws_bytes, int32_t ho_operand, int32_t heads, int32_t feat,
+                            const float* de, const float* a, const float* de2, const float* a2,
+                            msha_stream_t stream);
+/* msha_project_scores on bf16 X (M x K) and W (K x heads*feat): h bf16, el / er fp32
+ * from the fp32 accumulators.  K, heads*feat multiples of 8. */
+MSHA_API int msha_project_scores_bf16(int64_t M, int64_t K, int32_t heads, int32_t feat,
+                                      const void* X, const void* W, const float* al,
+                                      const float* ar, void* h, float* el, float* er,
+                                      msha_stream_t stream);
+
 /* out = dh + de (x) a [+ de2 (x) a2]  (rows x heads*feat; de (rows, heads), a (heads, feat)):
  * the gradient reaching h through el = h . a (the backward of msha_project_scores). */
 MSHA_API int msha_add_head_outer(int64_t rows, int32_t heads, int32_t feat, const float* dh,
@@ -231,9 +260,9 @@ MSHA_API int msha_add_head_outer(int64_t rows, int32_t heads, int32_t feat, cons
  * out1[h, f] = sum_r s1[r, h] h[r, h, f] (and out2 with s2); deterministic row-block
  * partials.  Workspace: msha_head_colsum_workspace_size(rows, heads, feat). */
 MSHA_API size_t msha_head_colsum_workspace_size(int64_t rows, int32_t heads, int32_t feat);
-MSHA_API int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, const float* s1,
-                              const float* s2, const float* T, float* out1, float* out2,
-                              void* ws, size_t ws_bytes, msha_stream_t stream);
+MSHA_API int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, int32_t dtype,
+                              const float* s1, const float* s2, const void* T, float* out1,
+                              float* out2, void* ws, size_t ws_bytes, msha_stream_t stream);
 
 /* ----------------------------------------------------------- link scoring --- */
 /* LLP.py:104-115 LinkPredictor with the caller's gather (LLP.py:233) fused:
@@ -274,11 +303,11 @@ MSHA_API int msha_pair_hadamard(int64_t n_pairs, int32_t feat, const float* G, i
  * keeps the per-batch statistics for the backward.  Dropout of att3/att4 uses Philox
  * offsets offset+1+2h / offset+2+2h on the dense (B, N) index. */
 MSHA_API int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, int64_t B,
-                                 const int64_t* src, int32_t heads, int32_t feat,
-                                 const float* h2, const float* a3s, const float* a4s,
+                                 const int64_t* src, int32_t heads, int32_t feat, int32_t dtype,
+                                 const void* h2, const float* a3s, const float* a4s,
                                  const float* el, const float* er, const float* lse,
-                                 const float* u_inter, float neg_slope, float drop_p,
-                                 uint64_t seed, uint64_t offset, float* bstat, float* u_out,
+                                 const void* u_inter, float neg_slope, float drop_p,
+                                 uint64_t seed, uint64_t offset, float* bstat, void* u_out,
                                  msha_stream_t stream);
 /* Backward, two stages around msha_edge_attention_bwd_rows:
  *   stage 0: G (B, 2, heads*feat) = group sums of dropout * dU; bgrad (B, heads, 4);
@@ -290,12 +319,12 @@ MSHA_API int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, in
 MSHA_API size_t msha_ours_workspace_size(const msha_groups* grp, int64_t B, int32_t heads,
                                          int32_t feat);
 MSHA_API int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, int64_t B,
-                                 const int64_t* src, int32_t heads, int32_t feat,
-                                 const float* h2, const float* a3s, const float* a4s,
-                                 const float* bstat, const float* dU, int32_t stage,
+                                 const int64_t* src, int32_t heads, int32_t feat, int32_t dtype,
+                                 const void* h2, const float* a3s, const float* a4s,
+                                 const float* bstat, const void* dU, int32_t stage,
                                  float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
                                  float* G, float* bgrad, float* row_coef, float* da3s,
-                                 float* da4s, float* d_hs, void* ws, size_t ws_bytes,
+                                 float* da4s, void* d_hs, void* ws, size_t ws_bytes,
                                  msha_stream_t stream);
 
 #ifdef __cplusplus

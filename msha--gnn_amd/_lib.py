@@ -61,12 +61,12 @@ SIGNATURES = {
     "msha_graph_count": (C.c_int, [P, I64, I64, P, P, P, P, SZ, P]),
     "msha_graph_fill": (C.c_int, [P, I64, I64, P, P, P, P, P, P, P, SZ, P]),
     "msha_edge_attention_supported": (C.c_int, [I32, I32]),
-    "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, P, P, P, F32, F32, U64, U64, P, P, P,
-                                          P]),
-    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, P, P, P, F32,
+    "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P, P,
+                                          P, P]),
+    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32,
                                                F32, U64, U64, P, P, P, P, P]),
     "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
-    "msha_csc_aggregate": (C.c_int, [GP, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "msha_csc_aggregate": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),
     "msha_gal_bwd": (C.c_int, [GP, P, P, F32, U64, U64, P, P]),
     "msha_gemm_workspace_size": (SZ, [I64, I64, I32]),
@@ -77,17 +77,21 @@ SIGNATURES = {
                                            I32, P, SZ, I32, I32, I32, P, P, P, P, P]),
     "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
     "msha_head_colsum_workspace_size": (SZ, [I64, I32, I32]),
-    "msha_head_colsum": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "msha_head_colsum": (C.c_int, [I64, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "msha_gemm_bf16_workspace_size": (SZ, [I64, I64, I32]),
+    "msha_gemm_bf16": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, P, SZ,
+                                 I32, I32, I32, P, P, P, P, P]),
+    "msha_project_scores_bf16": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
     "msha_pair_linear": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64, U64,
                                    P, P]),
     "msha_pair_inner_fwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
     "msha_pair_inner_bwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P, P]),
     "msha_pair_mlp_dz": (C.c_int, [I64, P, P, F32, I32, P, P]),
     "msha_pair_hadamard": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P]),
-    "msha_ours_intra_fwd": (C.c_int, [GP, GRP, I64, P, I32, I32, P, P, P, P, P, P, P, F32, F32,
+    "msha_ours_intra_fwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, P, P, F32, F32,
                                       U64, U64, P, P, P]),
     "msha_ours_workspace_size": (SZ, [GRP, I64, I32, I32]),
-    "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, P, P, P, P, P, I32, F32, F32,
+    "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, I32, F32, F32,
                                       U64, U64, P, P, P, P, P, P, P, SZ, P]),
 }
 
@@ -113,7 +117,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.msha_abi_version() != 1:
+    if lib.msha_abi_version() != 2:
         raise MshaLibraryError("ABI version mismatch")
     _lib = lib
     return lib

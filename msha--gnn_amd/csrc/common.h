@@ -66,6 +66,84 @@ __device__ __forceinline__ float4 f4_xor_add(float4 v, int o) {
 
 __device__ __forceinline__ float lrelu(float x, float slope) { return x > 0.f ? x : x * slope; }
 
+// ---- node-table storage types: fp32 or bf16 (MSHA_DTYPE_*), fp32 arithmetic ----
+typedef __bf16 bf16_t;
+
+// 16 bytes of a table row held as fp32 in registers: 4 fp32 or 8 bf16 elements
+template <typename T>
+struct Pk {
+  static constexpr int V = 16 / (int)sizeof(T);
+  float v[V];
+};
+
+template <typename T>
+__device__ __forceinline__ Pk<T> pk_zero() {
+  Pk<T> r;
+#pragma unroll
+  for (int i = 0; i < Pk<T>::V; ++i) r.v[i] = 0.f;
+  return r;
+}
+
+__device__ __forceinline__ Pk<float> pk_load(const float* p) {
+  const float4 x = *reinterpret_cast<const float4*>(p);
+  Pk<float> r;
+  r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
+  return r;
+}
+__device__ __forceinline__ Pk<bf16_t> pk_load(const bf16_t* p) {
+  const uint4 x = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  Pk<bf16_t> r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r.v[2 * i] = __uint_as_float(w[i] << 16);
+    r.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+  return r;
+}
+__device__ __forceinline__ void pk_store(float* p, const Pk<float>& a) {
+  *reinterpret_cast<float4*>(p) = make_float4(a.v[0], a.v[1], a.v[2], a.v[3]);
+}
+// round-to-nearest-even (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16_t l = (bf16_t)lo, h = (bf16_t)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, l) | ((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+}
+__device__ __forceinline__ void pk_store(bf16_t* p, const Pk<bf16_t>& a) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(a.v[0], a.v[1]), pack_bf16x2(a.v[2], a.v[3]),
+                                            pack_bf16x2(a.v[4], a.v[5]), pack_bf16x2(a.v[6], a.v[7]));
+}
+template <typename T>
+__device__ __forceinline__ Pk<T> pk_fma(float s, const Pk<T>& a, Pk<T> c) {
+#pragma unroll
+  for (int i = 0; i < Pk<T>::V; ++i) c.v[i] = fmaf(s, a.v[i], c.v[i]);
+  return c;
+}
+template <typename T>
+__device__ __forceinline__ Pk<T> pk_scale(Pk<T> a, float s) {
+#pragma unroll
+  for (int i = 0; i < Pk<T>::V; ++i) a.v[i] *= s;
+  return a;
+}
+template <typename T>
+__device__ __forceinline__ float pk_dot(const Pk<T>& a, const Pk<T>& b) {
+  float r = a.v[Pk<T>::V - 1] * b.v[Pk<T>::V - 1];
+#pragma unroll
+  for (int i = Pk<T>::V - 2; i >= 0; --i) r = fmaf(a.v[i], b.v[i], r);
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ Pk<T> pk_xor_add(Pk<T> a, int o) {
+#pragma unroll
+  for (int i = 0; i < Pk<T>::V; ++i) a.v[i] += __shfl_xor(a.v[i], o);
+  return a;
+}
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16_t x) { return (float)x; }
+template <typename T>
+__device__ __forceinline__ T from_f32(float x) { return (T)x; }
+
 // ---- counter-based dropout (Philox4x32-10) ----
 // keep(i) = philox(seed; counter = {i, offset}).x >= p * 2^32.  Deterministic per
 // element index, so forward and backward regenerate the same mask without storing it.

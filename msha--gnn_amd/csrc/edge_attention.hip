@@ -22,37 +22,35 @@
 
 namespace msha {
 
-template <int H, int F>
+template <int H, int F, typename T>
 struct Geo {
+  static constexpr int V = Pk<T>::V;        // elements per 16-byte chunk (4 fp32 / 8 bf16)
   static constexpr int D = H * F;
-  static constexpr int NQ = D / 4;
+  static constexpr int NQ = D / V;          // chunks per feature row
   static constexpr int QPL = NQ > 64 ? NQ / 64 : 1;
   static constexpr int EPI = NQ >= 64 ? 1 : 64 / NQ;
   static constexpr int CE = 64 / H;
-  static constexpr int QH = F / 4;
-  static_assert(F % 4 == 0, "feat must be a multiple of 4");
+  static constexpr int QH = F / V;          // chunks per head
+  static_assert(F % V == 0, "feat must be a multiple of the 16-byte chunk");
   static_assert(H >= 1 && H <= 64 && (64 % H) == 0, "heads must divide 64");
   static_assert(CE % EPI == 0, "score chunk must cover whole gather groups");
-  static_assert(QH <= 64 && (64 % QH) == 0, "quads per head must divide 64");
+  static_assert(QH <= 64 && (64 % QH) == 0, "chunks per head must divide 64");
 };
 
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-
-// quad index (within the feature row) owned by this lane for slot k
+// chunk index (within the feature row) owned by this lane for slot k
 template <class G>
 __device__ __forceinline__ int quad_of(int lane, int k) {
   return G::QPL == 1 ? (lane % G::NQ) : (lane + 64 * k);
 }
 
 // ------------------------------------------------------------------ forward ---
-template <int H, int F>
+template <int H, int F, typename T>
 __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
-    const float* __restrict__ er, const float* __restrict__ hc, float slope, Dropout dp,
-    float* __restrict__ u, float* __restrict__ lse, float* __restrict__ attd) {
-  using G = Geo<H, F>;
+    const float* __restrict__ er, const T* __restrict__ hc, float slope, Dropout dp,
+    T* __restrict__ u, float* __restrict__ lse, float* __restrict__ attd) {
+  using G = Geo<H, F, T>;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
   const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
@@ -64,9 +62,9 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     const bool virt = rowflag != nullptr && rowflag[row] != 0;
     const float elh = el[row * H + h_s];
     float m = -INFINITY, l = 0.f;
-    float4 acc[G::QPL];
+    Pk<T> acc[G::QPL];
 #pragma unroll
-    for (int k = 0; k < G::QPL; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < G::QPL; ++k) acc[k] = pk_zero<T>();
 
     for (int32_t cs = start; cs < end; cs += G::CE) {
       const int32_t e = cs + e_s;
@@ -83,7 +81,7 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 #pragma unroll
       for (int k = 0; k < G::QPL; ++k) {
         const int hd = quad_of<G>(lane, k) / G::QH;
-        acc[k] = f4_scale(acc[k], __shfl(alpha, hd));
+        acc[k] = pk_scale(acc[k], __shfl(alpha, hd));
       }
       const int nvalid = min(G::CE, (int)(end - cs));
 #pragma unroll
@@ -95,20 +93,20 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
         for (int k = 0; k < G::QPL; ++k) {
           const int q = quad_of<G>(lane, k);
           const float wq = __shfl(w, ei * H + q / G::QH);
-          if (ei < nvalid) acc[k] = f4_fma(wq, ld4(hc + (int64_t)jq * G::D + 4 * q), acc[k]);
+          if (ei < nvalid) acc[k] = pk_fma(wq, pk_load(hc + (int64_t)jq * G::D + G::V * q), acc[k]);
         }
       }
     }
     if (G::EPI > 1) {
 #pragma unroll
-      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = f4_xor_add(acc[0], o);
+      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = pk_xor_add(acc[0], o);
     }
 #pragma unroll
     for (int k = 0; k < G::QPL; ++k) {
       const int q = quad_of<G>(lane, k);
       const float lk = __shfl(l, q / G::QH);
       const float inv = lk > 0.f ? 1.f / lk : 0.f;
-      if (g_e == 0) st4(u + row * G::D + 4 * q, f4_scale(acc[k], inv));
+      if (g_e == 0) pk_store(u + row * G::D + G::V * q, pk_scale(acc[k], inv));
     }
     const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
     if (lane < H) lse[row * H + lane] = lse_h;
@@ -126,22 +124,22 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 }
 
 // --------------------------------------------------------------- backward rows ---
-template <int H, int F, bool DV>
+template <int H, int F, typename T, bool DV>
 __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
-    const float* __restrict__ er, const float* __restrict__ hc, const float* __restrict__ lse,
-    const float* __restrict__ u, const float* __restrict__ dU, const float* __restrict__ hs,
-    const float* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
+    const float* __restrict__ er, const T* __restrict__ hc, const float* __restrict__ lse,
+    const T* __restrict__ u, const T* __restrict__ dU, const T* __restrict__ hs,
+    const T* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
     float* __restrict__ d_el, float* __restrict__ de, float* __restrict__ attd,
-    float* __restrict__ d_hs) {
-  using G = Geo<H, F>;
+    T* __restrict__ d_hs) {
+  using G = Geo<H, F, T>;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
   const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // lane (in the gather layout) holding the first quad of head h_s, and its slot
+  // lane (in the gather layout) holding the first chunk of head h_s, and its slot
   const int dsrc_k = (h_s * G::QH) / 64;
   const int dsrc_l = (h_s * G::QH) % 64;
 
@@ -150,20 +148,20 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     const bool virt = rowflag != nullptr && rowflag[row] != 0;
     const float elh = el[row * H + h_s];
     const float lseh = lse[row * H + h_s];
-    float4 dUq[G::QPL], hsq[G::QPL];
+    Pk<T> dUq[G::QPL], hsq[G::QPL];
     float dpart[G::QPL];
 #pragma unroll
     for (int k = 0; k < G::QPL; ++k) {
       const int q = quad_of<G>(lane, k);
-      dUq[k] = ld4(dU + row * G::D + 4 * q);
-      dpart[k] = f4_dot(dUq[k], ld4(u + row * G::D + 4 * q));
-      hsq[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      dUq[k] = pk_load(dU + row * G::D + G::V * q);
+      dpart[k] = pk_dot(dUq[k], pk_load(u + row * G::D + G::V * q));
+      hsq[k] = pk_zero<T>();
     }
     if (DV) {
       // w_i = sum_e attd_e dV[j]   (== d hs_i of the v-branch)
-      float4 wacc[G::QPL];
+      Pk<T> wacc[G::QPL];
 #pragma unroll
-      for (int k = 0; k < G::QPL; ++k) wacc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < G::QPL; ++k) wacc[k] = pk_zero<T>();
       for (int32_t cs = start; cs < end; cs += G::CE) {
         const int32_t e = cs + e_s;
         const bool valid = e < end;
@@ -183,20 +181,21 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
           for (int k = 0; k < G::QPL; ++k) {
             const int q = quad_of<G>(lane, k);
             const float wq = __shfl(w, ei * H + q / G::QH);
-            if (ei < nvalid) wacc[k] = f4_fma(wq, ld4(dV + (int64_t)jq * G::D + 4 * q), wacc[k]);
+            if (ei < nvalid)
+              wacc[k] = pk_fma(wq, pk_load(dV + (int64_t)jq * G::D + G::V * q), wacc[k]);
           }
         }
       }
       if (G::EPI > 1) {
 #pragma unroll
-        for (int o = G::NQ; o < 64; o <<= 1) wacc[0] = f4_xor_add(wacc[0], o);
+        for (int o = G::NQ; o < 64; o <<= 1) wacc[0] = pk_xor_add(wacc[0], o);
       }
 #pragma unroll
       for (int k = 0; k < G::QPL; ++k) {
         const int q = quad_of<G>(lane, k);
-        if (g_e == 0) st4(d_hs + row * G::D + 4 * q, wacc[k]);
-        hsq[k] = ld4(hs + row * G::D + 4 * q);
-        dpart[k] += f4_dot(hsq[k], wacc[k]);
+        if (g_e == 0) pk_store(d_hs + row * G::D + G::V * q, wacc[k]);
+        hsq[k] = pk_load(hs + row * G::D + G::V * q);
+        dpart[k] += pk_dot(hsq[k], wacc[k]);
       }
     }
     // D_h = dU_i.u_i (+ hs_i.w_i) per head, delivered to the score layout
@@ -248,8 +247,8 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
           const int q = quad_of<G>(lane, k);
           float t = 0.f;
           if (ei < nvalid) {
-            t = f4_dot(dUq[k], ld4(hc + (int64_t)jq * G::D + 4 * q));
-            if (DV) t += f4_dot(hsq[k], ld4(dV + (int64_t)jq * G::D + 4 * q));
+            t = pk_dot(dUq[k], pk_load(hc + (int64_t)jq * G::D + G::V * q));
+            if (DV) t += pk_dot(hsq[k], pk_load(dV + (int64_t)jq * G::D + G::V * q));
           }
           t = group_sum<G::QH>(t);
           const float cand = __shfl(t, srcl);
@@ -271,15 +270,17 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
 }
 
 // ------------------------------------------------------- column (CSC) aggregate ---
-template <int H, int F, bool HASX>
+// Whole columns write the table type T directly; chunks of multi-chunk columns
+// write fp32 partials that csc_combine adds in chunk order.
+template <int H, int F, typename T, bool HASX>
 __global__ void __launch_bounds__(256) csc_aggregate_kernel(
     const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
     const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid,
-    const float* __restrict__ w, const float* __restrict__ x, const float* __restrict__ table,
-    float* __restrict__ out, float* __restrict__ out_x, float* __restrict__ part,
+    const float* __restrict__ w, const float* __restrict__ x, const T* __restrict__ table,
+    T* __restrict__ out, float* __restrict__ out_x, float* __restrict__ part,
     float* __restrict__ part_x) {
-  using G = Geo<H, F>;
+  using G = Geo<H, F, T>;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
   const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
@@ -289,9 +290,9 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
   for (int64_t c = wave; c < n_chunks; c += nwaves) {
     const int32_t jc = chunk_col[c], s0 = chunk_start[c], s1 = chunk_end[c];
     const bool whole = s0 == colptr[jc] && s1 == colptr[jc + 1];
-    float4 acc[G::QPL];
+    Pk<T> acc[G::QPL];
 #pragma unroll
-    for (int k = 0; k < G::QPL; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < G::QPL; ++k) acc[k] = pk_zero<T>();
     float xacc = 0.f;
     for (int32_t cs = s0; cs < s1; cs += G::CE) {
       const int32_t slot = cs + e_s;
@@ -310,18 +311,27 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
         for (int k = 0; k < G::QPL; ++k) {
           const int q = quad_of<G>(lane, k);
           const float wq = __shfl(wv, ei * H + q / G::QH);
-          if (ei < nvalid) acc[k] = f4_fma(wq, ld4(table + (int64_t)iq * G::D + 4 * q), acc[k]);
+          if (ei < nvalid) acc[k] = pk_fma(wq, pk_load(table + (int64_t)iq * G::D + G::V * q), acc[k]);
         }
       }
     }
     if (G::EPI > 1) {
 #pragma unroll
-      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = f4_xor_add(acc[0], o);
+      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = pk_xor_add(acc[0], o);
     }
-    float* dst = whole ? out + (int64_t)jc * G::D : part + c * G::D;
 #pragma unroll
     for (int k = 0; k < G::QPL; ++k) {
-      if (g_e == 0) st4(dst + 4 * quad_of<G>(lane, k), acc[k]);
+      if (g_e != 0) continue;
+      const int q = quad_of<G>(lane, k);
+      if (whole) {
+        pk_store(out + (int64_t)jc * G::D + G::V * q, acc[k]);
+      } else {
+        float* dst = part + c * G::D + G::V * q;
+#pragma unroll
+        for (int i = 0; i < G::V; i += 4)
+          *reinterpret_cast<float4*>(dst + i) =
+              make_float4(acc[k].v[i], acc[k].v[i + 1], acc[k].v[i + 2], acc[k].v[i + 3]);
+      }
     }
     if (HASX) {
       xacc = wave_xor_sum<H>(xacc);
@@ -331,10 +341,11 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
 }
 
 // multi-chunk columns: add the chunk partials in chunk order
+template <typename T>
 __global__ void __launch_bounds__(256) csc_combine_kernel(
     const int32_t* __restrict__ multi_col, const int32_t* __restrict__ multi_first,
     const int32_t* __restrict__ multi_count, int64_t n_multi, int D, int H,
-    const float* __restrict__ part, const float* __restrict__ part_x, float* __restrict__ out,
+    const float* __restrict__ part, const float* __restrict__ part_x, T* __restrict__ out,
     float* __restrict__ out_x) {
   const int W = D + (part_x != nullptr ? H : 0);
   const int64_t total = n_multi * W;
@@ -346,7 +357,7 @@ __global__ void __launch_bounds__(256) csc_combine_kernel(
     float s = 0.f;
     if (f < D) {
       for (int k = 0; k < cnt; ++k) s += part[(int64_t)(first + k) * D + f];
-      out[(int64_t)jc * D + f] = s;
+      out[(int64_t)jc * D + f] = from_f32<T>(s);
     } else {
       const int h = f - D;
       for (int k = 0; k < cnt; ++k) s += part_x[(int64_t)(first + k) * H + h];
@@ -396,60 +407,88 @@ extern "C" int msha_edge_attention_supported(int32_t heads, int32_t feat) {
   return shape_supported(heads, feat) ? 1 : 0;
 }
 
+static bool dtype_ok(int32_t dtype, int32_t feat) {
+  return dtype == MSHA_DTYPE_F32 || (dtype == MSHA_DTYPE_BF16 && feat % 8 == 0);
+}
+
 extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
-                                       const float* el, const float* er, const float* hc,
-                                       float neg_slope, float drop_p, uint64_t seed,
-                                       uint64_t offset, float* u, float* lse, float* attd,
-                                       msha_stream_t stream) {
+                                       int32_t dtype, const float* el, const float* er,
+                                       const void* hc, float neg_slope, float drop_p,
+                                       uint64_t seed, uint64_t offset, void* u, float* lse,
+                                       float* attd, msha_stream_t stream) {
   if (int rc = check_graph(g, false)) return rc;
   MSHA_ARG_CHECK(el && er && hc && u && lse, "edge_attention_fwd: null pointer");
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_fwd: p must be in [0,1]");
-  if (!shape_supported(heads, feat))
-    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: unsupported (heads, feat)");
+  if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: unsupported (heads, feat, dtype)");
   const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
-#define X(h, f)                                                                             \
-  if (heads == h && feat == f)                                                              \
-    hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f>), wave_grid(g->n_rows), dim3(256), 0, s, \
-                       g->rowptr, g->col, g->rowflag, g->n_rows, el, er, hc, neg_slope, dp, \
-                       u, lse, attd);
+#define X(h, f)                                                                                \
+  if (heads == h && feat == f) {                                                               \
+    if (dtype == MSHA_DTYPE_BF16) {                                                            \
+      if constexpr (f % 8 == 0)                                                                \
+        hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, bf16_t>), wave_grid(g->n_rows),         \
+                           dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,  \
+                           (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u, lse, attd);           \
+    } else {                                                                                   \
+      hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, float>), wave_grid(g->n_rows), dim3(256), \
+                         0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,               \
+                         (const float*)hc, neg_slope, dp, (float*)u, lse, attd);               \
+    }                                                                                          \
+  }
   MSHA_FOR_EACH_SHAPE(X)
 #undef X
   return check_launch("edge_attention_fwd");
 }
 
+template <typename T>
+static void launch_bwd_rows(const msha_graph* g, int heads, int feat, const float* el,
+                            const float* er, const void* hc, const float* lse, const void* u,
+                            const void* dU, const void* hs, const void* dV, const float* row_coef,
+                            float neg_slope, const Dropout& dp, float* d_el, float* de,
+                            float* attd, void* d_hs, hipStream_t s) {
+#define X(h, f)                                                                                  \
+  if (heads == h && feat == f) {                                                                 \
+    if constexpr (f % Pk<T>::V == 0) {                                                           \
+      if (dV)                                                                                    \
+        hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, T, true>), wave_grid(g->n_rows),     \
+                           dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,    \
+                           (const T*)hc, lse, (const T*)u, (const T*)dU, (const T*)hs,           \
+                           (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, (T*)d_hs);     \
+      else                                                                                       \
+        hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, T, false>), wave_grid(g->n_rows),    \
+                           dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,    \
+                           (const T*)hc, lse, (const T*)u, (const T*)dU, (const T*)hs,           \
+                           (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, (T*)d_hs);     \
+    }                                                                                            \
+  }
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+}
+
 extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
-                                            const float* el, const float* er, const float* hc,
-                                            const float* lse, const float* u, const float* dU,
-                                            const float* hs, const float* dV,
+                                            int32_t dtype, const float* el, const float* er,
+                                            const void* hc, const float* lse, const void* u,
+                                            const void* dU, const void* hs, const void* dV,
                                             const float* row_coef, float neg_slope,
                                             float drop_p, uint64_t seed, uint64_t offset,
-                                            float* d_el, float* de, float* attd, float* d_hs,
+                                            float* d_el, float* de, float* attd, void* d_hs,
                                             msha_stream_t stream) {
   if (int rc = check_graph(g, false)) return rc;
   MSHA_ARG_CHECK(el && er && hc && lse && u && dU && d_el && de && attd,
                  "edge_attention_bwd_rows: null pointer");
   MSHA_ARG_CHECK(dV == nullptr || (hs && d_hs), "edge_attention_bwd_rows: dV needs hs and d_hs");
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_bwd_rows: p must be in [0,1]");
-  if (!shape_supported(heads, feat))
-    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_rows: unsupported (heads, feat)");
+  if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_rows: unsupported (heads, feat, dtype)");
   const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
-#define X(h, f)                                                                               \
-  if (heads == h && feat == f) {                                                              \
-    if (dV)                                                                                   \
-      hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, true>), wave_grid(g->n_rows),       \
-                         dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,   \
-                         hc, lse, u, dU, hs, dV, row_coef, neg_slope, dp, d_el, de, attd,     \
-                         d_hs);                                                               \
-    else                                                                                      \
-      hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, false>), wave_grid(g->n_rows),      \
-                         dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,   \
-                         hc, lse, u, dU, hs, dV, row_coef, neg_slope, dp, d_el, de, attd,     \
-                         d_hs);                                                               \
-  }
-  MSHA_FOR_EACH_SHAPE(X)
-#undef X
+  if (dtype == MSHA_DTYPE_BF16)
+    launch_bwd_rows<bf16_t>(g, heads, feat, el, er, hc, lse, u, dU, hs, dV, row_coef, neg_slope,
+                            dp, d_el, de, attd, d_hs, s);
+  else
+    launch_bwd_rows<float>(g, heads, feat, el, er, hc, lse, u, dU, hs, dV, row_coef, neg_slope,
+                           dp, d_el, de, attd, d_hs, s);
   return check_launch("edge_attention_bwd_rows");
 }
 
@@ -460,14 +499,45 @@ extern "C" size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t
   return (size_t)g->n_chunks * per * sizeof(float) + 256;
 }
 
+template <typename T>
+static void launch_csc(const msha_graph* g, int heads, int feat, const float* w, const float* x,
+                       const void* table, void* out, float* out_x, float* part, float* part_x,
+                       hipStream_t s) {
+#define X(h, f)                                                                                 \
+  if (heads == h && feat == f) {                                                                \
+    if constexpr (f % Pk<T>::V == 0) {                                                          \
+      if (x)                                                                                    \
+        hipLaunchKernelGGL((csc_aggregate_kernel<h, f, T, true>), wave_grid(g->n_chunks),       \
+                           dim3(256), 0, s, g->chunk_col, g->chunk_start, g->chunk_end,         \
+                           g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x,                \
+                           (const T*)table, (T*)out, out_x, part, part_x);                      \
+      else                                                                                      \
+        hipLaunchKernelGGL((csc_aggregate_kernel<h, f, T, false>), wave_grid(g->n_chunks),      \
+                           dim3(256), 0, s, g->chunk_col, g->chunk_start, g->chunk_end,         \
+                           g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x,                \
+                           (const T*)table, (T*)out, out_x, part, part_x);                      \
+    }                                                                                           \
+  }
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+  if (g->n_multi > 0) {
+    const int64_t D = (int64_t)heads * feat;
+    const int64_t W = D + (x ? heads : 0);
+    hipLaunchKernelGGL(csc_combine_kernel<T>, dim3(grid_for(g->n_multi * W, 256, 8192)),
+                       dim3(256), 0, s, g->multi_col, g->multi_first, g->multi_count, g->n_multi,
+                       (int)D, heads, part, x ? part_x : nullptr, (T*)out, out_x);
+  }
+}
+
 extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat,
-                                  const float* w, const float* x, const float* table, float* out,
-                                  float* out_x, void* ws, size_t ws_bytes, msha_stream_t stream) {
+                                  int32_t dtype, const float* w, const float* x,
+                                  const void* table, void* out, float* out_x, void* ws,
+                                  size_t ws_bytes, msha_stream_t stream) {
   if (int rc = check_graph(g, true)) return rc;
   MSHA_ARG_CHECK(w && table && out, "csc_aggregate: null pointer");
   MSHA_ARG_CHECK(x == nullptr || out_x != nullptr, "csc_aggregate: x needs out_x");
-  if (!shape_supported(heads, feat))
-    return fail(MSHA_ERR_UNSUPPORTED, "csc_aggregate: unsupported (heads, feat)");
+  if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "csc_aggregate: unsupported (heads, feat, dtype)");
   const int64_t D = (int64_t)heads * feat;
   float* part = nullptr;
   float* part_x = nullptr;
@@ -478,26 +548,9 @@ extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t fe
     part_x = part + g->n_chunks * D;
   }
   hipStream_t s = (hipStream_t)stream;
-#define X(h, f)                                                                                \
-  if (heads == h && feat == f) {                                                               \
-    if (x)                                                                                     \
-      hipLaunchKernelGGL((csc_aggregate_kernel<h, f, true>), wave_grid(g->n_chunks), dim3(256), \
-                         0, s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,        \
-                         g->colptr, g->csc_row, g->csc_eid, w, x, table, out, out_x, part,     \
-                         part_x);                                                              \
-    else                                                                                       \
-      hipLaunchKernelGGL((csc_aggregate_kernel<h, f, false>), wave_grid(g->n_chunks),          \
-                         dim3(256), 0, s, g->chunk_col, g->chunk_start, g->chunk_end,          \
-                         g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x, table, out,     \
-                         out_x, part, part_x);                                                 \
-  }
-  MSHA_FOR_EACH_SHAPE(X)
-#undef X
-  if (g->n_multi > 0) {
-    const int64_t W = D + (x ? heads : 0);
-    hipLaunchKernelGGL(csc_combine_kernel, dim3(grid_for(g->n_multi * W, 256, 8192)), dim3(256),
-                       0, s, g->multi_col, g->multi_first, g->multi_count, g->n_multi, (int)D,
-                       (int)heads, part, x ? part_x : nullptr, out, out_x);
-  }
+  if (dtype == MSHA_DTYPE_BF16)
+    launch_csc<bf16_t>(g, heads, feat, w, x, table, out, out_x, part, part_x, s);
+  else
+    launch_csc<float>(g, heads, feat, w, x, table, out, out_x, part, part_x, s);
   return check_launch("csc_aggregate");
 }

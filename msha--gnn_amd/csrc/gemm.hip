@@ -491,47 +491,54 @@ static bool vec_ok(const GemmArgs& p) {
 // order (deterministic).
 constexpr int kColsumRows = 64;
 
-template <int VEC>
-struct ColVec;
-template <>
-struct ColVec<4> {
-  using T = float4;
-  static __device__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-  static __device__ T fma(float a, T x, T c) { return f4_fma(a, x, c); }
-  static __device__ T add(T a, T b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+// N consecutive elements of one row, widened to fp32
+template <int N>
+struct Fv {
+  float v[N];
 };
-template <>
-struct ColVec<1> {
-  using T = float;
-  static __device__ T zero() { return 0.f; }
-  static __device__ T fma(float a, T x, T c) { return fmaf(a, x, c); }
-  static __device__ T add(T a, T b) { return a + b; }
-};
+__device__ __forceinline__ Fv<4> fv_load(const float* p, Fv<4>*) {
+  const float4 x = *reinterpret_cast<const float4*>(p);
+  return Fv<4>{{x.x, x.y, x.z, x.w}};
+}
+__device__ __forceinline__ Fv<1> fv_load(const float* p, Fv<1>*) { return Fv<1>{{*p}}; }
+__device__ __forceinline__ Fv<8> fv_load(const bf16_t* p, Fv<8>*) {
+  const Pk<bf16_t> x = pk_load(p);
+  Fv<8> r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = x.v[i];
+  return r;
+}
 
-// grid (row blocks, column tiles of <= 256 vectors); D % VEC == 0
-template <int VEC>
+// grid (row blocks, column tiles of <= 256 vectors); D % N == 0
+template <typename T, int N>
 __global__ void __launch_bounds__(256) head_colsum_partial_kernel(
     int64_t rows, int H, int F, const float* __restrict__ s1, const float* __restrict__ s2,
-    const float* __restrict__ T, float* __restrict__ part) {
-  using V = ColVec<VEC>;
-  using VT = typename V::T;
+    const T* __restrict__ tab, float* __restrict__ part) {
+  using VT = Fv<N>;
   __shared__ VT red[2 * 256];
-  const int D = H * F, QD = D / VEC;
+  const int D = H * F, QD = D / N;
   const int QT = QD < 256 ? QD : 256;  // vectors per column tile
   const int RG = 256 / QT;             // row groups
   const int qi = threadIdx.x % QT, rg = threadIdx.x / QT;
   const int q = blockIdx.y * QT + qi;
   const bool live = rg < RG && q < QD;
-  const int h = live ? (VEC * q) / F : 0;
+  const int h = live ? (N * q) / F : 0;
   const int64_t r0 = (int64_t)blockIdx.x * kColsumRows;
   const int64_t r1 = min(rows, r0 + kColsumRows);
-  VT a1 = V::zero(), a2 = V::zero();
+  VT a1, a2;
+#pragma unroll
+  for (int i = 0; i < N; ++i) a1.v[i] = a2.v[i] = 0.f;
   if (live) {
 #pragma unroll 4
     for (int64_t r = r0 + rg; r < r1; r += RG) {
-      const VT x = reinterpret_cast<const VT*>(T + r * D)[q];
-      a1 = V::fma(s1[r * H + h], x, a1);
-      if (s2) a2 = V::fma(s2[r * H + h], x, a2);
+      const VT x = fv_load(tab + r * D + N * q, (VT*)nullptr);
+      const float c1 = s1[r * H + h];
+      const float c2 = s2 ? s2[r * H + h] : 0.f;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        a1.v[i] = fmaf(c1, x.v[i], a1.v[i]);
+        a2.v[i] = fmaf(c2, x.v[i], a2.v[i]);
+      }
     }
   }
   red[threadIdx.x] = a1;
@@ -542,14 +549,20 @@ __global__ void __launch_bounds__(256) head_colsum_partial_kernel(
   for (w >>= 1; w >= 1; w >>= 1) {  // fixed-order tree over the row groups
     if (rg < w && rg + w < RG) {
       const int i = rg * QT + qi, j = (rg + w) * QT + qi;
-      red[i] = V::add(red[i], red[j]);
-      red[256 + i] = V::add(red[256 + i], red[256 + j]);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        red[i].v[e] += red[j].v[e];
+        red[256 + i].v[e] += red[256 + j].v[e];
+      }
     }
     __syncthreads();
   }
   if (rg == 0 && q < QD) {
-    reinterpret_cast<VT*>(part + ((int64_t)blockIdx.x * 2 + 0) * D)[q] = red[qi];
-    reinterpret_cast<VT*>(part + ((int64_t)blockIdx.x * 2 + 1) * D)[q] = red[256 + qi];
+#pragma unroll
+    for (int e = 0; e < N; ++e) {
+      part[((int64_t)blockIdx.x * 2 + 0) * D + N * q + e] = red[qi].v[e];
+      part[((int64_t)blockIdx.x * 2 + 1) * D + N * q + e] = red[256 + qi].v[e];
+    }
   }
 }
 
@@ -794,26 +807,33 @@ extern "C" size_t msha_head_colsum_workspace_size(int64_t rows, int32_t heads, i
   return (size_t)nblk * 2 * (size_t)heads * (size_t)feat * sizeof(float);
 }
 
-extern "C" int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, const float* s1,
-                                const float* s2, const float* T, float* out1, float* out2,
-                                void* ws, size_t ws_bytes, msha_stream_t stream) {
+extern "C" int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, int32_t dtype,
+                                const float* s1, const float* s2, const void* T, float* out1,
+                                float* out2, void* ws, size_t ws_bytes, msha_stream_t stream) {
   MSHA_ARG_CHECK(rows > 0 && heads > 0 && feat > 0, "head_colsum: bad sizes");
   MSHA_ARG_CHECK(s1 && T && out1 && ((s2 == nullptr) == (out2 == nullptr)),
                  "head_colsum: null pointer");
   MSHA_ARG_CHECK(ws && ws_bytes >= msha_head_colsum_workspace_size(rows, heads, feat),
                  "head_colsum: workspace too small");
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "head_colsum: bad dtype");
   const int D = heads * feat;
   const int nblk = (int)((rows + kColsumRows - 1) / kColsumRows);
   hipStream_t s = (hipStream_t)stream;
-  const bool v4 = feat % 4 == 0 && ((uintptr_t)T & 15) == 0;
-  const int QD = v4 ? D / 4 : D;
-  const dim3 grid(nblk, (QD + 255) / 256);
-  if (v4)
-    hipLaunchKernelGGL(head_colsum_partial_kernel<4>, grid, dim3(256), 0, s, rows, (int)heads,
-                       (int)feat, s1, s2, T, (float*)ws);
-  else
-    hipLaunchKernelGGL(head_colsum_partial_kernel<1>, grid, dim3(256), 0, s, rows, (int)heads,
-                       (int)feat, s1, s2, T, (float*)ws);
+  if (dtype == MSHA_DTYPE_BF16) {
+    if (feat % 8 != 0 || !aligned16(T))
+      return fail(MSHA_ERR_UNSUPPORTED, "head_colsum: bf16 needs feat % 8 == 0, 16-B aligned T");
+    const dim3 grid(nblk, (D / 8 + 255) / 256);
+    hipLaunchKernelGGL((head_colsum_partial_kernel<bf16_t, 8>), grid, dim3(256), 0, s, rows,
+                       (int)heads, (int)feat, s1, s2, (const bf16_t*)T, (float*)ws);
+  } else if (feat % 4 == 0 && aligned16(T)) {
+    const dim3 grid(nblk, (D / 4 + 255) / 256);
+    hipLaunchKernelGGL((head_colsum_partial_kernel<float, 4>), grid, dim3(256), 0, s, rows,
+                       (int)heads, (int)feat, s1, s2, (const float*)T, (float*)ws);
+  } else {
+    const dim3 grid(nblk, (D + 255) / 256);
+    hipLaunchKernelGGL((head_colsum_partial_kernel<float, 1>), grid, dim3(256), 0, s, rows,
+                       (int)heads, (int)feat, s1, s2, (const float*)T, (float*)ws);
+  }
   hipLaunchKernelGGL(head_colsum_reduce_kernel, dim3((2 * D + 3) / 4), dim3(256), 0, s, nblk,
                      D, (const float*)ws, out1, out2);
   return check_launch("head_colsum");

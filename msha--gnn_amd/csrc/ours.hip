@@ -34,7 +34,7 @@ struct OursArgs {
   const int32_t* gid4;
   const int32_t* gptr4;
   const int32_t* gmem4;
-  const float* h2;   // (N, H, F)
+  const void* h2;    // (N, H, F), fp32 or bf16 (the kernels' T)
   const float* a3s;  // (H, F) = a3[:F] + a3[F:]
   const float* a4s;
   float slope;
@@ -43,6 +43,11 @@ struct OursArgs {
 
 enum { BS_PRE3 = 0, BS_PRE4, BS_E3, BS_E4, BS_SUM, BS_W3, BS_W4, BS_I, BS_N };
 
+template <typename T>
+__device__ __forceinline__ float ldt(const void* p, int64_t i) {
+  return to_f32(reinterpret_cast<const T*>(p)[i]);
+}
+
 __device__ __forceinline__ float intra_drop(const Dropout& d, int kind, int h, uint64_t idx) {
   if (!d.active) return 1.f;
   return philox_x(d.seed, d.offset + 1 + 2 * (uint64_t)h + (uint64_t)kind, idx) >= d.threshold
@@ -50,6 +55,7 @@ __device__ __forceinline__ float intra_drop(const Dropout& d, int kind, int h, u
 }
 
 // ---------------------------------------------------------------------- prep ---
+template <typename T>
 __global__ void __launch_bounds__(256) ours_prep_kernel(
     OursArgs a, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, const float* __restrict__ el,
@@ -66,7 +72,7 @@ __global__ void __launch_bounds__(256) ours_prep_kernel(
   for (int h = 0; h < H; ++h) {
     float p3 = 0.f, p4 = 0.f;
     for (int f = lane; f < F; f += 64) {
-      const float x = a.h2[(i * H + h) * F + f];
+      const float x = ldt<T>(a.h2, (i * H + h) * F + f);
       p3 = fmaf(x, a.a3s[h * F + f], p3);
       p4 = fmaf(x, a.a4s[h * F + f], p4);
     }
@@ -94,9 +100,10 @@ __global__ void __launch_bounds__(256) ours_prep_kernel(
 // ---------------------------------------------------------------- forward ---
 // u_out[n] = u_in[n] + sum_{b: city(src_b) = city(n)} drop * w3_b h2[src_b]
 //                    + sum_{b: prov(src_b) = prov(n)} drop * w4_b h2[src_b]
+template <typename T>
 __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* __restrict__ bstat,
-                                                       const float* __restrict__ u_in,
-                                                       float* __restrict__ u_out) {
+                                                       const T* __restrict__ u_in,
+                                                       T* __restrict__ u_out) {
   const int lane = lane_id();
   const int D = a.H * a.F;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -127,7 +134,7 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
               const int h = d / a.F;
               const float w = bstat[(bb * a.H + h) * BS_N + (kind == 0 ? BS_W3 : BS_W4)] *
                               intra_drop(a.dp, kind, h, (uint64_t)bb * a.N + n);
-              const float x = a.h2[ibb * D + d];
+              const float x = ldt<T>(a.h2, ibb * D + d);
               if (kind == 0) acc3[k] = fmaf(w, x, acc3[k]); else acc4[k] = fmaf(w, x, acc4[k]);
             }
           }
@@ -137,7 +144,7 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 #pragma unroll
     for (int k = 0; k < KD; ++k) {
       const int d = lane + 64 * k;
-      if (d < D) u_out[n * D + d] = u_in[n * D + d] + (acc3[k] + acc4[k]);
+      if (d < D) u_out[n * D + d] = from_f32<T>(to_f32(u_in[n * D + d]) + (acc3[k] + acc4[k]));
     }
   }
 }
@@ -148,8 +155,9 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 // in chunk order: one wave per (b, kind, chunk) keeps thousands of members in flight.
 constexpr int kGatherChunk = 64;
 
+template <typename T>
 __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
-                                                              const float* __restrict__ dU,
+                                                              const T* __restrict__ dU,
                                                               int nck, float* __restrict__ Gp) {
   const int lane = lane_id();
   const int D = a.H * a.F;
@@ -176,7 +184,8 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
       const int d = lane + 64 * k;
       if (d < D) {
         const int h = d / a.F;
-        acc[k] = fmaf(intra_drop(a.dp, kind, h, (uint64_t)b * a.N + n), dU[n * D + d], acc[k]);
+        acc[k] = fmaf(intra_drop(a.dp, kind, h, (uint64_t)b * a.N + n), to_f32(dU[n * D + d]),
+                      acc[k]);
       }
     }
   }
@@ -209,10 +218,11 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, 
 //   da3s[h, f] = sum_b dpre3 h2_b, da4s likewise.
 // mode 1 (after it): d_hs[src_b] += w3 G3 + w4 G4 + dpre3 a3s + dpre4 a4s (per row,
 //   batch order).  One workgroup: B is a mini-batch (train.py:33, 64 flows).
+template <typename T>
 __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     OursArgs a, int mode, const float* __restrict__ bstat, const float* __restrict__ G,
     float* __restrict__ bgrad, float* __restrict__ row_coef, float* __restrict__ da3s,
-    float* __restrict__ da4s, float* __restrict__ d_hs) {
+    float* __restrict__ da4s, T* __restrict__ d_hs) {
   const int H = a.H, F = a.F, D = H * F;
   const int64_t B = a.B;
   if (mode == 0) {
@@ -223,7 +233,7 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       const float* st = bstat + (b * H + h) * BS_N;
       float dw3 = 0.f, dw4 = 0.f;
       for (int f = 0; f < F; ++f) {
-        const float x = a.h2[i * D + h * F + f];
+        const float x = ldt<T>(a.h2, i * D + h * F + f);
         dw3 = fmaf(G[(b * 2 + 0) * D + h * F + f], x, dw3);
         dw4 = fmaf(G[(b * 2 + 1) * D + h * F + f], x, dw4);
       }
@@ -256,7 +266,7 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       const int h = (int)(t / F);
       float s3 = 0.f, s4 = 0.f;
       for (int64_t b = 0; b < B; ++b) {
-        const float x = a.h2[a.src[b] * D + t];
+        const float x = ldt<T>(a.h2, a.src[b] * D + t);
         s3 = fmaf(bgrad[(b * H + h) * 4 + 0], x, s3);
         s4 = fmaf(bgrad[(b * H + h) * 4 + 1], x, s4);
       }
@@ -280,7 +290,7 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
         s += st[BS_W3] * G[(q * 2 + 0) * D + d] + st[BS_W4] * G[(q * 2 + 1) * D + d] +
              gq[0] * a.a3s[d] + gq[1] * a.a4s[d];
       }
-      d_hs[i * D + d] += s;
+      d_hs[i * D + d] = from_f32<T>(to_f32(d_hs[i * D + d]) + s);
     }
   }
 }
@@ -298,7 +308,7 @@ static int check(const msha_graph* g, const msha_groups* grp, int64_t B, const i
 }
 
 static OursArgs make_args(const msha_graph* g, const msha_groups* grp, int64_t B,
-                          const int64_t* src, int32_t heads, int32_t feat, const float* h2,
+                          const int64_t* src, int32_t heads, int32_t feat, const void* h2,
                           const float* a3s, const float* a4s, float slope, float drop_p,
                           uint64_t seed, uint64_t offset) {
   OursArgs a;
@@ -314,24 +324,35 @@ static OursArgs make_args(const msha_graph* g, const msha_groups* grp, int64_t B
 
 using namespace msha;
 
+template <typename T>
+static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const float* el,
+                       const float* er, const float* lse, const void* u_inter, float* bstat,
+                       void* u_out, hipStream_t s) {
+  if (B > 0)
+    hipLaunchKernelGGL(ours_prep_kernel<T>, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
+                       g->col, g->rowflag, el, er, lse, bstat);
+  hipLaunchKernelGGL(ours_fwd_kernel<T>, dim3(grid_for(g->n_rows, 4, 1 << 16)), dim3(256), 0, s,
+                     a, (const float*)bstat, (const T*)u_inter, (T*)u_out);
+}
+
 extern "C" int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, int64_t B,
-                                   const int64_t* src, int32_t heads, int32_t feat,
-                                   const float* h2, const float* a3s, const float* a4s,
+                                   const int64_t* src, int32_t heads, int32_t feat, int32_t dtype,
+                                   const void* h2, const float* a3s, const float* a4s,
                                    const float* el, const float* er, const float* lse,
-                                   const float* u_inter, float neg_slope, float drop_p,
-                                   uint64_t seed, uint64_t offset, float* bstat, float* u_out,
+                                   const void* u_inter, float neg_slope, float drop_p,
+                                   uint64_t seed, uint64_t offset, float* bstat, void* u_out,
                                    msha_stream_t stream) {
   if (int rc = check(g, grp, B, src, heads, feat)) return rc;
   MSHA_ARG_CHECK(h2 && a3s && a4s && el && er && lse && u_inter && bstat && u_out,
                  "ours_intra_fwd: null pointer");
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "ours_intra_fwd: bad dtype");
   const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
                                seed, offset);
   hipStream_t s = (hipStream_t)stream;
-  if (B > 0)
-    hipLaunchKernelGGL(ours_prep_kernel, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
-                       g->col, g->rowflag, el, er, lse, bstat);
-  hipLaunchKernelGGL(ours_fwd_kernel, dim3(grid_for(g->n_rows, 4, 1 << 16)), dim3(256), 0, s, a,
-                     (const float*)bstat, u_inter, u_out);
+  if (dtype == MSHA_DTYPE_BF16)
+    launch_fwd<bf16_t>(a, g, B, el, er, lse, u_inter, bstat, u_out, s);
+  else
+    launch_fwd<float>(a, g, B, el, er, lse, u_inter, bstat, u_out, s);
   return check_launch("ours_intra_fwd");
 }
 
@@ -343,16 +364,37 @@ extern "C" size_t msha_ours_workspace_size(const msha_groups* grp, int64_t B, in
   return (size_t)(2 * B * nck) * (size_t)heads * (size_t)feat * sizeof(float);
 }
 
+template <typename T>
+static void launch_bwd(const OursArgs& a, int stage, int64_t B, int nck, int heads, int feat,
+                       const float* bstat, const void* dU, float* G, float* bgrad,
+                       float* row_coef, float* da3s, float* da4s, void* d_hs, float* Gp,
+                       hipStream_t s) {
+  if (stage == 0) {
+    hipLaunchKernelGGL(ours_bwd_gather_kernel<T>, dim3(grid_for(2 * B * nck, 4)), dim3(256), 0, s,
+                       a, (const T*)dU, nck, Gp);
+    hipLaunchKernelGGL(ours_bwd_gather_reduce_kernel,
+                       dim3(grid_for(2 * B * heads * feat, 256, 4096)), dim3(256), 0, s, B,
+                       heads * feat, nck, (const float*)Gp, G);
+    hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(1), dim3(1024), 0, s, a, 0, bstat,
+                       (const float*)G, bgrad, row_coef, da3s, da4s, (T*)nullptr);
+  } else {
+    hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(1), dim3(1024), 0, s, a, 1, bstat,
+                       (const float*)G, bgrad, (float*)nullptr, (float*)nullptr,
+                       (float*)nullptr, (T*)d_hs);
+  }
+}
+
 extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, int64_t B,
-                                   const int64_t* src, int32_t heads, int32_t feat,
-                                   const float* h2, const float* a3s, const float* a4s,
-                                   const float* bstat, const float* dU, int32_t stage,
+                                   const int64_t* src, int32_t heads, int32_t feat, int32_t dtype,
+                                   const void* h2, const float* a3s, const float* a4s,
+                                   const float* bstat, const void* dU, int32_t stage,
                                    float neg_slope, float drop_p, uint64_t seed,
                                    uint64_t offset, float* G, float* bgrad, float* row_coef,
-                                   float* da3s, float* da4s, float* d_hs, void* ws,
+                                   float* da3s, float* da4s, void* d_hs, void* ws,
                                    size_t ws_bytes, msha_stream_t stream) {
   if (int rc = check(g, grp, B, src, heads, feat)) return rc;
   MSHA_ARG_CHECK(stage == 0 || stage == 1, "ours_intra_bwd: stage must be 0 or 1");
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "ours_intra_bwd: bad dtype");
   MSHA_ARG_CHECK(h2 && a3s && a4s && bstat && G && bgrad, "ours_intra_bwd: null pointer");
   MSHA_ARG_CHECK(stage == 1 || (dU && row_coef && da3s && da4s), "ours_intra_bwd: stage 0 outputs");
   MSHA_ARG_CHECK(stage == 0 || d_hs, "ours_intra_bwd: stage 1 needs d_hs");
@@ -367,23 +409,20 @@ extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, 
     }
     return MSHA_OK;
   }
+  int nck = 0;
+  float* Gp = nullptr;
   if (stage == 0) {
     const int maxg = grp->max_group > 0 ? grp->max_group : (int)g->n_rows;
-    const int nck = (maxg + kGatherChunk - 1) / kGatherChunk;
+    nck = (maxg + kGatherChunk - 1) / kGatherChunk;
     MSHA_ARG_CHECK(ws && ws_bytes >= msha_ours_workspace_size(grp, B, heads, feat),
                    "ours_intra_bwd: workspace too small");
-    float* Gp = (float*)ws;
-    hipLaunchKernelGGL(ours_bwd_gather_kernel, dim3(grid_for(2 * B * nck, 4)), dim3(256), 0, s,
-                       a, dU, nck, Gp);
-    hipLaunchKernelGGL(ours_bwd_gather_reduce_kernel,
-                       dim3(grid_for(2 * B * heads * feat, 256, 4096)), dim3(256), 0, s, B,
-                       heads * feat, nck, (const float*)Gp, G);
-    hipLaunchKernelGGL(ours_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, a, 0, bstat,
-                       (const float*)G, bgrad, row_coef, da3s, da4s, (float*)nullptr);
-  } else {
-    hipLaunchKernelGGL(ours_bwd_finish_kernel, dim3(1), dim3(1024), 0, s, a, 1, bstat,
-                       (const float*)G, bgrad, (float*)nullptr, (float*)nullptr,
-                       (float*)nullptr, d_hs);
+    Gp = (float*)ws;
   }
+  if (dtype == MSHA_DTYPE_BF16)
+    launch_bwd<bf16_t>(a, stage, B, nck, heads, feat, bstat, dU, G, bgrad, row_coef, da3s, da4s,
+                       d_hs, Gp, s);
+  else
+    launch_bwd<float>(a, stage, B, nck, heads, feat, bstat, dU, G, bgrad, row_coef, da3s, da4s,
+                      d_hs, Gp, s);
   return check_launch("ours_intra_bwd");
 }

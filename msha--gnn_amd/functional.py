@@ -33,6 +33,23 @@ def _f32c(t):
     return t.to(torch.float32).contiguous() if t is not None else None
 
 
+BF16 = torch.bfloat16
+
+
+def _table_dtype(*ts):
+    """Storage type of node tables: bf16 when any given table is bf16, else fp32."""
+    return BF16 if any(t is not None and t.dtype == BF16 for t in ts) else torch.float32
+
+
+def _code(dt) -> int:
+    """MSHA_DTYPE_* of a torch dtype."""
+    return 1 if dt == BF16 else 0
+
+
+def _tc(t, dt):
+    return t.to(dt).contiguous() if t is not None else None
+
+
 def new_seed() -> int:
     """Per-call dropout seed drawn from torch's CPU generator (no device sync;
     reproducible under torch.manual_seed)."""
@@ -49,25 +66,26 @@ class _EdgeAttention(torch.autograd.Function):
         n, H = el.shape
         m, H2, F = hc.shape
         assert H2 == H and m == graph.n_cols and n == graph.n_rows
-        el, er, hc = _f32c(el), _f32c(er), _f32c(hc)
-        hs = _f32c(hs)
+        dt = _table_dtype(hc, hs)
+        el, er = _f32c(el), _f32c(er)
+        hc, hs = _tc(hc, dt), _tc(hs, dt)
         dev = el.device
         s = _stream(el)
         g = graph.desc
-        u = torch.empty(n, H, F, device=dev, dtype=torch.float32)
+        u = torch.empty(n, H, F, device=dev, dtype=dt)
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)
         attd = None
         if hs is not None:
             attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
         ev = _timed("edge_attention_fwd")
-        _lib.call("msha_edge_attention_fwd", g, H, F, el.data_ptr(), er.data_ptr(),
+        _lib.call("msha_edge_attention_fwd", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
                   hc.data_ptr(), slope, p, seed, 0, u.data_ptr(), lse.data_ptr(),
                   _lib.ptr(attd), s)
         if ev is not None:
             ev[1].record()
         v = None
         if hs is not None:
-            v = torch.empty(m, H, F, device=dev, dtype=torch.float32)
+            v = torch.empty(m, H, F, device=dev, dtype=dt)
             _csc_aggregate(graph, H, F, attd, None, hs, v, None, s)
         ctx.graph, ctx.p, ctx.seed, ctx.slope = graph, p, seed, slope
         ctx.has_hs = hs is not None
@@ -82,23 +100,23 @@ class _EdgeAttention(torch.autograd.Function):
         graph = ctx.graph
         n, H = el.shape
         m, _, F = hc.shape
+        dt = hc.dtype
         dev = el.device
         s = _stream(el)
         g = graph.desc
-        dU = torch.zeros_like(u) if dU is None else _f32c(dU)
+        dU = torch.zeros_like(u) if dU is None else _tc(dU, dt)
         use_dv = ctx.has_hs and dV is not None
-        dV = _f32c(dV) if use_dv else None
+        dV = _tc(dV, dt) if use_dv else None
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
         de = torch.empty(E, H, device=dev, dtype=torch.float32)
         attd = torch.empty(E, H, device=dev, dtype=torch.float32)
-        d_hs = torch.empty(n, H, F, device=dev, dtype=torch.float32) if use_dv else None
-        _lib.call("msha_edge_attention_bwd_rows", g, H, F, el.data_ptr(), er.data_ptr(),
-                  hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
+        d_hs = torch.empty(n, H, F, device=dev, dtype=dt) if use_dv else None
+        _lib.call("msha_edge_attention_bwd_rows", g, H, F, _code(dt), el.data_ptr(),
+                  er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
                   hs.data_ptr() if use_dv else None, _lib.ptr(dV), None, ctx.slope, ctx.p,
-                  ctx.seed, 0,
-                  d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), _lib.ptr(d_hs), s)
-        d_hc = torch.empty(m, H, F, device=dev, dtype=torch.float32)
+                  ctx.seed, 0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), _lib.ptr(d_hs), s)
+        d_hc = torch.empty(m, H, F, device=dev, dtype=dt)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
         _csc_aggregate(graph, H, F, attd, de, dU, d_hc, d_er, s)
         if ctx.has_hs and d_hs is None:
@@ -109,14 +127,15 @@ class _EdgeAttention(torch.autograd.Function):
 def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream):
     if not graph.has_csc:
         raise RuntimeError("graph has no CSC view (build it with_csc=True)")
+    assert out.dtype == table.dtype
     g = graph.desc
     wsb = _lib.load().msha_csc_aggregate_workspace_size(g, H, F)
     ws = None
     if graph._plan["n_multi"] > 0:
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=table.device)
-    _lib.call("msha_csc_aggregate", g, H, F, w.data_ptr(), _lib.ptr(x), table.data_ptr(),
-              out.data_ptr(), _lib.ptr(out_x), _lib.ptr(ws), 0 if ws is None else ws.numel(),
-              stream)
+    _lib.call("msha_csc_aggregate", g, H, F, _code(table.dtype), w.data_ptr(), _lib.ptr(x),
+              table.data_ptr(), out.data_ptr(), _lib.ptr(out_x), _lib.ptr(ws),
+              0 if ws is None else ws.numel(), stream)
 
 
 def edge_attention(graph: Graph, el, er, hc, hs=None, p: float = 0.0, training: bool = False,
@@ -125,6 +144,8 @@ def edge_attention(graph: Graph, el, er, hc, hs=None, p: float = 0.0, training: 
 
     el (N,H), er (M,H), hc (M,H,F) [, hs (N,H,F)] ->  u (N,H,F)  [, v (M,H,F)]
     with att = softmax_row(lrelu(el_i + er_j)), u = drop(att) @ hc, v = drop(att).T @ hs.
+    Tables (hc, hs, u, v and their gradients) are bf16 when hc or hs is bf16 (fp32
+    arithmetic, config C3), else fp32; scores and statistics are always fp32.
     """
     _lib.require_cuda(el, er, hc, hs)
     F = hc.shape[-1]
@@ -140,6 +161,7 @@ def edge_attention(graph: Graph, el, er, hc, hs=None, p: float = 0.0, training: 
 class _GAL(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, a, graph: Graph, p: float, seed: int):
+        ctx.h_dtype = h.dtype
         h = _f32c(h)
         ctx.a_shape = None if a is None else (a.shape, a.dtype, a.device)
         out = torch.empty_like(h)
@@ -160,7 +182,7 @@ class _GAL(torch.autograd.Function):
         if ctx.a_shape is not None:
             shape, dtype, dev = ctx.a_shape
             da = torch.zeros(shape, dtype=dtype, device=dev)
-        return dh, da, None, None, None
+        return dh.to(ctx.h_dtype), da, None, None, None
 
 
 def gal(graph: Graph, h, p: float = 0.0, training: bool = False, seed: int | None = None,
@@ -195,17 +217,21 @@ def _splits_for(rows: int) -> int:
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
-         accumulate: bool = False, splits: int | None = None) -> torch.Tensor:
+         accumulate: bool = False, splits: int | None = None, out_dtype=None) -> torch.Tensor:
     """C = A @ B (or C += A @ B) on the MFMA GEMM; A and B may be strided views
-    (transposes included).  Long reductions use deterministic split-K."""
+    (transposes included).  Long reductions use deterministic split-K.  bf16 operands
+    (either one) run the bf16 MFMA kernel; C is then out_dtype (default bf16)."""
     M, K = A.shape
     K2, N = B.shape
     assert K == K2
+    if splits is None:
+        splits = _splits_for(K) if K >= 4096 else 1
+    if A.dtype == BF16 or B.dtype == BF16:
+        assert not accumulate and out is None, "bf16 gemm: no accumulate / out"
+        return _gemm_bf16(A, B, splits, out_dtype or BF16, -1, None)
     if out is None:
         out = torch.empty(M, N, device=A.device, dtype=torch.float32)
     assert out.stride(1) == 1
-    if splits is None:
-        splits = _splits_for(K) if K >= 4096 else 1
     if accumulate and splits == 1:
         splits = 2
     ws = None
@@ -219,15 +245,41 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
     return out
 
 
-def gemm_head_outer(A: torch.Tensor, B: torch.Tensor, operand: int, outer) -> torch.Tensor:
+def _gemm_bf16(A, B, splits, out_dtype, operand, outer):
+    """msha_gemm_bf16: bf16 operands (strided views kept), C in out_dtype."""
+    A, B = A.to(BF16), B.to(BF16)
+    M, K = A.shape
+    N = B.shape[1]
+    out = torch.empty(M, N, device=A.device, dtype=out_dtype)
+    ws = None
+    if splits > 1:
+        ws = torch.empty(int(_lib.load().msha_gemm_bf16_workspace_size(M, N, splits)),
+                         dtype=torch.uint8, device=A.device)
+    H = Fd = 0
+    d1 = a1 = d2 = a2 = None
+    if outer is not None:
+        H, Fd, d1, a1, d2, a2 = outer
+        a1, a2 = _f32c(a1), _f32c(a2)
+    _lib.call("msha_gemm_bf16", M, N, K, A.data_ptr(), A.stride(0), A.stride(1), B.data_ptr(),
+              B.stride(0), B.stride(1), out.data_ptr(), out.stride(0), _code(out_dtype), splits,
+              _lib.ptr(ws), 0 if ws is None else ws.numel(), operand, H, Fd, _lib.ptr(d1),
+              _lib.ptr(a1), _lib.ptr(d2), _lib.ptr(a2), _stream(A))
+    return out
+
+
+def gemm_head_outer(A: torch.Tensor, B: torch.Tensor, operand: int, outer,
+                    out_dtype=None) -> torch.Tensor:
     """A @ B with operand 0 (A) or 1 (B) read as X + de (x) a [+ de2 (x) a2]
-    (outer = (heads, feat, de, a, de2, a2)); falls back to materialising the sum with
-    msha_add_head_outer only when the operand layout cannot take the fused loads."""
+    (outer = (heads, feat, de, a, de2, a2)).  fp32: falls back to materialising the
+    sum with msha_add_head_outer only when the operand layout cannot take the fused
+    loads.  bf16 operands: the bf16 kernel (C in out_dtype, default bf16)."""
     H, Fd, d1, a1, d2, a2 = outer
     M, K = A.shape
     N = B.shape[1]
-    out = torch.empty(M, N, device=A.device, dtype=torch.float32)
     splits = _splits_for(K) if K >= 4096 else 1
+    if A.dtype == BF16 or B.dtype == BF16:
+        return _gemm_bf16(A, B, splits, out_dtype or BF16, operand, outer)
+    out = torch.empty(M, N, device=A.device, dtype=torch.float32)
     ws = None
     if splits > 1:
         ws = torch.empty(int(_lib.load().msha_gemm_workspace_size(M, N, splits)),
@@ -248,20 +300,24 @@ def gemm_head_outer(A: torch.Tensor, B: torch.Tensor, operand: int, outer) -> to
 
 
 class _ProjectScores(torch.autograd.Function):
-    """h = X @ W, el = h . al, er = h . ar (per head) in one MFMA launch."""
+    """h = X @ W, el = h . al, er = h . ar (per head) in one MFMA launch.  fp32 X, W:
+    the exact-fp32 MFMA kernel; a bf16 X or W: the bf16 kernel (h bf16, el/er fp32)."""
 
     @staticmethod
     def forward(ctx, X, W, al, ar, heads: int, feat: int):
-        X, W = _f32c(X), _f32c(W)
+        ctx.dtypes = (X.dtype, W.dtype, None if al is None else al.dtype,
+                      None if ar is None else ar.dtype)
+        dt = _table_dtype(X, W)
+        X, W = _tc(X, dt), _tc(W, dt)
         al, ar = _f32c(al), _f32c(ar)
         M, K = X.shape
         dev = X.device
-        h = torch.empty(M, heads * feat, device=dev, dtype=torch.float32)
+        h = torch.empty(M, heads * feat, device=dev, dtype=dt)
         el = torch.empty(M, heads, device=dev, dtype=torch.float32) if al is not None else None
         er = torch.empty(M, heads, device=dev, dtype=torch.float32) if ar is not None else None
-        _lib.call("msha_project_scores", M, K, heads, feat, X.data_ptr(), W.data_ptr(),
-                  _lib.ptr(al), _lib.ptr(ar), h.data_ptr(), _lib.ptr(el), _lib.ptr(er),
-                  _stream(X))
+        fn = "msha_project_scores_bf16" if dt == BF16 else "msha_project_scores"
+        _lib.call(fn, M, K, heads, feat, X.data_ptr(), W.data_ptr(), _lib.ptr(al), _lib.ptr(ar),
+                  h.data_ptr(), _lib.ptr(el), _lib.ptr(er), _stream(X))
         ctx.heads, ctx.feat = heads, feat
         ctx.save_for_backward(X, W, al, ar, h)
         outs = [h]
@@ -275,15 +331,18 @@ class _ProjectScores(torch.autograd.Function):
     def backward(ctx, dh, *dscores):
         X, W, al, ar, h = ctx.saved_tensors
         H, Fd = ctx.heads, ctx.feat
+        xdt, wdt, aldt, ardt = ctx.dtypes
+        dt = h.dtype
         M = X.shape[0]
         dev = X.device
         s = _stream(X)
         it = iter(dscores)
         d_el = next(it) if al is not None else None
         d_er = next(it) if ar is not None else None
-        dh = torch.zeros_like(h) if dh is None else _f32c(dh)
+        dh = torch.zeros_like(h) if dh is None else _tc(dh, dt)
         terms = [(d, a) for d, a in ((d_el, al), (d_er, ar)) if d is not None]
         dX = dW = dal = dar = None
+        kw = {"out_dtype": None}
         if terms:
             # dh + d_el (x) al (+ d_er (x) ar) is folded into the GEMM operand loads
             (d1, a1) = terms[0]
@@ -291,14 +350,16 @@ class _ProjectScores(torch.autograd.Function):
             d1, d2 = _f32c(d1), _f32c(d2)
             outer = (H, Fd, d1, a1, d2, a2)
             if ctx.needs_input_grad[0]:
-                dX = gemm_head_outer(dh, W.t(), 0, outer)
+                kw["out_dtype"] = xdt if dt == BF16 else None
+                dX = gemm_head_outer(dh, W.t(), 0, outer, **kw)
             if ctx.needs_input_grad[1]:
-                dW = gemm_head_outer(X.t(), dh, 1, outer)
+                kw["out_dtype"] = wdt if dt == BF16 else None
+                dW = gemm_head_outer(X.t(), dh, 1, outer, **kw)
         else:
             if ctx.needs_input_grad[0]:
-                dX = gemm(dh, W.t())
+                dX = gemm(dh, W.t(), out_dtype=xdt if dt == BF16 else None)
             if ctx.needs_input_grad[1]:
-                dW = gemm(X.t(), dh)
+                dW = gemm(X.t(), dh, out_dtype=wdt if dt == BF16 else None)
         if terms and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
             # dal[h,f] = sum_m d_el[m,h] h[m,h,f] (and dar): one pass over h
             (d1, a1) = terms[0]
@@ -307,15 +368,16 @@ class _ProjectScores(torch.autograd.Function):
             o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
             wsb = int(_lib.load().msha_head_colsum_workspace_size(M, H, Fd))
             ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
-            _lib.call("msha_head_colsum", M, H, Fd, _f32c(d1).data_ptr(), _lib.ptr(_f32c(d2)),
-                      h.data_ptr(), o1.data_ptr(), _lib.ptr(o2), ws.data_ptr(), ws.numel(), s)
+            _lib.call("msha_head_colsum", M, H, Fd, _code(dt), _f32c(d1).data_ptr(),
+                      _lib.ptr(_f32c(d2)), h.data_ptr(), o1.data_ptr(), _lib.ptr(o2),
+                      ws.data_ptr(), ws.numel(), s)
             outs = [o1] + ([o2] if o2 is not None else [])
             k = 0
             if d_el is not None:
-                dal = outs[k].reshape(al.shape)
+                dal = outs[k].reshape(al.shape).to(aldt)
                 k += 1
             if d_er is not None:
-                dar = outs[k].reshape(ar.shape)
+                dar = outs[k].reshape(ar.shape).to(ardt)
         return dX, dW, dal, dar, None, None
 
 
@@ -450,24 +512,26 @@ class _OursAttention(torch.autograd.Function):
                 slope: float):
         n, H = el.shape
         m, _, Fd = h1.shape
-        el, er, h1, h2 = _f32c(el), _f32c(er), _f32c(h1), _f32c(h2)
+        dt = _table_dtype(h1, h2)
+        el, er, h1, h2 = _f32c(el), _f32c(er), _tc(h1, dt), _tc(h2, dt)
         a3s, a4s = _f32c(a3s), _f32c(a4s)
         src = src.to(torch.int64).contiguous()
         B = src.numel()
         dev = el.device
         s = _stream(el)
         g = graph.desc
-        u_inter = torch.empty(n, H, Fd, device=dev, dtype=torch.float32)
+        u_inter = torch.empty(n, H, Fd, device=dev, dtype=dt)
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)
         attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
-        _lib.call("msha_edge_attention_fwd", g, H, Fd, el.data_ptr(), er.data_ptr(),
+        _lib.call("msha_edge_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
                   h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(), lse.data_ptr(),
                   attd.data_ptr(), s)
-        v = torch.empty(m, H, Fd, device=dev, dtype=torch.float32)
+        v = torch.empty(m, H, Fd, device=dev, dtype=dt)
         _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
         bstat = torch.empty(max(B, 1), H, 8, device=dev, dtype=torch.float32)
         u = torch.empty_like(u_inter)
-        _lib.call("msha_ours_intra_fwd", g, groups.desc, B, src.data_ptr(), H, Fd, h2.data_ptr(),
+        _lib.call("msha_ours_intra_fwd", g, groups.desc, B, src.data_ptr(), H, Fd, _code(dt),
+                  h2.data_ptr(),
                   a3s.data_ptr(), a4s.data_ptr(), el.data_ptr(), er.data_ptr(), lse.data_ptr(),
                   u_inter.data_ptr(), slope, p, seed, 0, bstat.data_ptr(), u.data_ptr(), s)
         ctx.graph, ctx.groups, ctx.p, ctx.seed, ctx.slope = graph, groups, p, seed, slope
@@ -486,14 +550,16 @@ class _OursAttention(torch.autograd.Function):
         dev = el.device
         s = _stream(el)
         g, gr = graph.desc, groups.desc
-        dU = torch.zeros_like(u_inter) if dU is None else _f32c(dU)
-        dV = torch.zeros(m, H, Fd, device=dev) if dV is None else _f32c(dV)
+        dt = h1.dtype
+        dU = torch.zeros_like(u_inter) if dU is None else _tc(dU, dt)
+        dV = torch.zeros(m, H, Fd, device=dev, dtype=dt) if dV is None else _tc(dV, dt)
         G = torch.empty(max(B, 1), 2, H * Fd, device=dev, dtype=torch.float32)
         bgrad = torch.empty(max(B, 1), H, 4, device=dev, dtype=torch.float32)
         row_coef = torch.zeros(n, H, device=dev, dtype=torch.float32)
         da3s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
         da4s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
-        args = (g, gr, B, src.data_ptr(), H, Fd, h2.data_ptr(), a3s.data_ptr(), a4s.data_ptr(),
+        args = (g, gr, B, src.data_ptr(), H, Fd, _code(dt), h2.data_ptr(), a3s.data_ptr(),
+                a4s.data_ptr(),
                 bstat.data_ptr(), dU.data_ptr())
         wsb = int(_lib.load().msha_ours_workspace_size(gr, B, H, Fd))
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
@@ -504,14 +570,14 @@ class _OursAttention(torch.autograd.Function):
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
         de = torch.empty(E, H, device=dev, dtype=torch.float32)
         attd = torch.empty(E, H, device=dev, dtype=torch.float32)
-        d_hs = torch.empty(n, H, Fd, device=dev, dtype=torch.float32)
-        _lib.call("msha_edge_attention_bwd_rows", g, H, Fd, el.data_ptr(), er.data_ptr(),
+        d_hs = torch.empty(n, H, Fd, device=dev, dtype=dt)
+        _lib.call("msha_edge_attention_bwd_rows", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
                   h1.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), dU.data_ptr(),
                   h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p, ctx.seed,
                   0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), d_hs.data_ptr(), s)
         _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
                   bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), None, 0, s)
-        d_hc = torch.empty(m, H, Fd, device=dev, dtype=torch.float32)
+        d_hc = torch.empty(m, H, Fd, device=dev, dtype=dt)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
         _csc_aggregate(graph, H, Fd, attd, de, dU, d_hc, d_er, s)
         return d_el, d_er, d_hc, d_hs, da3s, da4s, None, None, None, None, None, None

@@ -1,0 +1,224 @@
+"""bf16 node tables (config C3: the same models in bf16) on the GPU.
+
+Every reference here is fp64 on the SAME bf16-rounded inputs, so the comparison
+measures the kernels (fp32 arithmetic, bf16 storage of their table outputs), not the
+input quantisation.  Bars (north_star): bf16 tables (h, u, v, dh) within 1e-2
+relative with a 1e-2 * max|ref| floor; fp32 outputs of fp32 arithmetic on bf16
+inputs (scores, GEMM with fp32 C) to 1e-4.  Module level: the bf16 model against the
+same model in fp32 with the bf16-rounded parameters, 3e-2 (two layers, BatchNorm
+and the log-softmax in bf16 between the kernels; documented in DESIGN.md)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from gpu_helpers import t, tol_close, virtual_csr, random_counts
+from oracle import gnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def rb(x):
+    """numpy fp32 -> bf16 (round to nearest even) -> fp32."""
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32)).to(BF).float().numpy()
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K,ta,tb,splits,cbf", [
+    (1000, 128, 136, False, False, 1, True),    # projection: A k-fast, B n-fast
+    (517, 64, 128, False, True, 1, False),      # dX: B = W^T (k-fast)
+    (128, 128, 20000, True, False, 64, False),  # dW: A = X^T, B n-fast, split-K
+    (128, 128, 5000, True, False, 8, True),     # dW, bf16 C
+    (264, 72, 40, True, True, 1, False),        # both transposed, ragged tiles
+])
+def test_gemm_bf16(cuda, M, N, K, ta, tb, splits, cbf):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M + N + K)
+    A = rb(rng.standard_normal((M, K)))
+    B = rb(rng.standard_normal((K, N)))
+    tA = t(A.T.copy(), cuda, BF).t() if ta else t(A, cuda, BF)
+    tB = t(B.T.copy(), cuda, BF).t() if tb else t(B, cuda, BF)
+    got = MF.gemm(tA, tB, splits=splits, out_dtype=BF if cbf else torch.float32)
+    assert got.dtype == (BF if cbf else torch.float32)
+    ref = A.astype(np.float64) @ B.astype(np.float64)
+    if cbf:
+        tol_close(got.float().cpu().numpy(), ref, 1e-2, 1e-2)
+    else:
+        tol_close(got.cpu().numpy(), ref, 1e-4, 1e-5)
+
+
+@pytest.mark.parametrize("operand", [0, 1])
+def test_gemm_bf16_head_outer(cuda, operand):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(operand + 3)
+    M, H, F, K = 3000, 8, 16, 128
+    D = H * F
+    dh = rb(rng.standard_normal((M, D)))
+    de, de2 = rng.standard_normal((M, H)).astype(np.float32), rng.standard_normal((M, H)).astype(np.float32)
+    a, a2 = rng.standard_normal((H, F)).astype(np.float32), rng.standard_normal((H, F)).astype(np.float32)
+    tot = dh.astype(np.float64) + np.repeat(de, F, 1) * a.reshape(-1) + np.repeat(de2, F, 1) * a2.reshape(-1)
+    outer = (H, F, t(de, cuda), t(a, cuda), t(de2, cuda), t(a2, cuda))
+    if operand == 0:
+        W = rb(rng.standard_normal((K, D)))
+        got = MF.gemm_head_outer(t(dh, cuda, BF), t(W, cuda, BF).t(), 0, outer,
+                                 out_dtype=torch.float32).cpu().numpy()
+        ref = tot @ W.T.astype(np.float64)
+    else:
+        X = rb(rng.standard_normal((M, K)))
+        got = MF.gemm_head_outer(t(X, cuda, BF).t(), t(dh, cuda, BF), 1, outer,
+                                 out_dtype=torch.float32).cpu().numpy()
+        ref = X.T.astype(np.float64) @ tot
+    # the operand sum is rounded to bf16 before the MFMA: 1e-2
+    tol_close(got, ref, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("M,K,H,F", [(3000, 128, 8, 16), (517, 128, 2, 64), (200, 64, 1, 128)])
+def test_project_scores_bf16(cuda, M, K, H, F):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M)
+    X = rb(rng.standard_normal((M, K)))
+    W = rb(rng.standard_normal((K, H * F)) / np.sqrt(K))
+    al = rng.standard_normal((H, F)).astype(np.float32)
+    ar = rng.standard_normal((H, F)).astype(np.float32)
+    tX, tW = t(X, cuda, BF).requires_grad_(True), t(W, cuda, BF).requires_grad_(True)
+    tal, tar = t(al, cuda).requires_grad_(True), t(ar, cuda).requires_grad_(True)
+    h, el, er = MF.project_scores(tX, tW, tal, tar, heads=H)
+    assert h.dtype == BF and el.dtype == torch.float32
+    rh = X.astype(np.float64) @ W.astype(np.float64)
+    tol_close(h.float().detach().cpu().numpy(), rh, 1e-2, 1e-2)
+    rel = (rh.reshape(M, H, F) * al).sum(-1)
+    rer = (rh.reshape(M, H, F) * ar).sum(-1)
+    tol_close(el.detach().cpu().numpy(), rel, 1e-4, 1e-5)   # from the fp32 accumulators
+    tol_close(er.detach().cpu().numpy(), rer, 1e-4, 1e-5)
+    dh = rb(rng.standard_normal((M, H * F)))
+    dl = rng.standard_normal((M, H)).astype(np.float32)
+    dr = rng.standard_normal((M, H)).astype(np.float32)
+    (h.float() * t(dh, cuda)).sum().add_((el * t(dl, cuda)).sum()).add_((er * t(dr, cuda)).sum()) \
+        .backward()
+    tot = dh.astype(np.float64) + np.repeat(dl, F, 1) * al.reshape(-1) + np.repeat(dr, F, 1) * ar.reshape(-1)
+    tol_close(tX.grad.float().cpu().numpy(), tot @ W.T.astype(np.float64), 1e-2, 1e-2)
+    tol_close(tW.grad.float().cpu().numpy(), X.T.astype(np.float64) @ tot, 1e-2, 1e-2)
+    hb = h.float().detach().cpu().numpy().astype(np.float64).reshape(M, H, F)  # the saved bf16 h
+    tol_close(tal.grad.cpu().numpy(), np.einsum("mh,mhf->hf", dl, hb), 1e-4, 1e-5)
+    tol_close(tar.grad.cpu().numpy(), np.einsum("mh,mhf->hf", dr, hb), 1e-4, 1e-5)
+
+
+# ------------------------------------------------------------ edge kernels
+EDGE_CASES = [
+    (300, 32, 2, 64, 30, dict(empty_rows=(0, 17), hot_col=5)),  # OursLayer3 @R15 shape
+    (400, 400, 8, 16, 70, dict(hot_col=9)),                      # synthetic GAT shape (C4)
+    (150, 80, 1, 8, 80, dict(empty_rows=(0,), full_rows=(2,))),  # deg > one wavefront, F = 8
+    (64, 40, 8, 128, 12, dict(empty_rows=(1,))),                 # 1024-wide rows
+]
+
+
+@pytest.mark.parametrize("case", EDGE_CASES, ids=lambda c: f"n{c[0]}m{c[1]}H{c[2]}F{c[3]}")
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_edge_attention_bf16(cuda, msha, case, p):
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    n, m, H, F, max_deg, kw = case
+    rng = np.random.default_rng(n * 11 + H)
+    c = random_counts(rng, n, m, max_deg, **kw)
+    rowptr, col, empty = virtual_csr(c)
+    el = rng.standard_normal((n, H)).astype(np.float32)
+    er = rng.standard_normal((m, H)).astype(np.float32)
+    hc, hs = rb(rng.standard_normal((m, H, F))), rb(rng.standard_normal((n, H, F)))
+    dU, dV = rb(rng.standard_normal((n, H, F))), rb(rng.standard_normal((m, H, F)))
+    graph = Graph.from_dense(t(c, cuda))
+    E = graph.n_edges
+    seed = 7
+    keep = None
+    if p > 0:
+        keep = MF.dropout_keep_mask(E * H, p, seed, cuda).cpu().numpy().reshape(E, H).astype(bool)
+    tel, ter = t(el, cuda).requires_grad_(True), t(er, cuda).requires_grad_(True)
+    thc, ths = t(hc, cuda, BF).requires_grad_(True), t(hs, cuda, BF).requires_grad_(True)
+    u, v = MF.edge_attention(graph, tel, ter, thc, hs=ths, p=p, training=p > 0, seed=seed)
+    assert u.dtype == BF and v.dtype == BF
+    ref = O.edge_aggregate_fwd(rowptr, col, el, er, hc, hs=hs, keep=keep, p=p, rowflag=empty)
+    tol_close(u.float().detach().cpu().numpy(), ref["u"], 1e-2, 1e-2)
+    tol_close(v.float().detach().cpu().numpy(), ref["v"], 1e-2, 1e-2)
+    (u.float() * t(dU, cuda)).sum().add_((v.float() * t(dV, cuda)).sum()).backward()
+    bw = O.edge_aggregate_bwd(rowptr, col, ref, hc, dU, hs=hs, dV=dV, keep=keep, p=p)
+    tol_close(tel.grad.cpu().numpy(), bw["d_el"], 1e-2, 1e-2)
+    tol_close(ter.grad.cpu().numpy(), bw["d_er"], 1e-2, 1e-2)
+    tol_close(thc.grad.float().cpu().numpy(), bw["d_hc"], 1e-2, 1e-2)
+    tol_close(ths.grad.float().cpu().numpy(), bw["d_hs"], 1e-2, 1e-2)
+
+
+def test_ours_attention_bf16_vs_fp32(cuda, msha):
+    """Full MSHA core (Ours.py:54-101) with bf16 tables vs the fp32 kernels on the same
+    bf16-rounded inputs (the fp32 path is itself pinned to the reference)."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph, Groups
+
+    rng = np.random.default_rng(5)
+    n, m, H, Fd, B = 1500, 32, 2, 64, 48
+    counts = np.zeros((n, m), np.float32)
+    for i in range(n):
+        counts[i, rng.choice(m, int(rng.integers(1, 8)), replace=False)] = 1
+    counts[[7, 100]] = 0
+    city = rng.integers(0, 60, n)
+    groups = Groups(city, city // 10, cuda)
+    graph = Graph.from_dense(t(counts, cuda))
+    src = torch.as_tensor(rng.integers(0, n, B), device=cuda)
+    ins = [rng.standard_normal((n, H)), rng.standard_normal((m, H)),
+           rb(rng.standard_normal((m, H, Fd)) * 0.3), rb(rng.standard_normal((n, H, Fd)) * 0.3),
+           rng.standard_normal((H, Fd)) * 0.2, rng.standard_normal((H, Fd)) * 0.2]
+    dU = rb(rng.standard_normal((n, H, Fd)))
+    dV = rb(rng.standard_normal((m, H, Fd)))
+    res = {}
+    for dt in (torch.float32, BF):
+        ts = [t(x, cuda).requires_grad_(True) for x in ins]
+        ts[2] = t(ins[2], cuda, dt).requires_grad_(True)
+        ts[3] = t(ins[3], cuda, dt).requires_grad_(True)
+        u, v = MF.ours_attention(graph, groups, src, *ts, p=0.3, training=True, seed=11)
+        assert u.dtype == dt
+        (u.float() * t(dU, cuda)).sum().add_((v.float() * t(dV, cuda)).sum()).backward()
+        res[dt] = [u.float().detach(), v.float().detach()] + [x.grad.float() for x in ts]
+    for a, b in zip(res[BF], res[torch.float32]):
+        tol_close(a.cpu().numpy(), b.cpu().numpy(), 1e-2, 1e-2)
+
+
+# ------------------------------------------------------------------ modules
+def test_ablation3_bf16_model(cuda, msha):
+    """ablation3.to(bfloat16) train step vs the same model in fp32 with the
+    bf16-rounded parameters (sub512 fixture graph)."""
+    import torch.nn.functional as Fn
+    from msha_gnn_amd import layers
+
+    z = golden("sub512.npz")
+    gdp = {i: float(x) for i, x in enumerate(z["gdp"])}
+    torch.manual_seed(0)
+    m32 = layers.ablation3(128, 64, 32, 2, 0.0, gdp, 512, 32).to(cuda)
+    with torch.no_grad():
+        for prm in m32.parameters():
+            prm.copy_(prm.to(BF).float())
+    m16 = layers.ablation3(128, 64, 32, 2, 0.0, gdp, 512, 32).to(cuda)
+    m16.load_state_dict(m32.state_dict())
+    m16 = m16.to(BF)
+    adj = torch.as_tensor(z["adj_norm"], device=cuda)
+    si = torch.as_tensor(z["source_index"], device=cuda)
+    ri = torch.as_tensor(z["recipient_index"], device=cuda)
+    outs = {}
+    for name, model in (("f32", m32), ("bf16", m16)):
+        model.train()
+        out = model(adj, None, None, si)
+        loss = Fn.nll_loss(out[si].float(), ri)
+        loss.backward()
+        outs[name] = (out.float().detach().cpu().numpy(), loss.item(),
+                      {k: p.grad.float().cpu().numpy() for k, p in model.named_parameters()
+                       if p.grad is not None})
+    tol_close(outs["bf16"][0], outs["f32"][0], 3e-2, 3e-2)
+    assert abs(outs["bf16"][1] - outs["f32"][1]) < 3e-2 * abs(outs["f32"][1])
+    assert outs["bf16"][2].keys() == outs["f32"][2].keys()
+    for k in ("attention_0.W1", "attention_0.W2", "attention_1.W1", "Sfeatures"):
+        g16, g32 = outs["bf16"][2][k], outs["f32"][2][k]
+        assert np.isfinite(g16).all(), k
+        cos = float((g16 * g32).sum() / (np.linalg.norm(g16) * np.linalg.norm(g32) + 1e-30))
+        assert cos > 0.99, (k, cos)

@@ -170,7 +170,7 @@ def test_edge_attention_weights_exported(cuda):
     lse = torch.empty(500, H, device=cuda)
     attd = torch.empty(E, H, device=cuda)
     tel, ter, thc = t(el, cuda), t(er, cuda), t(hc, cuda)  # keep alive across the launch
-    _lib.call("msha_edge_attention_fwd", graph.desc, H, F, tel.data_ptr(), ter.data_ptr(),
+    _lib.call("msha_edge_attention_fwd", graph.desc, H, F, 0, tel.data_ptr(), ter.data_ptr(),
               thc.data_ptr(), 0.2, 0.0, 0, 0, u.data_ptr(), lse.data_ptr(), attd.data_ptr(),
               _lib.stream_handle())
     torch.cuda.synchronize()
@@ -334,7 +334,7 @@ def test_head_colsum(cuda, M, H, F, two):
     st = torch.cuda.current_stream().cuda_stream
     outs = []
     for _ in range(2):
-        _lib.call("msha_head_colsum", M, H, F, t1.data_ptr(), _lib.ptr(t2), tT.data_ptr(),
+        _lib.call("msha_head_colsum", M, H, F, 0, t1.data_ptr(), _lib.ptr(t2), tT.data_ptr(),
                   o1.data_ptr(), _lib.ptr(o2), ws.data_ptr(), ws.numel(), st)
         outs.append([o1.cpu().numpy().copy()] + ([o2.cpu().numpy().copy()] if two else []))
     T3 = T.astype(np.float64).reshape(M, H, F)
