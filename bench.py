@@ -216,37 +216,66 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
     gdp = {i: float(x) for i, x in enumerate(gdp_arr)}
     torch.manual_seed(0)
     cls = layers.Ours if model_kind == "Ours" else layers.ablation3
-    model = cls(128, 64, m, 2, 0.5, gdp, n, m).to(dev, dtype)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
     g = torch.Generator().manual_seed(0)
     picks = [torch.randint(0, len(flows), (64,), generator=g).to(dev) for _ in range(8)]
     batches = [(src_t[b], dst_t[b]) for b in picks]
-    model.train()
-
-    def one(k):
-        si, ri = batches[k % len(batches)]
-        opt.zero_grad()
-        out = model(adj, cadj, padj, si)
-        loss = torch.nn.functional.nll_loss(out[si].float(), ri)
-        loss.backward()
-        opt.step()
-        return loss
-
-    for k in range(warmup):
-        one(k)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(steps):
-        loss = one(k)
-    torch.cuda.synchronize(dev)
-    dt = (time.perf_counter() - t0) / steps
     from msha_gnn_amd.graph import graph_for
 
     e = graph_for(adj).n_edges
-    return dict(model=model_kind, year=year, dtype=str(dtype).replace("torch.", ""), nodes=n,
-                recipients=m, edges=e,
-                flows="shipped" if year == "2015" else "synthetic (2015 degree law)",
-                ms_per_step=dt * 1e3, edges_per_sec=e / dt, loss=float(loss.detach()))
+    res = dict(model=model_kind, year=year, dtype=str(dtype).replace("torch.", ""), nodes=n,
+               recipients=m, edges=e,
+               flows="shipped" if year == "2015" else "synthetic (2015 degree law)")
+    for mode in ("eager", "hip_graph"):
+        torch.manual_seed(0)
+        model = cls(128, 64, m, 2, 0.5, gdp, n, m).to(dev, dtype)
+        graphed = mode == "hip_graph"
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4,
+                               capturable=graphed)
+        model.train()
+        si_s = torch.empty(64, dtype=torch.int64, device=dev)
+        ri_s = torch.empty(64, dtype=torch.int64, device=dev)
+
+        def body():
+            opt.zero_grad(set_to_none=True)
+            out = model(adj, cadj, padj, si_s)
+            loss = torch.nn.functional.nll_loss(out[si_s].float(), ri_s)
+            loss.backward()
+            opt.step()
+            return loss
+
+        def feed(k):
+            si_s.copy_(batches[k % len(batches)][0])
+            ri_s.copy_(batches[k % len(batches)][1])
+
+        if graphed:
+            from msha_gnn_amd.step import GraphedStep
+
+            feed(0)
+            gs = GraphedStep(body, dev, warmup=warmup)
+
+            def one(k):
+                feed(k)
+                return gs.replay()
+        else:
+            def one(k):
+                feed(k)
+                return body()
+
+            for k in range(warmup):
+                one(k)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            loss = one(k)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / steps
+        if graphed:
+            gs.close()
+        res[f"ms_per_step_{mode}"] = dt * 1e3
+        res[f"loss_{mode}"] = float(loss.detach())
+    res["ms_per_step"] = min(res["ms_per_step_eager"], res["ms_per_step_hip_graph"])
+    res["edges_per_sec"] = e / (res["ms_per_step"] * 1e-3)
+    return res
 
 
 def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):

@@ -99,6 +99,15 @@ MSHA_API int msha_abi_version(void);
 MSHA_API const char* msha_last_error(void);
 
 /* ---------------------------------------------------------------- dropout --- */
+/* Dropout under HIP-graph replay.  Every dropout draw of the library is Philox4x32-10
+ * keyed on (seed, offset, element); seeds are kernel arguments, so a captured graph
+ * would replay the same masks.  With a device counter installed here (a uint64 in
+ * device memory, NULL = none), each draw adds (*counter << 32) to its offset, read on
+ * the device at draw time: the caller increments *counter inside the captured region
+ * and every replay draws fresh masks.  Process-wide setting; set it before the
+ * launches it should apply to (launch-time snapshot of the pointer, not the value). */
+MSHA_API int msha_set_rng_counter(const uint64_t* counter);
+
 /* keep[i] = 1 iff element i survives F.dropout(p) under (seed, offset).  The
  * kernels below draw exactly these masks (stream-ordered Philox4x32-10), which
  * is how tests inject the same mask into the CPU oracle. */

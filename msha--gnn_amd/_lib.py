@@ -53,6 +53,7 @@ GRP = C.POINTER(MshaGroups)
 # name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
 SIGNATURES = {
     "msha_abi_version": (C.c_int, []),
+    "msha_set_rng_counter": (C.c_int, [P]),
     "msha_last_error": (C.c_char_p, []),
     "msha_dropout_keep_mask": (C.c_int, [U64, U64, I64, F32, P, P]),
     "msha_inter_adjacency": (C.c_int, [P, P, I64, I64, I64, P, P, P]),

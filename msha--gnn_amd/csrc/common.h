@@ -175,12 +175,17 @@ struct Dropout {
   uint32_t threshold;  // drop when philox < threshold
   float scale;         // 1 / (1 - p)
   bool active;
+  const uint64_t* ctr;  // device replay counter (msha_set_rng_counter), nullable
 };
+
+// the library-wide replay counter (runtime.hip): read by the kernels at draw time
+const uint64_t* rng_counter();
 
 inline Dropout make_dropout(float p, uint64_t seed, uint64_t offset) {
   Dropout d;
   d.seed = seed;
   d.offset = offset;
+  d.ctr = rng_counter();
   d.active = p > 0.f;
   double t = (double)p * 4294967296.0;
   d.threshold = p >= 1.f ? 0xFFFFFFFFu : (uint32_t)(t > 4294967295.0 ? 4294967295.0 : t);
@@ -188,9 +193,15 @@ inline Dropout make_dropout(float p, uint64_t seed, uint64_t offset) {
   return d;
 }
 
+// Philox offset of a draw: the call's offset, plus (replay counter << 32) when a device
+// counter is installed, so a captured HIP graph draws fresh masks on every replay
+__device__ __forceinline__ uint64_t dropout_offset(const Dropout& d, uint64_t offset) {
+  return d.ctr != nullptr ? offset + (*d.ctr << 32) : offset;
+}
+
 __device__ __forceinline__ float dropout_factor(const Dropout& d, uint64_t idx) {
   if (!d.active) return 1.f;
-  return philox_x(d.seed, d.offset, idx) >= d.threshold ? d.scale : 0.f;
+  return philox_x(d.seed, dropout_offset(d, d.offset), idx) >= d.threshold ? d.scale : 0.f;
 }
 
 inline int grid_for(int64_t work_items, int per_block, int cap = 1 << 20) {

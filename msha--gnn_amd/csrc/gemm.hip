@@ -333,9 +333,10 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
       uint32_t kb = 0xffffffffu;
       if (p.act & ACT_DROPOUT) {
         kb = 0u;
+        const uint64_t off = dropout_offset(p.dp, p.dp.offset);
 #pragma unroll 1
         for (int u = 0; u < 32; ++u)
-          if (philox_x(p.dp.seed, p.dp.offset, (uint64_t)(row * p.N + cbase + u)) >= p.dp.threshold)
+          if (philox_x(p.dp.seed, off, (uint64_t)(row * p.N + cbase + u)) >= p.dp.threshold)
             kb |= 1u << u;
       }
 #pragma unroll
@@ -465,12 +466,15 @@ static bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 // stride, its other stride and extent are multiples of 4, and bases are aligned.
 template <int AMODE>
 static bool vec_ok(const GemmArgs& p) {
-  if (p.K % 4 != 0) return false;
+  // K % 4 matters only to an operand loaded 4-along-k (k-contiguous); the
+  // row-contiguous layouts (X^T, W, dH as B) load one k per float4
+  const bool k4 = p.K % 4 == 0;
   bool a_ok;
   if (AMODE == A_GATHER_HADAMARD) {
-    a_ok = aligned16(p.G) && p.ldg % 4 == 0 && (p.G2 == nullptr || (aligned16(p.G2) && p.ldg2 % 4 == 0));
+    a_ok = k4 && aligned16(p.G) && p.ldg % 4 == 0 &&
+           (p.G2 == nullptr || (aligned16(p.G2) && p.ldg2 % 4 == 0));
   } else if (p.sAk == 1) {
-    a_ok = aligned16(p.A) && p.sAm % 4 == 0;
+    a_ok = k4 && aligned16(p.A) && p.sAm % 4 == 0;
   } else if (p.sAm == 1) {
     a_ok = aligned16(p.A) && p.sAk % 4 == 0 && p.M % 4 == 0;
   } else {
@@ -478,7 +482,7 @@ static bool vec_ok(const GemmArgs& p) {
   }
   bool b_ok;
   if (p.sBn == 1) b_ok = aligned16(p.B) && p.sBk % 4 == 0 && p.N % 4 == 0;
-  else if (p.sBk == 1) b_ok = aligned16(p.B) && p.sBn % 4 == 0;
+  else if (p.sBk == 1) b_ok = k4 && aligned16(p.B) && p.sBn % 4 == 0;
   else b_ok = false;
   return a_ok && b_ok;
 }

@@ -50,7 +50,8 @@ __device__ __forceinline__ float ldt(const void* p, int64_t i) {
 
 __device__ __forceinline__ float intra_drop(const Dropout& d, int kind, int h, uint64_t idx) {
   if (!d.active) return 1.f;
-  return philox_x(d.seed, d.offset + 1 + 2 * (uint64_t)h + (uint64_t)kind, idx) >= d.threshold
+  return philox_x(d.seed, dropout_offset(d, d.offset + 1 + 2 * (uint64_t)h + (uint64_t)kind), idx) >=
+                 d.threshold
              ? d.scale : 0.f;
 }
 
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(256) ours_prep_kernel(
 // ---------------------------------------------------------------- forward ---
 // u_out[n] = u_in[n] + sum_{b: city(src_b) = city(n)} drop * w3_b h2[src_b]
 //                    + sum_{b: prov(src_b) = prov(n)} drop * w4_b h2[src_b]
-template <typename T>
+template <typename T, int KD>
 __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* __restrict__ bstat,
                                                        const T* __restrict__ u_in,
                                                        T* __restrict__ u_out) {
@@ -108,7 +109,6 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
   const int D = a.H * a.F;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  constexpr int KD = kMaxD / 64;
   for (int64_t n = wave; n < a.N; n += nwaves) {
     const int32_t g3 = a.gid3[n], g4 = a.gid4[n];
     float acc3[KD], acc4[KD];
@@ -120,6 +120,16 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
       const int64_t ib = valid ? a.src[b] : 0;
       uint64_t bal3 = __ballot(valid && a.gid3[ib] == g3);
       uint64_t bal4 = __ballot(valid && a.gid4[ib] == g4);
+      // keep bits of (b = base + lane, n) for every head, drawn lane-parallel once per
+      // chunk (bit h of kb3 / kb4); heads >= 32 fall back to a per-use draw
+      uint32_t kb3 = 0xffffffffu, kb4 = 0xffffffffu;
+      if (a.dp.active && (bal3 | bal4)) {
+        kb3 = kb4 = 0u;
+        for (int h = 0; h < a.H && h < 32; ++h) {
+          kb3 |= (intra_drop(a.dp, 0, h, (uint64_t)b * a.N + n) != 0.f ? 1u : 0u) << h;
+          kb4 |= (intra_drop(a.dp, 1, h, (uint64_t)b * a.N + n) != 0.f ? 1u : 0u) << h;
+        }
+      }
       for (int kind = 0; kind < 2; ++kind) {
         uint64_t bal = kind == 0 ? bal3 : bal4;
         while (bal) {
@@ -127,13 +137,17 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
           bal &= bal - 1;
           const int64_t bb = base + bit;
           const int64_t ibb = __shfl(ib, bit);
+          const uint32_t kbits = __shfl(kind == 0 ? kb3 : kb4, bit);
 #pragma unroll
           for (int k = 0; k < KD; ++k) {
             const int d = lane + 64 * k;
             if (d < D) {
               const int h = d / a.F;
-              const float w = bstat[(bb * a.H + h) * BS_N + (kind == 0 ? BS_W3 : BS_W4)] *
-                              intra_drop(a.dp, kind, h, (uint64_t)bb * a.N + n);
+              float drop = 1.f;
+              if (a.dp.active)
+                drop = h < 32 ? (((kbits >> h) & 1u) ? a.dp.scale : 0.f)
+                              : intra_drop(a.dp, kind, h, (uint64_t)bb * a.N + n);
+              const float w = bstat[(bb * a.H + h) * BS_N + (kind == 0 ? BS_W3 : BS_W4)] * drop;
               const float x = ldt<T>(a.h2, ibb * D + d);
               if (kind == 0) acc3[k] = fmaf(w, x, acc3[k]); else acc4[k] = fmaf(w, x, acc4[k]);
             }
@@ -153,9 +167,9 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 // Gp[b, kind, c] = sum_{n in chunk c of group(kind, src_b)} drop(kind, b, n) * dU[n]
 // (chunks of kGatherChunk members, ascending), then G[b, kind] = sum_c Gp[b, kind, c]
 // in chunk order: one wave per (b, kind, chunk) keeps thousands of members in flight.
-constexpr int kGatherChunk = 64;
+constexpr int kGatherChunk = 64;  // one member per lane for the keep-bit draw
 
-template <typename T>
+template <typename T, int KD>
 __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
                                                               const T* __restrict__ dU,
                                                               int nck, float* __restrict__ Gp) {
@@ -173,19 +187,31 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
   const int32_t grp = kind == 0 ? a.gid3[i] : a.gid4[i];
   const int32_t m0 = gptr[grp] + c * kGatherChunk;
   const int32_t m1 = min(gptr[grp + 1], m0 + kGatherChunk);
-  constexpr int KD = kMaxD / 64;
   float acc[KD];
 #pragma unroll
   for (int k = 0; k < KD; ++k) acc[k] = 0.f;
-  for (int32_t t = m0; t < m1; ++t) {
-    const int64_t n = gmem[t];
+  // members of this chunk: lane j draws the keep bits of (b, member j) for every head
+  const int cnt = m1 - m0;  // <= kGatherChunk == 64
+  const int64_t nj = lane < cnt ? (int64_t)gmem[m0 + lane] : 0;
+  uint32_t kbits = 0xffffffffu;
+  if (a.dp.active) {
+    kbits = 0u;
+    for (int h = 0; h < a.H && h < 32; ++h)
+      kbits |= (intra_drop(a.dp, kind, h, (uint64_t)b * a.N + nj) != 0.f ? 1u : 0u) << h;
+  }
+  for (int t = 0; t < cnt; ++t) {
+    const int64_t n = __shfl(nj, t);
+    const uint32_t kb = __shfl(kbits, t);
 #pragma unroll
     for (int k = 0; k < KD; ++k) {
       const int d = lane + 64 * k;
       if (d < D) {
         const int h = d / a.F;
-        acc[k] = fmaf(intra_drop(a.dp, kind, h, (uint64_t)b * a.N + n), to_f32(dU[n * D + d]),
-                      acc[k]);
+        float drop = 1.f;
+        if (a.dp.active)
+          drop = h < 32 ? (((kb >> h) & 1u) ? a.dp.scale : 0.f)
+                        : intra_drop(a.dp, kind, h, (uint64_t)b * a.N + n);
+        acc[k] = fmaf(drop, to_f32(dU[n * D + d]), acc[k]);
       }
     }
   }
@@ -217,74 +243,93 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, 
 //   batch order) -- the extra gradient sum_j exp(attd_ij) puts on the inter attention;
 //   da3s[h, f] = sum_b dpre3 h2_b, da4s likewise.
 // mode 1 (after it): d_hs[src_b] += w3 G3 + w4 G4 + dpre3 a3s + dpre4 a4s (per row,
-//   batch order).  One workgroup: B is a mini-batch (train.py:33, 64 flows).
+//   batch order).  One workgroup (B is a mini-batch, train.py:33, 64 flows): the dots
+//   and the sums over b run a wave per output with lanes across f / b and a fixed xor
+//   tree; the batch sources sit in LDS for the repeated-source scans.
+constexpr int kFinishLds = 2048;
+
 template <typename T>
 __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     OursArgs a, int mode, const float* __restrict__ bstat, const float* __restrict__ G,
     float* __restrict__ bgrad, float* __restrict__ row_coef, float* __restrict__ da3s,
     float* __restrict__ da4s, T* __restrict__ d_hs) {
+  __shared__ int64_t s_src[kFinishLds];
   const int H = a.H, F = a.F, D = H * F;
   const int64_t B = a.B;
+  const bool in_lds = B <= kFinishLds;
+  if (in_lds)
+    for (int64_t t = threadIdx.x; t < B; t += blockDim.x) s_src[t] = a.src[t];
+  __syncthreads();
+  auto SRC = [&](int64_t b) { return in_lds ? s_src[b] : a.src[b]; };
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (mode == 0) {
-    for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
+    for (int64_t t = wv; t < B * H; t += nw) {
       const int64_t b = t / H;
       const int h = (int)(t % H);
-      const int64_t i = a.src[b];
-      const float* st = bstat + (b * H + h) * BS_N;
+      const int64_t i = SRC(b);
       float dw3 = 0.f, dw4 = 0.f;
-      for (int f = 0; f < F; ++f) {
+      for (int f = lane; f < F; f += 64) {
         const float x = ldt<T>(a.h2, i * D + h * F + f);
         dw3 = fmaf(G[(b * 2 + 0) * D + h * F + f], x, dw3);
         dw4 = fmaf(G[(b * 2 + 1) * D + h * F + f], x, dw4);
       }
-      const float sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
-      const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
-      const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
-      const float dsum = -(dw3 * E3 + dw4 * E4) / (sum * sum);
-      const float dE3 = dw3 / sum + dsum * c3;
-      const float dE4 = dw4 / sum + dsum * c4;
-      const float p3 = st[BS_PRE3], p4 = st[BS_PRE4];
-      float* o = bgrad + t * 4;
-      o[0] = dE3 * E3 * (p3 > 0.f ? 1.f : a.slope);
-      o[1] = dE4 * E4 * (p4 > 0.f ? 1.f : a.slope);
-      o[2] = dsum;
+      dw3 = wave_xor_sum<1>(dw3);
+      dw4 = wave_xor_sum<1>(dw4);
+      if (lane == 0) {
+        const float* st = bstat + (b * H + h) * BS_N;
+        const float sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
+        const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
+        const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
+        const float dsum = -(dw3 * E3 + dw4 * E4) / (sum * sum);
+        const float dE3 = dw3 / sum + dsum * c3;
+        const float dE4 = dw4 / sum + dsum * c4;
+        const float p3 = st[BS_PRE3], p4 = st[BS_PRE4];
+        float* o = bgrad + t * 4;
+        o[0] = dE3 * E3 * (p3 > 0.f ? 1.f : a.slope);
+        o[1] = dE4 * E4 * (p4 > 0.f ? 1.f : a.slope);
+        o[2] = dsum;
+      }
     }
     __syncthreads();
     for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
       const int64_t b = t / H;
       const int h = (int)(t % H);
-      const int64_t i = a.src[b];
+      const int64_t i = SRC(b);
       bool first = true;
-      for (int64_t q = 0; q < b && first; ++q) first = a.src[q] != i;
+      for (int64_t q = 0; q < b && first; ++q) first = SRC(q) != i;
       if (!first) continue;
       float s = 0.f;
       for (int64_t q = b; q < B; ++q)
-        if (a.src[q] == i) s += bgrad[(q * H + h) * 4 + 2];
+        if (SRC(q) == i) s += bgrad[(q * H + h) * 4 + 2];
       row_coef[i * H + h] = s;
     }
-    for (int64_t t = threadIdx.x; t < (int64_t)H * F; t += blockDim.x) {
+    for (int64_t t = wv; t < (int64_t)H * F; t += nw) {
       const int h = (int)(t / F);
       float s3 = 0.f, s4 = 0.f;
-      for (int64_t b = 0; b < B; ++b) {
-        const float x = ldt<T>(a.h2, a.src[b] * D + t);
+      for (int64_t b = lane; b < B; b += 64) {
+        const float x = ldt<T>(a.h2, SRC(b) * D + t);
         s3 = fmaf(bgrad[(b * H + h) * 4 + 0], x, s3);
         s4 = fmaf(bgrad[(b * H + h) * 4 + 1], x, s4);
       }
-      da3s[t] = s3;
-      da4s[t] = s4;
+      s3 = wave_xor_sum<1>(s3);
+      s4 = wave_xor_sum<1>(s4);
+      if (lane == 0) {
+        da3s[t] = s3;
+        da4s[t] = s4;
+      }
     }
   } else {
     for (int64_t t = threadIdx.x; t < B * D; t += blockDim.x) {
       const int64_t b = t / D;
       const int d = (int)(t % D);
       const int h = d / F;
-      const int64_t i = a.src[b];
+      const int64_t i = SRC(b);
       bool first = true;
-      for (int64_t q = 0; q < b && first; ++q) first = a.src[q] != i;
+      for (int64_t q = 0; q < b && first; ++q) first = SRC(q) != i;
       if (!first) continue;
       float s = 0.f;
       for (int64_t q = b; q < B; ++q) {
-        if (a.src[q] != i) continue;
+        if (SRC(q) != i) continue;
         const float* st = bstat + (q * H + h) * BS_N;
         const float* gq = bgrad + (q * H + h) * 4;
         s += st[BS_W3] * G[(q * 2 + 0) * D + d] + st[BS_W4] * G[(q * 2 + 1) * D + d] +
@@ -331,8 +376,15 @@ static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const 
   if (B > 0)
     hipLaunchKernelGGL(ours_prep_kernel<T>, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
                        g->col, g->rowflag, el, er, lse, bstat);
-  hipLaunchKernelGGL(ours_fwd_kernel<T>, dim3(grid_for(g->n_rows, 4, 1 << 16)), dim3(256), 0, s,
-                     a, (const float*)bstat, (const T*)u_inter, (T*)u_out);
+  const dim3 grid(grid_for(g->n_rows, 4, 1 << 16));
+  const int D = a.H * a.F;
+#define FWD(kd) hipLaunchKernelGGL((ours_fwd_kernel<T, kd>), grid, dim3(256), 0, s, a, \
+                                   (const float*)bstat, (const T*)u_inter, (T*)u_out)
+  if (D <= 64) FWD(1);
+  else if (D <= 128) FWD(2);
+  else if (D <= 256) FWD(4);
+  else FWD(8);
+#undef FWD
 }
 
 extern "C" int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, int64_t B,
@@ -370,8 +422,15 @@ static void launch_bwd(const OursArgs& a, int stage, int64_t B, int nck, int hea
                        float* row_coef, float* da3s, float* da4s, void* d_hs, float* Gp,
                        hipStream_t s) {
   if (stage == 0) {
-    hipLaunchKernelGGL(ours_bwd_gather_kernel<T>, dim3(grid_for(2 * B * nck, 4)), dim3(256), 0, s,
-                       a, (const T*)dU, nck, Gp);
+    const int D = heads * feat;
+    const dim3 grid(grid_for(2 * B * nck, 4));
+#define GATHER(kd) hipLaunchKernelGGL((ours_bwd_gather_kernel<T, kd>), grid, dim3(256), 0, s, a, \
+                                      (const T*)dU, nck, Gp)
+    if (D <= 64) GATHER(1);
+    else if (D <= 128) GATHER(2);
+    else if (D <= 256) GATHER(4);
+    else GATHER(8);
+#undef GATHER
     hipLaunchKernelGGL(ours_bwd_gather_reduce_kernel,
                        dim3(grid_for(2 * B * heads * feat, 256, 4096)), dim3(256), 0, s, B,
                        heads * feat, nck, (const float*)Gp, G);

@@ -6,6 +6,9 @@
 namespace msha {
 
 static thread_local std::string g_last_error;
+static const uint64_t* g_rng_counter = nullptr;
+
+const uint64_t* rng_counter() { return g_rng_counter; }
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 
@@ -34,6 +37,11 @@ __global__ void __launch_bounds__(256) dropout_mask_kernel(Dropout d, int64_t n,
 extern "C" int msha_abi_version(void) { return MSHA_ABI_VERSION; }
 
 extern "C" const char* msha_last_error(void) { return msha::g_last_error.c_str(); }
+
+extern "C" int msha_set_rng_counter(const uint64_t* counter) {
+  msha::g_rng_counter = counter;
+  return MSHA_OK;
+}
 
 extern "C" int msha_dropout_keep_mask(uint64_t seed, uint64_t offset, int64_t n, float p,
                                       uint8_t* keep, msha_stream_t stream) {

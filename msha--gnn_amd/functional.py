@@ -56,6 +56,22 @@ def new_seed() -> int:
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
 
 
+_RNG_COUNTER = None
+
+
+def set_rng_counter(counter: torch.Tensor | None):
+    """Install (or remove, None) a device int64 replay counter for every dropout draw
+    of the library (msha_set_rng_counter): increment it inside a captured HIP graph
+    (``counter.add_(1)``) and each replay draws fresh masks."""
+    global _RNG_COUNTER
+    if counter is not None:
+        _lib.require_cuda(counter)
+        if counter.dtype != torch.int64 or counter.numel() < 1:
+            raise ValueError("rng counter: a CUDA int64 tensor")
+    _RNG_COUNTER = counter  # keep it alive while installed
+    _lib.call("msha_set_rng_counter", None if counter is None else counter.data_ptr())
+
+
 def _stream(t):
     return _lib.stream_handle(t.device)
 
@@ -297,6 +313,38 @@ def gemm_head_outer(A: torch.Tensor, B: torch.Tensor, operand: int, outer,
     _lib.call("msha_add_head_outer", X.shape[0], H, Fd, _f32c(X).data_ptr(), d1.data_ptr(),
               a1.data_ptr(), _lib.ptr(d2), _lib.ptr(a2), tot.data_ptr(), _stream(X))
     return gemm(tot, B) if operand == 0 else gemm(A, tot)
+
+
+class _MatMul(torch.autograd.Function):
+    """C = A @ B with both products of the backward on the library GEMMs (split-K over
+    long reductions, deterministic)."""
+
+    @staticmethod
+    def forward(ctx, A, B):
+        ctx.save_for_backward(A, B)
+        return _mm(A, B)
+
+    @staticmethod
+    def backward(ctx, dC):
+        A, B = ctx.saved_tensors
+        dA = _mm(dC, B.t()).to(A.dtype) if ctx.needs_input_grad[0] else None
+        dB = _mm(A.t(), dC).to(B.dtype) if ctx.needs_input_grad[1] else None
+        return dA, dB
+
+
+def _mm(A, B):
+    if A.dtype == BF16 or B.dtype == BF16:
+        if B.shape[1] % 8 == 0:
+            return gemm(A, B)
+        # bf16 C needs N % 8 == 0: fp32 operands on the exact-fp32 kernel instead
+        return gemm(A.float(), B.float()).to(BF16)
+    return gemm(A.float(), B.float())
+
+
+def matmul(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """Differentiable A @ B on the library GEMMs (fp32, or bf16 when an operand is)."""
+    _lib.require_cuda(A, B)
+    return _MatMul.apply(A, B)
 
 
 class _ProjectScores(torch.autograd.Function):

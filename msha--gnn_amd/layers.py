@@ -140,7 +140,9 @@ class OursLayer3(nn.Module):
         backward is ~30x slower on the strided view, so they are made contiguous.)"""
         v_out = self.leakyrelu(self.bn1(v.contiguous()))
         u_out = self.leakyrelu(self.bn2(u.contiguous()))
-        return F.elu(u_out @ v_out.t())
+        # u_out @ v_out.T on the library GEMM: its backward's v-side product reduces over
+        # all N rows (deterministic split-K instead of a 2-workgroup BLAS tile)
+        return F.elu(MF.matmul(u_out, v_out.t()))
 
     def forward(self, Sinput, Rinput, inter_adj, city_adj, province_adj, source_index):
         return fused_ours_layer3([self], Sinput, Rinput, _graph(inter_adj), self.training)[0]

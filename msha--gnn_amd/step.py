@@ -1,0 +1,55 @@
+"""Whole-iteration HIP-graph capture for the train.py step (train.py:221-232).
+
+The shipped graphs are small (R15: 39k sources, 91k edges), so one training
+iteration -- forward, nll, backward, Adam -- is ~160 short launches and its wall
+time is host launch overhead, not kernel time.  ``GraphedStep`` captures the
+iteration once into a HIP graph (torch.cuda.CUDAGraph over the current HIP stream)
+and replays it: the library's kernels and the torch ops around them (BatchNorm,
+dropout, the loss, the capturable Adam) all become graph nodes.
+
+Dropout stays fresh across replays: the library's Philox draws take their seeds as
+kernel arguments (frozen at capture), so a device replay counter is installed with
+``functional.set_rng_counter`` and incremented as the first node of the graph
+(include/msha_gnn.h, msha_set_rng_counter); torch's own dropout uses its
+generator's graph-safe offsets.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+from . import functional as MF
+
+
+class GraphedStep:
+    """Capture ``body()`` (one full iteration; it reads its batch from static device
+    tensors the caller refills before each replay) and replay it.
+
+    The optimizer must be built with ``capturable=True``; gradients must be None
+    before capture (``zero_grad(set_to_none=True)``) so the captured backward writes
+    fresh gradient buffers on every replay instead of accumulating."""
+
+    def __init__(self, body: Callable[[], torch.Tensor], device, warmup: int = 3):
+        self.device = torch.device(device)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        MF.set_rng_counter(self.counter)
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):  # warm caches (graph views, workspaces) off-graph
+            for _ in range(warmup):
+                self.counter.add_(1)
+                body()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.counter.add_(1)
+            self.out = body()
+
+    def replay(self) -> torch.Tensor:
+        self.graph.replay()
+        return self.out
+
+    def close(self):
+        MF.set_rng_counter(None)
+        self.graph = None

@@ -1,0 +1,101 @@
+"""HIP-graph capture of a training iteration (step.GraphedStep) and the device replay
+counter of the library's dropout (msha_set_rng_counter)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden
+from gpu_helpers import random_counts, t
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rng_counter_fresh_masks_per_replay(cuda, msha):
+    """A captured dropout edge-attention replays with new masks after each counter
+    increment, and the same counter value reproduces the same mask."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(3)
+    c = random_counts(rng, 300, 32, 20)
+    graph = Graph.from_dense(t(c, cuda))
+    el, er = t(rng.standard_normal((300, 2)), cuda), t(rng.standard_normal((32, 2)), cuda)
+    hc = t(rng.standard_normal((32, 2, 64)), cuda)
+    ctr = torch.zeros(1, dtype=torch.int64, device=cuda)
+    MF.set_rng_counter(ctr)
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            MF.edge_attention(graph, el, er, hc, p=0.5, training=True, seed=5)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ctr.add_(1)
+            u = MF.edge_attention(graph, el, er, hc, p=0.5, training=True, seed=5)
+        outs = []
+        for _ in range(2):
+            g.replay()
+            outs.append(u.clone())
+        assert not torch.equal(outs[0], outs[1])
+        ctr.zero_()
+        g.replay()  # counter back to 1: the first replay's masks
+        assert torch.equal(u, outs[0])
+        # eager with the same counter value draws the same masks as the graph
+        ctr.fill_(1)
+        assert torch.equal(MF.edge_attention(graph, el, er, hc, p=0.5, training=True, seed=5),
+                           outs[0])
+    finally:
+        MF.set_rng_counter(None)
+
+
+def _ours_model(z, cuda, dropout):
+    from msha_gnn_amd import layers
+
+    n, m = z["counts"].shape
+    torch.manual_seed(0)
+    return layers.Ours(16, 8, m, 2, dropout, {i: 0.1 * i for i in range(n)}, n, m).to(cuda)
+
+
+def test_graphed_train_step_matches_eager(cuda, msha):
+    """Ours train step (forward, nll, backward, capturable Adam) replayed from a HIP
+    graph gives the eager losses and parameters (dropout 0: deterministic)."""
+    from msha_gnn_amd.data import GroupAdjacency
+    from msha_gnn_amd.step import GraphedStep
+
+    z = golden("ours_small.npz")
+    inter = msha.normalize_adjacency_matrix(t(z["counts"], cuda))
+    city = GroupAdjacency(torch.as_tensor(z["city"], device=cuda))
+    prov = GroupAdjacency(torch.as_tensor(z["prov"], device=cuda))
+    src = torch.as_tensor(z["source_index"], device=cuda)
+    tgt = torch.as_tensor(np.arange(src.numel()) % z["counts"].shape[1], device=cuda)
+    runs = {}
+    for graphed in (False, True):
+        model = _ours_model(z, cuda, 0.0)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4,
+                               capturable=graphed)
+        model.train()
+
+        def body():
+            opt.zero_grad(set_to_none=True)
+            out = model(inter, city, prov, src)
+            loss = F.nll_loss(out[src], tgt)
+            loss.backward()
+            opt.step()
+            return loss
+
+        losses = []
+        if graphed:
+            gs = GraphedStep(body, cuda, warmup=1)
+            for _ in range(3):
+                losses.append(float(gs.replay().detach()))
+            gs.close()
+        else:
+            body()  # the graphed run's warm-up step
+            for _ in range(3):
+                losses.append(float(body().detach()))
+        runs[graphed] = (losses, {k: p.detach().clone() for k, p in model.named_parameters()})
+    np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=1e-6)
+    for k, p in runs[False][1].items():
+        torch.testing.assert_close(runs[True][1][k], p, rtol=1e-5, atol=1e-6, msg=k)

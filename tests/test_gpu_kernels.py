@@ -234,6 +234,7 @@ def test_gal_fwd_bwd(cuda, p):
     (1000, 128, 128, False, False, 1), (257, 64, 64, False, False, 1),
     (64, 200, 96, False, True, 1), (128, 128, 20000, True, False, 64),
     (33, 40, 5000, False, False, 8),
+    (64, 32, 10001, True, False, 16),  # K % 4 != 0 with row-contiguous operands (dW)
 ])
 def test_gemm_f32(cuda, M, N, K, trans_a, trans_b, splits):
     from msha_gnn_amd import functional as MF
@@ -284,6 +285,7 @@ def test_project_scores_fwd_bwd(cuda, M, K, H, F):
 
 @pytest.mark.parametrize("operand,M,H,F,K,two", [(1, 100000, 8, 16, 128, True),
                                                  (1, 5000, 2, 64, 96, False),
+                                                 (1, 50015, 2, 64, 128, True),
                                                  (0, 3000, 8, 16, 128, True),
                                                  (0, 517, 1, 8, 40, False)])
 def test_gemm_head_outer(cuda, operand, M, H, F, K, two):
