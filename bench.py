@@ -69,6 +69,28 @@ WORKLOADS = {
 }
 
 
+def pmc_traffic(H, F, bf16=False, workload="syn100k"):
+    """HBM bytes per launch of the forward edge kernel from the newest committed PMC
+    summary of this workload (profiles/*/pmc_summary.json, written by
+    scripts/profile.sh + summarize_profile.py from separate rocprofv3 --pmc passes:
+    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  None if absent."""
+    import glob
+    import re
+
+    pat = (re.compile(rf"edge_attn_fwd_kernelILi{H}ELi{F}EDF16b") if bf16 else
+           re.compile(rf"edge_attn_fwd_kernel<{H}, {F}(, float)?>"))
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{workload}*",
+                                              "pmc_summary.json")), reverse=True):
+        try:
+            summ = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for k, v in summ.items():
+            if pat.search(k) and v.get("hbm_bytes_per_launch_corrected"):
+                return float(v["hbm_bytes_per_launch_corrected"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def fwd_bytes(n, m, e, H, F, s=4):
     """Algorithmic bytes of one msha_edge_attention_fwd launch:
     rowptr + col + er gather + el + h gather (s*HF per edge) + u write + lse write;
@@ -388,13 +410,15 @@ def main():
         dt16, k16, n16 = timed(lay16, args.steps, args.warmup)
         fb16 = fwd_bytes(n, m, e, H, F, s=2)
         a16 = fb16 / (k16 * 1e-3) / 1e9
+        tr16, src16 = pmc_traffic(H, F, True, args.workload)
         bf16_leg = {"workload": f"gat_layer_{args.workload} (config C3: bf16 tables, bf16 MFMA "
                                 "projection, fp32 scores/softmax)",
                     "value": world * e * args.steps / dt16, "unit": "edges/s",
                     "ms_per_step": dt16 / args.steps * 1e3, "dtype": "bf16",
                     "roofline": {"kernel": "msha_edge_attention_fwd<bf16>", "bound": "hbm",
                                  "achieved": a16, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": a16 / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": fb16,
+                                 "frac": a16 / HBM_PEAK_GBS, "traffic": tr16,
+                                 "traffic_source": src16, "algorithmic_bytes_per_launch": fb16,
                                  "avg_launch_us": k16 * 1e3, "launches_timed": n16}}
         del lay16
     link = None
@@ -408,6 +432,7 @@ def main():
     value = world * e * args.steps / dt
     fb = fwd_bytes(n, m, e, H, F)
     achieved = fb / (k_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(H, F, False, args.workload)
     out = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
@@ -417,7 +442,9 @@ def main():
                    "in_features": fin, "heads": H, "feat": F, "parallelism": f"replicas{world}"},
         "roofline": {"kernel": "msha_edge_attention_fwd", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 PMC, same command)",
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": fb, "avg_launch_us": k_ms * 1e3,
                      "launches_timed": n_launch},
     }
