@@ -273,6 +273,28 @@ MSHA_API int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, int32_t
                               const float* s1, const float* s2, const void* T, float* out1,
                               float* out2, void* ws, size_t ws_bytes, msha_stream_t stream);
 
+/* ------------------------------------------------- BatchNorm + LeakyReLU --- */
+/* Ablation.py:273-274 / Ours.py:100-101 epilogue: y = lrelu(bn(x)) on (rows, channels)
+ * tables (dtype fp32 / bf16; weight, bias, statistics fp32; weight / bias nullable =
+ * 1 / 0).  training != 0: batch statistics (mean, invstd = 1/sqrt(var_biased + eps)
+ * written to mean / invstd), running_mean / running_var (nullable pair) updated with
+ * momentum and the unbiased variance, as torch.nn.BatchNorm1d; training == 0: the
+ * running statistics normalise.  Deterministic (fixed-order Welford / Chan combines).
+ * Backward (training statistics): dx, dweight = sum dz xhat, dbias = sum dz with
+ * dz = dy lrelu'(z).  Workspace: msha_bn_workspace_size(rows, channels) (0 for
+ * rows <= 256: one workgroup). */
+MSHA_API size_t msha_bn_workspace_size(int64_t rows, int32_t channels);
+MSHA_API int msha_bn_lrelu_fwd(int64_t rows, int32_t channels, int32_t dtype, const void* x,
+                               const float* weight, const float* bias, float eps, float slope,
+                               int32_t training, float momentum, float* running_mean,
+                               float* running_var, float* mean, float* invstd, void* y,
+                               void* ws, size_t ws_bytes, msha_stream_t stream);
+MSHA_API int msha_bn_lrelu_bwd(int64_t rows, int32_t channels, int32_t dtype, const void* x,
+                               const void* dy, const float* weight, const float* bias,
+                               const float* mean, const float* invstd, float slope, void* dx,
+                               float* dweight, float* dbias, void* ws, size_t ws_bytes,
+                               msha_stream_t stream);
+
 /* ----------------------------------------------------------- link scoring --- */
 /* LLP.py:104-115 LinkPredictor with the caller's gather (LLP.py:233) fused:
  * x_i = G[gi[b]], x_j = G2[gj[b]] (gi / gj NULL: row b).

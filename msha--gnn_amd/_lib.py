@@ -83,6 +83,10 @@ SIGNATURES = {
     "msha_gemm_bf16": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, I32, I32, P, SZ,
                                  I32, I32, I32, P, P, P, P, P]),
     "msha_project_scores_bf16": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
+    "msha_bn_workspace_size": (SZ, [I64, I32]),
+    "msha_bn_lrelu_fwd": (C.c_int, [I64, I32, I32, P, P, P, F32, F32, I32, F32, P, P, P, P, P, P,
+                                    SZ, P]),
+    "msha_bn_lrelu_bwd": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, F32, P, P, P, P, SZ, P]),
     "msha_pair_linear": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64, U64,
                                    P, P]),
     "msha_pair_inner_fwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),

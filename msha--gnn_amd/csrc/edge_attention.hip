@@ -57,21 +57,37 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
 
-  for (int64_t row = wave; row < n_rows; row += nwaves) {
-    const int32_t start = rowptr[row], end = rowptr[row + 1];
-    const bool virt = rowflag != nullptr && rowflag[row] != 0;
-    const float elh = el[row * H + h_s];
+  // Software pipeline (the kernel is latency-bound per row: rowptr -> col -> er ->
+  // gathers): the next row's bounds, flag, el and first two chunks' columns are loaded
+  // while this row runs, and inside a row the column two chunks ahead and the er one
+  // chunk ahead are in flight during the current chunk's gathers.
+  int64_t row = wave;
+  if (row >= n_rows) return;
+  int32_t start = rowptr[row], end = rowptr[row + 1];
+  bool virt = rowflag != nullptr && rowflag[row] != 0;
+  float elh = el[row * H + h_s];
+  int32_t j0 = start + e_s < end ? col[start + e_s] : 0;
+  int32_t j1 = start + G::CE + e_s < end ? col[start + G::CE + e_s] : 0;
+  while (true) {
+    const int64_t nrow = row + nwaves;
+    const bool has_next = nrow < n_rows;
+    const int32_t nstart = has_next ? rowptr[nrow] : 0;
+    const int32_t nend = has_next ? rowptr[nrow + 1] : 0;
     float m = -INFINITY, l = 0.f;
     Pk<T> acc[G::QPL];
 #pragma unroll
     for (int k = 0; k < G::QPL; ++k) acc[k] = pk_zero<T>();
+    float erv = start + e_s < end ? er[(int64_t)j0 * H + h_s] : 0.f;
 
     for (int32_t cs = start; cs < end; cs += G::CE) {
       const int32_t e = cs + e_s;
       const bool valid = e < end;
-      const int32_t j = valid ? col[e] : 0;
+      const int32_t j = j0;
+      const int32_t e2 = e + 2 * G::CE;
+      const int32_t j2 = e2 < end ? col[e2] : 0;
+      const float ern = e + G::CE < end ? er[(int64_t)j1 * H + h_s] : 0.f;
       float s = -INFINITY;
-      if (valid) s = virt ? 0.f : lrelu(elh + er[(int64_t)j * H + h_s], slope);
+      if (valid) s = virt ? 0.f : lrelu(elh + erv, slope);
       const float mn = fmaxf(m, wave_xor_max<H>(s));
       const float alpha = __expf(m - mn);
       const float pe = valid ? __expf(s - mn) : 0.f;
@@ -96,6 +112,18 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
           if (ei < nvalid) acc[k] = pk_fma(wq, pk_load(hc + (int64_t)jq * G::D + G::V * q), acc[k]);
         }
       }
+      j0 = j1;
+      j1 = j2;
+      erv = ern;
+    }
+    // the next row's first loads go out before this row's epilogue
+    bool nvirt = false;
+    float nelh = 0.f;
+    if (has_next) {
+      nvirt = rowflag != nullptr && rowflag[nrow] != 0;
+      nelh = el[nrow * H + h_s];
+      j0 = nstart + e_s < nend ? col[nstart + e_s] : 0;
+      j1 = nstart + G::CE + e_s < nend ? col[nstart + G::CE + e_s] : 0;
     }
     if (G::EPI > 1) {
 #pragma unroll
@@ -120,6 +148,12 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
         }
       }
     }
+    if (!has_next) break;
+    row = nrow;
+    start = nstart;
+    end = nend;
+    virt = nvirt;
+    elh = nelh;
   }
 }
 
@@ -340,28 +374,50 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
   }
 }
 
-// multi-chunk columns: add the chunk partials in chunk order
+// multi-chunk columns: add the chunk partials.  Block = one column x a tile of 256
+// output elements (D table columns then H x-sums); its 16 waves stride the column's
+// chunks (wave g takes chunks g, g+16, ...) and the 16 partial sums are added in a
+// fixed LDS tree (deterministic).
+constexpr int kCombineWaves = 16;
+
 template <typename T>
-__global__ void __launch_bounds__(256) csc_combine_kernel(
+__global__ void __launch_bounds__(1024) csc_combine_kernel(
     const int32_t* __restrict__ multi_col, const int32_t* __restrict__ multi_first,
     const int32_t* __restrict__ multi_count, int64_t n_multi, int D, int H,
     const float* __restrict__ part, const float* __restrict__ part_x, T* __restrict__ out,
     float* __restrict__ out_x) {
+  __shared__ float red[kCombineWaves][256];
   const int W = D + (part_x != nullptr ? H : 0);
-  const int64_t total = n_multi * W;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t mi = t / W;
-    const int f = (int)(t % W);
-    const int32_t jc = multi_col[mi], first = multi_first[mi], cnt = multi_count[mi];
-    float s = 0.f;
-    if (f < D) {
-      for (int k = 0; k < cnt; ++k) s += part[(int64_t)(first + k) * D + f];
-      out[(int64_t)jc * D + f] = from_f32<T>(s);
-    } else {
-      const int h = f - D;
-      for (int k = 0; k < cnt; ++k) s += part_x[(int64_t)(first + k) * H + h];
-      out_x[(int64_t)jc * H + h] = s;
+  const int64_t mi = blockIdx.x;
+  const int e0 = blockIdx.y * 256;
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int32_t jc = multi_col[mi], first = multi_first[mi], cnt = multi_count[mi];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k = g; k < cnt; k += kCombineWaves) {
+    const int64_t c = first + k;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = e0 + lane + 64 * q;
+      if (e < D) acc[q] += part[c * D + e];
+      else if (e < W) acc[q] += part_x[c * H + (e - D)];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[g][lane + 64 * q] = acc[q];
+  __syncthreads();
+  for (int w = kCombineWaves / 2; w >= 1; w >>= 1) {
+    if (g < w) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[g][lane + 64 * q] += red[g + w][lane + 64 * q];
+    }
+    __syncthreads();
+  }
+  if (g == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = e0 + lane + 64 * q;
+      if (e < D) out[(int64_t)jc * D + e] = from_f32<T>(red[0][lane + 64 * q]);
+      else if (e < W) out_x[(int64_t)jc * H + (e - D)] = red[0][lane + 64 * q];
     }
   }
 }
@@ -523,9 +579,10 @@ static void launch_csc(const msha_graph* g, int heads, int feat, const float* w,
   if (g->n_multi > 0) {
     const int64_t D = (int64_t)heads * feat;
     const int64_t W = D + (x ? heads : 0);
-    hipLaunchKernelGGL(csc_combine_kernel<T>, dim3(grid_for(g->n_multi * W, 256, 8192)),
-                       dim3(256), 0, s, g->multi_col, g->multi_first, g->multi_count, g->n_multi,
-                       (int)D, heads, part, x ? part_x : nullptr, (T*)out, out_x);
+    hipLaunchKernelGGL(csc_combine_kernel<T>, dim3(g->n_multi, (W + 255) / 256),
+                       dim3(64 * kCombineWaves), 0, s, g->multi_col, g->multi_first,
+                       g->multi_count, g->n_multi, (int)D, heads, part, x ? part_x : nullptr,
+                       (T*)out, out_x);
   }
 }
 

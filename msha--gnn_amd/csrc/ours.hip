@@ -254,6 +254,8 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     float* __restrict__ bgrad, float* __restrict__ row_coef, float* __restrict__ da3s,
     float* __restrict__ da4s, T* __restrict__ d_hs) {
   __shared__ int64_t s_src[kFinishLds];
+  __shared__ int32_t s_next[kFinishLds];  // next batch entry with the same source, -1 = none
+  __shared__ uint8_t s_first[kFinishLds];  // first batch entry of its source
   const int H = a.H, F = a.F, D = H * F;
   const int64_t B = a.B;
   const bool in_lds = B <= kFinishLds;
@@ -261,8 +263,38 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     for (int64_t t = threadIdx.x; t < B; t += blockDim.x) s_src[t] = a.src[t];
   __syncthreads();
   auto SRC = [&](int64_t b) { return in_lds ? s_src[b] : a.src[b]; };
+  if (in_lds) {
+    for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+      const int64_t i = s_src[b];
+      bool first = true;
+      for (int64_t q = 0; q < b && first; ++q) first = s_src[q] != i;
+      int32_t nx = -1;
+      for (int64_t q = b + 1; q < B; ++q)
+        if (s_src[q] == i) { nx = (int32_t)q; break; }
+      s_first[b] = first ? 1 : 0;
+      s_next[b] = nx;
+    }
+    __syncthreads();
+  }
+  // batch entries of b's source in batch order (b first): the per-row sums below
+  auto is_first = [&](int64_t b) {
+    if (in_lds) return s_first[b] != 0;
+    const int64_t i = a.src[b];
+    for (int64_t q = 0; q < b; ++q)
+      if (a.src[q] == i) return false;
+    return true;
+  };
+  auto next_same = [&](int64_t q) -> int64_t {
+    if (in_lds) return s_next[q];
+    const int64_t i = a.src[q];
+    for (int64_t r = q + 1; r < B; ++r)
+      if (a.src[r] == i) return r;
+    return -1;
+  };
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (mode == 0) {
+    // dots dw3 = G3 . h2_b, dw4 = G4 . h2_b: a wave per (b, h), lanes across f; parked
+    // in bgrad[.., 0..1], then the scalar chain runs a thread per (b, h) in parallel
     for (int64_t t = wv; t < B * H; t += nw) {
       const int64_t b = t / H;
       const int h = (int)(t % H);
@@ -276,18 +308,8 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       dw3 = wave_xor_sum<1>(dw3);
       dw4 = wave_xor_sum<1>(dw4);
       if (lane == 0) {
-        const float* st = bstat + (b * H + h) * BS_N;
-        const float sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
-        const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
-        const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
-        const float dsum = -(dw3 * E3 + dw4 * E4) / (sum * sum);
-        const float dE3 = dw3 / sum + dsum * c3;
-        const float dE4 = dw4 / sum + dsum * c4;
-        const float p3 = st[BS_PRE3], p4 = st[BS_PRE4];
-        float* o = bgrad + t * 4;
-        o[0] = dE3 * E3 * (p3 > 0.f ? 1.f : a.slope);
-        o[1] = dE4 * E4 * (p4 > 0.f ? 1.f : a.slope);
-        o[2] = dsum;
+        bgrad[t * 4 + 0] = dw3;
+        bgrad[t * 4 + 1] = dw4;
       }
     }
     __syncthreads();
@@ -295,13 +317,28 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       const int64_t b = t / H;
       const int h = (int)(t % H);
       const int64_t i = SRC(b);
-      bool first = true;
-      for (int64_t q = 0; q < b && first; ++q) first = SRC(q) != i;
-      if (!first) continue;
+      const float dw3 = bgrad[t * 4 + 0], dw4 = bgrad[t * 4 + 1];
+      const float* st = bstat + (b * H + h) * BS_N;
+      const float sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
+      const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
+      const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
+      const float dsum = -(dw3 * E3 + dw4 * E4) / (sum * sum);
+      const float dE3 = dw3 / sum + dsum * c3;
+      const float dE4 = dw4 / sum + dsum * c4;
+      const float p3 = st[BS_PRE3], p4 = st[BS_PRE4];
+      float* o = bgrad + t * 4;
+      o[0] = dE3 * E3 * (p3 > 0.f ? 1.f : a.slope);
+      o[1] = dE4 * E4 * (p4 > 0.f ? 1.f : a.slope);
+      o[2] = dsum;
+    }
+    __syncthreads();
+    for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
+      const int64_t b = t / H;
+      const int h = (int)(t % H);
+      if (!is_first(b)) continue;
       float s = 0.f;
-      for (int64_t q = b; q < B; ++q)
-        if (SRC(q) == i) s += bgrad[(q * H + h) * 4 + 2];
-      row_coef[i * H + h] = s;
+      for (int64_t q = b; q >= 0; q = next_same(q)) s += bgrad[(q * H + h) * 4 + 2];
+      row_coef[SRC(b) * H + h] = s;
     }
     for (int64_t t = wv; t < (int64_t)H * F; t += nw) {
       const int h = (int)(t / F);
@@ -324,12 +361,9 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       const int d = (int)(t % D);
       const int h = d / F;
       const int64_t i = SRC(b);
-      bool first = true;
-      for (int64_t q = 0; q < b && first; ++q) first = SRC(q) != i;
-      if (!first) continue;
+      if (!is_first(b)) continue;
       float s = 0.f;
-      for (int64_t q = b; q < B; ++q) {
-        if (SRC(q) != i) continue;
+      for (int64_t q = b; q >= 0; q = next_same(q)) {
         const float* st = bstat + (q * H + h) * BS_N;
         const float* gq = bgrad + (q * H + h) * 4;
         s += st[BS_W3] * G[(q * 2 + 0) * D + d] + st[BS_W4] * G[(q * 2 + 1) * D + d] +

@@ -227,9 +227,12 @@ def dropout_keep_mask(n: int, p: float, seed: int, device, offset: int = 0) -> t
 
 
 # ------------------------------------------------------------------ projections ---
-def _splits_for(rows: int) -> int:
-    """split-K factor for reductions over `rows`: ~256 workgroups of >= 256 rows."""
-    return max(1, min(256, rows // 256))
+def _splits_for(rows: int, M: int = 128, N: int = 128) -> int:
+    """split-K factor for reductions over `rows`: >= 64 rows per split, <= ~1024
+    workgroups in all, and the fp32 slab (splits x M x N) within 16 MB."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    slab_cap = max(1, (16 << 20) // (4 * M * N))
+    return max(1, min(rows // 64, slab_cap, max(1, 1024 // tiles)))
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
@@ -241,7 +244,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None,
     K2, N = B.shape
     assert K == K2
     if splits is None:
-        splits = _splits_for(K) if K >= 4096 else 1
+        splits = _splits_for(K, M, N) if K >= 4096 else 1
     if A.dtype == BF16 or B.dtype == BF16:
         assert not accumulate and out is None, "bf16 gemm: no accumulate / out"
         return _gemm_bf16(A, B, splits, out_dtype or BF16, -1, None)
@@ -292,7 +295,7 @@ def gemm_head_outer(A: torch.Tensor, B: torch.Tensor, operand: int, outer,
     H, Fd, d1, a1, d2, a2 = outer
     M, K = A.shape
     N = B.shape[1]
-    splits = _splits_for(K) if K >= 4096 else 1
+    splits = _splits_for(K, M, N) if K >= 4096 else 1
     if A.dtype == BF16 or B.dtype == BF16:
         return _gemm_bf16(A, B, splits, out_dtype or BF16, operand, outer)
     out = torch.empty(M, N, device=A.device, dtype=torch.float32)
@@ -440,6 +443,87 @@ def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = No
     if ar is not None:
         ar = ar.reshape(heads, feat)
     return _ProjectScores.apply(X, W, al, ar, heads, feat)
+
+
+# --------------------------------------------------- BatchNorm + LeakyReLU ---
+class _BnLRelu(torch.autograd.Function):
+    """lrelu(batch_norm(x)) with training batch statistics (Ablation.py:273-274)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, slope, momentum):
+        dt = _table_dtype(x)
+        x = _tc(x, dt)
+        R, C = x.shape
+        dev = x.device
+        w32, b32 = _f32c(weight), _f32c(bias)
+        rm = rv = None
+        if running_mean is not None:
+            rm, rv = _f32c(running_mean), _f32c(running_var)
+        mean = torch.empty(C, device=dev, dtype=torch.float32)
+        invstd = torch.empty(C, device=dev, dtype=torch.float32)
+        y = torch.empty_like(x)
+        wsb = int(_lib.load().msha_bn_workspace_size(R, C))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        _lib.call("msha_bn_lrelu_fwd", R, C, _code(dt), x.data_ptr(), _lib.ptr(w32),
+                  _lib.ptr(b32), eps, slope, 1, momentum, _lib.ptr(rm), _lib.ptr(rv),
+                  mean.data_ptr(), invstd.data_ptr(), y.data_ptr(), ws.data_ptr(), ws.numel(),
+                  _stream(x))
+        if rm is not None and rm.data_ptr() != running_mean.data_ptr():
+            running_mean.copy_(rm)  # non-fp32 / strided buffers: write the update back
+            running_var.copy_(rv)
+        ctx.slope = slope
+        ctx.pdtypes = (None if weight is None else weight.dtype, None if bias is None else bias.dtype)
+        ctx.save_for_backward(x, w32, b32, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w32, b32, mean, invstd = ctx.saved_tensors
+        R, C = x.shape
+        dev = x.device
+        dy = _tc(dy, x.dtype)
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, device=dev, dtype=torch.float32) if w32 is not None else None
+        db = torch.empty(C, device=dev, dtype=torch.float32) if b32 is not None else None
+        wsb = int(_lib.load().msha_bn_workspace_size(R, C))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        _lib.call("msha_bn_lrelu_bwd", R, C, _code(x.dtype), x.data_ptr(), dy.data_ptr(),
+                  _lib.ptr(w32), _lib.ptr(b32), mean.data_ptr(), invstd.data_ptr(), ctx.slope,
+                  dx.data_ptr(), _lib.ptr(dw), _lib.ptr(db), ws.data_ptr(), ws.numel(),
+                  _stream(x))
+        wdt, bdt = ctx.pdtypes
+        return (dx, None if dw is None else dw.to(wdt), None if db is None else db.to(bdt),
+                None, None, None, None, None)
+
+
+def bn_lrelu(x: torch.Tensor, bn: torch.nn.BatchNorm1d, slope: float) -> torch.Tensor:
+    """``lrelu(bn(x), slope)`` for a (rows, C) table on the fused kernels: batch
+    statistics and the running-statistics update as torch.nn.BatchNorm1d in training
+    mode (momentum set; num_batches_tracked advanced on the device), running
+    statistics in eval mode."""
+    _lib.require_cuda(x)
+    if x.dim() != 2 or bn.momentum is None:
+        # cumulative-average momentum needs the host-side batch count: torch's path
+        return torch.nn.functional.leaky_relu(bn(x), slope)
+    use_batch = bn.training or not bn.track_running_stats
+    if not use_batch:
+        if torch.is_grad_enabled() and (x.requires_grad or bn.weight.requires_grad):
+            return torch.nn.functional.leaky_relu(bn(x), slope)  # eval with autograd
+        dt = _table_dtype(x)
+        xc = _tc(x, dt)
+        R, C = xc.shape
+        y = torch.empty_like(xc)
+        rm, rv = _f32c(bn.running_mean), _f32c(bn.running_var)
+        _lib.call("msha_bn_lrelu_fwd", R, C, _code(dt), xc.data_ptr(), _lib.ptr(_f32c(bn.weight)),
+                  _lib.ptr(_f32c(bn.bias)), bn.eps, slope, 0, 0.0, rm.data_ptr(), rv.data_ptr(),
+                  None, None, y.data_ptr(), None, 0, _stream(xc))
+        return y
+    track = bn.training and bn.track_running_stats
+    if track:
+        bn.num_batches_tracked.add_(1)
+    return _BnLRelu.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
+                          bn.running_var if track else None, bn.eps, slope,
+                          float(bn.momentum))
 
 
 # ------------------------------------------------------------------ link scoring ---

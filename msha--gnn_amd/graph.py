@@ -18,21 +18,28 @@ import torch
 
 from . import _lib
 
-CSC_CHUNK = 512  # CSC slots per work chunk of the column aggregate
+CSC_CHUNK = 512  # max CSC slots per work chunk of the column aggregate
+
+
+def csc_chunk_for(n_edges: int) -> int:
+    """Slots per CSC chunk: up to CSC_CHUNK, smaller on small graphs so the column
+    aggregate has >= ~8k chunk-waves in flight (R15: 91k edges over 32 columns)."""
+    c = n_edges // 8192
+    return int(min(CSC_CHUNK, max(32, 1 << max(0, c.bit_length() - 1)))) if c > 0 else 32
 
 
 class Graph:
     """CSR + CSC of an (n_rows x n_cols) mask with virtual full rows for empty rows."""
 
     def __init__(self, n_rows, n_cols, rowptr, col, rowflag=None, colptr=None, csc_row=None,
-                 csc_eid=None, chunk=CSC_CHUNK):
+                 csc_eid=None, chunk=None):
         self.n_rows, self.n_cols = int(n_rows), int(n_cols)
         self.rowptr, self.col, self.rowflag = rowptr, col, rowflag
         self.colptr, self.csc_row, self.csc_eid = colptr, csc_row, csc_eid
         self.n_edges = int(col.numel())
         self.device = rowptr.device
         self._plan = None
-        self._chunk = chunk
+        self._chunk = chunk if chunk is not None else csc_chunk_for(self.n_edges)
         self._desc = None
         if colptr is not None:
             self._build_plan(colptr.cpu().numpy().astype(np.int64))

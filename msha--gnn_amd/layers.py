@@ -138,8 +138,8 @@ class OursLayer3(nn.Module):
         """Ablation.py:273-277 on the aggregates: BN + LeakyReLU + u @ v.T + elu.
         (u, v arrive as head slices of the fused (rows, H, F) outputs; BatchNorm1d's
         backward is ~30x slower on the strided view, so they are made contiguous.)"""
-        v_out = self.leakyrelu(self.bn1(v.contiguous()))
-        u_out = self.leakyrelu(self.bn2(u.contiguous()))
+        v_out = MF.bn_lrelu(v.contiguous(), self.bn1, self.alpha)
+        u_out = MF.bn_lrelu(u.contiguous(), self.bn2, self.alpha)
         # u_out @ v_out.T on the library GEMM: its backward's v-side product reduces over
         # all N rows (deterministic split-K instead of a 2-workgroup BLAS tile)
         return F.elu(MF.matmul(u_out, v_out.t()))

@@ -415,3 +415,49 @@ def test_score_pairs_fused_gather(cuda, F):
     tol_close(inner, O.score_pairs(h, src, dst, "inner"), 1e-5, 1e-6)
     mlp = MF.score_pairs(th, ts, td, "mlp", t(W, cuda), t(b, cuda)).cpu().numpy()
     tol_close(mlp, O.score_pairs(h, src, dst, "mlp", [(W, b), (None, None)]), 1e-5, 1e-6)
+
+
+# ------------------------------------------------------- BatchNorm + LeakyReLU
+@pytest.mark.parametrize("R,C,dtype", [(32, 64, "f32"), (39179, 64, "f32"), (1000, 300, "f32"),
+                                       (5000, 64, "bf16")])
+def test_bn_lrelu_matches_torch(cuda, msha, R, C, dtype):
+    """functional.bn_lrelu vs torch BatchNorm1d + LeakyReLU (train step: output, running
+    statistics, num_batches_tracked, grads; then eval)."""
+    import torch.nn as nn
+    import torch.nn.functional as Fn
+    from msha_gnn_amd import functional as MF
+
+    torch.manual_seed(R)
+    x0 = (torch.randn(R, C) * 3 + 1.5).to(cuda)
+    dy = torch.randn(R, C, device=cuda)
+    ref_bn = nn.BatchNorm1d(C).to(cuda).double()
+    with torch.no_grad():
+        ref_bn.weight.uniform_(0.5, 1.5)
+        ref_bn.bias.uniform_(-0.5, 0.5)
+    bn = nn.BatchNorm1d(C).to(cuda)
+    bn.load_state_dict({k: v.float() for k, v in ref_bn.state_dict().items()})
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    if dtype == "bf16":
+        x0 = x0.to(dt).float()
+        dy = dy.to(dt).float()
+    xr = x0.double().requires_grad_(True)
+    yr = Fn.leaky_relu(ref_bn(xr), 0.2)
+    yr.backward(dy.double())
+    x = x0.to(dt).requires_grad_(True)
+    y = MF.bn_lrelu(x, bn, 0.2)
+    assert y.dtype == dt
+    y.backward(dy.to(dt))
+    tol = (1e-2, 1e-2) if dtype == "bf16" else (1e-5, 1e-5)
+    tol_close(y.float().detach().cpu().numpy(), yr.detach().cpu().numpy(), *tol)
+    tol_close(x.grad.float().cpu().numpy(), xr.grad.cpu().numpy(), *((1e-2, 1e-2) if dtype == "bf16" else (1e-4, 1e-5)))
+    tol_close(bn.weight.grad.cpu().numpy(), ref_bn.weight.grad.cpu().numpy(), 1e-4, 1e-5)
+    tol_close(bn.bias.grad.cpu().numpy(), ref_bn.bias.grad.cpu().numpy(), 1e-4, 1e-5)
+    tol_close(bn.running_mean.cpu().numpy(), ref_bn.running_mean.cpu().numpy(), 1e-5, 1e-6)
+    tol_close(bn.running_var.cpu().numpy(), ref_bn.running_var.cpu().numpy(), 1e-5, 1e-6)
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
+    bn.eval()
+    ref_bn.eval()
+    with torch.no_grad():
+        ye = MF.bn_lrelu(x0.to(dt), bn, 0.2)
+        yre = Fn.leaky_relu(ref_bn(x0.double()), 0.2)
+    tol_close(ye.float().cpu().numpy(), yre.cpu().numpy(), *tol)
