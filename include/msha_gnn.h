@@ -67,7 +67,8 @@ typedef struct msha_graph {
   const uint8_t* rowflag; /* n_rows, 1 = virtual full row (nullable: none) */
   const int32_t* colptr;  /* n_cols + 1 (CSC) */
   const int32_t* csc_row; /* n_edges, source row of each CSC slot */
-  const int32_t* csc_eid; /* n_edges, CSR edge id of each CSC slot */
+  const int32_t* csc_eid; /* n_edges, CSR edge id of each CSC slot (NULL: the slot IS the
+                           * edge id -- a CSR presented as a CSC, msha_csc_aggregate only) */
   /* CSC work split: chunk c covers CSC slots [chunk_start[c], chunk_end[c]) of
    * column chunk_col[c]; a column with more than one chunk is listed in
    * multi_col with its first chunk and chunk count (partials summed in order). */
@@ -182,8 +183,11 @@ MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, in
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
  *   out_x[j] = sum_{e in col j} x[e]                   (when x != NULL)
  * Forward v = attd^T @ h2 (Ablation.py:273) and backward d_hc = attd^T @ dU,
- * d_er = colsum(de).  Long columns are split into chunks whose partial sums are
- * added in chunk order: deterministic, no atomics. */
+ * d_er = colsum(de).  With heads = 1 and w = the adjacency values it is the GCN
+ * SpMM adj^T @ support (model.py:37); on a CSR-as-CSC view (colptr = rowptr,
+ * csc_row = col, csc_eid = NULL, chunks over rows) it is adj @ support.
+ * Long columns are split into chunks whose partial sums are added in a fixed order:
+ * deterministic, no atomics. */
 MSHA_API size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);
 MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype,
                                 const float* w, const float* x, const void* table, void* out,

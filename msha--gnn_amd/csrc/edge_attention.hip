@@ -332,7 +332,8 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
       const int32_t slot = cs + e_s;
       const bool valid = slot < s1;
       const int32_t i = valid ? csc_row[slot] : 0;
-      const int64_t eid = valid ? (int64_t)csc_eid[slot] : 0;
+      // csc_eid NULL: slot order is the edge order (the CSR-as-CSC view of a graph)
+      const int64_t eid = valid ? (csc_eid != nullptr ? (int64_t)csc_eid[slot] : slot) : 0;
       const float wv = valid ? w[eid * H + h_s] : 0.f;
       if (HASX && valid) xacc += x[eid * H + h_s];
       const int nvalid = min(G::CE, (int)(s1 - cs));
@@ -445,8 +446,7 @@ static int check_graph(const msha_graph* g, bool need_csc) {
   MSHA_ARG_CHECK(g->n_rows > 0 && g->n_cols > 0 && g->n_edges >= 0, "graph: bad sizes");
   MSHA_ARG_CHECK(g->rowptr && (g->n_edges == 0 || g->col), "graph: CSR arrays missing");
   if (need_csc) {
-    MSHA_ARG_CHECK(g->colptr && (g->n_edges == 0 || (g->csc_row && g->csc_eid)),
-                   "graph: CSC arrays missing");
+    MSHA_ARG_CHECK(g->colptr && (g->n_edges == 0 || g->csc_row), "graph: CSC arrays missing");
     MSHA_ARG_CHECK(g->n_chunks >= g->n_cols && g->chunk_col && g->chunk_start && g->chunk_end,
                    "graph: CSC chunk plan missing (need >= 1 chunk per column)");
     MSHA_ARG_CHECK(g->n_multi == 0 || (g->multi_col && g->multi_first && g->multi_count),

@@ -445,6 +445,45 @@ def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = No
     return _ProjectScores.apply(X, W, al, ar, heads, feat)
 
 
+# ----------------------------------------------------------------- GCN SpMM ---
+class _SpMM(torch.autograd.Function):
+    """out = A^T @ table (transpose) or A @ table, A = the graph with edge values
+    ``vals``: msha_csc_aggregate over the CSC view or the CSR-as-CSC row view."""
+
+    @staticmethod
+    def forward(ctx, table, vals, graph: Graph, transpose: bool):
+        ctx.graph, ctx.transpose = graph, transpose
+        ctx.save_for_backward(vals)
+        return _spmm(graph, vals, table, transpose)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (vals,) = ctx.saved_tensors
+        return _spmm(ctx.graph, vals, dout, not ctx.transpose), None, None, None
+
+
+def _spmm(graph: Graph, vals, table, transpose):
+    view = graph if transpose else graph.row_view()
+    dt = _table_dtype(table)
+    table = _tc(table, dt)
+    D = table.shape[1]
+    if table.shape[0] != view.n_rows:
+        raise ValueError(f"spmm: table has {table.shape[0]} rows, expected {view.n_rows}")
+    out = torch.empty(view.n_cols, D, device=table.device, dtype=dt)
+    _csc_aggregate(view, 1, D, _f32c(vals), None, table, out, None, _stream(table))
+    return out
+
+
+def spmm(graph: Graph, vals: torch.Tensor, table: torch.Tensor, transpose: bool = True):
+    """GCN propagation (model.py:37): ``A^T @ table`` (transpose) or ``A @ table`` with
+    A's values ``vals`` on the graph's CSR edges (Graph.values); deterministic, fp32 or
+    bf16 tables; feature width in {8, 16, 32, 64, 128}."""
+    _lib.require_cuda(table, vals)
+    if not _lib.load().msha_edge_attention_supported(1, table.shape[1]):
+        raise NotImplementedError(f"spmm: width {table.shape[1]} not compiled")
+    return _SpMM.apply(table, vals, graph, transpose)
+
+
 # --------------------------------------------------- BatchNorm + LeakyReLU ---
 class _BnLRelu(torch.autograd.Function):
     """lrelu(batch_norm(x)) with training batch statistics (Ablation.py:273-274)."""

@@ -87,6 +87,28 @@ class Graph:
     def has_csc(self):
         return self.colptr is not None
 
+    def row_view(self) -> "Graph":
+        """The CSR presented as a CSC (colptr = rowptr, csc_row = col, csc_eid = NULL:
+        slot = edge id) with a chunk plan over the rows: msha_csc_aggregate on it
+        computes A @ table instead of A^T @ table (GCN's second layer, the SpMM
+        backward)."""
+        if getattr(self, "_row_view", None) is None:
+            self._row_view = Graph(self.n_cols, self.n_rows, self.colptr, self.csc_row, None,
+                                   self.rowptr, self.col, None)
+        return self._row_view
+
+    def values(self, adj: torch.Tensor) -> torch.Tensor:
+        """fp32 adjacency values on the CSR edges (0 on virtual rows), cached per
+        (tensor, version): the weights of the GCN SpMM."""
+        key = (id(adj), adj._version)
+        if getattr(self, "_vals_key", None) != key:
+            rows = torch.repeat_interleave(torch.arange(self.n_rows, device=self.device),
+                                           self.deg().long())
+            self._vals = adj.detach()[rows, self.col.long()].to(torch.float32).contiguous()
+            self._vals_key = key
+            self._vals_ref = weakref.ref(adj)
+        return self._vals
+
     def deg(self):
         return self.rowptr[1:] - self.rowptr[:-1]
 
@@ -156,6 +178,16 @@ def graph_for(adj: torch.Tensor) -> Graph:
         del _CACHE[k]
     _CACHE[key] = (weakref.ref(adj), g)
     return g
+
+
+def graph_of(adj: torch.Tensor):
+    """(Graph, transposed): a transposed view of a cached adjacency (``adj.t()``, as
+    GCN's second layer passes it, model.py:62) maps to the base tensor's graph."""
+    if (adj.dim() == 2 and adj._base is not None and not adj.is_contiguous()
+            and adj.t().is_contiguous() and adj._base.shape == adj.t().shape
+            and adj._base.data_ptr() == adj.data_ptr()):
+        return graph_for(adj._base), True
+    return graph_for(adj), False
 
 
 def clear_cache():

@@ -11,6 +11,7 @@ and RNG consumption order as the reference, so a model built after
   ablation3             Ablation.py:279-301  (its heads run as ONE multi-head launch)
   LinkPredictor         LLP.py:86-115
   OursLayer, Ours       Ours.py:29-167 (full MSHA: inter + city/province attention)
+  GraphConvolution, GCN model.py:11-64     (SpMM over the same CSR/CSC machinery)
 
 Adjacency arguments may be dense (N, M) tensors (as in train.py; the CSR/CSC view
 is built once on the GPU and cached) or prebuilt ``Graph`` objects.  Every
@@ -23,7 +24,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as MF
-from .graph import Graph, graph_for, groups_for
+import math
+
+from .graph import Graph, graph_for, graph_of, groups_for
 
 ALPHA = 0.2  # LeakyReLU slope of the reference layers (Ablation.py:241, :267)
 
@@ -337,4 +340,63 @@ class Ours(nn.Module):
                                        Coeff12, Coeff3, Coeff4), dim=1)
         x = F.dropout(x, self.dropout, training=self.training)
         x = F.elu(self.out_att(x, g))
+        return F.log_softmax(x, dim=1)
+
+
+class GraphConvolution(nn.Module):
+    """model.py:11-45: ``adj^T @ (input @ W) + b`` with the reference's SCALAR bias
+    (``Parameter(torch.tensor(out_features))``, model.py:23) and its init order
+    (rand weight, then uniform(-1/sqrt(out), 1/sqrt(out)) for weight and bias).
+    ``adj`` may be the dense adjacency (A^T @ support) or its ``.t()`` view
+    (A @ support); both run the HIP SpMM on A's cached CSR/CSC."""
+
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = nn.Parameter(torch.rand([in_features, out_features]))
+        if bias:
+            self.bias = nn.Parameter(torch.tensor(out_features, dtype=torch.float32))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        stdv = 1.0 / math.sqrt(self.weight.size(1))
+        self.weight.data.uniform_(-stdv, stdv)
+        if self.bias is not None:
+            self.bias.data.uniform_(-stdv, stdv)
+
+    def forward(self, input, adj):
+        if isinstance(adj, Graph):
+            raise TypeError("GraphConvolution needs the dense adjacency (its values weight "
+                            "the propagation)")
+        g, transposed = graph_of(adj)
+        base = adj._base if transposed else adj
+        support = MF.project_scores(input, self.weight)  # model.py:36 on the MFMA GEMM
+        # model.py:37: adj.transpose(0, 1) @ support
+        output = MF.spmm(g, g.values(base), support, transpose=not transposed)
+        return output + self.bias if self.bias is not None else output
+
+    def __repr__(self):
+        return f"{self.__class__.__name__} ({self.in_features} -> {self.out_features})"
+
+
+class GCN(nn.Module):
+    """model.py:48-64: features (N, nfeat + 1) with the GDP column, gc1 on adj, gc2 on
+    adj.t(), log_softmax over nhid (gc3 is built and never used, as in the reference)."""
+
+    def __init__(self, nfeat, nhid, nclass, dropout, gdp, N):
+        super().__init__()
+        gdp_values = torch.tensor(list(gdp.values())).view(-1, 1)
+        self.features = nn.Parameter(torch.cat((torch.rand([N, nfeat])[:, :], gdp_values), dim=1))
+        self.gc1 = GraphConvolution(nfeat + 1, nhid)
+        self.gc2 = GraphConvolution(nhid, nhid)
+        self.gc3 = GraphConvolution(nhid, nclass)
+        self.dropout = dropout
+
+    def forward(self, adj):
+        x = F.relu(self.gc1(self.features, adj))
+        x = F.dropout(x, self.dropout, training=self.training)
+        x = F.relu(self.gc2(x, adj.t()))
         return F.log_softmax(x, dim=1)

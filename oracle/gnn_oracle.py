@@ -425,3 +425,28 @@ def ours_layer_fwd(S, R, p, rowptr, col, city, prov, src, training, rowflag=None
                            p["bn2_running_var"])
     out = elu(lrelu(u, slope) @ lrelu(v, slope).T)
     return dict(out=out, u_pre=u_pre, v_pre=v_pre, intra=it)
+
+
+# ------------------------------------------------------------------------- GCN ---
+def spmm_t(rowptr, col, vals, table, n_cols):
+    """``A^T @ table`` over the CSR edges with values ``vals`` (model.py:37)."""
+    rows = edge_rows(rowptr)
+    out = np.zeros((n_cols, table.shape[1]), table.dtype)
+    np.add.at(out, col, vals[:, None] * table[rows])
+    return out
+
+
+def spmm(rowptr, col, vals, table):
+    """``A @ table`` over the CSR edges (model.py:37 with adj.t(), model.py:62)."""
+    rows = edge_rows(rowptr)
+    out = np.zeros((len(rowptr) - 1, table.shape[1]), table.dtype)
+    np.add.at(out, rows, vals[:, None] * table[col])
+    return out
+
+
+def gcn_fwd(features, W1, b1, W2, b2, rowptr, col, vals, n_cols):
+    """model.py:57-64 (dropout 0): relu(A^T (X W1) + b1) -> relu(A (x W2) + b2) ->
+    log_softmax; b1 / b2 are the reference's scalar biases (model.py:23)."""
+    x = np.maximum(spmm_t(rowptr, col, vals, features @ W1, n_cols) + b1, 0)
+    x = np.maximum(spmm(rowptr, col, vals, x @ W2) + b2, 0)
+    return log_softmax(x, axis=1)

@@ -25,6 +25,11 @@ Fixtures
                   degree 65 and 80 (> one wavefront), one hot column; normalize
                   with a zero column (NaN spread) and on random counts.
   ours_small.npz  Ours.OursLayer (full MSHA with city / province attention).
+  gcn_sub512.npz  model.GCN (nfeat 64, nhid 128; adj^T @ (X W) + scalar bias) on the
+                  512-source subgraph: init, train output, nll loss, grads.
+  years.npz       per-year node counts, group ids and GDP (2015-2018).
+
+``python tests/golden/make_golden.py gcn`` regenerates only gcn_sub512.npz.
 """
 from __future__ import annotations
 
@@ -438,6 +443,32 @@ def make_ours_small(g):
     np.savez_compressed(os.path.join(OUT, "ours_small.npz"), **res)
 
 
+def make_gcn():
+    """model.GCN (model.py:11-64) on the sub512 graph: GraphConvolution is
+    adj^T @ (X @ W) + b with a SCALAR bias (model.py:23), the second layer runs on
+    adj.t() (so adj @ support), log_softmax over nhid (gc3 is built, never used)."""
+    z = np.load(os.path.join(OUT, "sub512.npz"))
+    counts = torch.as_tensor(z["counts"])
+    n, m = counts.shape
+    gdp = {i: float(x) for i, x in enumerate(z["gdp"])}
+    adj = refmodel.normalize_adjacency_matrix(counts)
+    torch.manual_seed(4)
+    model = refmodel.GCN(nfeat=64, nhid=128, nclass=m, dropout=0.0, gdp=gdp, N=n)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    si = torch.as_tensor(z["source_index"]).long()
+    ri = torch.as_tensor(z["recipient_index"]).long()
+    model.train()
+    out = model(adj)
+    loss = F.nll_loss(out[si], ri)
+    loss.backward()
+    res = dict(out=np32(out), loss=np32(loss))
+    flatten_sd("init.", sd, res)
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            res[f"grad.{k}"] = np32(p.grad)
+    np.savez_compressed(os.path.join(OUT, "gcn_sub512.npz"), **res)
+
+
 def make_years():
     """Per-year node tables of the shipped 2015-2018 graphs (Adjacent{Y}.json,
     GDP{Y}.json): N, city / province group ids, GDP.  Flows of 2016-2018 are not
@@ -460,6 +491,9 @@ def make_years():
 
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["gcn"]:
+        make_gcn()
+        return
     g = load_2015()
     mask = make_r15(g)
     counts, gdp_sub, flows_sub = make_sub512(g, mask)
@@ -467,6 +501,7 @@ def main():
     make_link()
     make_edge_cases()
     make_ours_small(g)
+    make_gcn()
     make_years()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):

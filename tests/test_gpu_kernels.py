@@ -461,3 +461,39 @@ def test_bn_lrelu_matches_torch(cuda, msha, R, C, dtype):
         ye = MF.bn_lrelu(x0.to(dt), bn, 0.2)
         yre = Fn.leaky_relu(ref_bn(x0.double()), 0.2)
     tol_close(ye.float().cpu().numpy(), yre.cpu().numpy(), *tol)
+
+
+@pytest.mark.parametrize("n,m,D,dt", [(500, 32, 128, "f32"), (3000, 700, 64, "f32"),
+                                      (800, 40, 32, "bf16")])
+def test_spmm_both_directions(cuda, msha, n, m, D, dt):
+    """functional.spmm A^T @ X and A @ Y (and their autograd) vs the oracle SpMM."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(n + D)
+    c = random_counts(rng, n, m, 60, empty_rows=(1,), hot_col=0)
+    adj = (c / np.maximum(c.sum(0, keepdims=True), 1)).astype(np.float32)
+    graph = Graph.from_dense(t(adj, cuda))
+    vals = graph.values(t(adj, cuda))
+    rowptr, col, _ = virtual_csr(c)
+    v_np = adj[O.edge_rows(rowptr), col].astype(np.float64)
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    X = rng.standard_normal((n, D)).astype(np.float32)
+    Y = rng.standard_normal((m, D)).astype(np.float32)
+    if dt == "bf16":
+        X = torch.as_tensor(X).to(tdt).float().numpy()
+        Y = torch.as_tensor(Y).to(tdt).float().numpy()
+    tX = t(X, cuda, tdt).requires_grad_(True)
+    tY = t(Y, cuda, tdt).requires_grad_(True)
+    a = MF.spmm(graph, vals, tX, transpose=True)
+    b = MF.spmm(graph, vals, tY, transpose=False)
+    tol = (1e-2, 1e-2) if dt == "bf16" else (1e-5, 1e-5)
+    ra = O.spmm_t(rowptr, col, v_np, X.astype(np.float64), m)
+    rb_ = O.spmm(rowptr, col, v_np, Y.astype(np.float64))
+    tol_close(a.float().detach().cpu().numpy(), ra, *tol)
+    tol_close(b.float().detach().cpu().numpy(), rb_, *tol)
+    ga = rng.standard_normal((m, D)).astype(np.float32)
+    gb = rng.standard_normal((n, D)).astype(np.float32)
+    (a.float() * t(ga, cuda)).sum().add_((b.float() * t(gb, cuda)).sum()).backward()
+    tol_close(tX.grad.float().cpu().numpy(), O.spmm(rowptr, col, v_np, ga.astype(np.float64)), *tol)
+    tol_close(tY.grad.float().cpu().numpy(), O.spmm_t(rowptr, col, v_np, gb.astype(np.float64), m), *tol)

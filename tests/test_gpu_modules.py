@@ -170,3 +170,30 @@ def test_ablation3_full_r15_forward_vs_oracle(cuda, msha):
     ref = O.ablation3_fwd(sd["Sfeatures"], sd["Rfeatures"], heads, sd["out_att.W"],
                           g["rowptr"], g["col"].astype(np.int32), training=False)
     tol_close(out, ref, 1e-4, 2e-5)
+
+
+def test_gcn_matches_reference(cuda, msha):
+    """layers.GCN train step vs model.GCN's own outputs / loss / grads (SpMM on the
+    CSC view for gc1, on the CSR-as-CSC row view for gc2's adj.t())."""
+    from msha_gnn_amd import layers
+
+    z = golden("gcn_sub512.npz")
+    s = golden("sub512.npz")
+    gdp = {i: float(x) for i, x in enumerate(s["gdp"])}
+    torch.manual_seed(4)
+    model = layers.GCN(nfeat=64, nhid=128, nclass=32, dropout=0.0, gdp=gdp, N=512).to(cuda)
+    adj = torch.as_tensor(s["adj_norm"], device=cuda)
+    si = torch.as_tensor(s["source_index"], device=cuda).long()
+    ri = torch.as_tensor(s["recipient_index"], device=cuda).long()
+    model.train()
+    out = model(adj)
+    tol_close(out.detach().cpu().numpy(), z["out"], 1e-4, 1e-5)
+    loss = F.nll_loss(out[si], ri)
+    assert abs(loss.item() - float(z["loss"])) < 1e-4 * abs(float(z["loss"]))
+    loss.backward()
+    for k, p in model.named_parameters():
+        key = f"grad.{k}"
+        if key in z.files:
+            tol_close(p.grad.cpu().numpy(), z[key], 1e-3, 1e-4)
+        else:
+            assert p.grad is None, k

@@ -131,3 +131,20 @@ def test_ops_refuse_cpu_tensors(msha):
     gal = layers.GraphAttentionLayer(4, 3, 0.0)
     with pytest.raises(RuntimeError, match="GPU only"):
         gal(torch.rand(5, 4), torch.ones(5, 3))
+
+
+def test_gcn_init_bit_identical(msha):
+    """layers.GCN (model.py:48-55) after the fixture's seed: same keys, shapes, values
+    (scalar biases included)."""
+    from conftest import golden
+    from msha_gnn_amd import layers
+
+    z = golden("gcn_sub512.npz")
+    s = golden("sub512.npz")
+    gdp = {i: float(x) for i, x in enumerate(s["gdp"])}
+    torch.manual_seed(4)
+    model = layers.GCN(nfeat=64, nhid=128, nclass=32, dropout=0.0, gdp=gdp, N=512)
+    sd = model.state_dict()
+    assert sorted(sd) == sorted(k[len("init."):] for k in z.files if k.startswith("init."))
+    for k, v in sd.items():
+        assert np.array_equal(v.numpy(), z["init." + k]), k

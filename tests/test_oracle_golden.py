@@ -216,3 +216,18 @@ def test_ours_layer_forward(tag, tol):
                              rowflag=empty)
         ref = z[tag + key]
         np.testing.assert_allclose(r["out"], ref, rtol=tol, atol=tol * np.abs(ref).max())
+
+
+def test_gcn_oracle_matches_reference():
+    """model.GCN (model.py:48-64) on the sub512 graph: oracle SpMM restatement vs the
+    reference's own dense forward (fixture from make_golden.py)."""
+    z = golden("gcn_sub512.npz")
+    s = golden("sub512.npz")
+    adj = s["adj_norm"].astype(np.float64)
+    rowptr, col = O.dense_to_csr((s["counts"] > 0).astype(np.float32))
+    rows = O.edge_rows(rowptr)
+    vals = adj[rows, col]
+    out = O.gcn_fwd(z["init.features"].astype(np.float64), z["init.gc1.weight"].astype(np.float64),
+                    float(z["init.gc1.bias"]), z["init.gc2.weight"].astype(np.float64),
+                    float(z["init.gc2.bias"]), rowptr, col, vals, adj.shape[1])
+    np.testing.assert_allclose(out, z["out"], rtol=1e-4, atol=1e-5)
