@@ -114,6 +114,8 @@ class Layer:
         self.n, self.m, self.H, self.F = n, m, H, F
         # dtype = storage of the feature table, W and the node tables (bf16: config C3)
         self.X = torch.rand(n, fin, generator=g).to(dev, dtype)
+        # bipartite graphs (R15: sources x recipients) take a recipient feature table
+        self.Xr = torch.rand(m, fin, generator=g).to(dev, dtype) if m != n else None
         self.W = (torch.randn(fin, H * F, generator=g) * fin ** -0.5).to(dev, dtype) \
             .requires_grad_(True)
         self.al = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
@@ -124,8 +126,14 @@ class Layer:
         for p in (self.W, self.al, self.ar):
             p.grad = None
         # h = X @ W with the per-head score halves fused into the MFMA epilogue
-        h, el, er = self.MF.project_scores(self.X, self.W, self.al, self.ar, heads=self.H)
-        u = self.MF.edge_attention(self.graph, el, er, h.view(self.n, self.H, self.F))
+        if self.Xr is None:
+            h, el, er = self.MF.project_scores(self.X, self.W, self.al, self.ar, heads=self.H)
+            hc = h.view(self.n, self.H, self.F)
+        else:  # OursLayer3 shape (Ablation.py:262-274): h1 = R W (recipients), h2 = S W
+            h1, er = self.MF.project_scores(self.Xr, self.W, ar=self.ar, heads=self.H)
+            _, el = self.MF.project_scores(self.X, self.W, al=self.al, heads=self.H)
+            hc = h1.view(self.m, self.H, self.F)
+        u = self.MF.edge_attention(self.graph, el, er, hc)
         u.backward(self.dU)
 
 
