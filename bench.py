@@ -138,7 +138,7 @@ class Layer:
 
 
 def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup=3,
-                     hidden=128, n_pairs=4_000_000):
+                     hidden=128, n_pairs=4_000_000, dtype=torch.float32):
     """score P = 4M pairs (2M graph edges + 2M uniform negatives,
     seed 1) against h (n x F) with LinkPredictor 'mlp' (hidden 128) and 'inner'.
     Rank r owns rows [r R, (r+1) R) of h (sharding.ShardedTable); one RCCL
@@ -154,11 +154,11 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
     dst = np.concatenate([col[pick], torch.randint(0, n, (n_pairs // 2,), generator=g).numpy()])
     t_src = torch.as_tensor(src, device=dev)
     t_dst = torch.as_tensor(dst, device=dev)
-    table = sharding.ShardedTable(n, F, world, rank, dev)
+    table = sharding.ShardedTable(n, F, world, rank, dev, dtype=dtype)
     lo, hi = sharding.row_range(n, world, rank)
     table.set_local(torch.rand(hi - lo, F, generator=torch.Generator().manual_seed(10 + rank))
-                    .to(dev))
-    W = (torch.randn(hidden, F, generator=g) * F ** -0.5).to(dev)
+                    .to(dev, dtype))
+    W = (torch.randn(hidden, F, generator=g) * F ** -0.5).to(dev, dtype)
     b = torch.randn(hidden, generator=g).to(dev)
     plo, phi = sharding.pair_range(n_pairs, world, rank)
     out_mlp = torch.empty(phi - plo, hidden, device=dev)
@@ -195,7 +195,8 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
         table.gather()
     torch.cuda.synchronize(dev)
     res["allgather_ms"] = (time.perf_counter() - t0) / steps * 1e3
-    res.update(pairs_per_batch=n_pairs, feat=F, hidden=hidden, world=world, dtype="f32",
+    res.update(pairs_per_batch=n_pairs, feat=F, hidden=hidden, world=world,
+               dtype="bf16" if dtype == torch.bfloat16 else "f32",
                sharding="h rows all-gathered over RCCL (all_gather_into_tensor), pairs split "
                "contiguously per rank" if dist else "single GPU (no collective)")
     return res
@@ -432,6 +433,9 @@ def main():
     link = None
     if not args.no_link_score and args.workload != "r15":
         link = link_score_bench(dev, rowptr, col, n, H * F, world, rank, dist)
+        if not args.no_bf16:  # C5 names a bf16 table
+            link["bf16"] = link_score_bench(dev, rowptr, col, n, H * F, world, rank, dist,
+                                            dtype=torch.bfloat16)
     if rank != 0:
         if dist:
             tdist.destroy_process_group()

@@ -277,6 +277,18 @@ MSHA_API int msha_head_colsum(int64_t rows, int32_t heads, int32_t feat, int32_t
                               const float* s1, const float* s2, const void* T, float* out1,
                               float* out2, void* ws, size_t ws_bytes, msha_stream_t stream);
 
+/* bf16 link scoring (config C5 names a bf16 embedding table): msha_pair_inner_fwd and
+ * msha_pair_linear on bf16 tables G / G2 (and a bf16 nn.Linear weight W); fp32
+ * products and accumulation, fp32 scores out.  feat / K, N multiples of 8. */
+MSHA_API int msha_pair_inner_fwd_bf16(int64_t n_pairs, int32_t feat, const void* G, int64_t ldg,
+                                      const int64_t* gi, const void* G2, int64_t ldg2,
+                                      const int64_t* gj, float* out, msha_stream_t stream);
+MSHA_API int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, const void* G,
+                                   int64_t ldg, const int64_t* gi, const void* G2, int64_t ldg2,
+                                   const int64_t* gj, const void* W, const float* bias,
+                                   int32_t act, float drop_p, uint64_t seed, uint64_t offset,
+                                   float* out, msha_stream_t stream);
+
 /* ------------------------------------------------- BatchNorm + LeakyReLU --- */
 /* Ablation.py:273-274 / Ours.py:100-101 epilogue: y = lrelu(bn(x)) on (rows, channels)
  * tables (dtype fp32 / bf16; weight, bias, statistics fp32; weight / bias nullable =

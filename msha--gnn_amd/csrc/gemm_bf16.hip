@@ -34,7 +34,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-enum : int { EPI_STORE = 0, EPI_SCORE = 2 };
+enum : int { EPI_STORE = 0, EPI_ACT = 1, EPI_SCORE = 2 };
+enum : int { ACT_BIAS = 1, ACT_RELU = 2, ACT_DROPOUT = 4, ACT_SIGMOID = 8 };
 enum : int { HO_NONE = 0, HO_A = 1, HO_B = 2 };
 
 struct Args {
@@ -58,11 +59,23 @@ struct Args {
   const float* de2;
   const float* ha2;
   int hH, hF;
+  // A as a gather(-hadamard) of table rows: A[m, k] = G[gi[m], k] * G2[gj[m], k]
+  // (the fused pair gather of the link scorer, LLP.py:233; G = A, ldg = sAm)
+  const int64_t* gi;
+  const int64_t* gj;
+  const bf16_t* G2;  // NULL: G
+  int64_t ldg2;
+  bool hadamard;
+  // EPI_ACT (nn.Linear of the link predictor): bias, relu, dropout, sigmoid
+  int act;
+  const float* bias;
+  Dropout dp;
 };
 
 // One operand's staged 16-byte chunks (4 per thread) + head-outer terms.
 struct Stage {
   uint4 x[4];
+  uint4 y[4];  // second gathered row of the hadamard A loader
   uint32_t ok;
   float d1[4], d2[4];
   float4 h1[2], h2[2];  // ha / ha2 of the thread's 8 columns (same for all 4 chunks)
@@ -70,7 +83,7 @@ struct Stage {
 
 // KF: the operand's k is contiguous in memory (else its row is).
 // rows: M (A) or N (B); srow / sk: element strides; RO: HO on this operand.
-template <int KF, bool RO>
+template <int KF, bool RO, bool GA = false>
 __device__ __forceinline__ void load_operand(const Args& p, const bf16_t* X, int64_t srow,
                                              int64_t sk, int64_t nrows, int64_t r0, int64_t k0,
                                              int64_t ke, int tid, Stage& st) {
@@ -87,8 +100,18 @@ __device__ __forceinline__ void load_operand(const Args& p, const bf16_t* X, int
       row = r0 + 8 * (c & 15);
     }
     const bool v = row < nrows && k < ke;
-    const int64_t off = v ? (KF ? row * srow + k : k * sk + row) : 0;
-    st.x[it] = *reinterpret_cast<const uint4*>(X + off);
+    if (GA) {  // KF: rows of the table picked by gi / gj
+      const int64_t rr = v ? row : 0, kk = v ? k : 0;
+      const int64_t i = p.gi ? p.gi[rr] : rr;
+      st.x[it] = *reinterpret_cast<const uint4*>(X + i * srow + kk);
+      if (p.hadamard) {
+        const int64_t j = p.gj ? p.gj[rr] : rr;
+        st.y[it] = *reinterpret_cast<const uint4*>((p.G2 ? p.G2 : X) + j * p.ldg2 + kk);
+      }
+    } else {
+      const int64_t off = v ? (KF ? row * srow + k : k * sk + row) : 0;
+      st.x[it] = *reinterpret_cast<const uint4*>(X + off);
+    }
     ok |= (v ? 1u : 0u) << it;
     if (RO) {
       // head-outer: KF (A = dH [m][d]): r = row, cols = k..k+7; row-fast (B = dH [k][n]):
@@ -126,12 +149,25 @@ __device__ __forceinline__ uint4 head_outer8(uint4 x, float d1, float d2, const 
   return o;
 }
 
-template <int KF, bool RO>
-__device__ __forceinline__ void store_operand(const Stage& st, bf16_t* img, int tid) {
+__device__ __forceinline__ uint4 hadamard8(uint4 x, uint4 y) {
+  const Pk<bf16_t> a = pk_load(reinterpret_cast<const bf16_t*>(&x));
+  const Pk<bf16_t> b = pk_load(reinterpret_cast<const bf16_t*>(&y));
+  Pk<bf16_t> r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = a.v[i] * b.v[i];
+  uint4 o;
+  pk_store(reinterpret_cast<bf16_t*>(&o), r);
+  return o;
+}
+
+template <int KF, bool RO, bool GH = false>
+__device__ __forceinline__ void store_operand(const Stage& st, bf16_t* img, int tid,
+                                              bool hadamard = false) {
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int c = tid + 256 * it;
     uint4 x = st.x[it];
+    if (GH && hadamard) x = hadamard8(x, st.y[it]);
     if (RO) x = head_outer8(x, st.d1[it], st.d2[it], st.h1, st.h2);
     if (!((st.ok >> it) & 1u)) x = make_uint4(0u, 0u, 0u, 0u);
     const int off = KF ? (c >> 3) * PKF + 8 * (c & 7) : (c >> 4) * PRF + 8 * (c & 15);
@@ -158,7 +194,7 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16_t* img, int rt, int s, in
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int EPI, int FEPI, int AK, int BK_, int HO>
+template <int EPI, int FEPI, int AK, int BK_, int HO, bool GA = false>
 __global__ void __launch_bounds__(256) gemm_bf16_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * IMG];
   bf16_t* As = smem;
@@ -181,16 +217,16 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(Args p) {
   // A: rows m (sAm), k (sAk); B: rows n (sBn), k (sBk)
   Stage sa, sb;
   if (kb < ke) {
-    load_operand<AK, HO == HO_A>(p, p.A, p.sAm, p.sAk, p.M, m0, kb, ke, tid, sa);
+    load_operand<AK, HO == HO_A, GA>(p, p.A, p.sAm, p.sAk, p.M, m0, kb, ke, tid, sa);
     load_operand<BK_, HO == HO_B>(p, p.B, p.sBn, p.sBk, p.N, n0, kb, ke, tid, sb);
   }
   for (int64_t k0 = kb; k0 < ke; k0 += BK) {
     __syncthreads();
-    store_operand<AK, HO == HO_A>(sa, As, tid);
+    store_operand<AK, HO == HO_A, GA>(sa, As, tid, p.hadamard);
     store_operand<BK_, HO == HO_B>(sb, Bs, tid);
     __syncthreads();
     if (k0 + BK < ke) {
-      load_operand<AK, HO == HO_A>(p, p.A, p.sAm, p.sAk, p.M, m0, k0 + BK, ke, tid, sa);
+      load_operand<AK, HO == HO_A, GA>(p, p.A, p.sAm, p.sAk, p.M, m0, k0 + BK, ke, tid, sa);
       load_operand<BK_, HO == HO_B>(p, p.B, p.sBn, p.sBk, p.N, n0, k0 + BK, ke, tid, sb);
     }
 #pragma unroll
@@ -235,6 +271,31 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(Args p) {
     float4 v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(T + rl * TP + seg * 32 + 4 * q);
+    if (EPI == EPI_ACT) {
+      uint32_t kbits = 0xffffffffu;
+      if (p.act & ACT_DROPOUT) {  // keep bits of the lane's 32 outputs (rolled loop)
+        kbits = 0u;
+        const uint64_t off = dropout_offset(p.dp, p.dp.offset);
+#pragma unroll 1
+        for (int u = 0; u < 32; ++u)
+          if (philox_x(p.dp.seed, off, (uint64_t)(row * p.N + cbase + u)) >= p.dp.threshold)
+            kbits |= 1u << u;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t col = cbase + 4 * q + u;
+          float x = e[u] + ((p.act & ACT_BIAS) && col < p.N ? p.bias[col] : 0.f);
+          if (p.act & ACT_RELU) x = fmaxf(x, 0.f);
+          if (p.act & ACT_DROPOUT) x *= ((kbits >> (4 * q + u)) & 1u) ? p.dp.scale : 0.f;
+          if (p.act & ACT_SIGMOID) x = 1.f / (1.f + __expf(-x));
+          e[u] = x;
+        }
+        v[q] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
     if (row < p.M) {
       if (to_slab) {
         float* o = p.slab + (int64_t)blockIdx.z * p.M * p.N + row * p.N;
@@ -461,4 +522,32 @@ extern "C" int msha_project_scores_bf16(int64_t M, int64_t K, int32_t heads, int
                                         "when score vectors are given");
   }
   return check_launch("project_scores_bf16");
+}
+
+extern "C" int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, const void* G,
+                                     int64_t ldg, const int64_t* gi, const void* G2,
+                                     int64_t ldg2, const int64_t* gj, const void* W,
+                                     const float* bias, int32_t act, float drop_p, uint64_t seed,
+                                     uint64_t offset, float* out, msha_stream_t stream) {
+  MSHA_ARG_CHECK(n_pairs > 0 && K > 0 && N > 0, "pair_linear_bf16: bad sizes");
+  MSHA_ARG_CHECK(G && W && out, "pair_linear_bf16: null pointer");
+  MSHA_ARG_CHECK(!(act & ACT_BIAS) || bias, "pair_linear_bf16: bias missing");
+  MSHA_ARG_CHECK(K % 8 == 0 && N % 8 == 0 && ldg % 8 == 0 && (G2 == nullptr || ldg2 % 8 == 0) &&
+                     al16(G) && (G2 == nullptr || al16(G2)) && al16(W) && al16(out),
+                 "pair_linear_bf16: K, N, ld multiples of 8 and 16-byte aligned tables");
+  Args p;
+  memset(&p, 0, sizeof(p));
+  p.M = n_pairs; p.N = N; p.K = K;
+  p.A = (const bf16_t*)G; p.sAm = ldg; p.sAk = 1;
+  p.gi = gi; p.gj = gj; p.G2 = (const bf16_t*)G2; p.ldg2 = G2 ? ldg2 : ldg;
+  p.hadamard = G2 != nullptr || gj != nullptr;
+  p.B = (const bf16_t*)W; p.sBk = 1; p.sBn = K;  // nn.Linear weight (N x K)
+  p.C = out; p.ldc = N; p.c_bf16 = 0;
+  p.act = act; p.bias = bias;
+  p.dp = make_dropout(drop_p, seed, offset);
+  if (!p.dp.active) p.act &= ~ACT_DROPOUT;
+  const dim3 grid((unsigned)((n_pairs + BM - 1) / BM), (unsigned)((N + BN - 1) / BN), 1);
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI_ACT, 0, 1, 1, HO_NONE, true>), grid, dim3(256), 0,
+                     (hipStream_t)stream, p);
+  return check_launch("pair_linear_bf16");
 }

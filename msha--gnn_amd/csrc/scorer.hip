@@ -14,12 +14,14 @@ namespace msha {
 
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
 
+template <typename T>
 __global__ void __launch_bounds__(256) pair_inner_kernel(
-    int64_t n_pairs, int F, const float* __restrict__ G, int64_t ldg,
-    const int64_t* __restrict__ gi, const float* __restrict__ G2, int64_t ldg2,
+    int64_t n_pairs, int F, const T* __restrict__ G, int64_t ldg,
+    const int64_t* __restrict__ gi, const T* __restrict__ G2, int64_t ldg2,
     const int64_t* __restrict__ gj, float* __restrict__ out) {
+  constexpr int V = Pk<T>::V;          // elements per 16-byte lane chunk
   const int lane = lane_id();
-  const int QP = F >> 2;               // lanes per pair
+  const int QP = F / V;                // lanes per pair
   const int PPW = 64 / QP;             // pairs per wave-instruction
   const int slot = lane / QP, q = lane % QP;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -34,9 +36,7 @@ __global__ void __launch_bounds__(256) pair_inner_kernel(
       if (b < n_pairs && slot < PPW) {
         const int64_t i = gi ? gi[b] : b;
         const int64_t j = gj ? gj[b] : b;
-        const float4 x = *reinterpret_cast<const float4*>(G + i * ldg + 4 * q);
-        const float4 y = *reinterpret_cast<const float4*>(G2 + j * ldg2 + 4 * q);
-        acc[u] = f4_dot(x, y);
+        acc[u] = pk_dot(pk_load(G + i * ldg + V * q), pk_load(G2 + j * ldg2 + V * q));
       }
     }
 #pragma unroll
@@ -122,10 +122,29 @@ extern "C" int msha_pair_inner_fwd(int64_t n_pairs, int32_t feat, const float* G
                  "pair_inner_fwd: tables must be 16-byte aligned with ld % 4 == 0");
   if (n_pairs == 0) return MSHA_OK;
   const int ppw = 64 / (feat / 4) * 4;
-  hipLaunchKernelGGL(pair_inner_kernel, dim3(grid_for((n_pairs + ppw - 1) / ppw, 4, 1 << 20)),
-                     dim3(256), 0, (hipStream_t)stream, n_pairs, (int)feat, G, ldg, gi, G2, ldg2,
-                     gj, out);
+  hipLaunchKernelGGL(pair_inner_kernel<float>,
+                     dim3(grid_for((n_pairs + ppw - 1) / ppw, 4, 1 << 20)), dim3(256), 0,
+                     (hipStream_t)stream, n_pairs, (int)feat, G, ldg, gi, G2, ldg2, gj, out);
   return check_launch("pair_inner_fwd");
+}
+
+extern "C" int msha_pair_inner_fwd_bf16(int64_t n_pairs, int32_t feat, const void* G,
+                                        int64_t ldg, const int64_t* gi, const void* G2,
+                                        int64_t ldg2, const int64_t* gj, float* out,
+                                        msha_stream_t stream) {
+  MSHA_ARG_CHECK(n_pairs >= 0 && feat >= 8 && feat <= 512 && (feat & (feat - 1)) == 0,
+                 "pair_inner_fwd_bf16: feat must be a power of two in [8, 512]");
+  MSHA_ARG_CHECK(G && G2 && out, "pair_inner_fwd_bf16: null pointer");
+  MSHA_ARG_CHECK(ldg % 8 == 0 && ldg2 % 8 == 0 && ((uintptr_t)G % 16) == 0 &&
+                     ((uintptr_t)G2 % 16) == 0,
+                 "pair_inner_fwd_bf16: tables must be 16-byte aligned with ld % 8 == 0");
+  if (n_pairs == 0) return MSHA_OK;
+  const int ppw = 64 / (feat / 8) * 4;
+  hipLaunchKernelGGL(pair_inner_kernel<bf16_t>,
+                     dim3(grid_for((n_pairs + ppw - 1) / ppw, 4, 1 << 20)), dim3(256), 0,
+                     (hipStream_t)stream, n_pairs, (int)feat, (const bf16_t*)G, ldg, gi,
+                     (const bf16_t*)G2, ldg2, gj, out);
+  return check_launch("pair_inner_fwd_bf16");
 }
 
 extern "C" int msha_pair_inner_bwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,

@@ -653,24 +653,29 @@ def pair_layer(x_i, x_j, W, b, p=0.0, training=False, sigmoid=False, seed=None):
 def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None):
     """Fused caller gather + predictor (LLP.py:233 + LLP.py:104-115), inference:
     ``predictor(h[src], h[dst])`` without materialising the gathered rows.
-    'inner' -> (P,), 'mlp' (one used Linear W (hidden, F), b) -> (P, hidden)."""
+    'inner' -> (P,), 'mlp' (one used Linear W (hidden, F), b) -> (P, hidden).
+    A bf16 ``h`` runs the bf16 kernels (bf16 MFMA for 'mlp'; fp32 scores)."""
     _lib.require_cuda(h, src, dst)
-    h = _f32c(h)
+    dt = _table_dtype(h)
+    h = _tc(h, dt)
+    bf = dt == BF16
     src = src.to(torch.int64).contiguous()
     dst = dst.to(torch.int64).contiguous()
     P, Fd = src.numel(), h.shape[1]
     s = _stream(h)
     if mode == "inner":
         out = torch.empty(P, device=h.device, dtype=torch.float32) if out is None else out
-        _lib.call("msha_pair_inner_fwd", P, Fd, h.data_ptr(), h.stride(0), src.data_ptr(),
-                  h.data_ptr(), h.stride(0), dst.data_ptr(), out.data_ptr(), s)
+        _lib.call("msha_pair_inner_fwd_bf16" if bf else "msha_pair_inner_fwd", P, Fd,
+                  h.data_ptr(), h.stride(0), src.data_ptr(), h.data_ptr(), h.stride(0),
+                  dst.data_ptr(), out.data_ptr(), s)
         return out
-    W, b = _f32c(W), _f32c(b)
+    W, b = _tc(W, dt), _f32c(b)
     N = W.shape[0]
     out = torch.empty(P, N, device=h.device, dtype=torch.float32) if out is None else out
-    _lib.call("msha_pair_linear", P, Fd, N, h.data_ptr(), h.stride(0), src.data_ptr(),
-              h.data_ptr(), h.stride(0), dst.data_ptr(), W.data_ptr(), b.data_ptr(),
-              ACT_BIAS | ACT_RELU | ACT_SIGMOID, 0.0, 0, 0, out.data_ptr(), s)
+    _lib.call("msha_pair_linear_bf16" if bf else "msha_pair_linear", P, Fd, N, h.data_ptr(),
+              h.stride(0), src.data_ptr(), h.data_ptr(), h.stride(0), dst.data_ptr(),
+              W.data_ptr(), b.data_ptr(), ACT_BIAS | ACT_RELU | ACT_SIGMOID, 0.0, 0, 0,
+              out.data_ptr(), s)
     return out
 
 

@@ -222,3 +222,28 @@ def test_ablation3_bf16_model(cuda, msha):
         assert np.isfinite(g16).all(), k
         cos = float((g16 * g32).sum() / (np.linalg.norm(g16) * np.linalg.norm(g32) + 1e-30))
         assert cos > 0.99, (k, cos)
+
+
+@pytest.mark.parametrize("mode", ["inner", "mlp"])
+def test_score_pairs_bf16(cuda, mode):
+    """Fused gather + LinkPredictor (LLP.py:104-115, :233) on a bf16 table (config C5)
+    vs fp64 on the same bf16-rounded table/weights: sigmoid outputs within 1e-2."""
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(9)
+    n, F, P, hidden = 3000, 128, 20000, 128
+    h = rb(rng.standard_normal((n, F)) * 0.2)
+    src, dst = rng.integers(0, n, P), rng.integers(0, n, P)
+    th = t(h, cuda, BF)
+    ts, td = torch.as_tensor(src, device=cuda), torch.as_tensor(dst, device=cuda)
+    hd = h.astype(np.float64)
+    if mode == "inner":
+        got = MF.score_pairs(th, ts, td, "inner").cpu().numpy()
+        ref = 1 / (1 + np.exp(-(hd[src] * hd[dst]).sum(1)))
+    else:
+        W = rb(rng.standard_normal((hidden, F)) / np.sqrt(F))
+        b = rng.standard_normal(hidden).astype(np.float32) * 0.1
+        got = MF.score_pairs(th, ts, td, "mlp", t(W, cuda, BF), t(b, cuda)).cpu().numpy()
+        z = (hd[src] * hd[dst]) @ W.T.astype(np.float64) + b
+        ref = 1 / (1 + np.exp(-np.maximum(z, 0)))
+    tol_close(got, ref, 1e-2, 1e-2)
