@@ -170,14 +170,18 @@ MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t
  * sum_e attd_e dV[j] when dV != NULL.  The column half (d_er, d_hc) is
  * msha_csc_aggregate over (attd, de).  row_coef (n_rows, heads), nullable: an extra
  * gradient row_coef[i] * exp(attd_e) on the attention of row i -- the full MSHA
- * layer's normaliser sums exp(attention_inter) of its batch rows (Ours.py:84-86). */
+ * layer's normaliser sums exp(attention_inter) of its batch rows (Ours.py:84-86).
+ * edge_ld: floats between consecutive edges in de / attd (0 = heads); with
+ * edge_ld = 2*heads and attd = de + heads the two share one 2H-float record per edge,
+ * which msha_csc_aggregate then reads as one 64-B segment (w = attd, x = de). */
 MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
                                           int32_t dtype, const float* el, const float* er,
                                           const void* hc, const float* lse, const void* u,
                                           const void* dU, const void* hs, const void* dV,
                                           const float* row_coef, float neg_slope, float drop_p,
                                           uint64_t seed, uint64_t offset, float* d_el, float* de,
-                                          float* attd, void* d_hs, msha_stream_t stream);
+                                          float* attd, int32_t edge_ld, void* d_hs,
+                                          msha_stream_t stream);
 
 /* Column-side (transposed) aggregate over the CSC view:
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
@@ -186,12 +190,14 @@ MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, in
  * d_er = colsum(de).  With heads = 1 and w = the adjacency values it is the GCN
  * SpMM adj^T @ support (model.py:37); on a CSR-as-CSC view (colptr = rowptr,
  * csc_row = col, csc_eid = NULL, chunks over rows) it is adj @ support.
+ * edge_ld: floats between consecutive edges in w / x (0 = heads).
  * Long columns are split into chunks whose partial sums are added in a fixed order:
  * deterministic, no atomics. */
 MSHA_API size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);
 MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype,
-                                const float* w, const float* x, const void* table, void* out,
-                                float* out_x, void* ws, size_t ws_bytes, msha_stream_t stream);
+                                const float* w, const float* x, int32_t edge_ld,
+                                const void* table, void* out, float* out_x, void* ws,
+                                size_t ws_bytes, msha_stream_t stream);
 
 /* ----------------------------------------------- GraphAttentionLayer (GAL) --- */
 /* GAT.py:20-35 / Ablation.py:100-115.  The layer's score is constant along a row

@@ -65,9 +65,9 @@ SIGNATURES = {
     "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P, P,
                                           P, P]),
     "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32,
-                                               F32, U64, U64, P, P, P, P, P]),
+                                               F32, U64, U64, P, P, P, I32, P, P]),
     "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
-    "msha_csc_aggregate": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "msha_csc_aggregate": (C.c_int, [GP, I32, I32, I32, P, P, I32, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),
     "msha_gal_bwd": (C.c_int, [GP, P, P, F32, U64, U64, P, P]),
     "msha_gemm_workspace_size": (SZ, [I64, I64, I32]),

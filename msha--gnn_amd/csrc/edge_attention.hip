@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     const float* __restrict__ er, const T* __restrict__ hc, const float* __restrict__ lse,
     const T* __restrict__ u, const T* __restrict__ dU, const T* __restrict__ hs,
     const T* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
-    float* __restrict__ d_el, float* __restrict__ de, float* __restrict__ attd,
+    float* __restrict__ d_el, float* __restrict__ de, float* __restrict__ attd, int ld,
     T* __restrict__ d_hs) {
   using G = Geo<H, F, T>;
   const int lane = lane_id();
@@ -293,8 +293,8 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
         if (coef != 0.f) gsum += coef * expf(att * dropf);
         const float ds = att * (gsum * dropf - Ds);
         const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
-        de[(int64_t)e * H + h_s] = dev;
-        attd[(int64_t)e * H + h_s] = att * dropf;
+        de[(int64_t)e * ld + h_s] = dev;
+        attd[(int64_t)e * ld + h_s] = att * dropf;
         del += dev;
       }
     }
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
     const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
     const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid,
-    const float* __restrict__ w, const float* __restrict__ x, const T* __restrict__ table,
+    const float* __restrict__ w, const float* __restrict__ x, int ld, const T* __restrict__ table,
     T* __restrict__ out, float* __restrict__ out_x, float* __restrict__ part,
     float* __restrict__ part_x) {
   using G = Geo<H, F, T>;
@@ -334,8 +334,8 @@ __global__ void __launch_bounds__(256) csc_aggregate_kernel(
       const int32_t i = valid ? csc_row[slot] : 0;
       // csc_eid NULL: slot order is the edge order (the CSR-as-CSC view of a graph)
       const int64_t eid = valid ? (csc_eid != nullptr ? (int64_t)csc_eid[slot] : slot) : 0;
-      const float wv = valid ? w[eid * H + h_s] : 0.f;
-      if (HASX && valid) xacc += x[eid * H + h_s];
+      const float wv = valid ? w[eid * ld + h_s] : 0.f;
+      if (HASX && valid) xacc += x[eid * ld + h_s];
       const int nvalid = min(G::CE, (int)(s1 - cs));
 #pragma unroll
       for (int g = 0; g < G::CE; g += G::EPI) {
@@ -502,7 +502,7 @@ static void launch_bwd_rows(const msha_graph* g, int heads, int feat, const floa
                             const float* er, const void* hc, const float* lse, const void* u,
                             const void* dU, const void* hs, const void* dV, const float* row_coef,
                             float neg_slope, const Dropout& dp, float* d_el, float* de,
-                            float* attd, void* d_hs, hipStream_t s) {
+                            float* attd, int ld, void* d_hs, hipStream_t s) {
 #define X(h, f)                                                                                  \
   if (heads == h && feat == f) {                                                                 \
     if constexpr (f % Pk<T>::V == 0) {                                                           \
@@ -510,12 +510,12 @@ static void launch_bwd_rows(const msha_graph* g, int heads, int feat, const floa
         hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, T, true>), wave_grid(g->n_rows),     \
                            dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,    \
                            (const T*)hc, lse, (const T*)u, (const T*)dU, (const T*)hs,           \
-                           (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, (T*)d_hs);     \
+                           (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, ld, (T*)d_hs); \
       else                                                                                       \
         hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, T, false>), wave_grid(g->n_rows),    \
                            dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,    \
                            (const T*)hc, lse, (const T*)u, (const T*)dU, (const T*)hs,           \
-                           (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, (T*)d_hs);     \
+                           (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, ld, (T*)d_hs); \
     }                                                                                            \
   }
   MSHA_FOR_EACH_SHAPE(X)
@@ -528,23 +528,25 @@ extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, 
                                             const void* dU, const void* hs, const void* dV,
                                             const float* row_coef, float neg_slope,
                                             float drop_p, uint64_t seed, uint64_t offset,
-                                            float* d_el, float* de, float* attd, void* d_hs,
-                                            msha_stream_t stream) {
+                                            float* d_el, float* de, float* attd,
+                                            int32_t edge_ld, void* d_hs, msha_stream_t stream) {
   if (int rc = check_graph(g, false)) return rc;
   MSHA_ARG_CHECK(el && er && hc && lse && u && dU && d_el && de && attd,
                  "edge_attention_bwd_rows: null pointer");
   MSHA_ARG_CHECK(dV == nullptr || (hs && d_hs), "edge_attention_bwd_rows: dV needs hs and d_hs");
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_bwd_rows: p must be in [0,1]");
+  const int ld = edge_ld > 0 ? edge_ld : heads;
+  MSHA_ARG_CHECK(ld >= heads, "edge_attention_bwd_rows: edge_ld < heads");
   if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_rows: unsupported (heads, feat, dtype)");
   const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MSHA_DTYPE_BF16)
     launch_bwd_rows<bf16_t>(g, heads, feat, el, er, hc, lse, u, dU, hs, dV, row_coef, neg_slope,
-                            dp, d_el, de, attd, d_hs, s);
+                            dp, d_el, de, attd, ld, d_hs, s);
   else
     launch_bwd_rows<float>(g, heads, feat, el, er, hc, lse, u, dU, hs, dV, row_coef, neg_slope,
-                           dp, d_el, de, attd, d_hs, s);
+                           dp, d_el, de, attd, ld, d_hs, s);
   return check_launch("edge_attention_bwd_rows");
 }
 
@@ -557,20 +559,20 @@ extern "C" size_t msha_csc_aggregate_workspace_size(const msha_graph* g, int32_t
 
 template <typename T>
 static void launch_csc(const msha_graph* g, int heads, int feat, const float* w, const float* x,
-                       const void* table, void* out, float* out_x, float* part, float* part_x,
-                       hipStream_t s) {
+                       int ld, const void* table, void* out, float* out_x, float* part,
+                       float* part_x, hipStream_t s) {
 #define X(h, f)                                                                                 \
   if (heads == h && feat == f) {                                                                \
     if constexpr (f % Pk<T>::V == 0) {                                                          \
       if (x)                                                                                    \
         hipLaunchKernelGGL((csc_aggregate_kernel<h, f, T, true>), wave_grid(g->n_chunks),       \
                            dim3(256), 0, s, g->chunk_col, g->chunk_start, g->chunk_end,         \
-                           g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x,                \
+                           g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x, ld,            \
                            (const T*)table, (T*)out, out_x, part, part_x);                      \
       else                                                                                      \
         hipLaunchKernelGGL((csc_aggregate_kernel<h, f, T, false>), wave_grid(g->n_chunks),      \
                            dim3(256), 0, s, g->chunk_col, g->chunk_start, g->chunk_end,         \
-                           g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x,                \
+                           g->n_chunks, g->colptr, g->csc_row, g->csc_eid, w, x, ld,            \
                            (const T*)table, (T*)out, out_x, part, part_x);                      \
     }                                                                                           \
   }
@@ -587,7 +589,7 @@ static void launch_csc(const msha_graph* g, int heads, int feat, const float* w,
 }
 
 extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat,
-                                  int32_t dtype, const float* w, const float* x,
+                                  int32_t dtype, const float* w, const float* x, int32_t edge_ld,
                                   const void* table, void* out, float* out_x, void* ws,
                                   size_t ws_bytes, msha_stream_t stream) {
   if (int rc = check_graph(g, true)) return rc;
@@ -605,9 +607,11 @@ extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t fe
     part_x = part + g->n_chunks * D;
   }
   hipStream_t s = (hipStream_t)stream;
+  const int ld = edge_ld > 0 ? edge_ld : heads;
+  MSHA_ARG_CHECK(ld >= heads, "csc_aggregate: edge_ld < heads");
   if (dtype == MSHA_DTYPE_BF16)
-    launch_csc<bf16_t>(g, heads, feat, w, x, table, out, out_x, part, part_x, s);
+    launch_csc<bf16_t>(g, heads, feat, w, x, ld, table, out, out_x, part, part_x, s);
   else
-    launch_csc<float>(g, heads, feat, w, x, table, out, out_x, part, part_x, s);
+    launch_csc<float>(g, heads, feat, w, x, ld, table, out, out_x, part, part_x, s);
   return check_launch("csc_aggregate");
 }

@@ -125,22 +125,25 @@ class _EdgeAttention(torch.autograd.Function):
         dV = _tc(dV, dt) if use_dv else None
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
-        de = torch.empty(E, H, device=dev, dtype=torch.float32)
-        attd = torch.empty(E, H, device=dev, dtype=torch.float32)
+        # one (de, attd) record of 2H floats per edge: the column pass reads it as one
+        # 64-B segment at C4 (the CSC visits edges in random order)
+        rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)
+        de, attd = rec[:, 0], rec[:, 1]
         d_hs = torch.empty(n, H, F, device=dev, dtype=dt) if use_dv else None
         _lib.call("msha_edge_attention_bwd_rows", g, H, F, _code(dt), el.data_ptr(),
                   er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
                   hs.data_ptr() if use_dv else None, _lib.ptr(dV), None, ctx.slope, ctx.p,
-                  ctx.seed, 0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), _lib.ptr(d_hs), s)
+                  ctx.seed, 0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), 2 * H,
+                  _lib.ptr(d_hs), s)
         d_hc = torch.empty(m, H, F, device=dev, dtype=dt)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
-        _csc_aggregate(graph, H, F, attd, de, dU, d_hc, d_er, s)
+        _csc_aggregate(graph, H, F, attd, de, dU, d_hc, d_er, s, ld=2 * H)
         if ctx.has_hs and d_hs is None:
             d_hs = torch.zeros_like(hs)
         return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None
 
 
-def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream):
+def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream, ld=0):
     if not graph.has_csc:
         raise RuntimeError("graph has no CSC view (build it with_csc=True)")
     assert out.dtype == table.dtype
@@ -149,7 +152,7 @@ def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream):
     ws = None
     if graph._plan["n_multi"] > 0:
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=table.device)
-    _lib.call("msha_csc_aggregate", g, H, F, _code(table.dtype), w.data_ptr(), _lib.ptr(x),
+    _lib.call("msha_csc_aggregate", g, H, F, _code(table.dtype), w.data_ptr(), _lib.ptr(x), ld,
               table.data_ptr(), out.data_ptr(), _lib.ptr(out_x), _lib.ptr(ws),
               0 if ws is None else ws.numel(), stream)
 
@@ -744,18 +747,18 @@ class _OursAttention(torch.autograd.Function):
                   ws.data_ptr(), ws.numel(), s)
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
-        de = torch.empty(E, H, device=dev, dtype=torch.float32)
-        attd = torch.empty(E, H, device=dev, dtype=torch.float32)
+        rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)  # (de, attd) per edge
+        de, attd = rec[:, 0], rec[:, 1]
         d_hs = torch.empty(n, H, Fd, device=dev, dtype=dt)
         _lib.call("msha_edge_attention_bwd_rows", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
                   h1.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), dU.data_ptr(),
                   h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p, ctx.seed,
-                  0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), d_hs.data_ptr(), s)
+                  0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), 2 * H, d_hs.data_ptr(), s)
         _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
                   bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), None, 0, s)
         d_hc = torch.empty(m, H, Fd, device=dev, dtype=dt)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
-        _csc_aggregate(graph, H, Fd, attd, de, dU, d_hc, d_er, s)
+        _csc_aggregate(graph, H, Fd, attd, de, dU, d_hc, d_er, s, ld=2 * H)
         return d_el, d_er, d_hc, d_hs, da3s, da4s, None, None, None, None, None, None
 
 
