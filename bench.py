@@ -91,6 +91,21 @@ def pmc_traffic(H, F, bf16=False, workload="syn100k"):
     return None, None
 
 
+def bwd_rows_bytes(n, m, e, H, F, s=4):
+    """Algorithmic bytes of msha_edge_attention_bwd_rows (no v-branch): per edge col +
+    er gather + s*D hc gather + the (de, attd) record; per row rowptr, el, lse, dU, u,
+    d_el."""
+    D = H * F
+    return 4 * (n + 1) + e * (4 + 4 * H + s * D + 8 * H) + n * (12 * H + 2 * s * D)
+
+
+def csc_bytes(m, e, H, F, n_chunks, s=4):
+    """Algorithmic bytes of msha_csc_aggregate (d_hc, d_er): per CSC slot row + eid +
+    the (attd, de) record + s*D dU gather; per column the outputs; the chunk plan."""
+    D = H * F
+    return e * (8 + 8 * H + s * D) + m * (s * D + 4 * H) + 12 * n_chunks + 4 * (m + 1)
+
+
 def fwd_bytes(n, m, e, H, F, s=4):
     """Algorithmic bytes of one msha_edge_attention_fwd launch:
     rowptr + col + er gather + el + h gather (s*HF per edge) + u write + lse write;
@@ -401,14 +416,34 @@ def main():
             lay.step()
         barrier()
         dt_ = time.perf_counter() - t0
-        events = lay.MF.KERNEL_EVENTS.get("edge_attention_fwd", [])
+        evs = lay.MF.KERNEL_EVENTS
         lay.MF.KERNEL_EVENTS = None
-        k = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+        ms = {name: float(np.mean([a.elapsed_time(b) for a, b in lst]))
+              for name, lst in evs.items() if lst}
+        events = evs.get("edge_attention_fwd", [])
+        k = ms.get("edge_attention_fwd", float("nan"))
         if dist:
             tt = torch.tensor([dt_], device=dev)
             tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
             dt_ = float(tt.item())
+        lay.kernel_ms = ms
         return dt_, k, len(events)
+
+    def edge_kernels(lay, s):
+        """Rooflines of the three edge kernels of the step (HIP events, same run)."""
+        nch = lay.graph._plan["n_chunks"]
+        out = []
+        for name, nbytes in (("msha_edge_attention_fwd", fwd_bytes(n, m, e, H, F, s)),
+                             ("msha_edge_attention_bwd_rows", bwd_rows_bytes(n, m, e, H, F, s)),
+                             ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s))):
+            key = name[len("msha_"):]
+            if key not in lay.kernel_ms:
+                continue
+            us = lay.kernel_ms[key] * 1e3
+            gbs = nbytes / (us * 1e-6) / 1e9
+            out.append({"kernel": name, "algorithmic_bytes": nbytes, "avg_us": us,
+                        "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
+        return out
 
     dt, k_ms, n_launch = timed(layer, args.steps, args.warmup)
     bf16_leg = None
@@ -429,6 +464,7 @@ def main():
                                  "frac": a16 / HBM_PEAK_GBS, "traffic": tr16,
                                  "traffic_source": src16, "algorithmic_bytes_per_launch": fb16,
                                  "avg_launch_us": k16 * 1e3, "launches_timed": n16}}
+        bf16_leg["edge_kernels"] = edge_kernels(lay16, 2)
         del lay16
     link = None
     if not args.no_link_score and args.workload != "r15":
@@ -460,6 +496,7 @@ def main():
                      "algorithmic_bytes_per_launch": fb, "avg_launch_us": k_ms * 1e3,
                      "launches_timed": n_launch},
     }
+    out["edge_kernels"] = edge_kernels(layer, 4)
     if bf16_leg is not None:
         out["bf16"] = bf16_leg
     if link is not None:

@@ -130,14 +130,20 @@ class _EdgeAttention(torch.autograd.Function):
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)
         de, attd = rec[:, 0], rec[:, 1]
         d_hs = torch.empty(n, H, F, device=dev, dtype=dt) if use_dv else None
+        ev = _timed("edge_attention_bwd_rows")
         _lib.call("msha_edge_attention_bwd_rows", g, H, F, _code(dt), el.data_ptr(),
                   er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
                   hs.data_ptr() if use_dv else None, _lib.ptr(dV), None, ctx.slope, ctx.p,
                   ctx.seed, 0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), 2 * H,
                   _lib.ptr(d_hs), s)
+        if ev is not None:
+            ev[1].record()
         d_hc = torch.empty(m, H, F, device=dev, dtype=dt)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
+        ev = _timed("csc_aggregate")
         _csc_aggregate(graph, H, F, attd, de, dU, d_hc, d_er, s, ld=2 * H)
+        if ev is not None:
+            ev[1].record()
         if ctx.has_hs and d_hs is None:
             d_hs = torch.zeros_like(hs)
         return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None
