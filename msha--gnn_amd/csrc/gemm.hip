@@ -290,8 +290,10 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
   }
 
   // ---- epilogue.  MFMA C/D layout: col = lane & 15, row = (lane >> 4) * 4 + reg.
-  // Each wave stages its 16-row halves through LDS, then every lane finishes a
-  // 32-column segment of one row: activation, per-head score dots, 16-B stores.
+  // Each wave stages its 16-row halves through LDS, then writes them back in 8 passes
+  // of 2 rows: lane l covers columns 4(l & 31) .. +3 of row 2*pass + (l >> 5), so a
+  // wave-store is two 512-B row segments (coalesced).  Activation and per-head score
+  // dots (an xor tree over the head's F/4 lanes) happen on the way.
   static_assert(4 * 16 * TP <= BM * LDA + BK * LDP, "epilogue staging exceeds LDS");
   __syncthreads();  // all waves are done reading the operand tiles
   float* T = smem + w * (16 * TP);
@@ -301,20 +303,18 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
     out = p.slab + (int64_t)blockIdx.z * p.M * p.N;
     ldo = p.N;
   }
-  const int rl = lane >> 2;   // row within the 16-row half
-  const int seg = lane & 3;   // 32-column segment
-  const int64_t cbase = n0 + seg * 32;
-  // per-lane constants of its segment
-  float4 bia[8], alv[8], arv[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int64_t col = cbase + 4 * q;
-    const bool ok = col < p.N;
-    bia[q] = alv[q] = arv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (EPI == EPI_ACT && (p.act & ACT_BIAS) && ok) bia[q] = *reinterpret_cast<const float4*>(p.bias + col);
-    if (EPI == EPI_SCORE && p.al && ok) alv[q] = *reinterpret_cast<const float4*>(p.al + col);
-    if (EPI == EPI_SCORE && p.ar && ok) arv[q] = *reinterpret_cast<const float4*>(p.ar + col);
+  const int c4 = (lane & 31) * 4;  // column (within the tile) of this lane's float4
+  const int64_t col = n0 + c4;
+  const bool col_ok = col < p.N;
+  float4 bia = make_float4(0.f, 0.f, 0.f, 0.f), alv = bia, arv = bia;
+  if (EPI == EPI_ACT && (p.act & ACT_BIAS) && col_ok) {
+    const float b4[4] = {p.bias[col], col + 1 < p.N ? p.bias[col + 1] : 0.f,
+                         col + 2 < p.N ? p.bias[col + 2] : 0.f, col + 3 < p.N ? p.bias[col + 3] : 0.f};
+    bia = make_float4(b4[0], b4[1], b4[2], b4[3]);
   }
+  if (EPI == EPI_SCORE && p.al && col_ok) alv = *reinterpret_cast<const float4*>(p.al + col);
+  if (EPI == EPI_SCORE && p.ar && col_ok) arv = *reinterpret_cast<const float4*>(p.ar + col);
+  const bool vec = ((ldo & 3) == 0) && ((((uintptr_t)out) & 15) == 0);
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
 #pragma unroll
@@ -323,82 +323,56 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i) T[((lane >> 4) * 4 + i) * TP + c * 16 + (lane & 15)] = acc[r][c][i];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
     __builtin_amdgcn_wave_barrier();
-    const int64_t row = m0 + w * 32 + r * 16 + rl;
-    float4 v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(T + rl * TP + seg * 32 + 4 * q);
-    if (EPI == EPI_ACT) {
-      // keep bits of this lane's 32 outputs, drawn in a rolled loop (an inlined
-      // Philox per unrolled element spills to scratch)
-      uint32_t kb = 0xffffffffu;
-      if (p.act & ACT_DROPOUT) {
-        kb = 0u;
-        const uint64_t off = dropout_offset(p.dp, p.dp.offset);
+#pragma unroll 2
+    for (int pass = 0; pass < 8; ++pass) {
+      const int rr = 2 * pass + (lane >> 5);
+      const int64_t row = m0 + w * 32 + r * 16 + rr;
+      float4 v = *reinterpret_cast<const float4*>(T + rr * TP + c4);
+      if (EPI == EPI_ACT) {
+        uint32_t kb = 0xfu;
+        if (p.act & ACT_DROPOUT) {
+          kb = 0u;
+          const uint64_t off = dropout_offset(p.dp, p.dp.offset);
 #pragma unroll 1
-        for (int u = 0; u < 32; ++u)
-          if (philox_x(p.dp.seed, off, (uint64_t)(row * p.N + cbase + u)) >= p.dp.threshold)
-            kb |= 1u << u;
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-        const float bb[4] = {bia[q].x, bia[q].y, bia[q].z, bia[q].w};
+          for (int u = 0; u < 4; ++u)
+            if (philox_x(p.dp.seed, off, (uint64_t)(row * p.N + col + u)) >= p.dp.threshold)
+              kb |= 1u << u;
+        }
+        float e[4] = {v.x, v.y, v.z, v.w};
+        const float bb[4] = {bia.x, bia.y, bia.z, bia.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           float x = e[u] + bb[u];
           if (p.act & ACT_RELU) x = fmaxf(x, 0.f);
-          if (p.act & ACT_DROPOUT) x *= ((kb >> (4 * q + u)) & 1u) ? p.dp.scale : 0.f;
+          if (p.act & ACT_DROPOUT) x *= ((kb >> u) & 1u) ? p.dp.scale : 0.f;
           if (p.act & ACT_SIGMOID) x = 1.f / (1.f + __expf(-x));
           e[u] = x;
         }
-        v[q] = make_float4(e[0], e[1], e[2], e[3]);
+        v = make_float4(e[0], e[1], e[2], e[3]);
       }
-    }
-    if (row < p.M) {
-      const bool vec = ((ldo & 3) == 0) && ((((uintptr_t)out) & 15) == 0);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int64_t col = cbase + 4 * q;
+      if (row < p.M && col_ok) {
         if (vec && col + 3 < p.N) {
-          *reinterpret_cast<float4*>(out + row * ldo + col) = v[q];
+          *reinterpret_cast<float4*>(out + row * ldo + col) = v;
         } else {
-          const float e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+          const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u)
             if (col + u < p.N) out[row * ldo + col + u] = e[u];
         }
       }
-    }
-    if (EPI == EPI_SCORE) {
-      // FEPI <= 32: 32 / FEPI whole heads inside the segment; FEPI > 32: the head
-      // spans FEPI / 32 segments (lanes seg, seg^1, ...) -> reduce across them.
-      constexpr int FE = FEPI > 0 ? FEPI : 16;
-      constexpr int HS = FE <= 32 ? 32 / FE : 1;
-      constexpr int QPH = FE <= 32 ? FE / 4 : 8;  // float4 per head inside the segment
-      float sl[HS], sr[HS];
+      if (EPI == EPI_SCORE) {
+        // a head covers FE / 4 consecutive lanes of the row's 32 (FE <= 128)
+        constexpr int FE = FEPI > 0 ? FEPI : 16;
+        float sl = f4_dot(v, alv), sr = f4_dot(v, arv);
 #pragma unroll
-      for (int hh = 0; hh < HS; ++hh) {
-        sl[hh] = sr[hh] = 0.f;
-#pragma unroll
-        for (int q = hh * QPH; q < (hh + 1) * QPH; ++q) {
-          sl[hh] += f4_dot(v[q], alv[q]);
-          sr[hh] += f4_dot(v[q], arv[q]);
+        for (int o = 1; o < FE / 4; o <<= 1) {
+          sl += __shfl_xor(sl, o);
+          sr += __shfl_xor(sr, o);
         }
-      }
-      if (FE > 32) {
-#pragma unroll
-        for (int o = 1; o < FE / 32; o <<= 1) {
-          sl[0] += __shfl_xor(sl[0], o);
-          sr[0] += __shfl_xor(sr[0], o);
-        }
-      }
-#pragma unroll
-      for (int hh = 0; hh < HS; ++hh) {
-        const int64_t hg = FE <= 32 ? (cbase / FE) + hh : cbase / FE;
-        const bool writer = FE <= 32 ? true : (seg % (FE / 32)) == 0;
-        if (writer && row < p.M && hg < p.H && cbase < p.N) {
-          if (p.el) p.el[row * p.H + hg] = sl[hh];
-          if (p.er) p.er[row * p.H + hg] = sr[hh];
+        const int64_t hg = col / FE;
+        if ((c4 % FE) == 0 && row < p.M && hg < p.H && col_ok) {
+          if (p.el) p.el[row * p.H + hg] = sl;
+          if (p.er) p.er[row * p.H + hg] = sr;
         }
       }
     }

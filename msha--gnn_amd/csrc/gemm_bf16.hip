@@ -242,22 +242,23 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(Args p) {
     }
   }
 
-  // ---- epilogue (C/D layout: col = lane & 15, row = (lane >> 4) * 4 + reg)
+  // ---- epilogue (C/D layout: col = lane & 15, row = (lane >> 4) * 4 + reg).  The
+  // 16-row halves are staged through LDS and written back in 4 passes of 4 rows: lane l
+  // covers columns 8(l & 15) .. +7 of row 4*pass + (l >> 4) -- a wave-store is four
+  // contiguous row segments; per-head score dots reduce over the head's F/8 lanes.
   static_assert(4 * 16 * TP * 4 <= 2 * IMG * 2, "epilogue staging exceeds LDS");
   __syncthreads();
   float* T = reinterpret_cast<float*>(smem) + w * (16 * TP);
   const bool to_slab = p.slab != nullptr;
-  const int rl = lane >> 2, seg = lane & 3;
-  const int64_t cbase = n0 + seg * 32;
-  float4 alv[8], arv[8];
+  const int c8 = (lane & 15) * 8;
+  const int64_t col = n0 + c8;
+  const bool col_ok = col < p.N;  // N % 8 == 0: the 8 columns are all in or all out
+  float al8[8], ar8[8], bi8[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int64_t col = cbase + 4 * q;
-    alv[q] = arv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (EPI == EPI_SCORE && col < p.N) {
-      if (p.al) alv[q] = *reinterpret_cast<const float4*>(p.al + col);
-      if (p.ar) arv[q] = *reinterpret_cast<const float4*>(p.ar + col);
-    }
+  for (int u = 0; u < 8; ++u) {
+    al8[u] = EPI == EPI_SCORE && p.al && col_ok ? p.al[col + u] : 0.f;
+    ar8[u] = EPI == EPI_SCORE && p.ar && col_ok ? p.ar[col + u] : 0.f;
+    bi8[u] = EPI == EPI_ACT && (p.act & ACT_BIAS) && col_ok ? p.bias[col + u] : 0.f;
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -267,94 +268,62 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(Args p) {
       for (int i = 0; i < 4; ++i) T[((lane >> 4) * 4 + i) * TP + c * 16 + (lane & 15)] = acc[r][c][i];
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    const int64_t row = m0 + w * 32 + r * 16 + rl;
-    float4 v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const float4*>(T + rl * TP + seg * 32 + 4 * q);
-    if (EPI == EPI_ACT) {
-      uint32_t kbits = 0xffffffffu;
-      if (p.act & ACT_DROPOUT) {  // keep bits of the lane's 32 outputs (rolled loop)
-        kbits = 0u;
-        const uint64_t off = dropout_offset(p.dp, p.dp.offset);
 #pragma unroll 1
-        for (int u = 0; u < 32; ++u)
-          if (philox_x(p.dp.seed, off, (uint64_t)(row * p.N + cbase + u)) >= p.dp.threshold)
-            kbits |= 1u << u;
-      }
+    for (int pass = 0; pass < 4; ++pass) {
+      const int rr = 4 * pass + (lane >> 4);
+      const int64_t row = m0 + w * 32 + r * 16 + rr;
+      const float4 lo = *reinterpret_cast<const float4*>(T + rr * TP + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(T + rr * TP + c8 + 4);
+      float e[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      if (EPI == EPI_ACT) {
+        uint32_t kb = 0xffu;
+        if (p.act & ACT_DROPOUT) {
+          kb = 0u;
+          const uint64_t off = dropout_offset(p.dp, p.dp.offset);
+#pragma unroll 1
+          for (int u = 0; u < 8; ++u)
+            if (philox_x(p.dp.seed, off, (uint64_t)(row * p.N + col + u)) >= p.dp.threshold)
+              kb |= 1u << u;
+        }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int64_t col = cbase + 4 * q + u;
-          float x = e[u] + ((p.act & ACT_BIAS) && col < p.N ? p.bias[col] : 0.f);
+        for (int u = 0; u < 8; ++u) {
+          float x = e[u] + bi8[u];
           if (p.act & ACT_RELU) x = fmaxf(x, 0.f);
-          if (p.act & ACT_DROPOUT) x *= ((kbits >> (4 * q + u)) & 1u) ? p.dp.scale : 0.f;
+          if (p.act & ACT_DROPOUT) x *= ((kb >> u) & 1u) ? p.dp.scale : 0.f;
           if (p.act & ACT_SIGMOID) x = 1.f / (1.f + __expf(-x));
           e[u] = x;
         }
-        v[q] = make_float4(e[0], e[1], e[2], e[3]);
       }
-    }
-    if (row < p.M) {
-      if (to_slab) {
-        float* o = p.slab + (int64_t)blockIdx.z * p.M * p.N + row * p.N;
+      if (row < p.M && col_ok) {
+        if (to_slab || !p.c_bf16) {
+          float* o = to_slab ? p.slab + (int64_t)blockIdx.z * p.M * p.N + row * p.N + col
+                             : reinterpret_cast<float*>(p.C) + row * p.ldc + col;
+          *reinterpret_cast<float4*>(o) = make_float4(e[0], e[1], e[2], e[3]);
+          *reinterpret_cast<float4*>(o + 4) = make_float4(e[4], e[5], e[6], e[7]);
+        } else {
+          Pk<bf16_t> pk;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int64_t col = cbase + 4 * q;
-          if (col < p.N) *reinterpret_cast<float4*>(o + col) = v[q];  // N % 8 == 0
-        }
-      } else if (p.c_bf16) {
-        bf16_t* o = reinterpret_cast<bf16_t*>(p.C) + row * p.ldc;
-#pragma unroll
-        for (int q = 0; q < 8; q += 2) {
-          const int64_t col = cbase + 4 * q;
-          if (col < p.N) {
-            Pk<bf16_t> pk;
-            const float e[8] = {v[q].x, v[q].y, v[q].z, v[q].w,
-                                v[q + 1].x, v[q + 1].y, v[q + 1].z, v[q + 1].w};
-#pragma unroll
-            for (int u = 0; u < 8; ++u) pk.v[u] = e[u];
-            pk_store(o + col, pk);
-          }
-        }
-      } else {
-        float* o = reinterpret_cast<float*>(p.C) + row * p.ldc;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int64_t col = cbase + 4 * q;
-          if (col < p.N) *reinterpret_cast<float4*>(o + col) = v[q];
+          for (int u = 0; u < 8; ++u) pk.v[u] = e[u];
+          pk_store(reinterpret_cast<bf16_t*>(p.C) + row * p.ldc + col, pk);
         }
       }
-    }
-    if (EPI == EPI_SCORE) {
-      constexpr int FE = FEPI > 0 ? FEPI : 16;
-      constexpr int HS = FE <= 32 ? 32 / FE : 1;
-      constexpr int QPH = FE <= 32 ? FE / 4 : 8;
-      float sl[HS], sr[HS];
+      if (EPI == EPI_SCORE) {
+        constexpr int FE = FEPI > 0 ? FEPI : 16;  // >= 8: a head covers FE / 8 lanes
+        float sl = 0.f, sr = 0.f;
 #pragma unroll
-      for (int hh = 0; hh < HS; ++hh) {
-        sl[hh] = sr[hh] = 0.f;
-#pragma unroll
-        for (int q = hh * QPH; q < (hh + 1) * QPH; ++q) {
-          sl[hh] += f4_dot(v[q], alv[q]);
-          sr[hh] += f4_dot(v[q], arv[q]);
+        for (int u = 0; u < 8; ++u) {
+          sl = fmaf(e[u], al8[u], sl);
+          sr = fmaf(e[u], ar8[u], sr);
         }
-      }
-      if (FE > 32) {
 #pragma unroll
-        for (int o = 1; o < FE / 32; o <<= 1) {
-          sl[0] += __shfl_xor(sl[0], o);
-          sr[0] += __shfl_xor(sr[0], o);
+        for (int o = 1; o < FE / 8; o <<= 1) {
+          sl += __shfl_xor(sl, o);
+          sr += __shfl_xor(sr, o);
         }
-      }
-#pragma unroll
-      for (int hh = 0; hh < HS; ++hh) {
-        const int64_t hg = FE <= 32 ? (cbase / FE) + hh : cbase / FE;
-        const bool writer = FE <= 32 ? true : (seg % (FE / 32)) == 0;
-        if (writer && row < p.M && hg < p.H && cbase < p.N) {
-          if (p.el) p.el[row * p.H + hg] = sl[hh];
-          if (p.er) p.er[row * p.H + hg] = sr[hh];
+        const int64_t hg = col / FE;
+        if ((c8 % FE) == 0 && row < p.M && hg < p.H && col_ok) {
+          if (p.el) p.el[row * p.H + hg] = sl;
+          if (p.er) p.er[row * p.H + hg] = sr;
         }
       }
     }
