@@ -20,6 +20,10 @@
 // pass needs no second sweep over the gathered rows.
 #include "common.h"
 
+#ifndef FWD_EPL
+#define FWD_EPL 2
+#endif
+
 namespace msha {
 
 template <int H, int F, typename T>
@@ -44,13 +48,17 @@ __device__ __forceinline__ int quad_of(int lane, int k) {
 }
 
 // ------------------------------------------------------------------ forward ---
-template <int H, int F, typename T>
+// EPL = edges per lane in the score layout: a chunk covers EPL * 64/H edges, so the
+// per-chunk max / sum reductions, the accumulator rescale and the loop overhead are
+// amortised over EPL times as many edges (the bf16 kernel is issue-bound).
+template <int H, int F, typename T, int EPL>
 __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
     const float* __restrict__ er, const T* __restrict__ hc, float slope, Dropout dp,
     T* __restrict__ u, float* __restrict__ lse, float* __restrict__ attd) {
   using G = Geo<H, F, T>;
+  constexpr int CEL = EPL * G::CE;  // edges per chunk
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
   const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
@@ -59,15 +67,20 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 
   // Software pipeline (the kernel is latency-bound per row: rowptr -> col -> er ->
   // gathers): the next row's bounds, flag, el and first two chunks' columns are loaded
-  // while this row runs, and inside a row the column two chunks ahead and the er one
+  // while this row runs, and inside a row the columns two chunks ahead and the er one
   // chunk ahead are in flight during the current chunk's gathers.
   int64_t row = wave;
   if (row >= n_rows) return;
   int32_t start = rowptr[row], end = rowptr[row + 1];
   bool virt = rowflag != nullptr && rowflag[row] != 0;
   float elh = el[row * H + h_s];
-  int32_t j0 = start + e_s < end ? col[start + e_s] : 0;
-  int32_t j1 = start + G::CE + e_s < end ? col[start + G::CE + e_s] : 0;
+  int32_t j0[EPL], j1[EPL];
+#pragma unroll
+  for (int t = 0; t < EPL; ++t) {
+    const int32_t e0 = start + t * G::CE + e_s, e1 = e0 + CEL;
+    j0[t] = e0 < end ? col[e0] : 0;
+    j1[t] = e1 < end ? col[e1] : 0;
+  }
   while (true) {
     const int64_t nrow = row + nwaves;
     const bool has_next = nrow < n_rows;
@@ -77,44 +90,64 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     Pk<T> acc[G::QPL];
 #pragma unroll
     for (int k = 0; k < G::QPL; ++k) acc[k] = pk_zero<T>();
-    float erv = start + e_s < end ? er[(int64_t)j0 * H + h_s] : 0.f;
+    float erv[EPL];
+#pragma unroll
+    for (int t = 0; t < EPL; ++t)
+      erv[t] = start + t * G::CE + e_s < end ? er[(int64_t)j0[t] * H + h_s] : 0.f;
 
-    for (int32_t cs = start; cs < end; cs += G::CE) {
-      const int32_t e = cs + e_s;
-      const bool valid = e < end;
-      const int32_t j = j0;
-      const int32_t e2 = e + 2 * G::CE;
-      const int32_t j2 = e2 < end ? col[e2] : 0;
-      const float ern = e + G::CE < end ? er[(int64_t)j1 * H + h_s] : 0.f;
-      float s = -INFINITY;
-      if (valid) s = virt ? 0.f : lrelu(elh + erv, slope);
-      const float mn = fmaxf(m, wave_xor_max<H>(s));
+    for (int32_t cs = start; cs < end; cs += CEL) {
+      int32_t j[EPL], j2[EPL];
+      float ern[EPL], sc[EPL];
+      bool valid[EPL];
+      float smax = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const int32_t e = cs + t * G::CE + e_s;
+        valid[t] = e < end;
+        j[t] = j0[t];
+        j2[t] = e + 2 * CEL < end ? col[e + 2 * CEL] : 0;
+        ern[t] = e + CEL < end ? er[(int64_t)j1[t] * H + h_s] : 0.f;
+        sc[t] = valid[t] ? (virt ? 0.f : lrelu(elh + erv[t], slope)) : -INFINITY;
+        smax = fmaxf(smax, sc[t]);
+      }
+      const float mn = fmaxf(m, wave_xor_max<H>(smax));
       const float alpha = __expf(m - mn);
-      const float pe = valid ? __expf(s - mn) : 0.f;
-      l = fmaf(l, alpha, wave_xor_sum<H>(pe));
+      float w[EPL], psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const float pe = valid[t] ? __expf(sc[t] - mn) : 0.f;
+        psum += pe;
+        w[t] = valid[t] ? pe * dropout_factor(dp, (uint64_t)(cs + t * G::CE + e_s) * H + h_s)
+                        : 0.f;
+      }
+      l = fmaf(l, alpha, wave_xor_sum<H>(psum));
       m = mn;
-      const float w = valid ? pe * dropout_factor(dp, (uint64_t)e * H + h_s) : 0.f;
 #pragma unroll
       for (int k = 0; k < G::QPL; ++k) {
         const int hd = quad_of<G>(lane, k) / G::QH;
         acc[k] = pk_scale(acc[k], __shfl(alpha, hd));
       }
-      const int nvalid = min(G::CE, (int)(end - cs));
+      const int nvalid = min(CEL, (int)(end - cs));
 #pragma unroll
-      for (int g = 0; g < G::CE; g += G::EPI) {
+      for (int g = 0; g < CEL; g += G::EPI) {
         if (g >= nvalid) break;
-        const int ei = g + g_e;
-        const int32_t jq = __shfl(j, ei * H);
+        const int t = g / G::CE;        // half of the chunk (compile time)
+        const int ei = g % G::CE + g_e;  // edge slot inside that half
+        const int32_t jq = __shfl(j[t], ei * H);
 #pragma unroll
         for (int k = 0; k < G::QPL; ++k) {
           const int q = quad_of<G>(lane, k);
-          const float wq = __shfl(w, ei * H + q / G::QH);
-          if (ei < nvalid) acc[k] = pk_fma(wq, pk_load(hc + (int64_t)jq * G::D + G::V * q), acc[k]);
+          const float wq = __shfl(w[t], ei * H + q / G::QH);
+          if (g + g_e < nvalid)
+            acc[k] = pk_fma(wq, pk_load(hc + (int64_t)jq * G::D + G::V * q), acc[k]);
         }
       }
-      j0 = j1;
-      j1 = j2;
-      erv = ern;
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        j0[t] = j1[t];
+        j1[t] = j2[t];
+        erv[t] = ern[t];
+      }
     }
     // the next row's first loads go out before this row's epilogue
     bool nvirt = false;
@@ -122,8 +155,12 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     if (has_next) {
       nvirt = rowflag != nullptr && rowflag[nrow] != 0;
       nelh = el[nrow * H + h_s];
-      j0 = nstart + e_s < nend ? col[nstart + e_s] : 0;
-      j1 = nstart + G::CE + e_s < nend ? col[nstart + G::CE + e_s] : 0;
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const int32_t e0 = nstart + t * G::CE + e_s, e1 = e0 + CEL;
+        j0[t] = e0 < nend ? col[e0] : 0;
+        j1[t] = e1 < nend ? col[e1] : 0;
+      }
     }
     if (G::EPI > 1) {
 #pragma unroll
@@ -142,9 +179,9 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
       for (int32_t cs = start; cs < end; cs += G::CE) {
         const int32_t e = cs + e_s;
         if (e < end) {
-          const float s = virt ? 0.f : lrelu(elh + er[(int64_t)col[e] * H + h_s], slope);
+          const float sv = virt ? 0.f : lrelu(elh + er[(int64_t)col[e] * H + h_s], slope);
           attd[(int64_t)e * H + h_s] =
-              __expf(s - lse_h) * dropout_factor(dp, (uint64_t)e * H + h_s);
+              __expf(sv - lse_h) * dropout_factor(dp, (uint64_t)e * H + h_s);
         }
       }
     }
@@ -431,6 +468,14 @@ __global__ void __launch_bounds__(1024) csc_combine_kernel(
   X(4, 8) X(4, 16) X(4, 32) X(4, 64) X(4, 128) \
   X(8, 8) X(8, 16) X(8, 32) X(8, 64) X(8, 128)
 
+// edges per lane of the forward's score layout (2: amortise the per-chunk reductions
+// where a chunk is short and the gathers are single 16-byte pieces per lane)
+template <int H, int F, typename T>
+constexpr int fwd_epl() {
+  using G = Geo<H, F, T>;
+  return (G::QPL == 1 && G::CE <= 16) ? FWD_EPL : 1;
+}
+
 static bool shape_supported(int H, int F) {
 #define X(h, f) if (H == h && F == f) return true;
   MSHA_FOR_EACH_SHAPE(X)
@@ -483,13 +528,15 @@ extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32
   if (heads == h && feat == f) {                                                               \
     if (dtype == MSHA_DTYPE_BF16) {                                                            \
       if constexpr (f % 8 == 0)                                                                \
-        hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, bf16_t>), wave_grid(g->n_rows),         \
-                           dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,  \
-                           (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u, lse, attd);           \
+        hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>()>),      \
+                           wave_grid(g->n_rows), dim3(256), 0, s, g->rowptr, g->col,           \
+                           g->rowflag, g->n_rows, el, er, (const bf16_t*)hc, neg_slope, dp,    \
+                           (bf16_t*)u, lse, attd);                                             \
     } else {                                                                                   \
-      hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, float>), wave_grid(g->n_rows), dim3(256), \
-                         0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,               \
-                         (const float*)hc, neg_slope, dp, (float*)u, lse, attd);               \
+      hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, float, fwd_epl<h, f, float>()>),          \
+                         wave_grid(g->n_rows), dim3(256), 0, s, g->rowptr, g->col, g->rowflag, \
+                         g->n_rows, el, er, (const float*)hc, neg_slope, dp, (float*)u, lse,   \
+                         attd);                                                                \
     }                                                                                          \
   }
   MSHA_FOR_EACH_SHAPE(X)
