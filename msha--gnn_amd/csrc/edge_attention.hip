@@ -214,8 +214,18 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
   const int dsrc_k = (h_s * G::QH) / 64;
   const int dsrc_l = (h_s * G::QH) % 64;
 
-  for (int64_t row = wave; row < n_rows; row += nwaves) {
-    const int32_t start = rowptr[row], end = rowptr[row + 1];
+  // same software pipeline as the forward: next row's bounds during this row, the
+  // main loop's columns two chunks ahead and er one chunk ahead
+  int64_t row = wave;
+  if (row >= n_rows) return;
+  int32_t start = rowptr[row], end = rowptr[row + 1];
+  int32_t j0 = start + e_s < end ? col[start + e_s] : 0;
+  int32_t j1 = start + G::CE + e_s < end ? col[start + G::CE + e_s] : 0;
+  while (true) {
+    const int64_t nrow = row + nwaves;
+    const bool has_next = nrow < n_rows;
+    const int32_t nstart = has_next ? rowptr[nrow] : 0;
+    const int32_t nend = has_next ? rowptr[nrow + 1] : 0;
     const bool virt = rowflag != nullptr && rowflag[row] != 0;
     const float elh = el[row * H + h_s];
     const float lseh = lse[row * H + h_s];
@@ -293,13 +303,14 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
       Ds += coef * wave_xor_sum<H>(t);
     }
     float del = 0.f;
+    float erv = start + e_s < end ? er[(int64_t)j0 * H + h_s] : 0.f;
     for (int32_t cs = start; cs < end; cs += G::CE) {
       const int32_t e = cs + e_s;
       const bool valid = e < end;
-      const int32_t j = valid ? col[e] : 0;
+      const int32_t j = j0;
       float pre = 0.f, att = 0.f, dropf = 0.f;
       if (valid) {
-        pre = elh + er[(int64_t)j * H + h_s];
+        pre = elh + erv;
         const float s = virt ? 0.f : lrelu(pre, slope);
         att = __expf(s - lseh);
         dropf = dropout_factor(dp, (uint64_t)e * H + h_s);
@@ -326,6 +337,9 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
           if (mine && (G::QPL == 1 || k == dsrc_k)) gsum = cand;
         }
       }
+      // prefetch after the gathers: they are not queued behind these loads
+      const int32_t j2 = e + 2 * G::CE < end ? col[e + 2 * G::CE] : 0;
+      const float ern = e + G::CE < end ? er[(int64_t)j1 * H + h_s] : 0.f;
       if (valid) {
         if (coef != 0.f) gsum += coef * expf(att * dropf);
         const float ds = att * (gsum * dropf - Ds);
@@ -334,9 +348,20 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
         attd[(int64_t)e * ld + h_s] = att * dropf;
         del += dev;
       }
+      j0 = j1;
+      j1 = j2;
+      erv = ern;
+    }
+    if (has_next) {
+      j0 = nstart + e_s < nend ? col[nstart + e_s] : 0;
+      j1 = nstart + G::CE + e_s < nend ? col[nstart + G::CE + e_s] : 0;
     }
     del = wave_xor_sum<H>(del);
     if (lane < H) d_el[row * H + lane] = del;
+    if (!has_next) break;
+    row = nrow;
+    start = nstart;
+    end = nend;
   }
 }
 
