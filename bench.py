@@ -78,7 +78,7 @@ def pmc_traffic(H, F, bf16=False, workload="syn100k"):
     import re
 
     pat = (re.compile(rf"edge_attn_fwd_kernelILi{H}ELi{F}EDF16b") if bf16 else
-           re.compile(rf"edge_attn_fwd_kernel<{H}, {F}(, float)?>"))
+           re.compile(rf"edge_attn_fwd_kernel<{H}, {F}(, float)?(, \d+)?>"))
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{workload}*",
                                               "pmc_summary.json")), reverse=True):
         try:
