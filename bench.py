@@ -106,6 +106,19 @@ def csc_bytes(m, e, H, F, n_chunks, s=4):
     return e * (8 + 8 * H + s * D) + m * (s * D + 4 * H) + 12 * n_chunks + 4 * (m + 1)
 
 
+def bwd_fused_bytes(n, m, e, H, F, n_chunks, s=4):
+    """Algorithmic bytes of msha_edge_attention_bwd_fused (its three launches):
+    row stats (dU, u, el, lse in; the 3H-float row record out); the column pass (per
+    CSC slot row + eid + the record gather + s*D dU gather + de write; per column hc,
+    er in, d_hc, d_er out; the chunk plan); the row sum (rowptr, de, d_el)."""
+    D = H * F
+    stats = n * (2 * s * D + 8 * H + 12 * H)
+    cols = e * (8 + 12 * H + s * D + 4 * H) + m * (2 * s * D + 8 * H) + 12 * n_chunks \
+        + 4 * (m + 1)
+    rsum = 4 * (n + 1) + e * 4 * H + n * 4 * H
+    return stats + cols + rsum
+
+
 def fwd_bytes(n, m, e, H, F, s=4):
     """Algorithmic bytes of one msha_edge_attention_fwd launch:
     rowptr + col + er gather + el + h gather (s*HF per edge) + u write + lse write;
@@ -430,12 +443,15 @@ def main():
         return dt_, k, len(events)
 
     def edge_kernels(lay, s):
-        """Rooflines of the three edge kernels of the step (HIP events, same run)."""
+        """Rooflines of the edge kernels of the step (HIP events, same run): the forward
+        and either the fused backward or bwd_rows + csc_aggregate."""
         nch = lay.graph._plan["n_chunks"]
         out = []
         for name, nbytes in (("msha_edge_attention_fwd", fwd_bytes(n, m, e, H, F, s)),
                              ("msha_edge_attention_bwd_rows", bwd_rows_bytes(n, m, e, H, F, s)),
-                             ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s))):
+                             ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s)),
+                             ("msha_edge_attention_bwd_fused",
+                              bwd_fused_bytes(n, m, e, H, F, nch, s))):
             key = name[len("msha_"):]
             if key not in lay.kernel_ms:
                 continue

@@ -199,6 +199,24 @@ MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat
                                 const void* table, void* out, float* out_x, void* ws,
                                 size_t ws_bytes, msha_stream_t stream);
 
+/* Fused backward of u = drop(att) @ hc alone (no v branch, no row coefficients):
+ * the same d_el, d_er, d_hc as msha_edge_attention_bwd_rows + msha_csc_aggregate,
+ * bitwise, from one pass over the CSC (the column owns hc_j, so dU_i . hc_j comes from
+ * the dU[i] gather the column pass makes anyway) plus two light row passes.
+ * Replaces the reference's autograd of Ablation.py:266-274 for that case.
+ * de (n_edges, heads) fp32: scratch (left holding de in CSR edge order).
+ * ws: msha_edge_attention_bwd_fused_workspace_size bytes.  Needs the CSC view with
+ * csc_eid. */
+MSHA_API size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph* g,
+                                                             int32_t heads, int32_t feat);
+MSHA_API int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads, int32_t feat,
+                                           int32_t dtype, const float* el, const float* er,
+                                           const void* hc, const float* lse, const void* u,
+                                           const void* dU, float neg_slope, float drop_p,
+                                           uint64_t seed, uint64_t offset, float* d_el,
+                                           float* d_er, void* d_hc, float* de, void* ws,
+                                           size_t ws_bytes, msha_stream_t stream);
+
 /* ----------------------------------------------- GraphAttentionLayer (GAL) --- */
 /* GAT.py:20-35 / Ablation.py:100-115.  The layer's score is constant along a row
  * (it concatenates h_i with itself), so its attention is mask/deg (uniform on

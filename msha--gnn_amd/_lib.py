@@ -66,6 +66,9 @@ SIGNATURES = {
                                           P, P]),
     "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32,
                                                F32, U64, U64, P, P, P, I32, P, P]),
+    "msha_edge_attention_bwd_fused_workspace_size": (SZ, [GP, I32, I32]),
+    "msha_edge_attention_bwd_fused": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, F32, F32,
+                                                U64, U64, P, P, P, P, P, SZ, P]),
     "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
     "msha_csc_aggregate": (C.c_int, [GP, I32, I32, I32, P, P, I32, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),

@@ -139,6 +139,49 @@ __device__ __forceinline__ Pk<T> pk_xor_add(Pk<T> a, int o) {
   return a;
 }
 
+// ---- buffer (descriptor) memory ops: 32-bit byte offsets, hardware range check ----
+// A lane whose offset is past the descriptor's byte count reads 0 and its store is
+// dropped, so "load or 0" and masked stores need no branch: the loop bodies stay
+// straight-line and the compiler's vmcnt waits stay exact (a divergent branch around
+// a load makes the count path-dependent and forces vmcnt(0)).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // offset of a masked lane (descriptors < 2 GiB)
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? bytes : 0, 0x00020000);
+}
+__device__ __forceinline__ float buf_f32(rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ int32_t buf_i32(rsrc_t r, uint32_t off) {
+  return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t buf_u8(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_store_f32(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ Pk<float> pk_load_buf(rsrc_t r, uint32_t off, float*) {
+  const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  Pk<float> p;
+  p.v[0] = __uint_as_float(x.x); p.v[1] = __uint_as_float(x.y);
+  p.v[2] = __uint_as_float(x.z); p.v[3] = __uint_as_float(x.w);
+  return p;
+}
+__device__ __forceinline__ Pk<bf16_t> pk_load_buf(rsrc_t r, uint32_t off, bf16_t*) {
+  const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  Pk<bf16_t> p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p.v[2 * i] = __uint_as_float(w[i] << 16);
+    p.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+  return p;
+}
+
 __device__ __forceinline__ float to_f32(float x) { return x; }
 __device__ __forceinline__ float to_f32(bf16_t x) { return (float)x; }
 template <typename T>

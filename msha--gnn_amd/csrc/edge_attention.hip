@@ -20,6 +20,9 @@
 // pass needs no second sweep over the gathered rows.
 #include "common.h"
 
+#ifndef COLS_EH
+#define COLS_EH 1
+#endif
 #ifndef FWD_EPL
 #define FWD_EPL 2
 #endif
@@ -485,6 +488,341 @@ __global__ void __launch_bounds__(1024) csc_combine_kernel(
   }
 }
 
+// ------------------------------------------------ fused backward (u only) ---
+// Column-major backward for u = drop(att) @ hc (no v branch, no row coefficients).
+// The row pass of the split backward gathers hc[j] only for g_ij = dU_i . hc_j and
+// the column pass gathers dU[i]; a column owns hc_j, so one pass over the CSC gets
+// g_ij from the dU[i] gather it does anyway: per edge one 16-B/lane gather instead
+// of two, and no (de, attd) record written and re-read.  Three launches:
+//   row_stats : rec_i = (el_i, lse_i, D_i = dU_i . u_i)  per head   (N x 3H fp32)
+//   cols      : d_hc[j] = sum attd_ij dU_i, d_er[j] = sum de_ij, de_ij -> edge order
+//   row_sum   : d_el[i] = sum_j de_ij                                (CSR order)
+// Every value is computed with the same operands in the same order as
+// edge_attn_bwd_rows + csc_aggregate: the results are bitwise identical.
+template <int H, int F, typename T>
+__global__ void __launch_bounds__(256) bwd_row_stats_kernel(
+    int64_t n_rows, const float* __restrict__ el, const float* __restrict__ lse,
+    const T* __restrict__ u, const T* __restrict__ dU, float* __restrict__ rec) {
+  using G = Geo<H, F, T>;
+  const int lane = lane_id();
+  const int h_s = lane % H;
+  const int dsrc_k = (h_s * G::QH) / 64;
+  const int dsrc_l = (h_s * G::QH) % 64;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = wave; row < n_rows; row += nwaves) {
+    float Ds = 0.f;
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      const int q = quad_of<G>(lane, k);
+      const float dp = pk_dot(pk_load(dU + row * G::D + G::V * q),
+                              pk_load(u + row * G::D + G::V * q));
+      const float dk = group_sum<G::QH>(dp);
+      const float cand = __shfl(dk, dsrc_l);
+      if (k == dsrc_k) Ds = cand;
+    }
+    if (lane < H) {
+      float* r = rec + row * 3 * H;
+      r[lane] = el[row * H + lane];
+      r[H + lane] = lse[row * H + lane];
+      r[2 * H + lane] = Ds;
+    }
+  }
+}
+
+template <int H, int F, typename T>
+__global__ void __launch_bounds__(256) bwd_cols_kernel(
+    const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
+    const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
+    const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid,
+    const uint8_t* __restrict__ rowflag, const float* __restrict__ rec,
+    const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
+    float slope, Dropout dp, float* __restrict__ de, T* __restrict__ d_hc,
+    float* __restrict__ d_er, float* __restrict__ part, float* __restrict__ part_x) {
+  using G = Geo<H, F, T>;
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;
+  const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
+  const int dsrc_k = (h_s * G::QH) / 64;
+  const int dsrc_l = (h_s * G::QH) % 64;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+
+  // software pipeline: the next chunk's plan entry during this chunk; CSC slot rows
+  // two slot-groups ahead, issued after each group's gathers
+  int64_t c = wave;
+  if (c >= n_chunks) return;
+  int32_t jc = chunk_col[c], s0 = chunk_start[c], s1 = chunk_end[c];
+  int32_t i0 = s0 + e_s < s1 ? csc_row[s0 + e_s] : 0;
+  int32_t i1 = s0 + G::CE + e_s < s1 ? csc_row[s0 + G::CE + e_s] : 0;
+  while (true) {
+    const int64_t nc = c + nwaves;
+    const bool has_next = nc < n_chunks;
+    const int32_t njc = has_next ? chunk_col[nc] : 0;
+    const int32_t ns0 = has_next ? chunk_start[nc] : 0;
+    const int32_t ns1 = has_next ? chunk_end[nc] : 0;
+    const bool whole = s0 == colptr[jc] && s1 == colptr[jc + 1];
+    const float erh = er[(int64_t)jc * H + h_s];
+    Pk<T> hcq[G::QPL], acc[G::QPL];
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      hcq[k] = pk_load(hc + (int64_t)jc * G::D + G::V * quad_of<G>(lane, k));
+      acc[k] = pk_zero<T>();
+    }
+    float xacc = 0.f;
+    for (int32_t cs = s0; cs < s1; cs += G::CE) {
+      const int32_t slot = cs + e_s;
+      const bool valid = slot < s1;
+      const int32_t i = i0;
+      const int64_t eid = valid ? (int64_t)csc_eid[slot] : 0;
+      float pre = 0.f, att = 0.f, dropf = 0.f, Dsi = 0.f;
+      bool virt = false;
+      if (valid) {
+        const float* r = rec + (int64_t)i * 3 * H;
+        virt = rowflag != nullptr && rowflag[i] != 0;
+        pre = r[h_s] + erh;
+        const float sv = virt ? 0.f : lrelu(pre, slope);
+        att = __expf(sv - r[H + h_s]);
+        Dsi = r[2 * H + h_s];
+        dropf = dropout_factor(dp, (uint64_t)eid * H + h_s);
+      }
+      const float wv = att * dropf;
+      const int nvalid = min(G::CE, (int)(s1 - cs));
+      float gsum = 0.f;
+#pragma unroll
+      for (int g = 0; g < G::CE; g += G::EPI) {
+        if (g >= nvalid) break;
+        const int ei = g + g_e;
+        const int32_t iq = __shfl(i, ei * H);
+        const bool mine = e_s >= g && e_s < g + G::EPI;
+        const int srcl = G::QPL == 1 ? ((e_s - g) & (G::EPI - 1)) * G::NQ + h_s * G::QH : dsrc_l;
+#pragma unroll
+        for (int k = 0; k < G::QPL; ++k) {
+          const int q = quad_of<G>(lane, k);
+          const float wq = __shfl(wv, ei * H + q / G::QH);
+          float t = 0.f;
+          if (ei < nvalid) {
+            const Pk<T> dUi = pk_load(dU + (int64_t)iq * G::D + G::V * q);
+            acc[k] = pk_fma(wq, dUi, acc[k]);
+            t = pk_dot(dUi, hcq[k]);
+          }
+          t = group_sum<G::QH>(t);
+          const float cand = __shfl(t, srcl);
+          if (mine && (G::QPL == 1 || k == dsrc_k)) gsum = cand;
+        }
+      }
+      const int32_t sl2 = slot + 2 * G::CE;
+      const int32_t i2 = sl2 < s1 ? csc_row[sl2] : 0;
+      if (valid) {
+        const float ds = att * (gsum * dropf - Dsi);
+        const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
+        de[eid * H + h_s] = dev;
+        xacc += dev;
+      }
+      i0 = i1;
+      i1 = i2;
+    }
+    if (has_next) {
+      const int32_t a0 = ns0 + e_s, a1 = ns0 + G::CE + e_s;
+      i0 = a0 < ns1 ? csc_row[a0] : 0;
+      i1 = a1 < ns1 ? csc_row[a1] : 0;
+    }
+    if (G::EPI > 1) {
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) acc[0] = pk_xor_add(acc[0], o);
+    }
+#pragma unroll
+    for (int k = 0; k < G::QPL; ++k) {
+      if (g_e != 0) continue;
+      const int q = quad_of<G>(lane, k);
+      if (whole) {
+        pk_store(d_hc + (int64_t)jc * G::D + G::V * q, acc[k]);
+      } else {
+        float* dst = part + c * G::D + G::V * q;
+#pragma unroll
+        for (int v = 0; v < G::V; v += 4)
+          *reinterpret_cast<float4*>(dst + v) =
+              make_float4(acc[k].v[v], acc[k].v[v + 1], acc[k].v[v + 2], acc[k].v[v + 3]);
+      }
+    }
+    xacc = wave_xor_sum<H>(xacc);
+    if (lane < H) (whole ? d_er + (int64_t)jc * H : part_x + c * H)[lane] = xacc;
+    if (!has_next) break;
+    c = nc;
+    jc = njc;
+    s0 = ns0;
+    s1 = ns1;
+  }
+}
+
+// Head-per-lane variant of the column pass for narrow heads (F * sizeof(T) <= 64 B):
+// lane = (slot e_s, head h_s) holds that head's F features of dU[i] (QH 16-B loads at
+// stride QH * 16 B; the edge's H lanes together cover its whole row), so the score,
+// the dot dU_i[h] . hc_j[h], the weight and the accumulation all stay in the lane: no
+// per-edge shuffles; the CE slot lanes are combined once per chunk.  Memory ops go
+// through buffer descriptors (masked lanes read 0 / drop their store), so the slot
+// loop is branch-free and its waits exact; two slot groups per trip, each group's
+// CSC rows loaded two groups ahead into the register it just consumed.
+// Needs every table below 2 GiB (msha_edge_attention_bwd_fused checks).
+template <int H, int F, typename T>
+__global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
+    const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
+    const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
+    const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid, int64_t n_edges,
+    const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ rec,
+    const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
+    float slope, Dropout dp, float* __restrict__ de, T* __restrict__ d_hc,
+    float* __restrict__ d_er, float* __restrict__ part, float* __restrict__ part_x) {
+  using G = Geo<H, F, T>;
+  constexpr int NV = G::QH;  // 16-B pieces per head
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const rsrc_t r_row = make_rsrc(csc_row, (uint32_t)(n_edges * 4));
+  const rsrc_t r_eid = make_rsrc(csc_eid, (uint32_t)(n_edges * 4));
+  const rsrc_t r_flag = make_rsrc(rowflag, (uint32_t)n_rows);
+  const rsrc_t r_rec = make_rsrc(rec, (uint32_t)(n_rows * 12 * H));
+  const rsrc_t r_dU = make_rsrc(dU, (uint32_t)(n_rows * G::D * sizeof(T)));
+  const rsrc_t r_de = make_rsrc(de, (uint32_t)(n_edges * 4 * H));
+  const uint32_t h_off = h_s * F * sizeof(T);
+
+  int64_t c = wave;
+  if (c >= n_chunks) return;
+  int32_t jc = chunk_col[c], s0 = chunk_start[c], s1 = chunk_end[c];
+  int32_t i0 = buf_i32(r_row, s0 + e_s < s1 ? (s0 + e_s) * 4u : kOOB);
+  int32_t i1 = buf_i32(r_row, s0 + G::CE + e_s < s1 ? (s0 + G::CE + e_s) * 4u : kOOB);
+  while (true) {
+    const int64_t nc = c + nwaves;
+    const bool has_next = nc < n_chunks;
+    const int32_t njc = has_next ? chunk_col[nc] : 0;
+    const int32_t ns0 = has_next ? chunk_start[nc] : 0;
+    const int32_t ns1 = has_next ? chunk_end[nc] : 0;
+    const bool whole = s0 == colptr[jc] && s1 == colptr[jc + 1];
+    const float erh = er[(int64_t)jc * H + h_s];
+    Pk<T> hcv[NV], acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      hcv[k] = pk_load(hc + (int64_t)jc * G::D + h_s * F + G::V * k);
+      acc[k] = pk_zero<T>();
+    }
+    float xacc = 0.f;
+    auto slot_group = [&](int32_t cs, int32_t i) {
+      const int32_t slot = cs + e_s;
+      const bool valid = slot < s1;
+      Pk<T> dUv[NV];
+      const uint32_t row_off = valid ? (uint32_t)i * (G::D * sizeof(T)) + h_off : kOOB;
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        dUv[k] = pk_load_buf(r_dU, row_off + (valid ? k * 16u : 0u), (T*)nullptr);
+      const int32_t eid = buf_i32(r_eid, valid ? slot * 4u : kOOB);
+      const uint32_t rec_off = valid ? (uint32_t)i * (12u * H) + h_s * 4u : kOOB;
+      const float r_el = buf_f32(r_rec, rec_off);
+      const float r_lse = buf_f32(r_rec, valid ? rec_off + 4u * H : kOOB);
+      const float Dsi = buf_f32(r_rec, valid ? rec_off + 8u * H : kOOB);
+      const bool virt = buf_u8(r_flag, valid ? (uint32_t)i : kOOB) != 0;
+      const float pre = r_el + erh;
+      const float sv = virt ? 0.f : lrelu(pre, slope);
+      const float att = __expf(sv - r_lse);
+      const float dropf = dropout_factor(dp, (uint64_t)eid * H + h_s);
+      const float wv = valid ? att * dropf : 0.f;
+      // dU_i[h] . hc_j[h] in group_sum's order over the head's pieces
+      float d[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        d[k] = pk_dot(dUv[k], hcv[k]);
+        acc[k] = pk_fma(wv, dUv[k], acc[k]);
+      }
+#pragma unroll
+      for (int o = 1; o < NV; o <<= 1)
+#pragma unroll
+        for (int k = 0; k < NV; k += 2 * o) d[k] = d[k] + d[k + o];
+      const float ds = att * (d[0] * dropf - Dsi);
+      const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
+      buf_store_f32(r_de, valid ? (uint32_t)eid * (4u * H) + h_s * 4u : kOOB, dev);
+      xacc += valid ? dev : 0.f;
+    };
+    for (int32_t cs = s0; cs < s1; cs += 2 * G::CE) {
+      slot_group(cs, i0);
+      const int32_t a0 = cs + 2 * G::CE + e_s;
+      i0 = buf_i32(r_row, a0 < s1 ? a0 * 4u : kOOB);
+      slot_group(cs + G::CE, i1);
+      const int32_t a1 = cs + 3 * G::CE + e_s;
+      i1 = buf_i32(r_row, a1 < s1 ? a1 * 4u : kOOB);
+    }
+    {
+      const int32_t a0 = ns0 + e_s, a1 = ns0 + G::CE + e_s;
+      i0 = buf_i32(r_row, a0 < ns1 ? a0 * 4u : kOOB);
+      i1 = buf_i32(r_row, a1 < ns1 ? a1 * 4u : kOOB);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int o = H; o < 64; o <<= 1) acc[k] = pk_xor_add(acc[k], o);
+    if (e_s == 0) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (whole) {
+          pk_store(d_hc + (int64_t)jc * G::D + h_s * F + G::V * k, acc[k]);
+        } else {
+          float* dst = part + c * G::D + h_s * F + G::V * k;
+#pragma unroll
+          for (int v = 0; v < G::V; v += 4)
+            *reinterpret_cast<float4*>(dst + v) =
+                make_float4(acc[k].v[v], acc[k].v[v + 1], acc[k].v[v + 2], acc[k].v[v + 3]);
+        }
+      }
+    }
+    xacc = wave_xor_sum<H>(xacc);
+    if (lane < H) (whole ? d_er + (int64_t)jc * H : part_x + c * H)[lane] = xacc;
+    if (!has_next) break;
+    c = nc;
+    jc = njc;
+    s0 = ns0;
+    s1 = ns1;
+  }
+}
+
+// d_el[i] = sum over the row's edges of de.  Lane = (row slot, head): 64/H rows per
+// wave, each lane walking its row's edges with independent loads.  The sum keeps
+// bwd_rows' order (lane e_s of a CE-edge chunk accumulates edges e_s, e_s + CE, ...;
+// then the xor tree over e_s), so the result is the same bits.
+template <int H>
+__global__ void __launch_bounds__(256) bwd_row_sum_kernel(
+    const int32_t* __restrict__ rowptr, int64_t n_rows, const float* __restrict__ de,
+    float* __restrict__ d_el) {
+  constexpr int CE = 64 / H;
+  const int lane = lane_id();
+  const int r_s = lane / H, h_s = lane % H;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r0 = wave * CE; r0 < n_rows; r0 += nwaves * CE) {
+    const int64_t row = r0 + r_s;
+    if (row >= n_rows) continue;
+    const int32_t start = rowptr[row], end = rowptr[row + 1];
+    float p[CE];
+#pragma unroll
+    for (int k = 0; k < CE; ++k) p[k] = 0.f;
+    for (int32_t cs = start; cs < end; cs += CE) {
+      float v[CE];
+#pragma unroll
+      for (int k = 0; k < CE; ++k)
+        v[k] = cs + k < end ? de[(int64_t)(cs + k) * H + h_s] : 0.f;
+#pragma unroll
+      for (int k = 0; k < CE; ++k)
+        if (cs + k < end) p[k] += v[k];
+    }
+    // the xor tree of wave_xor_sum<H> over the CE edge slots
+#pragma unroll
+    for (int o = 1; o < CE; o <<= 1) {
+#pragma unroll
+      for (int k = 0; k < CE; ++k)
+        if ((k & o) == 0 && (k & (2 * o - 1)) == 0) p[k] = p[k] + p[k + o];
+    }
+    d_el[row * H + h_s] = p[0];
+  }
+}
+
 // ------------------------------------------------------------------- dispatch ---
 // Compiled (heads, feat) set.  Extend here (and in msha_edge_attention_supported).
 #define MSHA_FOR_EACH_SHAPE(X) \
@@ -686,4 +1024,86 @@ extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t fe
   else
     launch_csc<float>(g, heads, feat, w, x, ld, table, out, out_x, part, part_x, s);
   return check_launch("csc_aggregate");
+}
+
+extern "C" size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph* g,
+                                                               int32_t heads, int32_t feat) {
+  if (g == nullptr || heads <= 0 || feat <= 0) return 0;
+  const size_t rec = ((size_t)g->n_rows * 3 * heads * sizeof(float) + 255) & ~(size_t)255;
+  return rec + msha_csc_aggregate_workspace_size(g, heads, feat);
+}
+
+template <typename T>
+static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const float* el,
+                             const float* er, const void* hc, const float* lse, const void* u,
+                             const void* dU, float neg_slope, const Dropout& dp, float* d_el,
+                             float* d_er, void* d_hc, float* de, float* rec, float* part,
+                             float* part_x, hipStream_t s) {
+  // the buffer-descriptor kernel addresses each table with 32-bit byte offsets
+  const int64_t lim = (int64_t)1 << 31;
+  const bool buf_ok = g->n_rows * (int64_t)heads * feat * (int64_t)sizeof(T) < lim &&
+                      g->n_edges * 4 * (int64_t)heads < lim && g->n_rows * 12 * heads < lim;
+#define X(h, f)                                                                                \
+  if (heads == h && feat == f) {                                                               \
+    if constexpr (f % Pk<T>::V == 0) {                                                         \
+      hipLaunchKernelGGL((bwd_row_stats_kernel<h, f, T>), wave_grid(g->n_rows), dim3(256), 0,  \
+                         s, g->n_rows, el, lse, (const T*)u, (const T*)dU, rec);               \
+      if (f * sizeof(T) <= 64 && COLS_EH && buf_ok)                                            \
+        hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \
+                           s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
+                           g->colptr, g->csc_row, g->csc_eid, g->n_edges, g->rowflag,          \
+                           g->n_rows, rec, er, (const T*)hc, (const T*)dU, neg_slope, dp, de,  \
+                           (T*)d_hc, d_er, part, part_x);                                      \
+      else                                                                                     \
+        hipLaunchKernelGGL((bwd_cols_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0,   \
+                           s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
+                           g->colptr, g->csc_row, g->csc_eid, g->rowflag, rec, er,             \
+                           (const T*)hc, (const T*)dU, neg_slope, dp, de, (T*)d_hc, d_er,      \
+                           part, part_x);                                                      \
+      hipLaunchKernelGGL((bwd_row_sum_kernel<h>), wave_grid(g->n_rows), dim3(256), 0, s,       \
+                         g->rowptr, g->n_rows, de, d_el);                                      \
+    }                                                                                          \
+  }
+  MSHA_FOR_EACH_SHAPE(X)
+#undef X
+  if (g->n_multi > 0) {
+    const int64_t D = (int64_t)heads * feat;
+    hipLaunchKernelGGL(csc_combine_kernel<T>, dim3(g->n_multi, (D + heads + 255) / 256),
+                       dim3(64 * kCombineWaves), 0, s, g->multi_col, g->multi_first,
+                       g->multi_count, g->n_multi, (int)D, heads, part, part_x, (T*)d_hc, d_er);
+  }
+}
+
+extern "C" int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads, int32_t feat,
+                                             int32_t dtype, const float* el, const float* er,
+                                             const void* hc, const float* lse, const void* u,
+                                             const void* dU, float neg_slope, float drop_p,
+                                             uint64_t seed, uint64_t offset, float* d_el,
+                                             float* d_er, void* d_hc, float* de, void* ws,
+                                             size_t ws_bytes, msha_stream_t stream) {
+  if (int rc = check_graph(g, true)) return rc;
+  MSHA_ARG_CHECK(el && er && hc && lse && u && dU && d_el && d_er && d_hc,
+                 "edge_attention_bwd_fused: null pointer");
+  MSHA_ARG_CHECK(g->n_edges == 0 || (de && g->csc_eid),
+                 "edge_attention_bwd_fused: needs de scratch and csc_eid");
+  MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_bwd_fused: p must be in [0,1]");
+  if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_fused: unsupported (heads, feat, dtype)");
+  MSHA_ARG_CHECK(ws != nullptr &&
+                     ws_bytes >= msha_edge_attention_bwd_fused_workspace_size(g, heads, feat),
+                 "edge_attention_bwd_fused: workspace too small");
+  const int64_t D = (int64_t)heads * feat;
+  float* rec = (float*)ws;
+  const size_t rec_bytes = ((size_t)g->n_rows * 3 * heads * sizeof(float) + 255) & ~(size_t)255;
+  float* part = (float*)((char*)ws + rec_bytes);
+  float* part_x = part + g->n_chunks * D;
+  const Dropout dp = make_dropout(drop_p, seed, offset);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MSHA_DTYPE_BF16)
+    launch_bwd_fused<bf16_t>(g, heads, feat, el, er, hc, lse, u, dU, neg_slope, dp, d_el, d_er,
+                             d_hc, de, rec, part, part_x, s);
+  else
+    launch_bwd_fused<float>(g, heads, feat, el, er, hc, lse, u, dU, neg_slope, dp, d_el, d_er,
+                            d_hc, de, rec, part, part_x, s);
+  return check_launch("edge_attention_bwd_fused");
 }

@@ -125,6 +125,8 @@ class _EdgeAttention(torch.autograd.Function):
         dV = _tc(dV, dt) if use_dv else None
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
+        if not use_dv and FUSED_BWD:
+            return _bwd_fused(ctx, el, er, hc, lse, u, dU, d_el, hs)
         # one (de, attd) record of 2H floats per edge: the column pass reads it as one
         # 64-B segment at C4 (the CSC visits edges in random order)
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)
@@ -147,6 +149,36 @@ class _EdgeAttention(torch.autograd.Function):
         if ctx.has_hs and d_hs is None:
             d_hs = torch.zeros_like(hs)
         return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None
+
+
+# u-only backward as one column pass (msha_edge_attention_bwd_fused) instead of
+# bwd_rows + csc_aggregate; same bits.  Module switch for A/B measurements.
+FUSED_BWD = True
+
+
+def _bwd_fused(ctx, el, er, hc, lse, u, dU, d_el, hs):
+    graph = ctx.graph
+    n, H = el.shape
+    m, _, F = hc.shape
+    dev = el.device
+    s = _stream(el)
+    g = graph.desc
+    if not graph.has_csc:
+        raise RuntimeError("graph has no CSC view (build it with_csc=True)")
+    de = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
+    wsb = int(_lib.load().msha_edge_attention_bwd_fused_workspace_size(g, H, F))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    d_hc = torch.empty(m, H, F, device=dev, dtype=hc.dtype)
+    d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
+    ev = _timed("edge_attention_bwd_fused")
+    _lib.call("msha_edge_attention_bwd_fused", g, H, F, _code(hc.dtype), el.data_ptr(),
+              er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
+              ctx.slope, ctx.p, ctx.seed, 0, d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
+              de.data_ptr(), ws.data_ptr(), wsb, s)
+    if ev is not None:
+        ev[1].record()
+    d_hs = torch.zeros_like(hs) if ctx.has_hs else None
+    return d_el, d_er, d_hc, d_hs, None, None, None, None
 
 
 def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream, ld=0):

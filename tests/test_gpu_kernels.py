@@ -156,6 +156,77 @@ def test_edge_attention_fwd_bwd(cuda, msha, case, p):
     tol_close(ths.grad.cpu().numpy(), bw["d_hs"], EMB_RTOL, 1e-5)
 
 
+def _u_only_grads(MF, graph, el, er, hc, dU, p, seed, dev, dtype, fused):
+    MF.FUSED_BWD = fused
+    try:
+        tel, ter = (t(x, dev).requires_grad_(True) for x in (el, er))
+        thc = t(hc, dev, dtype).requires_grad_(True)
+        u = MF.edge_attention(graph, tel, ter, thc, p=p, training=p > 0, seed=seed)
+        u.backward(t(dU, dev, dtype))
+        return u.detach(), tel.grad, ter.grad, thc.grad
+    finally:
+        MF.FUSED_BWD = True
+
+
+def _same_as_split(got, split, dtype=torch.float32):
+    """Fused vs split backward: the per-edge scores and their sums (u, d_el, d_er) are
+    the same bits; d_hc adds the same products in another order when the column pass
+    runs head-per-lane (narrow heads): within a few ulps of the split sum."""
+    for a, b, name in zip(got[:3], split[:3], ("u", "d_el", "d_er")):
+        assert torch.equal(a, b), (name, dtype)
+    a, b = got[3].float(), split[3].float()
+    # a reordered fp32 sum of many terms moves by a few ulps of the largest partial
+    # sums; a bf16 table may then round the other way (one bf16 ulp)
+    bound = 16 * 2.0 ** -23 * (b.abs() + b.abs().amax())
+    if dtype == torch.bfloat16:
+        bound = bound + 2.0 ** -7 * b.abs()
+    assert bool(((a - b).abs() <= bound).all()), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}m{c[1]}H{c[2]}F{c[3]}")
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_edge_attention_fused_backward(cuda, msha, case, p):
+    """u-only backward: msha_edge_attention_bwd_fused (one CSC pass) agrees with
+    bwd_rows + csc_aggregate (bitwise but for d_hc's summation order) and the oracle."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    n, m, H, F, max_deg, kw = case
+    rng = np.random.default_rng(n * 5 + H)
+    c, rowptr, col, empty, el, er, hc, hs, dU, dV = _edge_case(rng, n, m, H, F, max_deg, **kw)
+    graph = Graph.from_dense(t(c, cuda))
+    seed = 7
+    got = _u_only_grads(MF, graph, el, er, hc, dU, p, seed, cuda, torch.float32, True)
+    split = _u_only_grads(MF, graph, el, er, hc, dU, p, seed, cuda, torch.float32, False)
+    _same_as_split(got, split)
+    keep = _keep_mask(graph.n_edges, H, p, seed, cuda)
+    ref = O.edge_aggregate_fwd(rowptr, col, el, er, hc, keep=keep, p=p, rowflag=empty)
+    bw = O.edge_aggregate_bwd(rowptr, col, ref, hc, dU, keep=keep, p=p)
+    tol_close(got[1].cpu().numpy(), bw["d_el"], 1e-4, 1e-5)
+    tol_close(got[2].cpu().numpy(), bw["d_er"], 1e-4, 1e-5)
+    tol_close(got[3].cpu().numpy(), bw["d_hc"], EMB_RTOL, 1e-5)
+
+
+def test_edge_attention_fused_backward_bf16_multichunk(cuda, msha):
+    """bf16 tables and the full 2015 graph's multi-chunk columns: fused == split."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    g, c = _r15_counts()
+    rng = np.random.default_rng(11)
+    n, m, H, F = int(g["n"]), 32, 2, 64
+    graph = Graph.from_dense(t(c, cuda))
+    assert graph._plan["n_multi"] > 0
+    el = rng.standard_normal((n, H)).astype(np.float32)
+    er = rng.standard_normal((m, H)).astype(np.float32)
+    hc = rng.standard_normal((m, H, F)).astype(np.float32)
+    dU = rng.standard_normal((n, H, F)).astype(np.float32)
+    for dtype in (torch.float32, torch.bfloat16):
+        got = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True)
+        split = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, False)
+        _same_as_split(got, split, dtype)
+
+
 def test_edge_attention_weights_exported(cuda):
     """attd output of the forward vs oracle attention (absolute 1e-5)."""
     from msha_gnn_amd import _lib
