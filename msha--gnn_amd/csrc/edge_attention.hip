@@ -499,33 +499,47 @@ __global__ void __launch_bounds__(1024) csc_combine_kernel(
 //   row_sum   : d_el[i] = sum_j de_ij                                (CSR order)
 // Every value is computed with the same operands in the same order as
 // edge_attn_bwd_rows + csc_aggregate: the results are bitwise identical.
+// Row statistics: RPW rows per wave trip (EPI rows per load instruction, all loads of
+// the trip issued before the first use), D_i = dU_i . u_i per head in group_sum order.
 template <int H, int F, typename T>
 __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
     int64_t n_rows, const float* __restrict__ el, const float* __restrict__ lse,
     const T* __restrict__ u, const T* __restrict__ dU, float* __restrict__ rec) {
   using G = Geo<H, F, T>;
+  constexpr int UNR = G::QPL == 1 ? 4 : 1;        // load groups per trip
+  constexpr int RPW = G::EPI * UNR;               // rows per trip
   const int lane = lane_id();
-  const int h_s = lane % H;
-  const int dsrc_k = (h_s * G::QH) / 64;
-  const int dsrc_l = (h_s * G::QH) % 64;
+  const int r_s = G::QPL == 1 ? lane / G::NQ : 0;  // row slot of this lane in a group
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t row = wave; row < n_rows; row += nwaves) {
-    float Ds = 0.f;
+  for (int64_t r0 = wave * RPW; r0 < n_rows; r0 += nwaves * RPW) {
+    Pk<T> a[UNR][G::QPL], b[UNR][G::QPL];
 #pragma unroll
-    for (int k = 0; k < G::QPL; ++k) {
-      const int q = quad_of<G>(lane, k);
-      const float dp = pk_dot(pk_load(dU + row * G::D + G::V * q),
-                              pk_load(u + row * G::D + G::V * q));
-      const float dk = group_sum<G::QH>(dp);
-      const float cand = __shfl(dk, dsrc_l);
-      if (k == dsrc_k) Ds = cand;
+    for (int g = 0; g < UNR; ++g) {
+      const int64_t row = min(r0 + g * G::EPI + r_s, n_rows - 1);
+#pragma unroll
+      for (int k = 0; k < G::QPL; ++k) {
+        const int q = quad_of<G>(lane, k);
+        a[g][k] = pk_load(dU + row * G::D + G::V * q);
+        b[g][k] = pk_load(u + row * G::D + G::V * q);
+      }
     }
-    if (lane < H) {
-      float* r = rec + row * 3 * H;
-      r[lane] = el[row * H + lane];
-      r[H + lane] = lse[row * H + lane];
-      r[2 * H + lane] = Ds;
+#pragma unroll
+    for (int g = 0; g < UNR; ++g) {
+      const int64_t row = r0 + g * G::EPI + r_s;
+#pragma unroll
+      for (int k = 0; k < G::QPL; ++k) {
+        const int q = quad_of<G>(lane, k);
+        const float dk = group_sum<G::QH>(pk_dot(a[g][k], b[g][k]));
+        // the head's first chunk lane writes D; el and lse ride along
+        if (q % G::QH == 0 && row < n_rows) {
+          const int h = q / G::QH;
+          float* r = rec + row * 3 * H;
+          r[h] = el[row * H + h];
+          r[H + h] = lse[row * H + h];
+          r[2 * H + h] = dk;
+        }
+      }
     }
   }
 }
@@ -1046,7 +1060,7 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
 #define X(h, f)                                                                                \
   if (heads == h && feat == f) {                                                               \
     if constexpr (f % Pk<T>::V == 0) {                                                         \
-      hipLaunchKernelGGL((bwd_row_stats_kernel<h, f, T>), wave_grid(g->n_rows), dim3(256), 0,  \
+      hipLaunchKernelGGL((bwd_row_stats_kernel<h, f, T>), wave_grid(g->n_rows / 8 + 1), dim3(256), 0,  \
                          s, g->n_rows, el, lse, (const T*)u, (const T*)dU, rec);               \
       if (f * sizeof(T) <= 64 && COLS_EH && buf_ok)                                            \
         hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \

@@ -467,7 +467,7 @@ static bool vec_ok(const GemmArgs& p) {
 // each row group strides the block's rows with 16-byte loads; the row groups are
 // added in a fixed LDS tree, and a second pass adds the block partials in block
 // order (deterministic).
-constexpr int kColsumRows = 64;
+constexpr int kColsumRows = 128;
 
 // N consecutive elements of one row, widened to fp32
 template <int N>
