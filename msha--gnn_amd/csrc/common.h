@@ -163,15 +163,18 @@ __device__ __forceinline__ uint32_t buf_u8(rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void buf_store_f32(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
-__device__ __forceinline__ Pk<float> pk_load_buf(rsrc_t r, uint32_t off, float*) {
-  const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+__device__ __forceinline__ u32x4_t buf_b128(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+// 16 raw bytes -> fp32 lanes (kept raw in registers while in flight: a bf16 piece
+// widens only at its use, so a batch of loads costs 4 VGPRs each)
+__device__ __forceinline__ Pk<float> pk_from_raw(u32x4_t x, float*) {
   Pk<float> p;
   p.v[0] = __uint_as_float(x.x); p.v[1] = __uint_as_float(x.y);
   p.v[2] = __uint_as_float(x.z); p.v[3] = __uint_as_float(x.w);
   return p;
 }
-__device__ __forceinline__ Pk<bf16_t> pk_load_buf(rsrc_t r, uint32_t off, bf16_t*) {
-  const u32x4_t x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+__device__ __forceinline__ Pk<bf16_t> pk_from_raw(u32x4_t x, bf16_t*) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
   Pk<bf16_t> p;
 #pragma unroll
@@ -180,6 +183,12 @@ __device__ __forceinline__ Pk<bf16_t> pk_load_buf(rsrc_t r, uint32_t off, bf16_t
     p.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
   return p;
+}
+__device__ __forceinline__ Pk<float> pk_load_buf(rsrc_t r, uint32_t off, float* t) {
+  return pk_from_raw(buf_b128(r, off), t);
+}
+__device__ __forceinline__ Pk<bf16_t> pk_load_buf(rsrc_t r, uint32_t off, bf16_t* t) {
+  return pk_from_raw(buf_b128(r, off), t);
 }
 
 __device__ __forceinline__ float to_f32(float x) { return x; }

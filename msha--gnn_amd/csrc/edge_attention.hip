@@ -18,6 +18,8 @@
 // (row, head); the backward recomputes the attention from it and uses
 // sum_e att_e * g_e = dU_i . u_i (FlashAttention's "D" identity), so the row
 // pass needs no second sweep over the gathered rows.
+#include <stdlib.h>
+
 #include "common.h"
 
 #ifndef COLS_EH
@@ -194,6 +196,145 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     end = nend;
     virt = nvirt;
     elh = nelh;
+  }
+}
+
+// ------------------------------------------------------ forward, batched gathers ---
+// Rows of at most 64 16-byte pieces (QPL == 1: every C4/R15 shape).  The same values in
+// the same order as edge_attn_fwd_kernel (bitwise-identical u / lse), but every memory
+// op of the chunk loop goes through a buffer descriptor (a masked lane reads 0), so the
+// loop body is straight-line: the NGI gathers of a chunk leave back to back before the
+// chunk's scores are reduced, and the compiler's vmcnt waits count them down instead of
+// draining after each one (a divergent branch around a load forces vmcnt(0), which
+// serialised the gathers of edge_attn_fwd_kernel to one in flight per wave).
+// Issue order per chunk c: gathers(c), er(c+1), col(c+2); the softmax of c uses er(c),
+// issued a chunk earlier, so it runs while the gathers are in flight.
+// Row bounds are wave-uniform (readfirstlane): scalar loads and scalar loop control.
+// Needs every table below 2 GiB (the dispatcher checks and otherwise runs the above).
+#ifndef FWD_WPE
+#define FWD_WPE 1
+#endif
+template <int H, int F, typename T, int EPL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
+edge_attn_fwd_bat_kernel(
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
+    const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
+    float slope, Dropout dp, T* __restrict__ u, float* __restrict__ lse,
+    float* __restrict__ attd) {
+  using G = Geo<H, F, T>;
+  static_assert(G::QPL == 1, "batched forward: one 16-byte piece per lane");
+  constexpr int CEL = EPL * G::CE;    // edges per chunk
+  constexpr int NGI = CEL / G::EPI;   // gather instructions per chunk
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;
+  const int g_e = lane / G::NQ, q = lane % G::NQ;
+  const rsrc_t r_col = make_rsrc(col, (uint32_t)n_edges * 4u);
+  const rsrc_t r_er = make_rsrc(er, (uint32_t)n_cols * (4u * H));
+  const rsrc_t r_hc = make_rsrc(hc, (uint32_t)n_cols * (uint32_t)(G::D * sizeof(T)));
+  const uint32_t q_off = 16u * q;
+  const int wave0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  const int nwaves = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
+
+  for (int row = wave0; row < n_rows; row += nwaves) {
+    const int32_t start = __builtin_amdgcn_readfirstlane(rowptr[row]);
+    const int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
+    const bool virt = rowflag != nullptr && rowflag[row] != 0;
+    const float elh = el[(int64_t)row * H + h_s];
+    int32_t j0[EPL], j1[EPL];
+    float erv[EPL];
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      const int32_t e0 = start + t * G::CE + e_s, e1 = e0 + CEL;
+      j0[t] = buf_i32(r_col, e0 < end ? (uint32_t)e0 * 4u : kOOB);
+      j1[t] = buf_i32(r_col, e1 < end ? (uint32_t)e1 * 4u : kOOB);
+    }
+#pragma unroll
+    for (int t = 0; t < EPL; ++t)
+      erv[t] = buf_f32(r_er, start + t * G::CE + e_s < end
+                                 ? (uint32_t)j0[t] * (4u * H) + 4u * h_s : kOOB);
+    float m = -INFINITY, l = 0.f;
+    Pk<T> acc = pk_zero<T>();
+    for (int32_t cs = start; cs < end; cs += CEL) {
+      const int nvalid = min(CEL, (int)(end - cs));
+      // (1) this chunk's gathers, all in flight together
+      u32x4_t raw[NGI];
+#pragma unroll
+      for (int gi = 0; gi < NGI; ++gi) {
+        const int g = gi * G::EPI;
+        const int t = g / G::CE;
+        const int ei = g % G::CE + g_e;
+        const int32_t jq = __shfl(j0[t], ei * H);
+        raw[gi] = buf_b128(r_hc, g + g_e < nvalid
+                                     ? (uint32_t)jq * (uint32_t)(G::D * sizeof(T)) + q_off
+                                     : kOOB);
+      }
+      // (2) er one chunk ahead, col two chunks ahead
+      float ern[EPL];
+      int32_t j2[EPL];
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const int32_t e1 = cs + CEL + t * G::CE + e_s, e2 = e1 + CEL;
+        ern[t] = buf_f32(r_er, e1 < end ? (uint32_t)j1[t] * (4u * H) + 4u * h_s : kOOB);
+        j2[t] = buf_i32(r_col, e2 < end ? (uint32_t)e2 * 4u : kOOB);
+      }
+      // (3) the chunk's online softmax (score layout), while the gathers fly
+      float sc[EPL], smax = -INFINITY;
+      bool valid[EPL];
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        valid[t] = cs + t * G::CE + e_s < end;
+        sc[t] = valid[t] ? (virt ? 0.f : lrelu(elh + erv[t], slope)) : -INFINITY;
+        smax = fmaxf(smax, sc[t]);
+      }
+      const float mn = fmaxf(m, wave_xor_max<H>(smax));
+      const float alpha = __expf(m - mn);
+      float w[EPL], psum = 0.f;
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const float pe = valid[t] ? __expf(sc[t] - mn) : 0.f;
+        psum += pe;
+        w[t] = valid[t] ? pe * dropout_factor(dp, (uint64_t)(cs + t * G::CE + e_s) * H + h_s)
+                        : 0.f;
+      }
+      l = fmaf(l, alpha, wave_xor_sum<H>(psum));
+      m = mn;
+      acc = pk_scale(acc, __shfl(alpha, q / G::QH));
+      // (4) accumulate in gather order (masked lanes carry w = 0 and a zero row)
+#pragma unroll
+      for (int gi = 0; gi < NGI; ++gi) {
+        const int g = gi * G::EPI;
+        const int t = g / G::CE;
+        const int ei = g % G::CE + g_e;
+        const float wq = __shfl(w[t], ei * H + q / G::QH);
+        acc = pk_fma(wq, pk_from_raw(raw[gi], (T*)nullptr), acc);
+      }
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        j0[t] = j1[t];
+        j1[t] = j2[t];
+        erv[t] = ern[t];
+      }
+    }
+    if (G::EPI > 1) {
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) acc = pk_xor_add(acc, o);
+    }
+    const float lk = __shfl(l, q / G::QH);
+    const float inv = lk > 0.f ? 1.f / lk : 0.f;
+    if (g_e == 0) pk_store(u + (int64_t)row * G::D + G::V * q, pk_scale(acc, inv));
+    const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
+    if (lane < H) lse[(int64_t)row * H + lane] = lse_h;
+    if (attd != nullptr) {
+      for (int32_t cs = start; cs < end; cs += G::CE) {
+        const int32_t e = cs + e_s;
+        if (e < end) {
+          const float sv = virt ? 0.f : lrelu(elh + er[(int64_t)col[e] * H + h_s], slope);
+          attd[(int64_t)e * H + h_s] =
+              __expf(sv - lse_h) * dropout_factor(dp, (uint64_t)e * H + h_s);
+        }
+      }
+    }
   }
 }
 
@@ -860,6 +1001,12 @@ static bool shape_supported(int H, int F) {
   return false;
 }
 
+// integer tuning knob from the environment (A/B measurements; default = shipped choice)
+static int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return v != nullptr && *v ? atoi(v) : def;
+}
+
 // one wave per row (or chunk), 4 waves per block; grid-stride beyond the cap
 static dim3 wave_grid(int64_t items) { return dim3(grid_for(items, 4, 1 << 20)); }
 
@@ -901,6 +1048,35 @@ extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: unsupported (heads, feat, dtype)");
   const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
+  // batched-gather kernel: one piece per lane and every table addressable by 32-bit offsets
+  const int64_t lim = (int64_t)1 << 31;
+  const int64_t esz = dtype == MSHA_DTYPE_BF16 ? 2 : 4;
+  const bool bat = env_int("MSHA_FWD_BAT", 1) != 0 && (int64_t)heads * feat * esz <= 1024 &&
+                   g->n_rows < lim && g->n_edges * 4 < lim && g->n_cols * 4 * heads < lim &&
+                   g->n_cols * heads * feat * esz < lim;
+  if (bat) {
+    const int64_t cap = env_int("MSHA_FWD_WAVES", 0);
+    const dim3 grid = wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
+#define XB(h, f)                                                                               \
+    if (heads == h && feat == f) {                                                             \
+      if (dtype == MSHA_DTYPE_BF16) {                                                          \
+        if constexpr (f % 8 == 0 && h * f * 2 <= 1024)                                         \
+          hipLaunchKernelGGL((edge_attn_fwd_bat_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>()>), \
+                             grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,             \
+                             (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,  \
+                             er, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u, lse, attd);     \
+      } else {                                                                                 \
+        if constexpr (h * f * 4 <= 1024)                                                       \
+          hipLaunchKernelGGL((edge_attn_fwd_bat_kernel<h, f, float, fwd_epl<h, f, float>()>),  \
+                             grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,             \
+                             (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,  \
+                             er, (const float*)hc, neg_slope, dp, (float*)u, lse, attd);       \
+      }                                                                                        \
+    }
+    MSHA_FOR_EACH_SHAPE(XB)
+#undef XB
+    return check_launch("edge_attention_fwd");
+  }
 #define X(h, f)                                                                                \
   if (heads == h && feat == f) {                                                               \
     if (dtype == MSHA_DTYPE_BF16) {                                                            \
