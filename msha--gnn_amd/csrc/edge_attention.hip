@@ -28,6 +28,9 @@
 #ifndef FWD_EPL
 #define FWD_EPL 2
 #endif
+#ifndef FWD_EPL_BF16
+#define FWD_EPL_BF16 2
+#endif
 
 namespace msha {
 
@@ -991,7 +994,7 @@ __global__ void __launch_bounds__(256) bwd_row_sum_kernel(
 template <int H, int F, typename T>
 constexpr int fwd_epl() {
   using G = Geo<H, F, T>;
-  return (G::QPL == 1 && G::CE <= 16) ? FWD_EPL : 1;
+  return (G::QPL == 1 && G::CE <= 16) ? (sizeof(T) == 2 ? FWD_EPL_BF16 : FWD_EPL) : 1;
 }
 
 static bool shape_supported(int H, int F) {
