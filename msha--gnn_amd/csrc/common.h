@@ -256,6 +256,17 @@ __device__ __forceinline__ float dropout_factor(const Dropout& d, uint64_t idx) 
   return philox_x(d.seed, dropout_offset(d, d.offset), idx) >= d.threshold ? d.scale : 0.f;
 }
 
+// skinny.hip: resident-W projection and whole-tile weight gradient (1 = launched,
+// 0 = shape not covered: the caller runs its tiled GEMM)
+template <typename T>
+int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, const void* W,
+                   const float* al, const float* ar, void* h, float* el, float* er,
+                   hipStream_t s);
+int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
+                 const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
+                 int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
+                 const float* a, const float* de2, const float* a2, hipStream_t s);
+
 inline int grid_for(int64_t work_items, int per_block, int cap = 1 << 20) {
   int64_t g = (work_items + per_block - 1) / per_block;
   if (g < 1) g = 1;

@@ -642,6 +642,10 @@ static void launch_ho(const GemmArgs& p, int splits, hipStream_t s) {
 static int gemm_run(GemmArgs& p, int ho, float beta, int32_t splits, void* ws, size_t ws_bytes,
                     hipStream_t s) {
   const int64_t M = p.M, N = p.N, K = p.K;
+  if (ho != HO_A && p.slab == nullptr &&
+      skinny_wgrad(M, N, K, p.A, p.sAm, p.sAk, p.B, p.sBk, p.sBn, p.C, p.ldc, beta, splits, ws,
+                   ws_bytes, p.hH, p.hF, ho == HO_B ? p.de : nullptr, p.ha, p.de2, p.ha2, s))
+    return check_launch("gemm_f32");
   auto go = [&](int used) {
     if (ho == HO_A) launch_ho<HO_A>(p, used, s);
     else if (ho == HO_B) launch_ho<HO_B>(p, used, s);
@@ -727,6 +731,8 @@ extern "C" int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t 
   p.C = h; p.ldc = N;
   p.al = al; p.ar = ar; p.el = el; p.er = er; p.H = heads;
   hipStream_t s = (hipStream_t)stream;
+  if (skinny_project<float>(M, K, heads, feat, X, W, al, ar, h, el, er, s))
+    return check_launch("project_scores");
   if (al == nullptr && ar == nullptr) {
     launch<A_STRIDED, EPI_STORE, 0>(p, 1, s);
   } else if (feat == 4) {

@@ -476,6 +476,8 @@ extern "C" int msha_project_scores_bf16(int64_t M, int64_t K, int32_t heads, int
   p.C = h; p.ldc = N; p.c_bf16 = 1;
   p.al = al; p.ar = ar; p.el = el; p.er = er; p.H = heads;
   hipStream_t s = (hipStream_t)stream;
+  if (skinny_project<bf16_t>(M, K, heads, feat, X, W, al, ar, h, el, er, s))
+    return check_launch("project_scores_bf16");
   if (al == nullptr && ar == nullptr) {
     launch<EPI_STORE, 0, HO_NONE>(p, true, false, 1, s);
   } else {

@@ -1,0 +1,476 @@
+// Skinny projections of the hot path on the gfx950 matrix cores.
+//
+// Reference: Ablation.py:262-263 (h1 = R @ W1, h2 = S @ W2), GAT.py:21 (h = x @ W):
+// a tall node table (100k+ rows) times a small weight (K, N <= 128), and the weight
+// gradient dW = X^T (dh + de (x) a) of the same product, a reduction over all rows.
+// The tiled GEMMs of gemm.hip / gemm_bf16.hip re-stage W through LDS for every
+// 128-row tile behind two block barriers per k-stage; these kernels keep the skinny
+// operand resident instead:
+//
+//   proj_kernel   W sits in LDS for the whole (persistent) block; each wave streams
+//                 16-row tiles of X straight from HBM into MFMA A registers (the next
+//                 tile's loads in flight during this tile's MFMAs) and runs with no
+//                 block barrier after the W load.  The k order of a lane's A values
+//                 is permuted (lane group g takes k = g*K/4 + s at step s) so each lane
+//                 reads K/4 contiguous elements of its row with 16-byte loads; W's LDS
+//                 image is laid out in the same permuted order.
+//   wgrad_kernel  one wave accumulates the whole 128 x 128 dW of its row range in 256
+//                 accumulator registers with v_mfma_f32_32x32x2_f32: per two rows a
+//                 lane loads one float4 of X and one of dh (+ de (x) a folded in), whose
+//                 4 elements feed 4 row (column) blocks, so the operands need no LDS at
+//                 all; the 4 waves of a block add their tiles in LDS in wave order and
+//                 the block writes one partial, reduced over blocks in block order.
+//
+// Both are deterministic (fixed summation orders); numerics are the fp32 MFMA's exact
+// fma chain (fp32) or fp32 accumulation of bf16 products (bf16).
+#include <cstring>
+
+#include "common.h"
+
+namespace msha {
+namespace sk {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kProjWaves = 8;  // 2 waves per SIMD
+
+template <typename T, int K, int N>
+struct ProjGeo {
+  static constexpr bool F32 = sizeof(T) == 4;
+  static constexpr int NB = N / 16;                    // 16-column MFMA blocks
+  static constexpr int KL = K / 4;                     // k per lane group (g = lane >> 4)
+  static constexpr int NLD = KL * (int)sizeof(T) / 16; // 16-B A loads per lane per tile
+  static constexpr int S = F32 ? KL : KL / 8;          // MFMA steps per tile
+  // W image: fp32 [k'][n] with k' = 4 s + g (pitch N + 16: the 4 groups' rows of a read
+  // sit 16 banks apart); bf16 [n][k] (pitch K + 8 elements, one ds_read_b128 per lane)
+  static constexpr int PW = F32 ? N + 16 : K + 8;
+  static constexpr int WROWS = F32 ? K : N;
+  static constexpr int WBYTES = WROWS * PW * (int)sizeof(T);
+  static constexpr int TPS = N + 4;                    // fp32 staging pitch of a tile
+  static constexpr int SBYTES = 16 * TPS * 4;
+  static constexpr int EPL = 16 / (int)sizeof(T);      // output elements per lane store
+  static constexpr int LPR = N / EPL;                  // lanes per output row
+  static constexpr int RPP = 64 / LPR;                 // rows per store pass
+  static_assert(K % 64 == 0 && N % 16 == 0 && N <= 128 && K <= 128, "skinny projection shape");
+  static_assert(64 % LPR == 0, "a row must map onto whole lanes");
+};
+
+template <typename T, int K, int N, int FE>
+__global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
+    int M, const T* __restrict__ X, const T* __restrict__ W, const float* __restrict__ al,
+    const float* __restrict__ ar, T* __restrict__ h, float* __restrict__ el,
+    float* __restrict__ er, int H) {
+  using G = ProjGeo<T, K, N>;
+  __shared__ __attribute__((aligned(16))) char smem[G::WBYTES + kProjWaves * G::SBYTES];
+  T* Wl = reinterpret_cast<T*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // ---- W -> LDS once per block
+  if (G::F32) {
+    for (int idx = tid; idx < K * N / 4; idx += 64 * kProjWaves) {
+      const int k = idx / (N / 4), n4 = idx % (N / 4);
+      const float4 v = *reinterpret_cast<const float4*>(W + k * N + 4 * n4);
+      const int kr = 4 * (k % G::KL) + k / G::KL;
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(Wl) + kr * G::PW + 4 * n4) = v;
+    }
+  } else {
+    for (int idx = tid; idx < K * N / 8; idx += 64 * kProjWaves) {
+      const int k = idx / (N / 8), n8 = idx % (N / 8);
+      const uint4 v = *reinterpret_cast<const uint4*>(W + k * N + 8 * n8);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+      uint16_t* Wt = reinterpret_cast<uint16_t*>(Wl);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        Wt[(8 * n8 + e) * G::PW + k] = (uint16_t)(wv[e >> 1] >> (16 * (e & 1)));
+    }
+  }
+  __syncthreads();
+
+  float* Tw = reinterpret_cast<float*>(smem + G::WBYTES) + w * 16 * G::TPS;
+  const int cl = (lane % G::LPR) * G::EPL;  // first output column of this lane
+  float alv[G::EPL], arv[G::EPL];
+#pragma unroll
+  for (int u = 0; u < G::EPL; ++u) {
+    alv[u] = FE > 0 && al != nullptr ? al[cl + u] : 0.f;
+    arv[u] = FE > 0 && ar != nullptr ? ar[cl + u] : 0.f;
+  }
+
+  // tiles: the first pass of waves covers every SIMD once (wave w & 3 of each block)
+  // before any SIMD takes a second wave's share, so the tail tiles spread out
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kProjWaves;
+  const int tiles = (M + 15) / 16;
+  if (gw >= tiles) return;
+
+  auto load_tile = [&](int t, u32x4_t* raw) {
+    const int row = min(t * 16 + r16, M - 1);
+    const T* p = X + (int64_t)row * K + g * G::KL;
+#pragma unroll
+    for (int i = 0; i < G::NLD; ++i) raw[i] = *reinterpret_cast<const u32x4_t*>(p + i * G::EPL);
+  };
+  // one tile: MFMAs over the resident W (B operands of step s + 1 read from LDS while
+  // step s's MFMAs issue), then the epilogue
+  auto tile = [&](int t, const u32x4_t* cur) {
+    f32x4 acc[G::NB];
+#pragma unroll
+    for (int c = 0; c < G::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (G::F32) {
+      const float* Wf = reinterpret_cast<const float*>(Wl) + g * G::PW + r16;
+      float bc[G::NB], bn[G::NB];
+#pragma unroll
+      for (int c = 0; c < G::NB; ++c) bc[c] = Wf[c * 16];
+#pragma unroll
+      for (int s = 0; s < G::S; ++s) {
+        if (s + 1 < G::S) {
+#pragma unroll
+          for (int c = 0; c < G::NB; ++c) bn[c] = Wf[4 * (s + 1) * G::PW + c * 16];
+        }
+        // keep step s + 1's LDS reads ahead of step s's MFMAs (the scheduler would
+        // otherwise sink each read to just before its MFMA and wait on it there)
+        __builtin_amdgcn_sched_barrier(0);
+        const float a = __uint_as_float(cur[s >> 2][s & 3]);
+#pragma unroll
+        for (int c = 0; c < G::NB; ++c)
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < G::NB; ++c) bc[c] = bn[c];
+      }
+    } else {
+      const bf16_t* Wb = reinterpret_cast<const bf16_t*>(Wl) + r16 * G::PW + g * G::KL;
+      bf16x8 bc[G::NB], bn[G::NB];
+#pragma unroll
+      for (int c = 0; c < G::NB; ++c) bc[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW);
+#pragma unroll
+      for (int s = 0; s < G::S; ++s) {
+        if (s + 1 < G::S) {
+#pragma unroll
+          for (int c = 0; c < G::NB; ++c)
+            bn[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW + 8 * (s + 1));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, cur[s]);
+#pragma unroll
+        for (int c = 0; c < G::NB; ++c)
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bc[c], acc[c], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < G::NB; ++c) bc[c] = bn[c];
+      }
+    }
+    // ---- epilogue: stage the 16 x N tile (MFMA C layout: col = lane & 15, row =
+    // 4 (lane >> 4) + reg), then whole-row segments per wave store + score dots
+#pragma unroll
+    for (int c = 0; c < G::NB; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * G::TPS + c * 16 + r16] = acc[c][i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pass = 0; pass < 16 / G::RPP; ++pass) {
+      const int rr = pass * G::RPP + lane / G::LPR;
+      const int row = t * 16 + rr;
+      float e[G::EPL];
+#pragma unroll
+      for (int u = 0; u < G::EPL; u += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(Tw + rr * G::TPS + cl + u);
+        e[u] = v.x; e[u + 1] = v.y; e[u + 2] = v.z; e[u + 3] = v.w;
+      }
+      if (row < M) {
+        if constexpr (G::F32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(h) + (int64_t)row * N + cl) =
+              make_float4(e[0], e[1], e[2], e[3]);
+        } else {
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(h) + (int64_t)row * N + cl) =
+              make_uint4(pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]),
+                         pack_bf16x2(e[4], e[5]), pack_bf16x2(e[6], e[7]));
+        }
+      }
+      if constexpr (FE > 0) {
+        float sl = 0.f, sr = 0.f;
+#pragma unroll
+        for (int u = 0; u < G::EPL; ++u) {
+          sl = fmaf(e[u], alv[u], sl);
+          sr = fmaf(e[u], arv[u], sr);
+        }
+#pragma unroll
+        for (int o = 1; o < FE / G::EPL; o <<= 1) {
+          sl += __shfl_xor(sl, o);
+          sr += __shfl_xor(sr, o);
+        }
+        if (cl % FE == 0 && row < M) {
+          if (el != nullptr) el[(int64_t)row * H + cl / FE] = sl;
+          if (er != nullptr) er[(int64_t)row * H + cl / FE] = sr;
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // staging reads done before the next tile's writes
+    __builtin_amdgcn_wave_barrier();
+  };
+  // two register buffers, alternating: tile t + nw's loads fly during tile t
+  u32x4_t bufA[G::NLD], bufB[G::NLD];
+  load_tile(gw, bufA);
+  for (int t = gw; t < tiles; t += 2 * nw) {
+    if (t + nw < tiles) load_tile(t + nw, bufB);
+    tile(t, bufA);
+    if (t + nw >= tiles) break;
+    if (t + 2 * nw < tiles) load_tile(t + 2 * nw, bufA);
+    tile(t + nw, bufB);
+  }
+}
+
+// ------------------------------------------------------------- weight gradient ---
+// dW[a, n] = sum_r X[r, a] * (D[r, n] + d1[r, n / hF] a1[n] + d2[r, n / hF] a2[n]),
+// a, n < 128.  A wave owns one column half nh (64 columns) of dW for a row range:
+// 4 x 2 blocks of 32 x 32 (128 accumulator registers, so two waves fit a SIMD).  Lane
+// l = (i = l & 31, q = l >> 5) of a two-row step takes row r + q: X[r+q, 4i .. 4i+3]
+// -> A of row blocks t = 0..3 (dW row 4i + t), D'[r+q, 64 nh + 2i .. +1] -> B of
+// column blocks u = 0..1 (dW column 64 nh + 2i + u).  v_mfma_f32_32x32x2_f32, k = q.
+// Block = 8 waves: column half nh = w & 1, row quarter w >> 1 of the block's rows.
+constexpr int kWgWaves = 8;
+constexpr int kWgPD = 4;    // two-row steps per load batch (two batches in flight)
+constexpr int kWgPitch = 132;
+
+template <bool HO>
+__global__ void __launch_bounds__(64 * kWgWaves) __attribute__((amdgpu_waves_per_eu(2, 2)))
+wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __restrict__ D,
+             int64_t ldd, const float* __restrict__ d1, const float* __restrict__ a1,
+             const float* __restrict__ d2, const float* __restrict__ a2, int hH, int hF,
+             float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float red[128 * kWgPitch];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
+  const int nh = w & 1, rq = w >> 1;
+  const int i32 = lane & 31, q = lane >> 5;
+  const int nq = gridDim.x * (kWgWaves / 2);  // row slices
+  const int gs = blockIdx.x * (kWgWaves / 2) + rq;
+  const int r0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)gs * M) / nq));
+  const int r1 = __builtin_amdgcn_readfirstlane((int)(((int64_t)(gs + 1) * M) / nq));
+  const int c0 = 64 * nh + 2 * i32;  // this lane's two dW columns
+  const int hh = HO ? c0 / hF : 0;
+  float2 av1 = make_float2(0.f, 0.f), av2 = av1;
+  if (HO) {
+    av1 = *reinterpret_cast<const float2*>(a1 + c0);
+    if (d2 != nullptr) av2 = *reinterpret_cast<const float2*>(a2 + c0);
+  }
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[t][u][v] = 0.f;
+
+  // buffer-descriptor loads (32-bit offsets, rows past r1 read 0): the load batches
+  // are branch-free, so their waits stay exact and no 64-bit address math is carried
+  const rsrc_t r_x = make_rsrc(X, (uint32_t)((int64_t)M * ldx * 4));
+  const rsrc_t r_d = make_rsrc(D, (uint32_t)((int64_t)M * ldd * 4));
+  const rsrc_t r_e1 = make_rsrc(HO ? d1 : nullptr, HO ? (uint32_t)((int64_t)M * hH * 4) : 0u);
+  const rsrc_t r_e2 = make_rsrc(HO ? d2 : nullptr, HO && d2 ? (uint32_t)((int64_t)M * hH * 4) : 0u);
+  const uint32_t sx = (uint32_t)ldx * 4u, sd = (uint32_t)ldd * 4u, se = (uint32_t)hH * 4u;
+  const uint32_t ox = 16u * i32, od = 4u * c0, oe = 4u * hh;
+  struct Batch {
+    u32x4_t x[kWgPD];
+    float d0[kWgPD], d1v[kWgPD];
+    float e1[kWgPD], e2[kWgPD];
+  };
+  auto load = [&](int rb, Batch& b) {
+#pragma unroll
+    for (int p = 0; p < kWgPD; ++p) {
+      const int row = rb + 2 * p + q;
+      const bool ok = row < r1;
+      const uint32_t ur = (uint32_t)row;
+      // a masked row's offsets are kOOB (+ small): past every descriptor's range
+      const uint32_t m = ok ? 0u : kOOB;
+      b.x[p] = buf_b128(r_x, (ur * sx + ox) | m);
+      const auto dd = __builtin_amdgcn_raw_buffer_load_b64(r_d, (ur * sd + od) | m, 0, 0);
+      b.d0[p] = __uint_as_float(dd[0]);
+      b.d1v[p] = __uint_as_float(dd[1]);
+      if (HO) {
+        b.e1[p] = buf_f32(r_e1, (ur * se + oe) | m);
+        b.e2[p] = buf_f32(r_e2, (ur * se + oe) | m);
+      }
+    }
+  };
+  auto compute = [&](int rb, const Batch& cb) {
+#pragma unroll
+    for (int p = 0; p < kWgPD; ++p) {
+      float d[2] = {cb.d0[p], cb.d1v[p]};
+      if (HO) {
+        d[0] = fmaf(cb.e2[p], av2.x, fmaf(cb.e1[p], av1.x, d[0]));
+        d[1] = fmaf(cb.e2[p], av2.y, fmaf(cb.e1[p], av1.y, d[1]));
+      }
+      const float xa[4] = {__uint_as_float(cb.x[p].x), __uint_as_float(cb.x[p].y),
+                           __uint_as_float(cb.x[p].z), __uint_as_float(cb.x[p].w)};
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[t], d[u], acc[t][u], 0, 0, 0);
+    }
+  };
+  // double-buffered loads: batch i + 1's loads are issued before batch i's MFMAs
+  // (kWgPD x 8 MFMAs of 64 cycles), and the other wave of the SIMD covers the rest.
+  // One compute body per trip: the accumulators keep one register assignment.
+  constexpr int R = 2 * kWgPD;
+  Batch nb;
+  load(r0, nb);
+  for (int rb = r0; rb < r1; rb += R) {
+    const Batch cb = nb;
+    load(rb + R, nb);  // past r1: masked (reads 0)
+    compute(rb, cb);
+  }
+  // ---- block sum (LDS): the 4 row quarters of each column half added in quarter order
+  // 32x32 C layout: reg v of lane l is row 8 (v / 4) + 4 (l >> 5) + (v % 4), col l & 31
+#pragma unroll 1
+  for (int qq = 0; qq < kWgWaves / 2; ++qq) {
+    if (rq == qq) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int a = 4 * (8 * (v >> 2) + 4 * q + (v & 3)) + t;
+          float2* dst = reinterpret_cast<float2*>(red + a * kWgPitch + c0);
+          float2 s = make_float2(acc[t][0][v], acc[t][1][v]);
+          if (qq > 0) {
+            const float2 o = *dst;
+            s = make_float2(o.x + s.x, o.y + s.y);
+          }
+          *dst = s;
+        }
+    }
+    __syncthreads();
+  }
+  float* out = slab + (int64_t)blockIdx.x * (128 * 128);
+#pragma unroll
+  for (int k = 0; k < 4096 / (64 * kWgWaves); ++k) {
+    const int idx = tid + 64 * kWgWaves * k;  // float4 index: row idx / 32, col 4 (idx % 32)
+    const int a = idx >> 5, c4 = (idx & 31) * 4;
+    *reinterpret_cast<float4*>(out + a * 128 + c4) =
+        *reinterpret_cast<const float4*>(red + a * kWgPitch + c4);
+  }
+}
+
+// C[a, n] (= or +=) sum over blocks b of slab[b, a, n], b ascending within each of 16
+// interleaved groups, the groups added in a fixed LDS tree.  Block = 16 groups x 16
+// float4 columns; grid = 128 * 128 / 64 blocks.
+template <typename TC>
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nb,
+                                                           TC* __restrict__ C, int64_t ldc,
+                                                           float beta) {
+  __shared__ float4 part[256];
+  const int zq = threadIdx.x >> 4, cq = threadIdx.x & 15;
+  const int f4 = blockIdx.x * 16 + cq;  // float4 index in the 128 x 128 tile
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = zq; b < nb; b += 16) {
+    const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)b * (128 * 128))[f4];
+    s = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 8; o >= 1; o >>= 1) {
+    if (zq < o) {
+      const float4 v = part[threadIdx.x + 16 * o];
+      float4& d = part[threadIdx.x];
+      d = make_float4(d.x + v.x, d.y + v.y, d.z + v.z, d.w + v.w);
+    }
+    __syncthreads();
+  }
+  if (zq == 0) {
+    const float4 r = part[cq];
+    const int a = f4 >> 5, c4 = (f4 & 31) * 4;
+    const float e[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      TC* dst = C + a * ldc + c4 + u;
+      float v = e[u];
+      if (beta != 0.f) v += beta * to_f32(*dst);
+      *dst = from_f32<TC>(v);
+    }
+  }
+}
+
+}  // namespace sk
+
+// ------------------------------------------------------------------ dispatch ---
+// Environment knob MSHA_SKINNY=0 routes every call to the tiled GEMMs (A/B runs).
+static bool skinny_enabled() {
+  static const int on = [] {
+    const char* v = getenv("MSHA_SKINNY");
+    return v != nullptr && *v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
+
+static int proj_grid(int64_t M) {
+  const int64_t tiles = (M + 15) / 16;
+  const int64_t blocks = (tiles + sk::kProjWaves - 1) / sk::kProjWaves;
+  return (int)(blocks < 256 ? blocks : 256);  // one 8-wave block per CU
+}
+
+// Returns 1 when it launched, 0 when the shape is not covered (caller falls back).
+template <typename T>
+int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, const void* W,
+                   const float* al, const float* ar, void* h, float* el, float* er,
+                   hipStream_t s) {
+  const int64_t N = (int64_t)heads * feat;
+  if (!skinny_enabled() || M < 1024 || M >= (1ll << 31)) return 0;
+  if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)h) & 15) return 0;
+  const bool score = al != nullptr || ar != nullptr;
+  const int minfe = 16 / (int)sizeof(T);
+  if (score && (feat < minfe || N % feat != 0)) return 0;
+  const dim3 grid(proj_grid(M)), block(64 * sk::kProjWaves);
+#define SKP(k, n, fe)                                                                           \
+  if (K == k && N == n && (score ? feat == fe : fe == 0)) {                                    \
+    hipLaunchKernelGGL((sk::proj_kernel<T, k, n, fe>), grid, block, 0, s, (int)M,              \
+                       (const T*)X, (const T*)W, al, ar, (T*)h, el, er, heads);                 \
+    return 1;                                                                                   \
+  }
+#define SKP_N(k, n) SKP(k, n, 0) SKP(k, n, 16) SKP(k, n, 32) SKP(k, n, 64) SKP(k, n, n)
+  SKP_N(128, 128)
+  SKP_N(64, 128)
+  SKP(128, 64, 0) SKP(128, 64, 16) SKP(128, 64, 32) SKP(128, 64, 64)
+  SKP(64, 64, 0) SKP(64, 64, 16) SKP(64, 64, 32) SKP(64, 64, 64)
+#undef SKP_N
+#undef SKP
+  return 0;
+}
+template int skinny_project<float>(int64_t, int64_t, int, int, const void*, const void*,
+                                   const float*, const float*, void*, float*, float*, hipStream_t);
+template int skinny_project<bf16_t>(int64_t, int64_t, int, int, const void*, const void*,
+                                    const float*, const float*, void*, float*, float*, hipStream_t);
+
+// dW (128 x 128, fp32) = X^T D' over K rows: A = X^T given as (A, sAm = 1, sAk = ldx),
+// B = D' = D (+ head outer) given as (B, sBk = ldd, sBn = 1).  Uses the caller's split-K
+// workspace (splits x 128 x 128 fp32) for the block partials; 0 = not covered.
+int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
+                 const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
+                 int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
+                 const float* a, const float* de2, const float* a2, hipStream_t s) {
+  if (!skinny_enabled() || M != 128 || N != 128 || sAm != 1 || sBn != 1) return 0;
+  if (K < 4096 || K >= (1ll << 31) || splits < 16) return 0;
+  if (sAk % 4 || sBk % 4 || ((uintptr_t)A | (uintptr_t)B) & 15) return 0;
+  if (de != nullptr && (hF % 4 || ((uintptr_t)a & 15) || (a2 && ((uintptr_t)a2 & 15)))) return 0;
+  const size_t per = (size_t)128 * 128 * sizeof(float);
+  int64_t nb = (int64_t)(ws_bytes / per);
+  if (nb > splits) nb = splits;
+  if (nb > 256) nb = 256;
+  if (nb < 16 || ws == nullptr) return 0;
+  float* slab = (float*)ws;
+  if (de != nullptr)
+    hipLaunchKernelGGL(sk::wgrad_kernel<true>, dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s, (int)K, A, sAk,
+                       B, sBk, de, a, de2, a2, hH, hF, slab);
+  else
+    hipLaunchKernelGGL(sk::wgrad_kernel<false>, dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s, (int)K, A,
+                       sAk, B, sBk, nullptr, nullptr, nullptr, nullptr, 1, 4, slab);
+  hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>, dim3(128 * 128 / 64), dim3(256), 0, s,
+                     (const float*)slab, (int)nb, C, ldc, beta);
+  return 1;
+}
+
+}  // namespace msha

@@ -1,0 +1,56 @@
+"""Time the C4 projection and weight-gradient GEMMs (one JSON line per case).
+
+    MSHA_SKINNY=0 python scripts/gemm_ab.py   # tiled GEMMs (gemm.hip / gemm_bf16.hip)
+    python scripts/gemm_ab.py                 # resident-W / whole-tile kernels (skinny.hip)
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import msha_loader  # noqa: E402
+
+msha_loader.load()
+from msha_gnn_amd import functional as MF  # noqa: E402
+
+
+def timeit(fn, reps=int(os.environ.get("GEMM_AB_REPS", 50)), warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    M, K, H, F = 100000, 128, 8, 16
+    D = H * F
+    for dt in (torch.float32, torch.bfloat16):
+        X = torch.rand(M, K, device=dev, generator=g).to(dt)
+        W = (torch.randn(K, D, device=dev, generator=g) / K ** 0.5).to(dt)
+        al = torch.randn(H, F, device=dev, generator=g)
+        ar = torch.randn(H, F, device=dev, generator=g)
+        dh = torch.randn(M, D, device=dev, generator=g).to(dt)
+        de = torch.randn(M, H, device=dev, generator=g)
+        de2 = torch.randn(M, H, device=dev, generator=g)
+        outer = (H, F, de, al, de2, ar)
+        us_p = timeit(lambda: MF.project_scores(X, W, al, ar, heads=H))
+        us_w = timeit(lambda: MF.gemm_head_outer(X.t(), dh, 1, outer))
+        flop = 2.0 * M * K * D
+        print(json.dumps({"skinny": os.environ.get("MSHA_SKINNY", "1"), "dtype": str(dt)[6:],
+                          "proj_us": round(us_p, 1), "proj_TFs": round(flop / us_p / 1e6, 1),
+                          "wgrad_us": round(us_w, 1), "wgrad_TFs": round(flop / us_w / 1e6, 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

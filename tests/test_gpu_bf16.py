@@ -75,7 +75,8 @@ def test_gemm_bf16_head_outer(cuda, operand):
     tol_close(got, ref, 1e-2, 1e-2)
 
 
-@pytest.mark.parametrize("M,K,H,F", [(3000, 128, 8, 16), (517, 128, 2, 64), (200, 64, 1, 128)])
+@pytest.mark.parametrize("M,K,H,F", [(3000, 128, 8, 16), (517, 128, 2, 64), (200, 64, 1, 128),
+                                     (5001, 128, 2, 64), (2049, 64, 4, 16)])
 def test_project_scores_bf16(cuda, M, K, H, F):
     from msha_gnn_amd import functional as MF
 

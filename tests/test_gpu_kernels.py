@@ -325,7 +325,9 @@ def test_gemm_f32(cuda, M, N, K, trans_a, trans_b, splits):
 
 
 @pytest.mark.parametrize("M,K,H,F", [(3000, 128, 8, 16), (517, 128, 2, 64), (80, 16, 1, 8),
-                                     (300, 64, 4, 32), (200, 32, 1, 128)])
+                                     (300, 64, 4, 32), (200, 32, 1, 128),
+                                     # resident-W kernel (skinny.hip): ragged last tile
+                                     (5001, 64, 2, 64), (2050, 128, 4, 32)])
 def test_project_scores_fwd_bwd(cuda, M, K, H, F):
     from msha_gnn_amd import functional as MF
 
@@ -383,6 +385,8 @@ def test_gemm_head_outer(cuda, operand, M, H, F, K, two):
     else:
         X = rng.standard_normal((M, K)).astype(np.float32)
         got = MF.gemm_head_outer(t(X, cuda).t(), t(dh, cuda), 1, outer).cpu().numpy()
+        again = MF.gemm_head_outer(t(X, cuda).t(), t(dh, cuda), 1, outer).cpu().numpy()
+        assert np.array_equal(got, again)  # block partials added in a fixed order
         ref = X.T.astype(np.float64) @ tot
     tol_close(got, ref, 1e-5, 1e-5)
 
