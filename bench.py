@@ -77,10 +77,15 @@ def pmc_traffic(H, F, bf16=False, workload="syn100k"):
     import glob
     import re
 
-    pat = (re.compile(rf"edge_attn_fwd_kernelILi{H}ELi{F}EDF16b") if bf16 else
-           re.compile(rf"edge_attn_fwd_kernel<{H}, {F}(, float)?(, \d+)?>"))
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{workload}*",
-                                              "pmc_summary.json")), reverse=True):
+    pat = (re.compile(rf"edge_attn_fwd(?:_bat)?_kernelILi{H}ELi{F}EDF16b") if bf16 else
+           re.compile(rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?>"))
+
+    def newest_first(path):  # round1_syn100k_v10 after _v9: compare the numbers
+        tag = os.path.basename(os.path.dirname(path))
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
+
+    paths = glob.glob(os.path.join(ROOT, "profiles", f"*{workload}_v*", "pmc_summary.json"))
+    for path in sorted(paths, key=newest_first, reverse=True):
         try:
             summ = json.load(open(path))
         except (OSError, ValueError):
