@@ -115,12 +115,13 @@ def bwd_fused_bytes(n, m, e, H, F, n_chunks, s=4):
     """Algorithmic bytes of msha_edge_attention_bwd_fused (its three launches):
     row stats (dU, u, el, lse in; the 3H-float row record out); the column pass (per
     CSC slot row + eid + the record gather + s*D dU gather + de write; per column hc,
-    er in, d_hc, d_er out; the chunk plan); the row sum (rowptr, de, d_el)."""
+    er in, d_hc, d_er out; the chunk plan); the row sum (rowptr, slot map, de, d_el)."""
     D = H * F
     stats = n * (2 * s * D + 8 * H + 12 * H)
     cols = e * (8 + 12 * H + s * D + 4 * H) + m * (2 * s * D + 8 * H) + 12 * n_chunks \
         + 4 * (m + 1)
-    rsum = 4 * (n + 1) + e * 4 * H + n * 4 * H
+    slot_map = 4 if e * 4 * H >= 192 << 20 else 0  # de in slot order (edge_attention.hip)
+    rsum = 4 * (n + 1) + e * (4 * H + slot_map) + n * 4 * H
     return stats + cols + rsum
 
 

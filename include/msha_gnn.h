@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 2
+#define MSHA_ABI_VERSION 3
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -80,6 +80,11 @@ typedef struct msha_graph {
   const int32_t* multi_col;
   const int32_t* multi_first;
   const int32_t* multi_count;
+  /* n_edges, CSC slot of each CSR edge (the inverse of csc_eid; nullable).  When set,
+   * msha_edge_attention_bwd_fused may keep its per-edge de scratch in CSC slot order
+   * (large graphs): the column pass writes it contiguously and the row pass gathers it
+   * through this map (ABI 3). */
+  const int32_t* csr_slot;
 } msha_graph;
 
 /* Same-group adjacency of the full MSHA layer (city and province, dataset.py:260-277
@@ -204,7 +209,8 @@ MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat
  * bitwise, from one pass over the CSC (the column owns hc_j, so dU_i . hc_j comes from
  * the dU[i] gather the column pass makes anyway) plus two light row passes.
  * Replaces the reference's autograd of Ablation.py:266-274 for that case.
- * de (n_edges, heads) fp32: scratch (left holding de in CSR edge order).
+ * de (n_edges, heads) fp32: scratch (left holding de in CSR edge order, or in CSC slot
+ * order when g->csr_slot is set and de exceeds 192 MB).
  * ws: msha_edge_attention_bwd_fused_workspace_size bytes.  Needs the CSC view with
  * csc_eid. */
 MSHA_API size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph* g,

@@ -30,7 +30,7 @@ class MshaGraph(C.Structure):
         ("n_chunks", C.c_int64), ("chunk_col", C.c_void_p), ("chunk_start", C.c_void_p),
         ("chunk_end", C.c_void_p),
         ("n_multi", C.c_int64), ("multi_col", C.c_void_p), ("multi_first", C.c_void_p),
-        ("multi_count", C.c_void_p),
+        ("multi_count", C.c_void_p), ("csr_slot", C.c_void_p),
     ]
 
 
@@ -128,7 +128,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.msha_abi_version() != 2:
+    if lib.msha_abi_version() != 3:
         raise MshaLibraryError("ABI version mismatch")
     _lib = lib
     return lib

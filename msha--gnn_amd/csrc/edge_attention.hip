@@ -25,6 +25,12 @@
 #ifndef COLS_EH
 #define COLS_EH 1
 #endif
+#ifndef DE_SLOT_MIN_BYTES
+#define DE_SLOT_MIN_BYTES (192ll << 20)
+#endif
+#ifndef COLS_NG
+#define COLS_NG 2  // slot groups whose loads are in flight together in the column pass
+#endif
 #ifndef FWD_EPL
 #define FWD_EPL 2
 #endif
@@ -645,6 +651,18 @@ __global__ void __launch_bounds__(1024) csc_combine_kernel(
 // edge_attn_bwd_rows + csc_aggregate: the results are bitwise identical.
 // Row statistics: RPW rows per wave trip (EPI rows per load instruction, all loads of
 // the trip issued before the first use), D_i = dU_i . u_i per head in group_sum order.
+// Row record stride in floats: the 3H values padded to a power of two (H = 8: 32 floats,
+// one 128-B line), so a record never straddles a line and a CSC slot's record gather
+// touches exactly one (the unpadded 96-B record straddled two lines half the time).
+#ifndef REC_PAD
+#define REC_PAD 1
+#endif
+__host__ __device__ constexpr int rec_stride(int H) {
+  int s = 1;
+  while (s < 3 * H) s <<= 1;
+  return REC_PAD ? s : 3 * H;
+}
+
 template <int H, int F, typename T>
 __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
     int64_t n_rows, const float* __restrict__ el, const float* __restrict__ lse,
@@ -678,7 +696,7 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
         // the head's first chunk lane writes D; el and lse ride along
         if (q % G::QH == 0 && row < n_rows) {
           const int h = q / G::QH;
-          float* r = rec + row * 3 * H;
+          float* r = rec + row * rec_stride(H);
           r[h] = el[row * H + h];
           r[H + h] = lse[row * H + h];
           r[2 * H + h] = dk;
@@ -695,7 +713,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
     const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid,
     const uint8_t* __restrict__ rowflag, const float* __restrict__ rec,
     const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
-    float slope, Dropout dp, float* __restrict__ de, T* __restrict__ d_hc,
+    float slope, Dropout dp, bool slot_de, float* __restrict__ de, T* __restrict__ d_hc,
     float* __restrict__ d_er, float* __restrict__ part, float* __restrict__ part_x) {
   using G = Geo<H, F, T>;
   const int lane = lane_id();
@@ -736,7 +754,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
       float pre = 0.f, att = 0.f, dropf = 0.f, Dsi = 0.f;
       bool virt = false;
       if (valid) {
-        const float* r = rec + (int64_t)i * 3 * H;
+        const float* r = rec + (int64_t)i * rec_stride(H);
         virt = rowflag != nullptr && rowflag[i] != 0;
         pre = r[h_s] + erh;
         const float sv = virt ? 0.f : lrelu(pre, slope);
@@ -774,7 +792,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
       if (valid) {
         const float ds = att * (gsum * dropf - Dsi);
         const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
-        de[eid * H + h_s] = dev;
+        de[(slot_de ? (int64_t)slot : eid) * H + h_s] = dev;
         xacc += dev;
       }
       i0 = i1;
@@ -829,10 +847,11 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
     const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid, int64_t n_edges,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ rec,
     const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
-    float slope, Dropout dp, float* __restrict__ de, T* __restrict__ d_hc,
+    float slope, Dropout dp, bool slot_de, float* __restrict__ de, T* __restrict__ d_hc,
     float* __restrict__ d_er, float* __restrict__ part, float* __restrict__ part_x) {
   using G = Geo<H, F, T>;
   constexpr int NV = G::QH;  // 16-B pieces per head
+  constexpr int NG = COLS_NG;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -840,7 +859,7 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
   const rsrc_t r_row = make_rsrc(csc_row, (uint32_t)(n_edges * 4));
   const rsrc_t r_eid = make_rsrc(csc_eid, (uint32_t)(n_edges * 4));
   const rsrc_t r_flag = make_rsrc(rowflag, (uint32_t)n_rows);
-  const rsrc_t r_rec = make_rsrc(rec, (uint32_t)(n_rows * 12 * H));
+  const rsrc_t r_rec = make_rsrc(rec, (uint32_t)(n_rows * 4 * rec_stride(H)));
   const rsrc_t r_dU = make_rsrc(dU, (uint32_t)(n_rows * G::D * sizeof(T)));
   const rsrc_t r_de = make_rsrc(de, (uint32_t)(n_edges * 4 * H));
   const uint32_t h_off = h_s * F * sizeof(T);
@@ -848,8 +867,12 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
   int64_t c = wave;
   if (c >= n_chunks) return;
   int32_t jc = chunk_col[c], s0 = chunk_start[c], s1 = chunk_end[c];
-  int32_t i0 = buf_i32(r_row, s0 + e_s < s1 ? (s0 + e_s) * 4u : kOOB);
-  int32_t i1 = buf_i32(r_row, s0 + G::CE + e_s < s1 ? (s0 + G::CE + e_s) * 4u : kOOB);
+  int32_t ii[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int32_t a = s0 + g * G::CE + e_s;
+    ii[g] = buf_i32(r_row, a < s1 ? (uint32_t)a * 4u : kOOB);
+  }
   while (true) {
     const int64_t nc = c + nwaves;
     const bool has_next = nc < n_chunks;
@@ -865,53 +888,68 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
       acc[k] = pk_zero<T>();
     }
     float xacc = 0.f;
-    auto slot_group = [&](int32_t cs, int32_t i) {
-      const int32_t slot = cs + e_s;
-      const bool valid = slot < s1;
-      Pk<T> dUv[NV];
-      const uint32_t row_off = valid ? (uint32_t)i * (G::D * sizeof(T)) + h_off : kOOB;
+    // one trip = COLS_NG slot groups: every group's loads leave before the first
+    // group's compute and de store (the compiler may not hoist a buffer load above a
+    // buffer store), then the groups are consumed in slot order
+    for (int32_t cs = s0; cs < s1; cs += NG * G::CE) {
+      Pk<T> dUv[NG][NV];
+      int32_t eid[NG];
+      float r_el[NG], r_lse[NG], Dsi[NG];
+      uint32_t vflag[NG];
 #pragma unroll
-      for (int k = 0; k < NV; ++k)
-        dUv[k] = pk_load_buf(r_dU, row_off + (valid ? k * 16u : 0u), (T*)nullptr);
-      const int32_t eid = buf_i32(r_eid, valid ? slot * 4u : kOOB);
-      const uint32_t rec_off = valid ? (uint32_t)i * (12u * H) + h_s * 4u : kOOB;
-      const float r_el = buf_f32(r_rec, rec_off);
-      const float r_lse = buf_f32(r_rec, valid ? rec_off + 4u * H : kOOB);
-      const float Dsi = buf_f32(r_rec, valid ? rec_off + 8u * H : kOOB);
-      const bool virt = buf_u8(r_flag, valid ? (uint32_t)i : kOOB) != 0;
-      const float pre = r_el + erh;
-      const float sv = virt ? 0.f : lrelu(pre, slope);
-      const float att = __expf(sv - r_lse);
-      const float dropf = dropout_factor(dp, (uint64_t)eid * H + h_s);
-      const float wv = valid ? att * dropf : 0.f;
-      // dU_i[h] . hc_j[h] in group_sum's order over the head's pieces
-      float d[NV];
+      for (int g = 0; g < NG; ++g) {
+        const bool valid = cs + g * G::CE + e_s < s1;
+        const uint32_t row_off = valid ? (uint32_t)ii[g] * (G::D * sizeof(T)) + h_off : kOOB;
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        d[k] = pk_dot(dUv[k], hcv[k]);
-        acc[k] = pk_fma(wv, dUv[k], acc[k]);
+        for (int k = 0; k < NV; ++k)
+          dUv[g][k] = pk_load_buf(r_dU, row_off + (valid ? k * 16u : 0u), (T*)nullptr);
+        eid[g] = buf_i32(r_eid, valid ? (uint32_t)(cs + g * G::CE + e_s) * 4u : kOOB);
+        const uint32_t rec_off = valid ? (uint32_t)ii[g] * (4u * rec_stride(H)) + h_s * 4u : kOOB;
+        r_el[g] = buf_f32(r_rec, rec_off);
+        r_lse[g] = buf_f32(r_rec, valid ? rec_off + 4u * H : kOOB);
+        Dsi[g] = buf_f32(r_rec, valid ? rec_off + 8u * H : kOOB);
+        vflag[g] = buf_u8(r_flag, valid ? (uint32_t)ii[g] : kOOB);
+      }
+      // CSC rows of the next trip
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int32_t a = cs + (NG + g) * G::CE + e_s;
+        ii[g] = buf_i32(r_row, a < s1 ? (uint32_t)a * 4u : kOOB);
       }
 #pragma unroll
-      for (int o = 1; o < NV; o <<= 1)
+      for (int g = 0; g < NG; ++g) {
+        const int32_t slot = cs + g * G::CE + e_s;
+        const bool valid = slot < s1;
+        const bool virt = vflag[g] != 0;
+        const float pre = r_el[g] + erh;
+        const float sv = virt ? 0.f : lrelu(pre, slope);
+        const float att = __expf(sv - r_lse[g]);
+        const float dropf = dropout_factor(dp, (uint64_t)eid[g] * H + h_s);
+        const float wv = valid ? att * dropf : 0.f;
+        // dU_i[h] . hc_j[h] in group_sum's order over the head's pieces
+        float d[NV];
 #pragma unroll
-        for (int k = 0; k < NV; k += 2 * o) d[k] = d[k] + d[k + o];
-      const float ds = att * (d[0] * dropf - Dsi);
-      const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
-      buf_store_f32(r_de, valid ? (uint32_t)eid * (4u * H) + h_s * 4u : kOOB, dev);
-      xacc += valid ? dev : 0.f;
-    };
-    for (int32_t cs = s0; cs < s1; cs += 2 * G::CE) {
-      slot_group(cs, i0);
-      const int32_t a0 = cs + 2 * G::CE + e_s;
-      i0 = buf_i32(r_row, a0 < s1 ? a0 * 4u : kOOB);
-      slot_group(cs + G::CE, i1);
-      const int32_t a1 = cs + 3 * G::CE + e_s;
-      i1 = buf_i32(r_row, a1 < s1 ? a1 * 4u : kOOB);
+        for (int k = 0; k < NV; ++k) {
+          d[k] = pk_dot(dUv[g][k], hcv[k]);
+          acc[k] = pk_fma(wv, dUv[g][k], acc[k]);
+        }
+#pragma unroll
+        for (int o = 1; o < NV; o <<= 1)
+#pragma unroll
+          for (int k = 0; k < NV; k += 2 * o) d[k] = d[k] + d[k + o];
+        const float ds = att * (d[0] * dropf - Dsi[g]);
+        const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
+#ifndef DIAG_NO_DE
+        const uint32_t at = slot_de ? (uint32_t)slot : (uint32_t)eid[g];
+        buf_store_f32(r_de, valid ? at * (4u * H) + h_s * 4u : kOOB, dev);
+#endif
+        xacc += valid ? dev : 0.f;
+      }
     }
-    {
-      const int32_t a0 = ns0 + e_s, a1 = ns0 + G::CE + e_s;
-      i0 = buf_i32(r_row, a0 < ns1 ? a0 * 4u : kOOB);
-      i1 = buf_i32(r_row, a1 < ns1 ? a1 * 4u : kOOB);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int32_t a = ns0 + g * G::CE + e_s;
+      ii[g] = buf_i32(r_row, a < ns1 ? (uint32_t)a * 4u : kOOB);
     }
 #pragma unroll
     for (int k = 0; k < NV; ++k)
@@ -948,7 +986,7 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
 template <int H>
 __global__ void __launch_bounds__(256) bwd_row_sum_kernel(
     const int32_t* __restrict__ rowptr, int64_t n_rows, const float* __restrict__ de,
-    float* __restrict__ d_el) {
+    const int32_t* __restrict__ slot_of, float* __restrict__ d_el) {
   constexpr int CE = 64 / H;
   const int lane = lane_id();
   const int r_s = lane / H, h_s = lane % H;
@@ -963,9 +1001,13 @@ __global__ void __launch_bounds__(256) bwd_row_sum_kernel(
     for (int k = 0; k < CE; ++k) p[k] = 0.f;
     for (int32_t cs = start; cs < end; cs += CE) {
       float v[CE];
+      int32_t at[CE];
 #pragma unroll
       for (int k = 0; k < CE; ++k)
-        v[k] = cs + k < end ? de[(int64_t)(cs + k) * H + h_s] : 0.f;
+        at[k] = slot_of == nullptr ? cs + k : (cs + k < end ? slot_of[cs + k] : 0);
+#pragma unroll
+      for (int k = 0; k < CE; ++k)
+        v[k] = cs + k < end ? de[(int64_t)at[k] * H + h_s] : 0.f;
 #pragma unroll
       for (int k = 0; k < CE; ++k)
         if (cs + k < end) p[k] += v[k];
@@ -1222,7 +1264,7 @@ extern "C" int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t fe
 extern "C" size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph* g,
                                                                int32_t heads, int32_t feat) {
   if (g == nullptr || heads <= 0 || feat <= 0) return 0;
-  const size_t rec = ((size_t)g->n_rows * 3 * heads * sizeof(float) + 255) & ~(size_t)255;
+  const size_t rec = ((size_t)g->n_rows * rec_stride(heads) * sizeof(float) + 255) & ~(size_t)255;
   return rec + msha_csc_aggregate_workspace_size(g, heads, feat);
 }
 
@@ -1234,8 +1276,13 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
                              float* part_x, hipStream_t s) {
   // the buffer-descriptor kernel addresses each table with 32-bit byte offsets
   const int64_t lim = (int64_t)1 << 31;
+  // de in CSC slot order (contiguous writes, gathered by the row sum) once it outgrows
+  // the Infinity Cache; below that the cache absorbs the scattered 4H-byte writes and
+  // the CSR-order row sum reads it contiguously (measured: syn100k's 64 MB de is faster
+  // in edge order, syn2m's 1.28 GB in slot order)
+  const bool slot_de = g->csr_slot != nullptr && g->n_edges * 4 * (int64_t)heads >= DE_SLOT_MIN_BYTES;
   const bool buf_ok = g->n_rows * (int64_t)heads * feat * (int64_t)sizeof(T) < lim &&
-                      g->n_edges * 4 * (int64_t)heads < lim && g->n_rows * 12 * heads < lim;
+                      g->n_edges * 4 * (int64_t)heads < lim && g->n_rows * 4 * rec_stride(heads) < lim;
 #define X(h, f)                                                                                \
   if (heads == h && feat == f) {                                                               \
     if constexpr (f % Pk<T>::V == 0) {                                                         \
@@ -1245,16 +1292,18 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
         hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
                            g->colptr, g->csc_row, g->csc_eid, g->n_edges, g->rowflag,          \
-                           g->n_rows, rec, er, (const T*)hc, (const T*)dU, neg_slope, dp, de,  \
+                           g->n_rows, rec, er, (const T*)hc, (const T*)dU, neg_slope, dp,      \
+                           slot_de, de,                                                        \
                            (T*)d_hc, d_er, part, part_x);                                      \
       else                                                                                     \
         hipLaunchKernelGGL((bwd_cols_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0,   \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
                            g->colptr, g->csc_row, g->csc_eid, g->rowflag, rec, er,             \
-                           (const T*)hc, (const T*)dU, neg_slope, dp, de, (T*)d_hc, d_er,      \
+                           (const T*)hc, (const T*)dU, neg_slope, dp, slot_de,                 \
+                           de, (T*)d_hc, d_er,                                                 \
                            part, part_x);                                                      \
       hipLaunchKernelGGL((bwd_row_sum_kernel<h>), wave_grid(g->n_rows), dim3(256), 0, s,       \
-                         g->rowptr, g->n_rows, de, d_el);                                      \
+                         g->rowptr, g->n_rows, de, slot_de ? g->csr_slot : nullptr, d_el);    \
     }                                                                                          \
   }
   MSHA_FOR_EACH_SHAPE(X)
@@ -1287,7 +1336,7 @@ extern "C" int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads,
                  "edge_attention_bwd_fused: workspace too small");
   const int64_t D = (int64_t)heads * feat;
   float* rec = (float*)ws;
-  const size_t rec_bytes = ((size_t)g->n_rows * 3 * heads * sizeof(float) + 255) & ~(size_t)255;
+  const size_t rec_bytes = ((size_t)g->n_rows * rec_stride(heads) * sizeof(float) + 255) & ~(size_t)255;
   float* part = (float*)((char*)ws + rec_bytes);
   float* part_x = part + g->n_chunks * D;
   const Dropout dp = make_dropout(drop_p, seed, offset);

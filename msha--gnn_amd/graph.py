@@ -11,6 +11,7 @@ Also the data-side entry points of the reference path:
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import numpy as np
@@ -19,6 +20,8 @@ import torch
 from . import _lib
 
 CSC_CHUNK = 512  # max CSC slots per work chunk of the column aggregate
+# fused backward keeps de in CSC slot order (csr_slot map); "0" = CSR edge order (A/B)
+DE_SLOT_ORDER = os.environ.get("MSHA_DE_SLOT", "1") != "0"
 
 
 def csc_chunk_for(n_edges: int) -> int:
@@ -80,6 +83,12 @@ class Graph:
                 d.multi_col, d.multi_first, d.multi_count = (_lib.ptr(p["multi_col"]),
                                                              _lib.ptr(p["multi_first"]),
                                                              _lib.ptr(p["multi_count"]))
+                if self.csc_eid is not None and self.n_edges > 0 and DE_SLOT_ORDER:
+                    # inverse of csc_eid: the fused backward's de scratch in slot order
+                    self.csr_slot = torch.empty_like(self.csc_eid)
+                    self.csr_slot[self.csc_eid.long()] = torch.arange(
+                        self.n_edges, dtype=torch.int32, device=self.device)
+                    d.csr_slot = _lib.ptr(self.csr_slot)
             self._desc = d
         return self._desc
 

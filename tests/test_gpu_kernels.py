@@ -572,3 +572,29 @@ def test_spmm_both_directions(cuda, msha, n, m, D, dt):
     (a.float() * t(ga, cuda)).sum().add_((b.float() * t(gb, cuda)).sum()).backward()
     tol_close(tX.grad.float().cpu().numpy(), O.spmm(rowptr, col, v_np, ga.astype(np.float64)), *tol)
     tol_close(tY.grad.float().cpu().numpy(), O.spmm_t(rowptr, col, v_np, gb.astype(np.float64), m), *tol)
+
+
+def test_edge_attention_fused_backward_slot_order(cuda, msha):
+    """A graph whose de scratch (E x H fp32) exceeds 192 MB: the fused backward keeps
+    de in CSC slot order (written contiguously, gathered through graph.csr_slot by the
+    row sum).  Same bits as the split backward for u, d_el, d_er; d_hc within the
+    reordered-sum bound."""
+    import bench
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    n, e, H, F = 400_000, 6_400_000, 8, 16
+    assert e * 4 * H >= 192 << 20
+    rowptr, col = bench.synth_graph(n, e, seed=5)
+    graph = Graph.from_csr(rowptr, col, n, cuda)
+    assert graph.desc.csr_slot  # the slot map is built with the CSC view
+    perm = graph.csr_slot[graph.csc_eid.long()]
+    assert torch.equal(perm, torch.arange(e, dtype=torch.int32, device=cuda))
+    rng = np.random.default_rng(2)
+    el = rng.standard_normal((n, H)).astype(np.float32)
+    er = rng.standard_normal((n, H)).astype(np.float32)
+    hc = rng.standard_normal((n, H, F)).astype(np.float32)
+    dU = rng.standard_normal((n, H, F)).astype(np.float32)
+    got = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, True)
+    split = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, False)
+    _same_as_split(got, split)
