@@ -107,11 +107,16 @@ __global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
   const int tiles = (M + 15) / 16;
   if (gw >= tiles) return;
 
+  // buffer-descriptor loads: a row past M (or a tile past the last) reads 0 without a
+  // branch, so the prefetch is unconditional and the waits on it stay exact (a load
+  // under "if (t + nw < tiles)" made the join wait on the tile just issued)
+  const rsrc_t r_x = make_rsrc(X, (uint32_t)((int64_t)M * K * sizeof(T)));
   auto load_tile = [&](int t, u32x4_t* raw) {
-    const int row = min(t * 16 + r16, M - 1);
-    const T* p = X + (int64_t)row * K + g * G::KL;
+    const int row = t * 16 + r16;
+    const uint32_t off = row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) +
+                                       (uint32_t)(g * G::KL * sizeof(T)) : kOOB;
 #pragma unroll
-    for (int i = 0; i < G::NLD; ++i) raw[i] = *reinterpret_cast<const u32x4_t*>(p + i * G::EPL);
+    for (int i = 0; i < G::NLD; ++i) raw[i] = buf_b128(r_x, off + 16u * i);
   };
   // one tile: MFMAs over the resident W (B operands of step s + 1 read from LDS while
   // step s's MFMAs issue), then the epilogue
@@ -216,10 +221,12 @@ __global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
   u32x4_t bufA[G::NLD], bufB[G::NLD];
   load_tile(gw, bufA);
   for (int t = gw; t < tiles; t += 2 * nw) {
-    if (t + nw < tiles) load_tile(t + nw, bufB);
+    load_tile(t + nw, bufB);
+    __builtin_amdgcn_sched_barrier(0);
     tile(t, bufA);
     if (t + nw >= tiles) break;
-    if (t + 2 * nw < tiles) load_tile(t + 2 * nw, bufA);
+    load_tile(t + 2 * nw, bufA);
+    __builtin_amdgcn_sched_barrier(0);
     tile(t + nw, bufB);
   }
 }
@@ -233,7 +240,10 @@ __global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
 // column blocks u = 0..1 (dW column 64 nh + 2i + u).  v_mfma_f32_32x32x2_f32, k = q.
 // Block = 8 waves: column half nh = w & 1, row quarter w >> 1 of the block's rows.
 constexpr int kWgWaves = 8;
-constexpr int kWgPD = 4;    // two-row steps per load batch (two batches in flight)
+#ifndef WG_PD
+#define WG_PD 2
+#endif
+constexpr int kWgPD = WG_PD;  // two-row steps per load batch (two batches in flight)
 constexpr int kWgPitch = 132;
 
 template <bool HO>
@@ -314,16 +324,24 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[t], d[u], acc[t][u], 0, 0, 0);
     }
   };
-  // double-buffered loads: batch i + 1's loads are issued before batch i's MFMAs
-  // (kWgPD x 8 MFMAs of 64 cycles), and the other wave of the SIMD covers the rest.
-  // One compute body per trip: the accumulators keep one register assignment.
+  // double-buffered loads in two named batches (no register copy between them: a
+  // "cur = next" copy made the compiler wait for the loads it had just issued): batch
+  // B's loads leave before batch A's MFMAs (kWgPD x 8 MFMAs of 64 cycles) and vice
+  // versa, and the other wave of the SIMD covers the rest.
   constexpr int R = 2 * kWgPD;
-  Batch nb;
-  load(r0, nb);
-  for (int rb = r0; rb < r1; rb += R) {
-    const Batch cb = nb;
-    load(rb + R, nb);  // past r1: masked (reads 0)
-    compute(rb, cb);
+  Batch ba, bb;
+  load(r0, ba);
+  for (int rb = r0; rb < r1; rb += 2 * R) {
+    // sched_barrier: the scheduler may not sink a batch's loads below the other
+    // batch's MFMAs (it did, and the loop then waited on loads just issued)
+    load(rb + R, bb);  // past r1: masked (reads 0, adds 0)
+    __builtin_amdgcn_sched_barrier(0);
+    compute(rb, ba);
+    __builtin_amdgcn_sched_barrier(0);
+    load(rb + 2 * R, ba);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(rb + R, bb);
+    __builtin_amdgcn_sched_barrier(0);
   }
   // ---- block sum (LDS): the 4 row quarters of each column half added in quarter order
   // 32x32 C layout: reg v of lane l is row 8 (v / 4) + 4 (l >> 5) + (v % 4), col l & 31
@@ -419,7 +437,7 @@ int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, con
                    const float* al, const float* ar, void* h, float* el, float* er,
                    hipStream_t s) {
   const int64_t N = (int64_t)heads * feat;
-  if (!skinny_enabled() || M < 1024 || M >= (1ll << 31)) return 0;
+  if (!skinny_enabled() || M < 1024 || M * K * (int64_t)sizeof(T) >= (1ll << 31)) return 0;
   if (((uintptr_t)X | (uintptr_t)W | (uintptr_t)h) & 15) return 0;
   const bool score = al != nullptr || ar != nullptr;
   const int minfe = 16 / (int)sizeof(T);
