@@ -13,8 +13,14 @@ Inputs are resident in HBM before the timed region.  For N > 1 GPUs the path
 does not shard (SURVEY.md §8e "replicas only"): every rank runs its own replica
 and value = total edges over all ranks / max-over-ranks time ("scaling": "weak").
 
+The K timed steps run twice: eagerly, with HIP events around every edge-kernel launch
+(the rooflines), then as ONE replay of a HIP graph that holds exactly those K steps
+(the headline value: same kernels and work, without the host launch gaps of Python
+autograd; ``--eager`` reports the eager pass instead).  Both are bracketed by a
+barrier + synchronize and maxed over ranks.
+
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP
-events around every launch of it inside the timed region) and the CPU baseline
+events around every launch of it inside the eager timed region) and the CPU baseline
 (the oracle's C restatement, timed on this host's cores, rank 0, N=1 only).
 """
 from __future__ import annotations
@@ -395,6 +401,8 @@ def main():
     ap.add_argument("--no-link-score", action="store_true")
     ap.add_argument("--no-r15", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="report the eager launches (no HIP-graph replay of the timed steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -424,6 +432,35 @@ def main():
             tdist.barrier()
         torch.cuda.synchronize(dev)
 
+    def max_over_ranks(x):
+        if dist:
+            tt = torch.tensor([x], device=dev)
+            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+            x = float(tt.item())
+        return x
+
+    def timed_graph(lay, steps):
+        """Max-over-ranks seconds of ONE replay of a HIP graph holding exactly `steps`
+        steps (captured after the eager pass, which warmed every cache; one untimed
+        replay first).  Same kernels, same work as the eager steps without the host
+        launch gaps (~2-10 us per launch, Python autograd).  None if capture fails."""
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(steps):
+                    lay.step()
+            g.replay()
+        except RuntimeError as ex:  # report the eager number instead
+            print(f"graph capture failed: {ex}", file=sys.stderr)
+            return None
+        barrier()
+        t0 = time.perf_counter()
+        g.replay()
+        barrier()
+        dt_ = max_over_ranks(time.perf_counter() - t0)
+        del g
+        return dt_
+
     def timed(lay, steps, warmup):
         """(max-over-ranks seconds for `steps` steps, mean fwd-kernel ms, launches)"""
         for _ in range(warmup):
@@ -441,10 +478,7 @@ def main():
               for name, lst in evs.items() if lst}
         events = evs.get("edge_attention_fwd", [])
         k = ms.get("edge_attention_fwd", float("nan"))
-        if dist:
-            tt = torch.tensor([dt_], device=dev)
-            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-            dt_ = float(tt.item())
+        dt_ = max_over_ranks(dt_)
         lay.kernel_ms = ms
         return dt_, k, len(events)
 
@@ -467,20 +501,29 @@ def main():
                         "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
         return out
 
-    dt, k_ms, n_launch = timed(layer, args.steps, args.warmup)
+    dt_eager, k_ms, n_launch = timed(layer, args.steps, args.warmup)
+    dt_graph = None if args.eager else timed_graph(layer, args.steps)
+    dt = dt_graph if dt_graph is not None else dt_eager
+    timing = ("value: one replay of a HIP graph holding exactly `steps` steps (captured after "
+              "the eager pass); roofline: HIP events around every launch over the eager timed "
+              "region of the same steps" if dt_graph is not None else
+              "value and roofline: eager launches, HIP events around every launch")
     bf16_leg = None
     if not args.no_bf16:
         # config C3: the same layer with bf16 tables / projection (bf16 MFMA)
         lay16 = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank, dtype=torch.bfloat16,
                       graph=layer.graph)
-        dt16, k16, n16 = timed(lay16, args.steps, args.warmup)
+        dt16e, k16, n16 = timed(lay16, args.steps, args.warmup)
+        dt16g = None if args.eager else timed_graph(lay16, args.steps)
+        dt16 = dt16g if dt16g is not None else dt16e
         fb16 = fwd_bytes(n, m, e, H, F, s=2)
         a16 = fb16 / (k16 * 1e-3) / 1e9
         tr16, src16 = pmc_traffic(H, F, True, args.workload)
         bf16_leg = {"workload": f"gat_layer_{args.workload} (config C3: bf16 tables, bf16 MFMA "
                                 "projection, fp32 scores/softmax)",
                     "value": world * e * args.steps / dt16, "unit": "edges/s",
-                    "ms_per_step": dt16 / args.steps * 1e3, "dtype": "bf16",
+                    "ms_per_step": dt16 / args.steps * 1e3,
+                    "ms_per_step_eager": dt16e / args.steps * 1e3, "dtype": "bf16",
                     "roofline": {"kernel": "msha_edge_attention_fwd<bf16>", "bound": "hbm",
                                  "achieved": a16, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": a16 / HBM_PEAK_GBS, "traffic": tr16,
@@ -506,6 +549,7 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "ms_per_step_eager": dt_eager / args.steps * 1e3, "timing": timing,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": f"gat_layer_{args.workload}", "nodes": n, "cols": m, "edges": e,
