@@ -201,7 +201,8 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
     W = (torch.randn(hidden, F, generator=g) * F ** -0.5).to(dev, dtype)
     b = torch.randn(hidden, generator=g).to(dev)
     plo, phi = sharding.pair_range(n_pairs, world, rank)
-    out_mlp = torch.empty(phi - plo, hidden, device=dev)
+    # a bf16 LinkPredictor returns bf16 scores (torch semantics); fp32 table: fp32
+    out_mlp = torch.empty(phi - plo, hidden, device=dev, dtype=dtype)
     out_inner = torch.empty(phi - plo, device=dev)
     if dist:
         import torch.distributed as tdist
@@ -237,6 +238,7 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
     res["allgather_ms"] = (time.perf_counter() - t0) / steps * 1e3
     res.update(pairs_per_batch=n_pairs, feat=F, hidden=hidden, world=world,
                dtype="bf16" if dtype == torch.bfloat16 else "f32",
+               mlp_scores_dtype="bf16" if dtype == torch.bfloat16 else "f32",
                sharding="h rows all-gathered over RCCL (all_gather_into_tensor), pairs split "
                "contiguously per rank" if dist else "single GPU (no collective)")
     return res

@@ -318,6 +318,16 @@ MSHA_API int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, const 
                                    const int64_t* gj, const void* W, const float* bias,
                                    int32_t act, float drop_p, uint64_t seed, uint64_t offset,
                                    float* out, msha_stream_t stream);
+/* The same with the output dtype chosen (MSHA_DTYPE_F32 or MSHA_DTYPE_BF16): a bf16
+ * LinkPredictor in PyTorch returns bf16 scores, and the (n_pairs, N) output is the
+ * dominant byte stream of the scorer.  The epilogue (bias, ReLU, dropout, sigmoid) runs
+ * in fp32 and rounds once. */
+MSHA_API int msha_pair_linear_bf16_ex(int64_t n_pairs, int64_t K, int64_t N, const void* G,
+                                      int64_t ldg, const int64_t* gi, const void* G2,
+                                      int64_t ldg2, const int64_t* gj, const void* W,
+                                      const float* bias, int32_t act, float drop_p,
+                                      uint64_t seed, uint64_t offset, int32_t out_dtype,
+                                      void* out, msha_stream_t stream);
 
 /* ------------------------------------------------- BatchNorm + LeakyReLU --- */
 /* Ablation.py:273-274 / Ours.py:100-101 epilogue: y = lrelu(bn(x)) on (rows, channels)

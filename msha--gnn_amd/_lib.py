@@ -96,6 +96,8 @@ SIGNATURES = {
     "msha_pair_inner_fwd_bf16": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
     "msha_pair_linear_bf16": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64,
                                         U64, P, P]),
+    "msha_pair_linear_bf16_ex": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32,
+                                           U64, U64, I32, P, P]),
     "msha_pair_inner_bwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P, P]),
     "msha_pair_mlp_dz": (C.c_int, [I64, P, P, F32, I32, P, P]),
     "msha_pair_hadamard": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P]),

@@ -495,14 +495,17 @@ extern "C" int msha_project_scores_bf16(int64_t M, int64_t K, int32_t heads, int
   return check_launch("project_scores_bf16");
 }
 
-extern "C" int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, const void* G,
-                                     int64_t ldg, const int64_t* gi, const void* G2,
-                                     int64_t ldg2, const int64_t* gj, const void* W,
-                                     const float* bias, int32_t act, float drop_p, uint64_t seed,
-                                     uint64_t offset, float* out, msha_stream_t stream) {
+extern "C" int msha_pair_linear_bf16_ex(int64_t n_pairs, int64_t K, int64_t N, const void* G,
+                                        int64_t ldg, const int64_t* gi, const void* G2,
+                                        int64_t ldg2, const int64_t* gj, const void* W,
+                                        const float* bias, int32_t act, float drop_p,
+                                        uint64_t seed, uint64_t offset, int32_t out_dtype,
+                                        void* out, msha_stream_t stream) {
   MSHA_ARG_CHECK(n_pairs > 0 && K > 0 && N > 0, "pair_linear_bf16: bad sizes");
   MSHA_ARG_CHECK(G && W && out, "pair_linear_bf16: null pointer");
   MSHA_ARG_CHECK(!(act & ACT_BIAS) || bias, "pair_linear_bf16: bias missing");
+  MSHA_ARG_CHECK(out_dtype == MSHA_DTYPE_F32 || out_dtype == MSHA_DTYPE_BF16,
+                 "pair_linear_bf16: out dtype must be fp32 or bf16");
   MSHA_ARG_CHECK(K % 8 == 0 && N % 8 == 0 && ldg % 8 == 0 && (G2 == nullptr || ldg2 % 8 == 0) &&
                      al16(G) && (G2 == nullptr || al16(G2)) && al16(W) && al16(out),
                  "pair_linear_bf16: K, N, ld multiples of 8 and 16-byte aligned tables");
@@ -513,7 +516,7 @@ extern "C" int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, cons
   p.gi = gi; p.gj = gj; p.G2 = (const bf16_t*)G2; p.ldg2 = G2 ? ldg2 : ldg;
   p.hadamard = G2 != nullptr || gj != nullptr;
   p.B = (const bf16_t*)W; p.sBk = 1; p.sBn = K;  // nn.Linear weight (N x K)
-  p.C = out; p.ldc = N; p.c_bf16 = 0;
+  p.C = out; p.ldc = N; p.c_bf16 = out_dtype == MSHA_DTYPE_BF16;
   p.act = act; p.bias = bias;
   p.dp = make_dropout(drop_p, seed, offset);
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
@@ -521,4 +524,13 @@ extern "C" int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, cons
   hipLaunchKernelGGL((gemm_bf16_kernel<EPI_ACT, 0, 1, 1, HO_NONE, true>), grid, dim3(256), 0,
                      (hipStream_t)stream, p);
   return check_launch("pair_linear_bf16");
+}
+
+extern "C" int msha_pair_linear_bf16(int64_t n_pairs, int64_t K, int64_t N, const void* G,
+                                     int64_t ldg, const int64_t* gi, const void* G2,
+                                     int64_t ldg2, const int64_t* gj, const void* W,
+                                     const float* bias, int32_t act, float drop_p, uint64_t seed,
+                                     uint64_t offset, float* out, msha_stream_t stream) {
+  return msha_pair_linear_bf16_ex(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, W, bias, act, drop_p,
+                                  seed, offset, MSHA_DTYPE_F32, out, stream);
 }

@@ -691,11 +691,12 @@ def pair_layer(x_i, x_j, W, b, p=0.0, training=False, sigmoid=False, seed=None):
     return _PairLayer.apply(x_i, x_j, W, b, p, seed, sigmoid)
 
 
-def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None):
+def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None, out_dtype=None):
     """Fused caller gather + predictor (LLP.py:233 + LLP.py:104-115), inference:
     ``predictor(h[src], h[dst])`` without materialising the gathered rows.
     'inner' -> (P,), 'mlp' (one used Linear W (hidden, F), b) -> (P, hidden).
-    A bf16 ``h`` runs the bf16 kernels (bf16 MFMA for 'mlp'; fp32 scores)."""
+    A bf16 ``h`` runs the bf16 kernels (bf16 MFMA for 'mlp'; fp32 scores, or bf16
+    'mlp' scores with ``out_dtype=torch.bfloat16``, as a bf16 LinkPredictor returns)."""
     _lib.require_cuda(h, src, dst)
     dt = _table_dtype(h)
     h = _tc(h, dt)
@@ -712,6 +713,13 @@ def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None):
         return out
     W, b = _tc(W, dt), _f32c(b)
     N = W.shape[0]
+    if bf and (out_dtype == BF16 or (out is not None and out.dtype == BF16)):
+        out = torch.empty(P, N, device=h.device, dtype=BF16) if out is None else out
+        _lib.call("msha_pair_linear_bf16_ex", P, Fd, N, h.data_ptr(), h.stride(0),
+                  src.data_ptr(), h.data_ptr(), h.stride(0), dst.data_ptr(), W.data_ptr(),
+                  b.data_ptr(), ACT_BIAS | ACT_RELU | ACT_SIGMOID, 0.0, 0, 0, 1,
+                  out.data_ptr(), s)
+        return out
     out = torch.empty(P, N, device=h.device, dtype=torch.float32) if out is None else out
     _lib.call("msha_pair_linear_bf16" if bf else "msha_pair_linear", P, Fd, N, h.data_ptr(),
               h.stride(0), src.data_ptr(), h.data_ptr(), h.stride(0), dst.data_ptr(),

@@ -247,4 +247,9 @@ def test_score_pairs_bf16(cuda, mode):
         got = MF.score_pairs(th, ts, td, "mlp", t(W, cuda, BF), t(b, cuda)).cpu().numpy()
         z = (hd[src] * hd[dst]) @ W.T.astype(np.float64) + b
         ref = 1 / (1 + np.exp(-np.maximum(z, 0)))
+        # bf16 scores (what a bf16 LinkPredictor returns): the fp32 epilogue rounded once
+        g16 = MF.score_pairs(th, ts, td, "mlp", t(W, cuda, BF), t(b, cuda), out_dtype=BF)
+        assert g16.dtype == BF
+        assert torch.equal(g16, torch.as_tensor(got, device=cuda).to(BF))
+        tol_close(g16.float().cpu().numpy(), ref, 1e-2, 1e-2)
     tol_close(got, ref, 1e-2, 1e-2)
