@@ -781,7 +781,9 @@ extern "C" int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const flo
   p.act = act; p.bias = bias;
   p.dp = make_dropout(drop_p, seed, offset);
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
-  launch<A_GATHER_HADAMARD, EPI_ACT, 0>(p, 1, (hipStream_t)stream);
+  if (!skinny_pair_linear(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, W, bias, p.act, p.dp, out,
+                          (hipStream_t)stream))
+    launch<A_GATHER_HADAMARD, EPI_ACT, 0>(p, 1, (hipStream_t)stream);
   return check_launch("pair_linear");
 }
 

@@ -231,6 +231,132 @@ __global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
   }
 }
 
+// ------------------------------------------------------ pair linear (LLP 'mlp') ---
+// out[p, n] = act(sum_k G[gi[p], k] G2[gj[p], k] Wlin[n, k] + b[n]) for the link scorer
+// (LLP.py:104-115 with the caller's gather LLP.py:233): the projection's structure with
+// the A rows gathered and multiplied (x_i (.) x_j) at the MFMA step, nn.Linear's W
+// transposed into the resident LDS image, and the activation epilogue of gemm.hip
+// (same bits: bias, ReLU, dropout keyed on p * N + n, sigmoid).  Row indices are
+// loaded one tile ahead of the row gathers they address; rows past the batch clamp to
+// its last pair (valid addresses, never stored), so the prefetch needs no branch.
+enum : int { SK_BIAS = 1, SK_RELU = 2, SK_DROPOUT = 4, SK_SIGMOID = 8 };  // gemm.hip ACT_*
+
+template <int K, int N>
+__global__ void __launch_bounds__(64 * kProjWaves) pair_kernel(
+    int M, const float* __restrict__ G, int64_t ldg, const int64_t* __restrict__ gi,
+    const float* __restrict__ G2, int64_t ldg2, const int64_t* __restrict__ gj,
+    const float* __restrict__ Wlin, const float* __restrict__ bias, int act, Dropout dp,
+    float* __restrict__ out) {
+  using Gm = ProjGeo<float, K, N>;
+  __shared__ __attribute__((aligned(16))) char smem[Gm::WBYTES + kProjWaves * Gm::SBYTES];
+  float* Wl = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // ---- B[k][n] = Wlin[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL
+  for (int idx = tid; idx < K * N; idx += 64 * kProjWaves) {
+    const int n = idx / K, k = idx % K;
+    Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = Wlin[idx];
+  }
+  __syncthreads();
+
+  float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
+  const int cl = (lane % Gm::LPR) * Gm::EPL;
+  float bv[Gm::EPL];
+#pragma unroll
+  for (int u = 0; u < Gm::EPL; ++u) bv[u] = (act & SK_BIAS) ? bias[cl + u] : 0.f;
+  const uint64_t doff = (act & SK_DROPOUT) ? dropout_offset(dp, dp.offset) : 0;
+
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kProjWaves;
+  const int tiles = (M + 15) / 16;
+  if (gw >= tiles) return;
+
+  auto load_idx = [&](int t, int64_t& a, int64_t& b) {
+    const int row = min(t * 16 + r16, M - 1);
+    a = gi[row];
+    b = gj[row];
+  };
+  auto load_rows = [&](int64_t a, int64_t b, u32x4_t* ri, u32x4_t* rj) {
+    const float* pa = G + a * ldg + g * Gm::KL;
+    const float* pb = G2 + b * ldg2 + g * Gm::KL;
+#pragma unroll
+    for (int i = 0; i < Gm::NLD; ++i) {
+      ri[i] = *reinterpret_cast<const u32x4_t*>(pa + 4 * i);
+      rj[i] = *reinterpret_cast<const u32x4_t*>(pb + 4 * i);
+    }
+  };
+  auto tile = [&](int t, const u32x4_t* ci, const u32x4_t* cj) {
+    f32x4 acc[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* Wf = Wl + g * Gm::PW + r16;
+    float bc[Gm::NB], bn[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) bc[c] = Wf[c * 16];
+#pragma unroll
+    for (int s = 0; s < Gm::S; ++s) {
+      if (s + 1 < Gm::S) {
+#pragma unroll
+        for (int c = 0; c < Gm::NB; ++c) bn[c] = Wf[4 * (s + 1) * Gm::PW + c * 16];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const float a = __uint_as_float(ci[s >> 2][s & 3]) * __uint_as_float(cj[s >> 2][s & 3]);
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c) bc[c] = bn[c];
+    }
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * Gm::TPS + c * 16 + r16] = acc[c][i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pass = 0; pass < 16 / Gm::RPP; ++pass) {
+      const int rr = pass * Gm::RPP + lane / Gm::LPR;
+      const int row = t * 16 + rr;
+      const float4 v = *reinterpret_cast<const float4*>(Tw + rr * Gm::TPS + cl);
+      float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float x = e[u] + bv[u];
+        if (act & SK_RELU) x = fmaxf(x, 0.f);
+        if (act & SK_DROPOUT)
+          x *= philox_x(dp.seed, doff, (uint64_t)row * N + cl + u) >= dp.threshold ? dp.scale
+                                                                                   : 0.f;
+        if (act & SK_SIGMOID) x = 1.f / (1.f + __expf(-x));
+        e[u] = x;
+      }
+      if (row < M)
+        *reinterpret_cast<float4*>(out + (int64_t)row * N + cl) = make_float4(e[0], e[1], e[2], e[3]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  };
+  u32x4_t ai[Gm::NLD], aj[Gm::NLD], bi[Gm::NLD], bj[Gm::NLD];
+  int64_t xa, xb;
+  load_idx(gw, xa, xb);
+  load_rows(xa, xb, ai, aj);
+  load_idx(gw + nw, xa, xb);
+  for (int t = gw; t < tiles; t += 2 * nw) {
+    load_rows(xa, xb, bi, bj);  // tile t + nw (clamped: valid rows, never stored)
+    load_idx(t + 2 * nw, xa, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t, ai, aj);
+    if (t + nw >= tiles) break;
+    load_rows(xa, xb, ai, aj);  // tile t + 2 nw
+    load_idx(t + 3 * nw, xa, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t + nw, bi, bj);
+  }
+}
+
 // ------------------------------------------------------------- weight gradient ---
 // dW[a, n] = sum_r X[r, a] * (D[r, n] + d1[r, n / hF] a1[n] + d2[r, n / hF] a2[n]),
 // a, n < 128.  A wave owns one column half nh (64 columns) of dW for a row range:
@@ -462,6 +588,27 @@ template int skinny_project<float>(int64_t, int64_t, int, int, const void*, cons
                                    const float*, const float*, void*, float*, float*, hipStream_t);
 template int skinny_project<bf16_t>(int64_t, int64_t, int, int, const void*, const void*,
                                     const float*, const float*, void*, float*, float*, hipStream_t);
+
+// pair linear on the resident-W kernel: fp32, both gathers given, K and N in {64, 128},
+// 16-byte aligned rows; 0 = not covered (the caller runs the tiled GEMM)
+int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t ldg,
+                       const int64_t* gi, const float* G2, int64_t ldg2, const int64_t* gj,
+                       const float* W, const float* bias, int act, const Dropout& dp, float* out,
+                       hipStream_t s) {
+  if (!skinny_enabled() || P < 1024 || P >= (1ll << 31) || gi == nullptr || gj == nullptr) return 0;
+  if (G2 == nullptr) { G2 = G; ldg2 = ldg; }
+  if (ldg % 4 || ldg2 % 4 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)out) & 15)) return 0;
+  const dim3 grid(proj_grid(P)), block(64 * sk::kProjWaves);
+#define SKPL(k, n)                                                                              \
+  if (K == k && N == n) {                                                                       \
+    hipLaunchKernelGGL((sk::pair_kernel<k, n>), grid, block, 0, s, (int)P, G, ldg, gi, G2,     \
+                       ldg2, gj, W, bias, act, dp, out);                                        \
+    return 1;                                                                                   \
+  }
+  SKPL(128, 128) SKPL(64, 128) SKPL(128, 64) SKPL(64, 64)
+#undef SKPL
+  return 0;
+}
 
 // dW (128 x 128, fp32) = X^T D' over K rows: A = X^T given as (A, sAm = 1, sAk = ldx),
 // B = D' = D (+ head outer) given as (B, sBk = ldd, sBn = 1).  Uses the caller's split-K

@@ -598,3 +598,31 @@ def test_edge_attention_fused_backward_slot_order(cuda, msha):
     got = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, True)
     split = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, False)
     _same_as_split(got, split)
+
+
+@pytest.mark.parametrize("K,N", [(128, 128), (64, 128), (128, 64)])
+def test_pair_linear_resident_w(cuda, msha, K, N):
+    """msha_pair_linear on the resident-W kernel (skinny.hip pair_kernel: fp32, both
+    gathers, P >= 1024): hadamard of the gathered rows @ W^T + b, ReLU, dropout keyed on
+    p * N + n (the library's Philox mask), sigmoid -- vs the oracle with that mask; a
+    ragged last tile (P % 16 != 0)."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(K + N)
+    n, P, p, seed = 3000, 4099, 0.5, 123
+    h = rng.standard_normal((n, K)).astype(np.float32)
+    src, dst = rng.integers(0, n, P), rng.integers(0, n, P)
+    W = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    th, ts, td = t(h, cuda), t(src, cuda, torch.int64), t(dst, cuda, torch.int64)
+    tW, tb = t(W, cuda), t(b, cuda)
+    out = torch.empty(P, N, device=cuda)
+    act = MF.ACT_BIAS | MF.ACT_RELU | MF.ACT_DROPOUT | MF.ACT_SIGMOID
+    _lib.call("msha_pair_linear", P, K, N, th.data_ptr(), K, ts.data_ptr(), th.data_ptr(), K,
+              td.data_ptr(), tW.data_ptr(), tb.data_ptr(), act, p, seed, 0, out.data_ptr(),
+              _lib.stream_handle(cuda))
+    keep = MF.dropout_keep_mask(P * N, p, seed, cuda).cpu().numpy().reshape(P, N)
+    z = np.maximum((h[src].astype(np.float64) * h[dst]) @ W.T.astype(np.float64) + b, 0)
+    ref = 1 / (1 + np.exp(-(z * keep / (1 - p))))
+    tol_close(out.cpu().numpy(), ref, 1e-5, 1e-6)
