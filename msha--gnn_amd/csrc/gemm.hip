@@ -467,7 +467,10 @@ static bool vec_ok(const GemmArgs& p) {
 // each row group strides the block's rows with 16-byte loads; the row groups are
 // added in a fixed LDS tree, and a second pass adds the block partials in block
 // order (deterministic).
-constexpr int kColsumRows = 128;
+#ifndef COLSUM_ROWS
+#define COLSUM_ROWS 128
+#endif
+constexpr int kColsumRows = COLSUM_ROWS;
 
 // N consecutive elements of one row, widened to fp32
 template <int N>
@@ -535,11 +538,14 @@ __global__ void __launch_bounds__(256) head_colsum_partial_kernel(
     }
     __syncthreads();
   }
+  // partials transposed, [which][d][block]: the reduce reads each output's blocks
+  // contiguously
   if (rg == 0 && q < QD) {
+    const int64_t nb = gridDim.x;
 #pragma unroll
     for (int e = 0; e < N; ++e) {
-      part[((int64_t)blockIdx.x * 2 + 0) * D + N * q + e] = red[qi].v[e];
-      part[((int64_t)blockIdx.x * 2 + 1) * D + N * q + e] = red[256 + qi].v[e];
+      part[((int64_t)0 * D + N * q + e) * nb + blockIdx.x] = red[qi].v[e];
+      part[((int64_t)1 * D + N * q + e) * nb + blockIdx.x] = red[256 + qi].v[e];
     }
   }
 }
@@ -557,12 +563,13 @@ __global__ void __launch_bounds__(256) head_colsum_reduce_kernel(int nblk, int D
   float* out = which == 0 ? out1 : out2;
   if (out == nullptr) return;
   float s0 = 0.f, s1 = 0.f;
+  const float* src = part + ((int64_t)which * D + d) * nblk;
   int b = lane;
   for (; b + 64 < nblk; b += 128) {
-    s0 += part[((int64_t)b * 2 + which) * D + d];
-    s1 += part[((int64_t)(b + 64) * 2 + which) * D + d];
+    s0 += src[b];
+    s1 += src[b + 64];
   }
-  if (b < nblk) s0 += part[((int64_t)b * 2 + which) * D + d];
+  if (b < nblk) s0 += src[b];
   float v = s0 + s1;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
