@@ -266,6 +266,10 @@ int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t 
                        const int64_t* gi, const float* G2, int64_t ldg2, const int64_t* gj,
                        const float* W, const float* bias, int act, const Dropout& dp, float* out,
                        hipStream_t s);
+int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int64_t ldg,
+                            const int64_t* gi, const void* G2, int64_t ldg2, const int64_t* gj,
+                            const void* W, const float* bias, int act, const Dropout& dp,
+                            void* out, bool out_bf16, hipStream_t s);
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,

@@ -520,6 +520,9 @@ extern "C" int msha_pair_linear_bf16_ex(int64_t n_pairs, int64_t K, int64_t N, c
   p.act = act; p.bias = bias;
   p.dp = make_dropout(drop_p, seed, offset);
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
+  if (skinny_pair_linear_bf16(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, W, bias, p.act, p.dp, out,
+                              p.c_bf16 != 0, (hipStream_t)stream))
+    return check_launch("pair_linear_bf16");
   const dim3 grid((unsigned)((n_pairs + BM - 1) / BM), (unsigned)((N + BN - 1) / BN), 1);
   hipLaunchKernelGGL((gemm_bf16_kernel<EPI_ACT, 0, 1, 1, HO_NONE, true>), grid, dim3(256), 0,
                      (hipStream_t)stream, p);

@@ -357,6 +357,137 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_kernel(
   }
 }
 
+// bf16 tables (config C5): the same structure on v_mfma_f32_16x16x32_bf16.  The hadamard
+// is rounded to bf16 before the MFMA, as a bf16 x_i * x_j is in PyTorch (and as the
+// tiled bf16 GEMM's gather-hadamard loader does); nn.Linear's (N, K) weight is already
+// the [n][k] image the bf16 B operand reads.  Scores out in fp32 or bf16 (OB).
+template <int K, int N, bool OB>
+__global__ void __launch_bounds__(64 * kProjWaves) pair_bf16_kernel(
+    int M, const bf16_t* __restrict__ G, int64_t ldg, const int64_t* __restrict__ gi,
+    const bf16_t* __restrict__ G2, int64_t ldg2, const int64_t* __restrict__ gj,
+    const bf16_t* __restrict__ Wlin, const float* __restrict__ bias, int act, Dropout dp,
+    void* __restrict__ out) {
+  using Gm = ProjGeo<bf16_t, K, N>;
+  __shared__ __attribute__((aligned(16))) char smem[Gm::WBYTES + kProjWaves * Gm::SBYTES];
+  bf16_t* Wl = reinterpret_cast<bf16_t*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+
+  for (int idx = tid; idx < N * K / 8; idx += 64 * kProjWaves) {
+    const int n = idx / (K / 8), k8 = idx % (K / 8);
+    *reinterpret_cast<uint4*>(Wl + n * Gm::PW + 8 * k8) =
+        *reinterpret_cast<const uint4*>(Wlin + (int64_t)n * K + 8 * k8);
+  }
+  __syncthreads();
+
+  float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
+  const int cl = (lane % Gm::LPR) * Gm::EPL;
+  float bv[Gm::EPL];
+#pragma unroll
+  for (int u = 0; u < Gm::EPL; ++u) bv[u] = (act & SK_BIAS) ? bias[cl + u] : 0.f;
+  const uint64_t doff = (act & SK_DROPOUT) ? dropout_offset(dp, dp.offset) : 0;
+
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kProjWaves;
+  const int tiles = (M + 15) / 16;
+  if (gw >= tiles) return;
+
+  auto load_idx = [&](int t, int64_t& a, int64_t& b) {
+    const int row = min(t * 16 + r16, M - 1);
+    a = gi[row];
+    b = gj[row];
+  };
+  auto load_rows = [&](int64_t a, int64_t b, u32x4_t* ri, u32x4_t* rj) {
+    const bf16_t* pa = G + a * ldg + g * Gm::KL;
+    const bf16_t* pb = G2 + b * ldg2 + g * Gm::KL;
+#pragma unroll
+    for (int i = 0; i < Gm::NLD; ++i) {
+      ri[i] = *reinterpret_cast<const u32x4_t*>(pa + 8 * i);
+      rj[i] = *reinterpret_cast<const u32x4_t*>(pb + 8 * i);
+    }
+  };
+  auto tile = [&](int t, const u32x4_t* ci, const u32x4_t* cj) {
+    f32x4 acc[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* Wb = Wl + r16 * Gm::PW + g * Gm::KL;
+#pragma unroll
+    for (int s = 0; s < Gm::S; ++s) {
+      bf16x8 bc[Gm::NB];
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c)
+        bc[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * Gm::PW + 8 * s);
+      // x_i (.) x_j rounded to bf16
+      const Pk<bf16_t> xa = pk_from_raw(ci[s], (bf16_t*)nullptr);
+      const Pk<bf16_t> xb = pk_from_raw(cj[s], (bf16_t*)nullptr);
+      bf16x8 a;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = (bf16_t)(xa.v[e] * xb.v[e]);
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bc[c], acc[c], 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * Gm::TPS + c * 16 + r16] = acc[c][i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pass = 0; pass < 16 / Gm::RPP; ++pass) {
+      const int rr = pass * Gm::RPP + lane / Gm::LPR;
+      const int row = t * 16 + rr;
+      float e[Gm::EPL];
+#pragma unroll
+      for (int u = 0; u < Gm::EPL; u += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(Tw + rr * Gm::TPS + cl + u);
+        e[u] = v.x; e[u + 1] = v.y; e[u + 2] = v.z; e[u + 3] = v.w;
+      }
+#pragma unroll
+      for (int u = 0; u < Gm::EPL; ++u) {
+        float x = e[u] + bv[u];
+        if (act & SK_RELU) x = fmaxf(x, 0.f);
+        if (act & SK_DROPOUT)
+          x *= philox_x(dp.seed, doff, (uint64_t)row * N + cl + u) >= dp.threshold ? dp.scale
+                                                                                   : 0.f;
+        if (act & SK_SIGMOID) x = 1.f / (1.f + __expf(-x));
+        e[u] = x;
+      }
+      if (row < M) {
+        if constexpr (OB) {
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(out) + (int64_t)row * N + cl) =
+              make_uint4(pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]),
+                         pack_bf16x2(e[4], e[5]), pack_bf16x2(e[6], e[7]));
+        } else {
+          float* o = reinterpret_cast<float*>(out) + (int64_t)row * N + cl;
+          *reinterpret_cast<float4*>(o) = make_float4(e[0], e[1], e[2], e[3]);
+          *reinterpret_cast<float4*>(o + 4) = make_float4(e[4], e[5], e[6], e[7]);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  };
+  u32x4_t ai[Gm::NLD], aj[Gm::NLD], bi[Gm::NLD], bj[Gm::NLD];
+  int64_t xa, xb;
+  load_idx(gw, xa, xb);
+  load_rows(xa, xb, ai, aj);
+  load_idx(gw + nw, xa, xb);
+  for (int t = gw; t < tiles; t += 2 * nw) {
+    load_rows(xa, xb, bi, bj);
+    load_idx(t + 2 * nw, xa, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t, ai, aj);
+    if (t + nw >= tiles) break;
+    load_rows(xa, xb, ai, aj);
+    load_idx(t + 3 * nw, xa, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t + nw, bi, bj);
+  }
+}
+
 // ------------------------------------------------------------- weight gradient ---
 // dW[a, n] = sum_r X[r, a] * (D[r, n] + d1[r, n / hF] a1[n] + d2[r, n / hF] a2[n]),
 // a, n < 128.  A wave owns one column half nh (64 columns) of dW for a row range:
@@ -607,6 +738,32 @@ int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t 
   }
   SKPL(128, 128) SKPL(64, 128) SKPL(128, 64) SKPL(64, 64)
 #undef SKPL
+  return 0;
+}
+
+int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int64_t ldg,
+                            const int64_t* gi, const void* G2, int64_t ldg2, const int64_t* gj,
+                            const void* W, const float* bias, int act, const Dropout& dp,
+                            void* out, bool out_bf16, hipStream_t s) {
+  if (!skinny_enabled() || P < 1024 || P >= (1ll << 31) || gi == nullptr || gj == nullptr) return 0;
+  if (G2 == nullptr) { G2 = G; ldg2 = ldg; }
+  if (ldg % 8 || ldg2 % 8 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)W | (uintptr_t)out) & 15))
+    return 0;
+  const dim3 grid(proj_grid(P)), block(64 * sk::kProjWaves);
+#define SKPB(k, n)                                                                              \
+  if (K == k && N == n) {                                                                       \
+    if (out_bf16)                                                                               \
+      hipLaunchKernelGGL((sk::pair_bf16_kernel<k, n, true>), grid, block, 0, s, (int)P,        \
+                         (const bf16_t*)G, ldg, gi, (const bf16_t*)G2, ldg2, gj,               \
+                         (const bf16_t*)W, bias, act, dp, out);                                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((sk::pair_bf16_kernel<k, n, false>), grid, block, 0, s, (int)P,       \
+                         (const bf16_t*)G, ldg, gi, (const bf16_t*)G2, ldg2, gj,               \
+                         (const bf16_t*)W, bias, act, dp, out);                                 \
+    return 1;                                                                                   \
+  }
+  SKPB(128, 128) SKPB(64, 128) SKPB(128, 64) SKPB(64, 64)
+#undef SKPB
   return 0;
 }
 

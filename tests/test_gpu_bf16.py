@@ -253,3 +253,32 @@ def test_score_pairs_bf16(cuda, mode):
         assert torch.equal(g16, torch.as_tensor(got, device=cuda).to(BF))
         tol_close(g16.float().cpu().numpy(), ref, 1e-2, 1e-2)
     tol_close(got, ref, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_pair_linear_bf16_resident_w(cuda, out_bf16):
+    """msha_pair_linear_bf16_ex on the resident-W bf16 kernel (skinny.hip pair_bf16_kernel,
+    P >= 1024, ragged last tile): bf16(x_i * x_j) @ W^T + b, ReLU, the library's dropout
+    mask, sigmoid -- vs fp64 on the same bf16 operands, 1e-2 (bf16 scores: one more
+    rounding)."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(21)
+    n, K, N, P, p, seed = 2000, 128, 128, 3001, 0.3, 9
+    h = rb(rng.standard_normal((n, K)) * 0.5)
+    src, dst = rng.integers(0, n, P), rng.integers(0, n, P)
+    W = rb(rng.standard_normal((N, K)) / np.sqrt(K))
+    b = rng.standard_normal(N).astype(np.float32) * 0.1
+    th = t(h, cuda, BF)
+    ts, td = torch.as_tensor(src, device=cuda), torch.as_tensor(dst, device=cuda)
+    tW, tb = t(W, cuda, BF), t(b, cuda)
+    out = torch.empty(P, N, device=cuda, dtype=BF if out_bf16 else torch.float32)
+    act = MF.ACT_BIAS | MF.ACT_RELU | MF.ACT_DROPOUT | MF.ACT_SIGMOID
+    _lib.call("msha_pair_linear_bf16_ex", P, K, N, th.data_ptr(), K, ts.data_ptr(),
+              th.data_ptr(), K, td.data_ptr(), tW.data_ptr(), tb.data_ptr(), act, p, seed, 0,
+              1 if out_bf16 else 0, out.data_ptr(), _lib.stream_handle(cuda))
+    keep = MF.dropout_keep_mask(P * N, p, seed, cuda).cpu().numpy().reshape(P, N)
+    had = rb(h[src].astype(np.float32) * h[dst].astype(np.float32)).astype(np.float64)
+    z = np.maximum(had @ W.T.astype(np.float64) + b, 0) * keep / (1 - p)
+    tol_close(out.float().cpu().numpy(), 1 / (1 + np.exp(-z)), 1e-2, 1e-2)
