@@ -22,6 +22,10 @@
 
 #include "common.h"
 
+#ifndef SLAB_U
+#define SLAB_U 8
+#endif
+
 namespace msha {
 
 constexpr int BM = 128, BN = 128, BK = 32, LDA = BK + 2, LDP = 144;
@@ -396,6 +400,21 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restric
     float s0 = 0.f, s1 = 0.f;
     if (t < total) {
       int z = zg;
+      // SLAB_U slab pairs loaded before they are added (same order as one pair per
+      // trip): the loads overlap instead of one L2 round trip per slab
+      for (; z + 4 + 8 * (SLAB_U - 1) < splits; z += 8 * SLAB_U) {
+        float a[SLAB_U], b[SLAB_U];
+#pragma unroll
+        for (int u = 0; u < SLAB_U; ++u) {
+          a[u] = slab[(int64_t)(z + 8 * u) * total + t];
+          b[u] = slab[(int64_t)(z + 8 * u + 4) * total + t];
+        }
+#pragma unroll
+        for (int u = 0; u < SLAB_U; ++u) {
+          s0 += a[u];
+          s1 += b[u];
+        }
+      }
       for (; z + 4 < splits; z += 8) {
         s0 += slab[(int64_t)z * total + t];
         s1 += slab[(int64_t)(z + 4) * total + t];
