@@ -168,7 +168,10 @@ def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
     h2, el = MF.project_scores(s_input, W2, al=a[:, Fd:], heads=H)  # (N, H*F), (N, H)
     u, v = MF.edge_attention(graph, el, er, h1.view(m, H, Fd), hs=h2.view(n, H, Fd),
                              p=heads[0].dropout, training=training)
-    return [head.epilogue(u[:, k], v[:, k]) for k, head in enumerate(heads)]
+    # unbind: the backward stacks the head gradients in one copy (u[:, k] selects would
+    # zero-fill and copy a full (rows, H, F) gradient per head and add them)
+    us, vs = u.unbind(1), v.unbind(1)
+    return [head.epilogue(us[k], vs[k]) for k, head in enumerate(heads)]
 
 
 class ablation3(nn.Module):  # noqa: N801  (reference class name)
@@ -288,7 +291,8 @@ def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_a
                                           training=training, return_aux=True)
     if record:
         _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4)
-    return [head.epilogue(u[:, k], v[:, k]) for k, head in enumerate(heads)]
+    us, vs = u.unbind(1), v.unbind(1)  # one stacked gradient copy (see fused_ours_layer3)
+    return [head.epilogue(us[k], vs[k]) for k, head in enumerate(heads)]
 
 
 def _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4):
