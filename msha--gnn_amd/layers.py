@@ -151,6 +151,13 @@ class OursLayer3(nn.Module):
         return fused_ours_layer3([self], Sinput, Rinput, _graph(inter_adj), self.training)[0]
 
 
+def _score_halves(heads, name):
+    """(H, 2, F) stack of the heads' (2F, 1) score vectors ``name``: [:, 0] = a[:F],
+    [:, 1] = a[F:]."""
+    Fd = heads[0].out_features
+    return torch.stack([getattr(h, name).view(2, Fd) for h in heads])
+
+
 def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
     """All heads of an ablation3 in one launch: projections stacked along features,
     one (H-head) edge-attention forward/backward, per-head BN epilogues."""
@@ -162,10 +169,10 @@ def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
                          f"sources x {m} recipients")
     W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
     W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
-    a = torch.stack([h.a.view(-1) for h in heads])  # (H, 2F)
     # Ablation.py:262-267: a[:F] scores the recipient (column) side h1, a[F:] the source h2
-    h1, er = MF.project_scores(r_input, W1, ar=a[:, :Fd], heads=H)  # (M, H*F), (M, H)
-    h2, el = MF.project_scores(s_input, W2, al=a[:, Fd:], heads=H)  # (N, H*F), (N, H)
+    a_r, a_l = _score_halves(heads, "a").unbind(1)  # (H, F) each
+    h1, er = MF.project_scores(r_input, W1, ar=a_r, heads=H)  # (M, H*F), (M, H)
+    h2, el = MF.project_scores(s_input, W2, al=a_l, heads=H)  # (N, H*F), (N, H)
     u, v = MF.edge_attention(graph, el, er, h1.view(m, H, Fd), hs=h2.view(n, H, Fd),
                              p=heads[0].dropout, training=training)
     # unbind: the backward stacks the head gradients in one copy (u[:, k] selects would
@@ -277,14 +284,14 @@ def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_a
     groups = groups_for(city_adj, province_adj, s_input.device)
     W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
     W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
-    a = torch.stack([h.a.view(-1) for h in heads])
-    a3 = torch.stack([h.a3.view(-1) for h in heads])
-    a4 = torch.stack([h.a4.view(-1) for h in heads])
-    h1, er = MF.project_scores(r_input, W1, ar=a[:, :Fd], heads=H)
-    h2, el = MF.project_scores(s_input, W2, al=a[:, Fd:], heads=H)
+    # (H, 2, F) views of the score vectors: their halves by unbind / sum, whose backward
+    # is one stack / expand kernel (two slices cost a zero-fill + copy each, and an add)
+    a_r, a_l = _score_halves(heads, "a").unbind(1)
+    h1, er = MF.project_scores(r_input, W1, ar=a_r, heads=H)
+    h2, el = MF.project_scores(s_input, W2, al=a_l, heads=H)
     # e3 = lrelu(cat(h2_b, h2_b) @ a3) = lrelu(h2_b . (a3[:F] + a3[F:]))  (Ours.py:74-75)
-    a3s = a3[:, :Fd] + a3[:, Fd:]
-    a4s = a4[:, :Fd] + a4[:, Fd:]
+    a3s = _score_halves(heads, "a3").sum(1)
+    a4s = _score_halves(heads, "a4").sum(1)
     src = torch.as_tensor(source_index, device=s_input.device)
     u, v, attd, bstat = MF.ours_attention(graph, groups, src, el, er, h1.view(m, H, Fd),
                                           h2.view(n, H, Fd), a3s, a4s, p=heads[0].dropout,
