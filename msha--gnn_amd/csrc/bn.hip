@@ -16,6 +16,9 @@
 namespace msha {
 
 constexpr int kBnRows = 256;  // rows per partial block
+#ifndef BN_U
+#define BN_U 8  // rows per thread whose loads are in flight together
+#endif
 constexpr int kBnThreads = 256;
 
 struct Wf {
@@ -41,7 +44,22 @@ __device__ __forceinline__ Wf block_stats(const T* __restrict__ x, int64_t r0, i
                                           int c, int rg, int RG, Wf* red, int CT, int ci) {
   Wf w{0.f, 0.f, 0.f};
   if (c < C && rg < RG) {
-    for (int64_t r = r0 + rg; r < r1; r += RG) {
+    // BN_U rows loaded before the Welford updates (same order): the loads overlap
+    // instead of one memory round trip per row
+    int64_t r = r0 + rg;
+    for (; r + (BN_U - 1) * RG < r1; r += BN_U * RG) {
+      float v[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) v[u] = to_f32(x[(r + u * RG) * C + c]);
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        w.n += 1.f;
+        const float d = v[u] - w.mean;
+        w.mean += d / w.n;
+        w.m2 += d * (v[u] - w.mean);
+      }
+    }
+    for (; r < r1; r += RG) {
       const float v = to_f32(x[r * C + c]);
       w.n += 1.f;
       const float d = v - w.mean;
@@ -184,14 +202,19 @@ struct BnBwd {
   float* dbias;
 };
 
+__device__ __forceinline__ void bwd_terms_v(const BnBwd& a, float xv, float gv, int c, float& dz,
+                                            float& xhat) {
+  const float w = a.weight != nullptr ? a.weight[c] : 1.f;
+  const float b = a.bias != nullptr ? a.bias[c] : 0.f;
+  xhat = (xv - a.mean[c]) * a.invstd[c];
+  const float z = fmaf(w, xhat, b);
+  dz = gv * (z > 0.f ? 1.f : a.slope);
+}
+
 template <typename T>
 __device__ __forceinline__ void bwd_terms(const BnBwd& a, const T* x, const T* dy, int64_t i,
                                           int c, float& dz, float& xhat) {
-  const float w = a.weight != nullptr ? a.weight[c] : 1.f;
-  const float b = a.bias != nullptr ? a.bias[c] : 0.f;
-  xhat = (to_f32(x[i]) - a.mean[c]) * a.invstd[c];
-  const float z = fmaf(w, xhat, b);
-  dz = to_f32(dy[i]) * (z > 0.f ? 1.f : a.slope);
+  bwd_terms_v(a, to_f32(x[i]), to_f32(dy[i]), c, dz, xhat);
 }
 
 // per block and channel: (sum dz, sum dz * xhat) over the block's rows, fixed tree
@@ -201,7 +224,23 @@ __device__ __forceinline__ float2 block_bwd_sums(const BnBwd& a, const T* x, con
                                                  float2* red, int CT, int ci) {
   float2 s = make_float2(0.f, 0.f);
   if (c < a.C && rg < RG) {
-    for (int64_t r = r0 + rg; r < r1; r += RG) {
+    int64_t r = r0 + rg;
+    for (; r + (BN_U - 1) * RG < r1; r += BN_U * RG) {  // loads first, sums in order
+      float xv[BN_U], gv[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        xv[u] = to_f32(x[(r + u * RG) * a.C + c]);
+        gv[u] = to_f32(dy[(r + u * RG) * a.C + c]);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        float dz, xh;
+        bwd_terms_v(a, xv[u], gv[u], c, dz, xh);
+        s.x += dz;
+        s.y = fmaf(dz, xh, s.y);
+      }
+    }
+    for (; r < r1; r += RG) {
       float dz, xh;
       bwd_terms(a, x, dy, r * a.C + c, c, dz, xh);
       s.x += dz;
