@@ -486,6 +486,9 @@ static bool vec_ok(const GemmArgs& p) {
 // each row group strides the block's rows with 16-byte loads; the row groups are
 // added in a fixed LDS tree, and a second pass adds the block partials in block
 // order (deterministic).
+#ifndef CS_U
+#define CS_U 8
+#endif
 #ifndef COLSUM_ROWS
 #define COLSUM_ROWS 128
 #endif
@@ -529,8 +532,27 @@ __global__ void __launch_bounds__(256) head_colsum_partial_kernel(
 #pragma unroll
   for (int i = 0; i < N; ++i) a1.v[i] = a2.v[i] = 0.f;
   if (live) {
-#pragma unroll 4
-    for (int64_t r = r0 + rg; r < r1; r += RG) {
+    // CS_U rows loaded before they are accumulated (same order): overlapping loads
+    int64_t r = r0 + rg;
+    for (; r + (CS_U - 1) * RG < r1; r += CS_U * RG) {
+      VT x[CS_U];
+      float c1[CS_U], c2[CS_U];
+#pragma unroll
+      for (int u = 0; u < CS_U; ++u) {
+        const int64_t ru = r + u * RG;
+        x[u] = fv_load(tab + ru * D + N * q, (VT*)nullptr);
+        c1[u] = s1[ru * H + h];
+        c2[u] = s2 ? s2[ru * H + h] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CS_U; ++u)
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          a1.v[i] = fmaf(c1[u], x[u].v[i], a1.v[i]);
+          a2.v[i] = fmaf(c2[u], x[u].v[i], a2.v[i]);
+        }
+    }
+    for (; r < r1; r += RG) {
       const VT x = fv_load(tab + r * D + N * q, (VT*)nullptr);
       const float c1 = s1[r * H + h];
       const float c2 = s2 ? s2[r * H + h] : 0.f;
