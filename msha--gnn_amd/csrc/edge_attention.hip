@@ -609,14 +609,26 @@ __global__ void __launch_bounds__(1024) csc_combine_kernel(
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int32_t jc = multi_col[mi], first = multi_first[mi], cnt = multi_count[mi];
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int k = g; k < cnt; k += kCombineWaves) {
-    const int64_t c = first + k;
+  auto ld = [&](int64_t c, int q) {
+    const int e = e0 + lane + 64 * q;
+    return e < D ? part[c * D + e] : (e < W ? part_x[c * H + (e - D)] : 0.f);
+  };
+  int k = g;
+  // 4 chunk partials per lane loaded before they are added (same order per lane)
+  for (; k + 3 * kCombineWaves < cnt; k += 4 * kCombineWaves) {
+    float v[4][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = e0 + lane + 64 * q;
-      if (e < D) acc[q] += part[c * D + e];
-      else if (e < W) acc[q] += part_x[c * H + (e - D)];
-    }
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[u][q] = ld(first + k + u * kCombineWaves, q);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += v[u][q];
+  }
+  for (; k < cnt; k += kCombineWaves) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] += ld(first + k, q);
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) red[g][lane + 64 * q] = acc[q];

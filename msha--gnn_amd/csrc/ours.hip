@@ -231,7 +231,15 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, 
     const int64_t bk = t / D;
     const int d = (int)(t % D);
     float s = 0.f;
-    for (int c = 0; c < nck; ++c) s += Gp[(bk * nck + c) * D + d];
+    int c = 0;
+    for (; c + 7 < nck; c += 8) {  // 8 chunk partials loaded, then added in order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = Gp[(bk * nck + c + u) * D + d];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; c < nck; ++c) s += Gp[(bk * nck + c) * D + d];
     G[t] = s;
   }
 }
