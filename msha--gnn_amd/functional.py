@@ -576,10 +576,12 @@ class _BnLRelu(torch.autograd.Function):
                 None, None, None, None, None)
 
 
-def bn_lrelu(x: torch.Tensor, bn: torch.nn.BatchNorm1d, slope: float) -> torch.Tensor:
+def bn_lrelu(x: torch.Tensor, bn: torch.nn.BatchNorm1d, slope: float,
+             count: bool = True) -> torch.Tensor:
     """``lrelu(bn(x), slope)`` for a (rows, C) table on the fused kernels: batch
     statistics and the running-statistics update as torch.nn.BatchNorm1d in training
-    mode (momentum set; num_batches_tracked advanced on the device), running
+    mode (momentum set; num_batches_tracked advanced on the device -- by the caller
+    when ``count`` is False, e.g. one foreach add for all heads), running
     statistics in eval mode."""
     _lib.require_cuda(x)
     if x.dim() != 2 or bn.momentum is None:
@@ -599,7 +601,7 @@ def bn_lrelu(x: torch.Tensor, bn: torch.nn.BatchNorm1d, slope: float) -> torch.T
                   None, None, y.data_ptr(), None, 0, _stream(xc))
         return y
     track = bn.training and bn.track_running_stats
-    if track:
+    if track and count:
         bn.num_batches_tracked.add_(1)
     return _BnLRelu.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
                           bn.running_var if track else None, bn.eps, slope,

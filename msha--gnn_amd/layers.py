@@ -137,18 +137,29 @@ class OursLayer3(nn.Module):
         self.bn2 = nn.BatchNorm1d(out_features)
         self.bn3 = nn.BatchNorm1d(out_features)
 
-    def epilogue(self, u, v):
+    def epilogue(self, u, v, count=True):
         """Ablation.py:273-277 on the aggregates: BN + LeakyReLU + u @ v.T + elu.
         (u, v arrive as head slices of the fused (rows, H, F) outputs; BatchNorm1d's
         backward is ~30x slower on the strided view, so they are made contiguous.)"""
-        v_out = MF.bn_lrelu(v.contiguous(), self.bn1, self.alpha)
-        u_out = MF.bn_lrelu(u.contiguous(), self.bn2, self.alpha)
+        v_out = MF.bn_lrelu(v.contiguous(), self.bn1, self.alpha, count)
+        u_out = MF.bn_lrelu(u.contiguous(), self.bn2, self.alpha, count)
         # u_out @ v_out.T on the library GEMM: its backward's v-side product reduces over
         # all N rows (deterministic split-K instead of a 2-workgroup BLAS tile)
         return F.elu(MF.matmul(u_out, v_out.t()))
 
     def forward(self, Sinput, Rinput, inter_adj, city_adj, province_adj, source_index):
         return fused_ours_layer3([self], Sinput, Rinput, _graph(inter_adj), self.training)[0]
+
+
+def _epilogues(heads, us, vs):
+    """Per-head BN epilogues; the heads' BatchNorm step counters advance in one foreach
+    add instead of one launch per BatchNorm."""
+    outs = [head.epilogue(us[k], vs[k], count=False) for k, head in enumerate(heads)]
+    ctr = [bn.num_batches_tracked for h in heads for bn in (h.bn1, h.bn2)
+           if bn.training and bn.track_running_stats and bn.momentum is not None]
+    if ctr:
+        torch._foreach_add_(ctr, 1)
+    return outs
 
 
 def _score_halves(heads, name):
@@ -178,7 +189,7 @@ def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
     # unbind: the backward stacks the head gradients in one copy (u[:, k] selects would
     # zero-fill and copy a full (rows, H, F) gradient per head and add them)
     us, vs = u.unbind(1), v.unbind(1)
-    return [head.epilogue(us[k], vs[k]) for k, head in enumerate(heads)]
+    return _epilogues(heads, us, vs)
 
 
 class ablation3(nn.Module):  # noqa: N801  (reference class name)
@@ -299,7 +310,7 @@ def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_a
     if record:
         _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4)
     us, vs = u.unbind(1), v.unbind(1)  # one stacked gradient copy (see fused_ours_layer3)
-    return [head.epilogue(us[k], vs[k]) for k, head in enumerate(heads)]
+    return _epilogues(heads, us, vs)
 
 
 def _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4):
