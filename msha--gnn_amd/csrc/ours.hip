@@ -199,19 +199,37 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
     for (int h = 0; h < a.H && h < 32; ++h)
       kbits |= (intra_drop(a.dp, kind, h, (uint64_t)b * a.N + nj) != 0.f ? 1u : 0u) << h;
   }
-  for (int t = 0; t < cnt; ++t) {
-    const int64_t n = __shfl(nj, t);
-    const uint32_t kb = __shfl(kbits, t);
+  // GU members' rows are loaded before they are accumulated (in member order, as one
+  // at a time): GU gathers in flight per wave instead of one
+  constexpr int GU = 8;
+  for (int t0 = 0; t0 < cnt; t0 += GU) {
+    float v[GU][KD];
+    int64_t nn[GU];
+    uint32_t kk[GU];
 #pragma unroll
-    for (int k = 0; k < KD; ++k) {
-      const int d = lane + 64 * k;
-      if (d < D) {
-        const int h = d / a.F;
-        float drop = 1.f;
-        if (a.dp.active)
-          drop = h < 32 ? (((kb >> h) & 1u) ? a.dp.scale : 0.f)
-                        : intra_drop(a.dp, kind, h, (uint64_t)b * a.N + n);
-        acc[k] = fmaf(drop, to_f32(dU[n * D + d]), acc[k]);
+    for (int u = 0; u < GU; ++u) {
+      nn[u] = __shfl(nj, t0 + u);  // lanes past cnt hold member 0: a valid row, unused
+      kk[u] = __shfl(kbits, t0 + u);
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        v[u][k] = d < D ? to_f32(dU[nn[u] * D + d]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      if (t0 + u >= cnt) break;
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        if (d < D) {
+          const int h = d / a.F;
+          float drop = 1.f;
+          if (a.dp.active)
+            drop = h < 32 ? (((kk[u] >> h) & 1u) ? a.dp.scale : 0.f)
+                          : intra_drop(a.dp, kind, h, (uint64_t)b * a.N + nn[u]);
+          acc[k] = fmaf(drop, v[u][k], acc[k]);
+        }
       }
     }
   }
