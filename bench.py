@@ -451,7 +451,9 @@ def main():
         launch gaps (~2-10 us per launch, Python autograd).  None if capture fails."""
         try:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: a communicator's watchdog thread (N > 1) may query its events
+            # while this thread captures
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 for _ in range(steps):
                     lay.step()
             g.replay()

@@ -28,17 +28,32 @@ int check_launch(const char* what);
 // ---- wave helpers ----
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
+// v of lane ^ o.  Offsets 1, 2 (quad_perm) and 8 (row_ror:8 inside a 16-lane row) are
+// DPP moves on the VALU; the rest go through ds_bpermute.  The same values either way.
+#ifndef XOR_DPP
+#define XOR_DPP 1
+#endif
+__device__ __forceinline__ float xor_shfl(float v, int o) {
+  if (XOR_DPP) {
+    const int x = __builtin_bit_cast(int, v);
+    if (o == 1) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true));
+    if (o == 2) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true));
+    if (o == 8) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true));
+  }
+  return __shfl_xor(v, o);
+}
+
 template <int FIRST>
 __device__ __forceinline__ float wave_xor_max(float v) {
 #pragma unroll
-  for (int o = FIRST; o < kWave; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+  for (int o = FIRST; o < kWave; o <<= 1) v = fmaxf(v, xor_shfl(v, o));
   return v;
 }
 
 template <int FIRST>
 __device__ __forceinline__ float wave_xor_sum(float v) {
 #pragma unroll
-  for (int o = FIRST; o < kWave; o <<= 1) v += __shfl_xor(v, o);
+  for (int o = FIRST; o < kWave; o <<= 1) v += xor_shfl(v, o);
   return v;
 }
 
@@ -46,7 +61,7 @@ __device__ __forceinline__ float wave_xor_sum(float v) {
 template <int G>
 __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll
-  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
+  for (int o = 1; o < G; o <<= 1) v += xor_shfl(v, o);
   return v;
 }
 
@@ -135,7 +150,7 @@ __device__ __forceinline__ float pk_dot(const Pk<T>& a, const Pk<T>& b) {
 template <typename T>
 __device__ __forceinline__ Pk<T> pk_xor_add(Pk<T> a, int o) {
 #pragma unroll
-  for (int i = 0; i < Pk<T>::V; ++i) a.v[i] += __shfl_xor(a.v[i], o);
+  for (int i = 0; i < Pk<T>::V; ++i) a.v[i] += xor_shfl(a.v[i], o);
   return a;
 }
 
