@@ -449,6 +449,7 @@ def main():
         steps (captured after the eager pass, which warmed every cache; one untimed
         replay first).  Same kernels, same work as the eager steps without the host
         launch gaps (~2-10 us per launch, Python autograd).  None if capture fails."""
+        ok, g = 1, None
         try:
             g = torch.cuda.CUDAGraph()
             # thread_local: a communicator's watchdog thread (N > 1) may query its events
@@ -459,6 +460,12 @@ def main():
             g.replay()
         except RuntimeError as ex:  # report the eager number instead
             print(f"graph capture failed: {ex}", file=sys.stderr)
+            ok = 0
+        if dist:  # every rank falls back together (no rank left waiting in a barrier)
+            t_ok = torch.tensor([ok], device=dev)
+            tdist.all_reduce(t_ok, op=tdist.ReduceOp.MIN)
+            ok = int(t_ok.item())
+        if not ok:
             return None
         barrier()
         t0 = time.perf_counter()
