@@ -264,6 +264,7 @@ edge_attn_fwd_bat_kernel(
                                  ? (uint32_t)j0[t] * (4u * H) + 4u * h_s : kOOB);
     float m = -INFINITY, l = 0.f;
     Pk<T> acc = pk_zero<T>();
+    float sc_keep[EPL];  // the last chunk's scores (record mode, one-chunk rows)
     for (int32_t cs = start; cs < end; cs += CEL) {
       const int nvalid = min(CEL, (int)(end - cs));
       // (1) this chunk's gathers, all in flight together
@@ -295,6 +296,7 @@ edge_attn_fwd_bat_kernel(
         valid[t] = cs + t * G::CE + e_s < end;
         sc[t] = valid[t] ? (virt ? 0.f : lrelu(elh + erv[t], slope)) : -INFINITY;
         smax = fmaxf(smax, sc[t]);
+        sc_keep[t] = sc[t];
       }
       const float mn = fmaxf(m, wave_xor_max<H>(smax));
       const float alpha = __expf(m - mn);
@@ -334,7 +336,17 @@ edge_attn_fwd_bat_kernel(
     if (g_e == 0) pk_store(u + (int64_t)row * G::D + G::V * q, pk_scale(acc, inv));
     const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
     if (lane < H) lse[(int64_t)row * H + lane] = lse_h;
-    if (attd != nullptr) {
+    if (attd != nullptr && end - start <= CEL) {
+      // one chunk (every R15 row): its scores are still in registers -- the same values
+      // the reload below would recompute, without the col -> er round trips
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const int32_t e = start + t * G::CE + e_s;
+        if (e < end)
+          attd[(int64_t)e * H + h_s] =
+              __expf(sc_keep[t] - lse_h) * dropout_factor(dp, (uint64_t)e * H + h_s);
+      }
+    } else if (attd != nullptr) {
       for (int32_t cs = start; cs < end; cs += G::CE) {
         const int32_t e = cs + e_s;
         if (e < end) {
