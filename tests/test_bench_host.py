@@ -1,0 +1,58 @@
+"""Host-side pieces of bench.py (no GPU): the C4 graph generator's contract, the
+algorithmic byte counts DESIGN.md quotes, and the PMC-traffic lookup of the committed
+profiles."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_synth_graph_contract():
+    """e unique (row, col) pairs, rows sorted, every row degree >= 1."""
+    n, e = 2000, 30000
+    rowptr, col = bench.synth_graph(n, e, seed=0)
+    assert rowptr[0] == 0 and rowptr[-1] == e and len(col) == e
+    deg = np.diff(rowptr)
+    assert (deg >= 1).all()
+    rows = np.repeat(np.arange(n), deg)
+    keys = rows * n + col
+    assert (np.diff(keys) > 0).all()  # sorted by (row, col), no duplicates
+    assert col.min() >= 0 and col.max() < n
+    r2, c2 = bench.synth_graph(n, e, seed=0)
+    assert np.array_equal(r2, rowptr) and np.array_equal(c2, col)  # seeded
+
+
+def test_algorithmic_bytes_match_design():
+    """The per-launch byte counts behind the bench's rooflines."""
+    n = m = 100_000
+    e, H, F = 2_000_000, 8, 16
+    assert bench.fwd_bytes(n, m, e, H, F) == 1_154_000_004
+    assert bench.fwd_bytes(n, m, e, H, F, s=2) == 616_400_004
+    # the fused backward: row stats + column pass + row sum, de in edge order at C4
+    nch = m  # one chunk per column at C4
+    b = bench.bwd_fused_bytes(n, m, e, H, F, nch)
+    assert 1.5e9 < b < 1.7e9
+    # de in CSC slot order past 192 MB (edge_attention.hip DE_SLOT_MIN_BYTES) adds the
+    # row sum's slot map, 4 B per edge
+    def by_hand(E, slot):
+        D, s = H * F, 4
+        stats = n * (2 * s * D + 8 * H + 12 * H)
+        cols = E * (8 + 12 * H + s * D + 4 * H) + m * (2 * s * D + 8 * H) + 12 * nch + 4 * (m + 1)
+        return stats + cols + 4 * (n + 1) + E * (4 * H + slot) + n * 4 * H
+    assert b == by_hand(e, 0)
+    assert bench.bwd_fused_bytes(n, m, 40 * e, H, F, nch) == by_hand(40 * e, 4)
+
+
+def test_pmc_traffic_reads_newest_profile():
+    """bench.pmc_traffic finds the forward kernel in the newest committed PMC summary
+    (FETCH_SIZE x 2 + WRITE_SIZE per launch), close to the algorithmic bytes."""
+    t32, src32 = bench.pmc_traffic(8, 16, False, "syn100k")
+    t16, src16 = bench.pmc_traffic(8, 16, True, "syn100k")
+    assert src32 is not None and src16 is not None
+    assert 1.0e9 < t32 < 1.4e9
+    assert 0.5e9 < t16 < 0.8e9
