@@ -28,6 +28,9 @@
 #ifndef DE_SLOT_MIN_BYTES
 #define DE_SLOT_MIN_BYTES (192ll << 20)
 #endif
+#ifndef COLS_WIDE_UG
+#define COLS_WIDE_UG 4  // wide-row column pass: edges whose dU rows are in flight together
+#endif
 #ifndef COLS_NG
 #define COLS_NG 2  // slot groups whose loads are in flight together in the column pass
 #endif
@@ -730,11 +733,11 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
   }
 }
 
-template <int H, int F, typename T>
+template <int H, int F, typename T, bool BUF>
 __global__ void __launch_bounds__(256) bwd_cols_kernel(
     const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
-    const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid,
+    const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid, int64_t n_rows,
     const uint8_t* __restrict__ rowflag, const float* __restrict__ rec,
     const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
     float slope, Dropout dp, bool slot_de, float* __restrict__ de, T* __restrict__ d_hc,
@@ -789,6 +792,50 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
       const float wv = att * dropf;
       const int nvalid = min(G::CE, (int)(s1 - cs));
       float gsum = 0.f;
+      if constexpr (BUF && G::EPI == 1) {
+        // wide rows (one edge per wave-instruction): UG edges' dU rows are loaded through
+        // the buffer descriptor (a slot past the chunk reads 0) before any is used, then
+        // consumed in slot order -- the same operations in the same order as below,
+        // with UG rows in flight instead of one (a load under "if (ei < nvalid)" drained
+        // the queue after every edge)
+        constexpr int UG = COLS_WIDE_UG;
+        const rsrc_t r_dU = make_rsrc(dU, (uint32_t)(n_rows * G::D * sizeof(T)));
+#pragma unroll
+        for (int g0 = 0; g0 < G::CE; g0 += UG) {
+          if (g0 >= nvalid) break;
+          Pk<T> dl[UG][G::QPL];
+#pragma unroll
+          for (int u = 0; u < UG; ++u) {
+            const int g = g0 + u;
+            const int32_t iq = __shfl(i, (g < G::CE ? g : 0) * H);
+#pragma unroll
+            for (int k = 0; k < G::QPL; ++k) {
+              const int q = quad_of<G>(lane, k);
+              const uint32_t off = g < nvalid
+                  ? (uint32_t)iq * (uint32_t)(G::D * sizeof(T)) + (uint32_t)(G::V * q * sizeof(T))
+                  : kOOB;
+              dl[u][k] = pk_load_buf(r_dU, off, (T*)nullptr);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < UG; ++u) {
+            const int g = g0 + u;
+            if (g >= nvalid) break;
+            const bool mine = e_s == g;
+            const int srcl = G::QPL == 1 ? h_s * G::QH : dsrc_l;
+#pragma unroll
+            for (int k = 0; k < G::QPL; ++k) {
+              const int q = quad_of<G>(lane, k);
+              const float wq = __shfl(wv, g * H + q / G::QH);
+              acc[k] = pk_fma(wq, dl[u][k], acc[k]);
+              float t = pk_dot(dl[u][k], hcq[k]);
+              t = group_sum<G::QH>(t);
+              const float cand = __shfl(t, srcl);
+              if (mine && (G::QPL == 1 || k == dsrc_k)) gsum = cand;
+            }
+          }
+        }
+      } else {
 #pragma unroll
       for (int g = 0; g < G::CE; g += G::EPI) {
         if (g >= nvalid) break;
@@ -810,6 +857,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
           const float cand = __shfl(t, srcl);
           if (mine && (G::QPL == 1 || k == dsrc_k)) gsum = cand;
         }
+      }
       }
       const int32_t sl2 = slot + 2 * G::CE;
       const int32_t i2 = sl2 < s1 ? csc_row[sl2] : 0;
@@ -1320,12 +1368,15 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
                            slot_de, de,                                                        \
                            (T*)d_hc, d_er, part, part_x);                                      \
       else                                                                                     \
-        hipLaunchKernelGGL((bwd_cols_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0,   \
+      {                                                                                        \
+        auto kern = buf_ok ? bwd_cols_kernel<h, f, T, true> : bwd_cols_kernel<h, f, T, false>; \
+        hipLaunchKernelGGL(kern, wave_grid(g->n_chunks), dim3(256), 0,                         \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
-                           g->colptr, g->csc_row, g->csc_eid, g->rowflag, rec, er,             \
+                           g->colptr, g->csc_row, g->csc_eid, g->n_rows, g->rowflag, rec, er,  \
                            (const T*)hc, (const T*)dU, neg_slope, dp, slot_de,                 \
                            de, (T*)d_hc, d_er,                                                 \
                            part, part_x);                                                      \
+      }                                                                                        \
       hipLaunchKernelGGL((bwd_row_sum_kernel<h>), wave_grid(g->n_rows), dim3(256), 0, s,       \
                          g->rowptr, g->n_rows, de, slot_de ? g->csr_slot : nullptr, d_el);    \
     }                                                                                          \
