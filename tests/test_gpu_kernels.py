@@ -227,6 +227,45 @@ def test_edge_attention_fused_backward_bf16_multichunk(cuda, msha):
         _same_as_split(got, split, dtype)
 
 
+WIDE_CASES = [
+    # (H, F): shapes whose backward column pass takes one edge per wave-instruction
+    # (EPI == 1) and so the buffer-load batch of COLS_WIDE_UG rows
+    (4, 64),   # fp32: one 16-B quad per lane (QPL 1); bf16: EPI 2 (control)
+    (8, 64),   # fp32 QPL 2; bf16 QPL 1
+    (2, 128),  # fp32 QPL 1
+    (8, 128),  # fp32 QPL 4; bf16 QPL 2
+]
+
+
+@pytest.mark.parametrize("H,F", WIDE_CASES, ids=lambda v: str(v))
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_edge_attention_fused_backward_wide_rows(cuda, msha, H, F, dtype):
+    """Wide rows through the column pass's batched buffer loads, with ragged slot
+    groups (nvalid < CE in the last group of a chunk: slots past it read 0) and split
+    columns (a hot column over several chunks): fused == split, and fp32 == oracle."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(31 * H + F)
+    n, m = 700, 48
+    c, rowptr, col, empty, el, er, hc, hs, dU, dV = _edge_case(
+        rng, n, m, H, F, 9, empty_rows=(2,), hot_col=7)
+    graph = Graph.from_dense(t(c, cuda))
+    assert graph._plan["n_multi"] > 0  # some column spans more than one chunk
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    for p in (0.0, 0.4):
+        got = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, True)
+        split = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, False)
+        _same_as_split(got, split, tdt)
+        if dtype == "f32":
+            keep = _keep_mask(graph.n_edges, H, p, 5, cuda)
+            ref = O.edge_aggregate_fwd(rowptr, col, el, er, hc, keep=keep, p=p, rowflag=empty)
+            bw = O.edge_aggregate_bwd(rowptr, col, ref, hc, dU, keep=keep, p=p)
+            tol_close(got[1].cpu().numpy(), bw["d_el"], 1e-4, 1e-5)
+            tol_close(got[2].cpu().numpy(), bw["d_er"], 1e-4, 1e-5)
+            tol_close(got[3].cpu().numpy(), bw["d_hc"], EMB_RTOL, 1e-5)
+
+
 def test_edge_attention_weights_exported(cuda):
     """attd output of the forward vs oracle attention (absolute 1e-5)."""
     from msha_gnn_amd import _lib
