@@ -29,9 +29,16 @@ int check_launch(const char* what);
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
 // v of lane ^ o.  Offsets 1, 2 (quad_perm) and 8 (row_ror:8 inside a 16-lane row) are
-// DPP moves on the VALU; the rest go through ds_bpermute.  The same values either way.
+// DPP moves on the VALU; 16 and 32 are gfx950's v_permlane16/32_swap (VALU, no LDS
+// round trip); the rest go through ds_bpermute.  The same values either way.
+// permlaneN_swap(x, x) exchanges the odd N-lane blocks of its first operand with the
+// even blocks of its second, so its two results hold x[l] and x[l ^ N] in some order:
+// lane l takes the one from the other block.
 #ifndef XOR_DPP
 #define XOR_DPP 1
+#endif
+#ifndef XOR_PERMLANE
+#define XOR_PERMLANE 0  // measured neutral-to-slower; kept for A/B
 #endif
 __device__ __forceinline__ float xor_shfl(float v, int o) {
   if (XOR_DPP) {
@@ -39,6 +46,16 @@ __device__ __forceinline__ float xor_shfl(float v, int o) {
     if (o == 1) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true));
     if (o == 2) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true));
     if (o == 8) return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true));
+  }
+  if (XOR_PERMLANE && (o == 16 || o == 32)) {
+    const unsigned x = __builtin_bit_cast(unsigned, v);
+    const int l = (int)(threadIdx.x & (kWave - 1));
+    if (o == 32) {
+      const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+      return __builtin_bit_cast(float, l < 32 ? r[1] : r[0]);
+    }
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return __builtin_bit_cast(float, (l & 16) ? r[0] : r[1]);
   }
   return __shfl_xor(v, o);
 }
