@@ -31,6 +31,12 @@
 #ifndef COLS_WIDE_UG
 #define COLS_WIDE_UG 4  // wide-row column pass: edges whose dU rows are in flight together
 #endif
+#ifndef COLS_EPI_BUF
+#define COLS_EPI_BUF 1  // the buffer-load batch above for EPI > 1 too
+#endif
+#ifndef COLS_NARROW_UG
+#define COLS_NARROW_UG 8  // gather instructions in flight together when EPI > 1
+#endif
 #ifndef COLS_NG
 #define COLS_NG 2  // slot groups whose loads are in flight together in the column pass
 #endif
@@ -792,26 +798,29 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
       const float wv = att * dropf;
       const int nvalid = min(G::CE, (int)(s1 - cs));
       float gsum = 0.f;
-      if constexpr (BUF && G::EPI == 1) {
-        // wide rows (one edge per wave-instruction): UG edges' dU rows are loaded through
-        // the buffer descriptor (a slot past the chunk reads 0) before any is used, then
-        // consumed in slot order -- the same operations in the same order as below,
-        // with UG rows in flight instead of one (a load under "if (ei < nvalid)" drained
-        // the queue after every edge)
-        constexpr int UG = COLS_WIDE_UG;
+      if constexpr (BUF && (G::EPI == 1 || COLS_EPI_BUF)) {
+        // UG gather instructions (EPI edges each; one edge per instruction on wide rows)
+        // load their dU rows through the buffer descriptor -- a slot past the chunk
+        // reads 0, so its fma adds 0 and its dot is 0, as the skipped branch below --
+        // before any is used, then are consumed in slot order: the same operations in
+        // the same order as below, with UG instructions in flight instead of one (a load
+        // under "if (ei < nvalid)" drained the queue after every instruction)
+        constexpr int UG = G::EPI == 1 ? COLS_WIDE_UG : COLS_NARROW_UG;
         const rsrc_t r_dU = make_rsrc(dU, (uint32_t)(n_rows * G::D * sizeof(T)));
 #pragma unroll
-        for (int g0 = 0; g0 < G::CE; g0 += UG) {
+        for (int g0 = 0; g0 < G::CE; g0 += UG * G::EPI) {
           if (g0 >= nvalid) break;
           Pk<T> dl[UG][G::QPL];
 #pragma unroll
           for (int u = 0; u < UG; ++u) {
-            const int g = g0 + u;
-            const int32_t iq = __shfl(i, (g < G::CE ? g : 0) * H);
+            const int g = g0 + u * G::EPI;
+            if (g >= G::CE) break;
+            const int ei = g + g_e;
+            const int32_t iq = __shfl(i, ei * H);
 #pragma unroll
             for (int k = 0; k < G::QPL; ++k) {
               const int q = quad_of<G>(lane, k);
-              const uint32_t off = g < nvalid
+              const uint32_t off = ei < nvalid
                   ? (uint32_t)iq * (uint32_t)(G::D * sizeof(T)) + (uint32_t)(G::V * q * sizeof(T))
                   : kOOB;
               dl[u][k] = pk_load_buf(r_dU, off, (T*)nullptr);
@@ -819,14 +828,16 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
           }
 #pragma unroll
           for (int u = 0; u < UG; ++u) {
-            const int g = g0 + u;
-            if (g >= nvalid) break;
-            const bool mine = e_s == g;
-            const int srcl = G::QPL == 1 ? h_s * G::QH : dsrc_l;
+            const int g = g0 + u * G::EPI;
+            if (g >= G::CE || g >= nvalid) break;
+            const int ei = g + g_e;
+            const bool mine = e_s >= g && e_s < g + G::EPI;
+            const int srcl =
+                G::QPL == 1 ? ((e_s - g) & (G::EPI - 1)) * G::NQ + h_s * G::QH : dsrc_l;
 #pragma unroll
             for (int k = 0; k < G::QPL; ++k) {
               const int q = quad_of<G>(lane, k);
-              const float wq = __shfl(wv, g * H + q / G::QH);
+              const float wq = __shfl(wv, ei * H + q / G::QH);
               acc[k] = pk_fma(wq, dl[u][k], acc[k]);
               float t = pk_dot(dl[u][k], hcq[k]);
               t = group_sum<G::QH>(t);
