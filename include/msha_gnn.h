@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 3
+#define MSHA_ABI_VERSION 4
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -110,9 +110,12 @@ MSHA_API const char* msha_last_error(void);
  * would replay the same masks.  With a device counter installed here (a uint64 in
  * device memory, NULL = none), each draw adds (*counter << 32) to its offset, read on
  * the device at draw time: the caller increments *counter inside the captured region
- * and every replay draws fresh masks.  Process-wide setting; set it before the
+ * and every replay draws fresh masks.  One slot per device: a launch on a stream of
+ * device d uses device d's counter (device < 0: the current device).  Set it before the
  * launches it should apply to (launch-time snapshot of the pointer, not the value). */
-MSHA_API int msha_set_rng_counter(const uint64_t* counter);
+MSHA_API int msha_set_rng_counter(int32_t device, const uint64_t* counter);
+/* the counter installed for `device` (< 0: current device), NULL if none */
+MSHA_API const uint64_t* msha_get_rng_counter(int32_t device);
 
 /* keep[i] = 1 iff element i survives F.dropout(p) under (seed, offset).  The
  * kernels below draw exactly these masks (stream-ordered Philox4x32-10), which
@@ -155,7 +158,10 @@ MSHA_API int msha_graph_fill(const float* adj, int64_t n_rows, int64_t n_cols, c
  *   u[i]  = sum_e dropout(att_e) * hc[j]             hc: (n_cols, heads, feat)
  * Outputs u (n_rows, heads, feat), lse (n_rows, heads) = log-sum-exp of the row's
  * scores (the backward recomputes att from it) and, if attd != NULL, the
- * post-dropout attention (n_edges, heads).
+ * post-dropout attention (n_edges, heads).  u_lo (nullable, bf16 tables only): the
+ * rounding residual of the bf16 u (u32 - bf16(u32), stored bf16); the backward's
+ * D = dU . u then reads u + u_lo, so a degree-1 row's d_el stays ~0 instead of
+ * carrying the 2^-9 rounding of u.
  * Supported (heads, feat): heads in {1,2,4,8}, feat in {8,16,32,64,128} (see
  * msha_edge_attention_supported).  dtype (MSHA_DTYPE_*) is the storage type of the
  * tables hc / u (and hs, dU, dV, d_hs, table, out below); fp32 arithmetic either way. */
@@ -163,8 +169,8 @@ MSHA_API int msha_edge_attention_supported(int32_t heads, int32_t feat);
 MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
                                      int32_t dtype, const float* el, const float* er,
                                      const void* hc, float neg_slope, float drop_p,
-                                     uint64_t seed, uint64_t offset, void* u, float* lse,
-                                     float* attd, msha_stream_t stream);
+                                     uint64_t seed, uint64_t offset, void* u, void* u_lo,
+                                     float* lse, float* attd, msha_stream_t stream);
 
 /* Row half of the backward (autograd of the chain above; Ablation.py:266-274):
  *   g_e  = dU[i]·hc[j] (+ dV[j]·hs[i] when dV != NULL: the v = att^T @ h2 branch,
@@ -178,11 +184,12 @@ MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t
  * layer's normaliser sums exp(attention_inter) of its batch rows (Ours.py:84-86).
  * edge_ld: floats between consecutive edges in de / attd (0 = heads); with
  * edge_ld = 2*heads and attd = de + heads the two share one 2H-float record per edge,
- * which msha_csc_aggregate then reads as one 64-B segment (w = attd, x = de). */
+ * which msha_csc_aggregate then reads as one 64-B segment (w = attd, x = de).
+ * u_lo: the forward's u_lo (nullable; bf16 tables). */
 MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
                                           int32_t dtype, const float* el, const float* er,
                                           const void* hc, const float* lse, const void* u,
-                                          const void* dU, const void* hs, const void* dV,
+                                          const void* u_lo, const void* dU, const void* hs, const void* dV,
                                           const float* row_coef, float neg_slope, float drop_p,
                                           uint64_t seed, uint64_t offset, float* d_el, float* de,
                                           float* attd, int32_t edge_ld, void* d_hs,
@@ -212,13 +219,14 @@ MSHA_API int msha_csc_aggregate(const msha_graph* g, int32_t heads, int32_t feat
  * de (n_edges, heads) fp32: scratch (left holding de in CSR edge order, or in CSC slot
  * order when g->csr_slot is set and de exceeds 192 MB).
  * ws: msha_edge_attention_bwd_fused_workspace_size bytes.  Needs the CSC view with
- * csc_eid. */
+ * csc_eid.  u_lo: the forward's u_lo (nullable; bf16 tables). */
 MSHA_API size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph* g,
                                                              int32_t heads, int32_t feat);
 MSHA_API int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads, int32_t feat,
                                            int32_t dtype, const float* el, const float* er,
                                            const void* hc, const float* lse, const void* u,
-                                           const void* dU, float neg_slope, float drop_p,
+                                           const void* u_lo, const void* dU, float neg_slope,
+                                           float drop_p,
                                            uint64_t seed, uint64_t offset, float* d_el,
                                            float* d_er, void* d_hc, float* de, void* ws,
                                            size_t ws_bytes, msha_stream_t stream);
@@ -379,6 +387,15 @@ MSHA_API int msha_pair_hadamard(int64_t n_pairs, int32_t feat, const float* G, i
                                 const int64_t* gi, const float* G2, int64_t ldg2,
                                 const int64_t* gj, const float* dx, float* x_or_dxi, float* dxj,
                                 msha_stream_t stream);
+
+/* LinkPredictor with a predictor string other than 'mlp' / 'inner' (LLP.py:104-115 takes
+ * neither branch): y = sigmoid(x_i * x_j), (B, F).  dy == NULL: forward into y_or_dxi;
+ * else the backward from the forward's y: dx_i into y_or_dxi, dx_j into dxj. */
+MSHA_API int msha_pair_hadamard_sigmoid(int64_t n_pairs, int32_t feat, const float* G,
+                                        int64_t ldg, const int64_t* gi, const float* G2,
+                                        int64_t ldg2, const int64_t* gj, const float* y,
+                                        const float* dy, float* y_or_dxi, float* dxj,
+                                        msha_stream_t stream);
 
 /* ----------------------------------------------- full MSHA layer (Ours.py) --- */
 /* Intra-source attention of a batch (Ours.py:71-101) on top of the inter forward:

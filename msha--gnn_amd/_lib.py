@@ -13,6 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
+ABI_VERSION = 4  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -53,7 +54,8 @@ GRP = C.POINTER(MshaGroups)
 # name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
 SIGNATURES = {
     "msha_abi_version": (C.c_int, []),
-    "msha_set_rng_counter": (C.c_int, [P]),
+    "msha_set_rng_counter": (C.c_int, [I32, P]),
+    "msha_get_rng_counter": (P, [I32]),
     "msha_last_error": (C.c_char_p, []),
     "msha_dropout_keep_mask": (C.c_int, [U64, U64, I64, F32, P, P]),
     "msha_inter_adjacency": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
@@ -63,12 +65,12 @@ SIGNATURES = {
     "msha_graph_fill": (C.c_int, [P, I64, I64, P, P, P, P, P, P, P, SZ, P]),
     "msha_edge_attention_supported": (C.c_int, [I32, I32]),
     "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P, P,
-                                          P, P]),
-    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, F32,
-                                               F32, U64, U64, P, P, P, I32, P, P]),
+                                          P, P, P]),
+    "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, P,
+                                               F32, F32, U64, U64, P, P, P, I32, P, P]),
     "msha_edge_attention_bwd_fused_workspace_size": (SZ, [GP, I32, I32]),
-    "msha_edge_attention_bwd_fused": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, F32, F32,
-                                                U64, U64, P, P, P, P, P, SZ, P]),
+    "msha_edge_attention_bwd_fused": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,
+                                                F32, U64, U64, P, P, P, P, P, SZ, P]),
     "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
     "msha_csc_aggregate": (C.c_int, [GP, I32, I32, I32, P, P, I32, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),
@@ -101,6 +103,7 @@ SIGNATURES = {
     "msha_pair_inner_bwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P, P]),
     "msha_pair_mlp_dz": (C.c_int, [I64, P, P, F32, I32, P, P]),
     "msha_pair_hadamard": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P]),
+    "msha_pair_hadamard_sigmoid": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P, P, P, P]),
     "msha_ours_intra_fwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, P, P, F32, F32,
                                       U64, U64, P, P, P]),
     "msha_ours_workspace_size": (SZ, [GRP, I64, I32, I32]),
@@ -130,7 +133,7 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.msha_abi_version() != 3:
+    if lib.msha_abi_version() != ABI_VERSION:
         raise MshaLibraryError("ABI version mismatch")
     _lib = lib
     return lib

@@ -164,6 +164,16 @@ __device__ __forceinline__ float pk_dot(const Pk<T>& a, const Pk<T>& b) {
   for (int i = Pk<T>::V - 2; i >= 0; --i) r = fmaf(a.v[i], b.v[i], r);
   return r;
 }
+// what a bf16 store of `a` rounds away: a - bf16(a) (round-to-nearest-even), exact in
+// fp32; stored as bf16 itself, hi + lo carries ~16 mantissa bits.  fp32 tables: zero.
+__device__ __forceinline__ Pk<bf16_t> pk_residual(const Pk<bf16_t>& a) {
+  Pk<bf16_t> r;
+#pragma unroll
+  for (int i = 0; i < Pk<bf16_t>::V; ++i) r.v[i] = a.v[i] - (float)(bf16_t)a.v[i];
+  return r;
+}
+__device__ __forceinline__ Pk<float> pk_residual(const Pk<float>&) { return pk_zero<float>(); }
+
 template <typename T>
 __device__ __forceinline__ Pk<T> pk_xor_add(Pk<T> a, int o) {
 #pragma unroll
@@ -262,14 +272,15 @@ struct Dropout {
   const uint64_t* ctr;  // device replay counter (msha_set_rng_counter), nullable
 };
 
-// the library-wide replay counter (runtime.hip): read by the kernels at draw time
-const uint64_t* rng_counter();
+// the replay counter installed for the device of `s` (runtime.hip, one slot per device):
+// read by the kernels at draw time
+const uint64_t* rng_counter(hipStream_t s);
 
-inline Dropout make_dropout(float p, uint64_t seed, uint64_t offset) {
+inline Dropout make_dropout(float p, uint64_t seed, uint64_t offset, hipStream_t s) {
   Dropout d;
   d.seed = seed;
   d.offset = offset;
-  d.ctr = rng_counter();
+  d.ctr = rng_counter(s);
   d.active = p > 0.f;
   double t = (double)p * 4294967296.0;
   d.threshold = p >= 1.f ? 0xFFFFFFFFu : (uint32_t)(t > 4294967295.0 ? 4294967295.0 : t);

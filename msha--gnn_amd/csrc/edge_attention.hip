@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
     const float* __restrict__ er, const T* __restrict__ hc, float slope, Dropout dp,
-    T* __restrict__ u, float* __restrict__ lse, float* __restrict__ attd) {
+    T* __restrict__ u, T* __restrict__ u_lo, float* __restrict__ lse, float* __restrict__ attd) {
   using G = Geo<H, F, T>;
   constexpr int CEL = EPL * G::CE;  // edges per chunk
   const int lane = lane_id();
@@ -194,7 +194,11 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
       const int q = quad_of<G>(lane, k);
       const float lk = __shfl(l, q / G::QH);
       const float inv = lk > 0.f ? 1.f / lk : 0.f;
-      if (g_e == 0) pk_store(u + row * G::D + G::V * q, pk_scale(acc[k], inv));
+      if (g_e == 0) {
+        const Pk<T> uk = pk_scale(acc[k], inv);
+        pk_store(u + row * G::D + G::V * q, uk);
+        if (sizeof(T) == 2 && u_lo != nullptr) pk_store(u_lo + row * G::D + G::V * q, pk_residual(uk));
+      }
     }
     const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
     if (lane < H) lse[row * H + lane] = lse_h;
@@ -238,7 +242,7 @@ edge_attn_fwd_bat_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
     const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
-    float slope, Dropout dp, T* __restrict__ u, float* __restrict__ lse,
+    float slope, Dropout dp, T* __restrict__ u, T* __restrict__ u_lo, float* __restrict__ lse,
     float* __restrict__ attd) {
   using G = Geo<H, F, T>;
   static_assert(G::QPL == 1, "batched forward: one 16-byte piece per lane");
@@ -342,7 +346,13 @@ edge_attn_fwd_bat_kernel(
     }
     const float lk = __shfl(l, q / G::QH);
     const float inv = lk > 0.f ? 1.f / lk : 0.f;
-    if (g_e == 0) pk_store(u + (int64_t)row * G::D + G::V * q, pk_scale(acc, inv));
+    if (g_e == 0) {
+      const Pk<T> uk = pk_scale(acc, inv);
+      pk_store(u + (int64_t)row * G::D + G::V * q, uk);
+      // bf16 tables: the rounding residual too, so the backward's D = dU . u is exact
+      if (sizeof(T) == 2 && u_lo != nullptr)
+        pk_store(u_lo + (int64_t)row * G::D + G::V * q, pk_residual(uk));
+    }
     const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
     if (lane < H) lse[(int64_t)row * H + lane] = lse_h;
     if (attd != nullptr && end - start <= CEL) {
@@ -374,8 +384,9 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ el,
     const float* __restrict__ er, const T* __restrict__ hc, const float* __restrict__ lse,
-    const T* __restrict__ u, const T* __restrict__ dU, const T* __restrict__ hs,
-    const T* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
+    const T* __restrict__ u, const T* __restrict__ u_lo, const T* __restrict__ dU,
+    const T* __restrict__ hs, const T* __restrict__ dV, const float* __restrict__ row_coef,
+    float slope, Dropout dp,
     float* __restrict__ d_el, float* __restrict__ de, float* __restrict__ attd, int ld,
     T* __restrict__ d_hs) {
   using G = Geo<H, F, T>;
@@ -410,6 +421,8 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
       const int q = quad_of<G>(lane, k);
       dUq[k] = pk_load(dU + row * G::D + G::V * q);
       dpart[k] = pk_dot(dUq[k], pk_load(u + row * G::D + G::V * q));
+      if (sizeof(T) == 2 && u_lo != nullptr)
+        dpart[k] += pk_dot(dUq[k], pk_load(u_lo + row * G::D + G::V * q));
       hsq[k] = pk_zero<T>();
     }
     if (DV) {
@@ -699,7 +712,8 @@ __host__ __device__ constexpr int rec_stride(int H) {
 template <int H, int F, typename T>
 __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
     int64_t n_rows, const float* __restrict__ el, const float* __restrict__ lse,
-    const T* __restrict__ u, const T* __restrict__ dU, float* __restrict__ rec) {
+    const T* __restrict__ u, const T* __restrict__ u_lo, const T* __restrict__ dU,
+    float* __restrict__ rec) {
   using G = Geo<H, F, T>;
   constexpr int UNR = G::QPL == 1 ? 4 : 1;        // load groups per trip
   constexpr int RPW = G::EPI * UNR;               // rows per trip
@@ -709,6 +723,7 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t r0 = wave * RPW; r0 < n_rows; r0 += nwaves * RPW) {
     Pk<T> a[UNR][G::QPL], b[UNR][G::QPL];
+    const bool lo = sizeof(T) == 2 && u_lo != nullptr;
 #pragma unroll
     for (int g = 0; g < UNR; ++g) {
       const int64_t row = min(r0 + g * G::EPI + r_s, n_rows - 1);
@@ -725,7 +740,12 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
 #pragma unroll
       for (int k = 0; k < G::QPL; ++k) {
         const int q = quad_of<G>(lane, k);
-        const float dk = group_sum<G::QH>(pk_dot(a[g][k], b[g][k]));
+        float dot = pk_dot(a[g][k], b[g][k]);
+        if (lo) {  // bf16: u = hi + lo (the forward's rounding residual)
+          const int64_t rr = min(row, n_rows - 1);
+          dot += pk_dot(a[g][k], pk_load(u_lo + rr * G::D + G::V * q));
+        }
+        const float dk = group_sum<G::QH>(dot);
         // the head's first chunk lane writes D; el and lse ride along
         if (q % G::QH == 0 && row < n_rows) {
           const int h = q / G::QH;
@@ -1167,15 +1187,15 @@ static bool dtype_ok(int32_t dtype, int32_t feat) {
 extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
                                        int32_t dtype, const float* el, const float* er,
                                        const void* hc, float neg_slope, float drop_p,
-                                       uint64_t seed, uint64_t offset, void* u, float* lse,
-                                       float* attd, msha_stream_t stream) {
+                                       uint64_t seed, uint64_t offset, void* u, void* u_lo,
+                                       float* lse, float* attd, msha_stream_t stream) {
   if (int rc = check_graph(g, false)) return rc;
   MSHA_ARG_CHECK(el && er && hc && u && lse, "edge_attention_fwd: null pointer");
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_fwd: p must be in [0,1]");
   if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: unsupported (heads, feat, dtype)");
-  const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
+  const Dropout dp = make_dropout(drop_p, seed, offset, s);
   // batched-gather kernel: one piece per lane and every table addressable by 32-bit offsets
   const int64_t lim = (int64_t)1 << 31;
   const int64_t esz = dtype == MSHA_DTYPE_BF16 ? 2 : 4;
@@ -1192,13 +1212,15 @@ extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32
           hipLaunchKernelGGL((edge_attn_fwd_bat_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>()>), \
                              grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,             \
                              (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,  \
-                             er, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u, lse, attd);     \
+                             er, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u,             \
+                             (bf16_t*)u_lo, lse, attd);                                        \
       } else {                                                                                 \
         if constexpr (h * f * 4 <= 1024)                                                       \
           hipLaunchKernelGGL((edge_attn_fwd_bat_kernel<h, f, float, fwd_epl<h, f, float>()>),  \
                              grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,             \
                              (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,  \
-                             er, (const float*)hc, neg_slope, dp, (float*)u, lse, attd);       \
+                             er, (const float*)hc, neg_slope, dp, (float*)u, (float*)nullptr, \
+                             lse, attd);                                                       \
       }                                                                                        \
     }
     MSHA_FOR_EACH_SHAPE(XB)
@@ -1212,12 +1234,12 @@ extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32
         hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>()>),      \
                            wave_grid(g->n_rows), dim3(256), 0, s, g->rowptr, g->col,           \
                            g->rowflag, g->n_rows, el, er, (const bf16_t*)hc, neg_slope, dp,    \
-                           (bf16_t*)u, lse, attd);                                             \
+                           (bf16_t*)u, (bf16_t*)u_lo, lse, attd);                              \
     } else {                                                                                   \
       hipLaunchKernelGGL((edge_attn_fwd_kernel<h, f, float, fwd_epl<h, f, float>()>),          \
                          wave_grid(g->n_rows), dim3(256), 0, s, g->rowptr, g->col, g->rowflag, \
-                         g->n_rows, el, er, (const float*)hc, neg_slope, dp, (float*)u, lse,   \
-                         attd);                                                                \
+                         g->n_rows, el, er, (const float*)hc, neg_slope, dp, (float*)u,        \
+                         (float*)nullptr, lse, attd);                                          \
     }                                                                                          \
   }
   MSHA_FOR_EACH_SHAPE(X)
@@ -1228,7 +1250,7 @@ extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32
 template <typename T>
 static void launch_bwd_rows(const msha_graph* g, int heads, int feat, const float* el,
                             const float* er, const void* hc, const float* lse, const void* u,
-                            const void* dU, const void* hs, const void* dV, const float* row_coef,
+                            const void* u_lo, const void* dU, const void* hs, const void* dV, const float* row_coef,
                             float neg_slope, const Dropout& dp, float* d_el, float* de,
                             float* attd, int ld, void* d_hs, hipStream_t s) {
 #define X(h, f)                                                                                  \
@@ -1237,12 +1259,14 @@ static void launch_bwd_rows(const msha_graph* g, int heads, int feat, const floa
       if (dV)                                                                                    \
         hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, T, true>), wave_grid(g->n_rows),     \
                            dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,    \
-                           (const T*)hc, lse, (const T*)u, (const T*)dU, (const T*)hs,           \
+                           (const T*)hc, lse, (const T*)u, (const T*)u_lo, (const T*)dU,         \
+                           (const T*)hs,                                                         \
                            (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, ld, (T*)d_hs); \
       else                                                                                       \
         hipLaunchKernelGGL((edge_attn_bwd_rows_kernel<h, f, T, false>), wave_grid(g->n_rows),    \
                            dim3(256), 0, s, g->rowptr, g->col, g->rowflag, g->n_rows, el, er,    \
-                           (const T*)hc, lse, (const T*)u, (const T*)dU, (const T*)hs,           \
+                           (const T*)hc, lse, (const T*)u, (const T*)u_lo, (const T*)dU,         \
+                           (const T*)hs,                                                         \
                            (const T*)dV, row_coef, neg_slope, dp, d_el, de, attd, ld, (T*)d_hs); \
     }                                                                                            \
   }
@@ -1253,7 +1277,8 @@ static void launch_bwd_rows(const msha_graph* g, int heads, int feat, const floa
 extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, int32_t feat,
                                             int32_t dtype, const float* el, const float* er,
                                             const void* hc, const float* lse, const void* u,
-                                            const void* dU, const void* hs, const void* dV,
+                                            const void* u_lo, const void* dU, const void* hs,
+                                            const void* dV,
                                             const float* row_coef, float neg_slope,
                                             float drop_p, uint64_t seed, uint64_t offset,
                                             float* d_el, float* de, float* attd,
@@ -1267,13 +1292,15 @@ extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, 
   MSHA_ARG_CHECK(ld >= heads, "edge_attention_bwd_rows: edge_ld < heads");
   if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_rows: unsupported (heads, feat, dtype)");
-  const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
+  const Dropout dp = make_dropout(drop_p, seed, offset, s);
   if (dtype == MSHA_DTYPE_BF16)
-    launch_bwd_rows<bf16_t>(g, heads, feat, el, er, hc, lse, u, dU, hs, dV, row_coef, neg_slope,
+    launch_bwd_rows<bf16_t>(g, heads, feat, el, er, hc, lse, u, u_lo, dU, hs, dV, row_coef,
+                            neg_slope,
                             dp, d_el, de, attd, ld, d_hs, s);
   else
-    launch_bwd_rows<float>(g, heads, feat, el, er, hc, lse, u, dU, hs, dV, row_coef, neg_slope,
+    launch_bwd_rows<float>(g, heads, feat, el, er, hc, lse, u, nullptr, dU, hs, dV, row_coef,
+                           neg_slope,
                            dp, d_el, de, attd, ld, d_hs, s);
   return check_launch("edge_attention_bwd_rows");
 }
@@ -1354,7 +1381,7 @@ extern "C" size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph*
 template <typename T>
 static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const float* el,
                              const float* er, const void* hc, const float* lse, const void* u,
-                             const void* dU, float neg_slope, const Dropout& dp, float* d_el,
+                             const void* u_lo, const void* dU, float neg_slope, const Dropout& dp, float* d_el,
                              float* d_er, void* d_hc, float* de, float* rec, float* part,
                              float* part_x, hipStream_t s) {
   // the buffer-descriptor kernel addresses each table with 32-bit byte offsets
@@ -1370,7 +1397,7 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
   if (heads == h && feat == f) {                                                               \
     if constexpr (f % Pk<T>::V == 0) {                                                         \
       hipLaunchKernelGGL((bwd_row_stats_kernel<h, f, T>), wave_grid(g->n_rows / 8 + 1), dim3(256), 0,  \
-                         s, g->n_rows, el, lse, (const T*)u, (const T*)dU, rec);               \
+                         s, g->n_rows, el, lse, (const T*)u, (const T*)u_lo, (const T*)dU, rec); \
       if (f * sizeof(T) <= 64 && COLS_EH && buf_ok)                                            \
         hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
@@ -1405,7 +1432,8 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
 extern "C" int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads, int32_t feat,
                                              int32_t dtype, const float* el, const float* er,
                                              const void* hc, const float* lse, const void* u,
-                                             const void* dU, float neg_slope, float drop_p,
+                                             const void* u_lo, const void* dU, float neg_slope,
+                                             float drop_p,
                                              uint64_t seed, uint64_t offset, float* d_el,
                                              float* d_er, void* d_hc, float* de, void* ws,
                                              size_t ws_bytes, msha_stream_t stream) {
@@ -1425,13 +1453,13 @@ extern "C" int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads,
   const size_t rec_bytes = ((size_t)g->n_rows * rec_stride(heads) * sizeof(float) + 255) & ~(size_t)255;
   float* part = (float*)((char*)ws + rec_bytes);
   float* part_x = part + g->n_chunks * D;
-  const Dropout dp = make_dropout(drop_p, seed, offset);
   hipStream_t s = (hipStream_t)stream;
+  const Dropout dp = make_dropout(drop_p, seed, offset, s);
   if (dtype == MSHA_DTYPE_BF16)
-    launch_bwd_fused<bf16_t>(g, heads, feat, el, er, hc, lse, u, dU, neg_slope, dp, d_el, d_er,
+    launch_bwd_fused<bf16_t>(g, heads, feat, el, er, hc, lse, u, u_lo, dU, neg_slope, dp, d_el, d_er,
                              d_hc, de, rec, part, part_x, s);
   else
-    launch_bwd_fused<float>(g, heads, feat, el, er, hc, lse, u, dU, neg_slope, dp, d_el, d_er,
+    launch_bwd_fused<float>(g, heads, feat, el, er, hc, lse, u, nullptr, dU, neg_slope, dp, d_el, d_er,
                             d_hc, de, rec, part, part_x, s);
   return check_launch("edge_attention_bwd_fused");
 }

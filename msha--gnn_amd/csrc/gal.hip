@@ -83,7 +83,7 @@ extern "C" int msha_gal_fwd(const msha_graph* g, const float* h, float drop_p, u
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "gal_fwd: p must be in [0,1]");
   hipLaunchKernelGGL(gal_kernel<false>, gal_grid(g->n_rows, g->n_cols), dim3(256), 0,
                      (hipStream_t)stream, g->rowptr, g->col, g->n_rows, g->n_cols, h,
-                     (const float*)nullptr, make_dropout(drop_p, seed, offset), out);
+                     (const float*)nullptr, make_dropout(drop_p, seed, offset, (hipStream_t)stream), out);
   return check_launch("gal_fwd");
 }
 
@@ -94,6 +94,6 @@ extern "C" int msha_gal_bwd(const msha_graph* g, const float* h, const float* do
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "gal_bwd: p must be in [0,1]");
   hipLaunchKernelGGL(gal_kernel<true>, gal_grid(g->n_rows, g->n_cols), dim3(256), 0,
                      (hipStream_t)stream, g->rowptr, g->col, g->n_rows, g->n_cols, h, dout,
-                     make_dropout(drop_p, seed, offset), dh);
+                     make_dropout(drop_p, seed, offset, (hipStream_t)stream), dh);
   return check_launch("gal_bwd");
 }

@@ -652,7 +652,7 @@ static GemmArgs base_args(int64_t M, int64_t N, int64_t K) {
   p.M = M;
   p.N = N;
   p.K = K;
-  p.dp = make_dropout(0.f, 0, 0);
+  p.dp = make_dropout(0.f, 0, 0, nullptr);
   return p;
 }
 
@@ -827,7 +827,7 @@ extern "C" int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const flo
   p.B = W; p.sBk = 1; p.sBn = K;  // nn.Linear weight (N x K): B[k, n] = W[n, k]
   p.C = out; p.ldc = N;
   p.act = act; p.bias = bias;
-  p.dp = make_dropout(drop_p, seed, offset);
+  p.dp = make_dropout(drop_p, seed, offset, (hipStream_t)stream);
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
   if (!skinny_pair_linear(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, W, bias, p.act, p.dp, out,
                           (hipStream_t)stream))

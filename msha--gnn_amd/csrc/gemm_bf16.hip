@@ -537,7 +537,7 @@ extern "C" int msha_pair_linear_bf16_ex(int64_t n_pairs, int64_t K, int64_t N, c
   p.B = (const bf16_t*)W; p.sBk = 1; p.sBn = K;  // nn.Linear weight (N x K)
   p.C = out; p.ldc = N; p.c_bf16 = out_dtype == MSHA_DTYPE_BF16;
   p.act = act; p.bias = bias;
-  p.dp = make_dropout(drop_p, seed, offset);
+  p.dp = make_dropout(drop_p, seed, offset, (hipStream_t)stream);
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
   if (skinny_pair_linear_bf16(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, W, bias, p.act, p.dp, out,
                               p.c_bf16 != 0, (hipStream_t)stream))

@@ -415,13 +415,13 @@ static int check(const msha_graph* g, const msha_groups* grp, int64_t B, const i
 static OursArgs make_args(const msha_graph* g, const msha_groups* grp, int64_t B,
                           const int64_t* src, int32_t heads, int32_t feat, const void* h2,
                           const float* a3s, const float* a4s, float slope, float drop_p,
-                          uint64_t seed, uint64_t offset) {
+                          uint64_t seed, uint64_t offset, hipStream_t s) {
   OursArgs a;
   a.B = B; a.N = g->n_rows; a.M = g->n_cols; a.H = heads; a.F = feat; a.src = src;
   a.gid3 = grp->gid3; a.gptr3 = grp->gptr3; a.gmem3 = grp->gmem3;
   a.gid4 = grp->gid4; a.gptr4 = grp->gptr4; a.gmem4 = grp->gmem4;
   a.h2 = h2; a.a3s = a3s; a.a4s = a4s; a.slope = slope;
-  a.dp = make_dropout(drop_p, seed, offset);
+  a.dp = make_dropout(drop_p, seed, offset, s);
   return a;
 }
 
@@ -458,9 +458,9 @@ extern "C" int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, 
   MSHA_ARG_CHECK(h2 && a3s && a4s && el && er && lse && u_inter && bstat && u_out,
                  "ours_intra_fwd: null pointer");
   MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "ours_intra_fwd: bad dtype");
-  const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
-                               seed, offset);
   hipStream_t s = (hipStream_t)stream;
+  const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
+                               seed, offset, s);
   if (dtype == MSHA_DTYPE_BF16)
     launch_fwd<bf16_t>(a, g, B, el, er, lse, u_inter, bstat, u_out, s);
   else
@@ -517,9 +517,9 @@ extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, 
   MSHA_ARG_CHECK(h2 && a3s && a4s && bstat && G && bgrad, "ours_intra_bwd: null pointer");
   MSHA_ARG_CHECK(stage == 1 || (dU && row_coef && da3s && da4s), "ours_intra_bwd: stage 0 outputs");
   MSHA_ARG_CHECK(stage == 0 || d_hs, "ours_intra_bwd: stage 1 needs d_hs");
-  const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
-                               seed, offset);
   hipStream_t s = (hipStream_t)stream;
+  const OursArgs a = make_args(g, grp, B, src, heads, feat, h2, a3s, a4s, neg_slope, drop_p,
+                               seed, offset, s);
   if (B == 0) {
     if (stage == 0) {
       if (hipMemsetAsync(da3s, 0, sizeof(float) * heads * feat, s) != hipSuccess ||

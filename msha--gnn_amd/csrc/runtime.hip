@@ -1,4 +1,5 @@
 // ABI plumbing: version, thread-local error string, dropout mask export.
+#include <atomic>
 #include <string>
 
 #include "common.h"
@@ -6,9 +7,26 @@
 namespace msha {
 
 static thread_local std::string g_last_error;
-static const uint64_t* g_rng_counter = nullptr;
 
-const uint64_t* rng_counter() { return g_rng_counter; }
+// dropout replay counters, one slot per device (msha_set_rng_counter): a kernel launched
+// on a stream of device d reads device d's counter, so two devices (or two processes'
+// graphs) never share one
+constexpr int kMaxDevices = 64;
+static std::atomic<const uint64_t*> g_rng_counter[kMaxDevices];
+
+static int stream_device(hipStream_t s) {
+  int dev = -1;
+  if (s == nullptr || hipStreamGetDevice(s, &dev) != hipSuccess) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  return dev;
+}
+
+const uint64_t* rng_counter(hipStream_t s) {
+  const int dev = stream_device(s);
+  return dev >= 0 && dev < kMaxDevices ? g_rng_counter[dev].load(std::memory_order_acquire)
+                                       : nullptr;
+}
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 
@@ -38,9 +56,18 @@ extern "C" int msha_abi_version(void) { return MSHA_ABI_VERSION; }
 
 extern "C" const char* msha_last_error(void) { return msha::g_last_error.c_str(); }
 
-extern "C" int msha_set_rng_counter(const uint64_t* counter) {
-  msha::g_rng_counter = counter;
+extern "C" int msha_set_rng_counter(int32_t device, const uint64_t* counter) {
+  if (device < 0 && hipGetDevice(&device) != hipSuccess)
+    return msha::fail(MSHA_ERR_HIP, "set_rng_counter: no current device");
+  MSHA_ARG_CHECK(device < msha::kMaxDevices, "set_rng_counter: device index out of range");
+  msha::g_rng_counter[device].store(counter, std::memory_order_release);
   return MSHA_OK;
+}
+
+extern "C" const uint64_t* msha_get_rng_counter(int32_t device) {
+  if (device < 0 && hipGetDevice(&device) != hipSuccess) return nullptr;
+  if (device >= msha::kMaxDevices) return nullptr;
+  return msha::g_rng_counter[device].load(std::memory_order_acquire);
 }
 
 extern "C" int msha_dropout_keep_mask(uint64_t seed, uint64_t offset, int64_t n, float p,
@@ -48,7 +75,7 @@ extern "C" int msha_dropout_keep_mask(uint64_t seed, uint64_t offset, int64_t n,
   MSHA_ARG_CHECK(n >= 0 && (n == 0 || keep != nullptr), "dropout_keep_mask: bad buffer");
   MSHA_ARG_CHECK(p >= 0.f && p <= 1.f, "dropout_keep_mask: p must be in [0, 1]");
   if (n == 0) return MSHA_OK;
-  msha::Dropout d = msha::make_dropout(p, seed, offset);
+  msha::Dropout d = msha::make_dropout(p, seed, offset, (hipStream_t)stream);
   d.active = true;  // p == 0 still runs the generator: every element kept
   hipLaunchKernelGGL(msha::dropout_mask_kernel, dim3(msha::grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, d, n, keep);

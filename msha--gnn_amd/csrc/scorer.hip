@@ -107,9 +107,50 @@ __global__ void __launch_bounds__(256) pair_hadamard_kernel(
   }
 }
 
+// any other predictor string (LLP.py:104-115 takes neither branch): y = sigmoid(x_i * x_j)
+// elementwise, shape (B, F); backward dx_i = dy y (1 - y) x_j, dx_j = dy y (1 - y) x_i
+__global__ void __launch_bounds__(256) pair_hadamard_sigmoid_kernel(
+    int64_t n_pairs, int F, const float* __restrict__ G, int64_t ldg,
+    const int64_t* __restrict__ gi, const float* __restrict__ G2, int64_t ldg2,
+    const int64_t* __restrict__ gj, const float* __restrict__ y, const float* __restrict__ dy,
+    float* __restrict__ y_or_dxi, float* __restrict__ dxj) {
+  const int64_t total = n_pairs * F;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = t / F;
+    const int f = (int)(t % F);
+    const float xi = G[(gi ? gi[b] : b) * ldg + f];
+    const float xj = G2[(gj ? gj[b] : b) * ldg2 + f];
+    if (dy == nullptr) {
+      y_or_dxi[t] = sigmoidf_(xi * xj);
+    } else {
+      const float yt = y[t];
+      const float dz = dy[t] * yt * (1.f - yt);
+      y_or_dxi[t] = dz * xj;
+      dxj[t] = dz * xi;
+    }
+  }
+}
+
 }  // namespace msha
 
 using namespace msha;
+
+extern "C" int msha_pair_hadamard_sigmoid(int64_t n_pairs, int32_t feat, const float* G,
+                                          int64_t ldg, const int64_t* gi, const float* G2,
+                                          int64_t ldg2, const int64_t* gj, const float* y,
+                                          const float* dy, float* y_or_dxi, float* dxj,
+                                          msha_stream_t stream) {
+  MSHA_ARG_CHECK(n_pairs >= 0 && feat > 0 && G && G2 && y_or_dxi,
+                 "pair_hadamard_sigmoid: bad arguments");
+  MSHA_ARG_CHECK(dy == nullptr || (y != nullptr && dxj != nullptr),
+                 "pair_hadamard_sigmoid: the backward needs y and dxj");
+  if (n_pairs == 0) return MSHA_OK;
+  hipLaunchKernelGGL(pair_hadamard_sigmoid_kernel, dim3(grid_for(n_pairs * feat, 256, 16384)),
+                     dim3(256), 0, (hipStream_t)stream, n_pairs, (int)feat, G, ldg, gi, G2, ldg2,
+                     gj, y, dy, y_or_dxi, dxj);
+  return check_launch("pair_hadamard_sigmoid");
+}
 
 extern "C" int msha_pair_inner_fwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
                                    const int64_t* gi, const float* G2, int64_t ldg2,

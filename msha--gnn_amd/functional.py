@@ -56,20 +56,38 @@ def new_seed() -> int:
     return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
 
 
-_RNG_COUNTER = None
+_RNG_COUNTERS: dict = {}  # device index -> installed counter tensor (kept alive)
 
 
-def set_rng_counter(counter: torch.Tensor | None):
+def set_rng_counter(counter: torch.Tensor | None, device=None):
     """Install (or remove, None) a device int64 replay counter for every dropout draw
-    of the library (msha_set_rng_counter): increment it inside a captured HIP graph
-    (``counter.add_(1)``) and each replay draws fresh masks."""
-    global _RNG_COUNTER
+    the library launches on ``device`` (default: the counter's device, else the
+    current one; msha_set_rng_counter keeps one slot per device): increment it inside
+    a captured HIP graph (``counter.add_(1)``) and each replay draws fresh masks.
+    Returns the counter previously installed for that device (None if none), so a
+    caller can restore it."""
     if counter is not None:
         _lib.require_cuda(counter)
         if counter.dtype != torch.int64 or counter.numel() < 1:
             raise ValueError("rng counter: a CUDA int64 tensor")
-    _RNG_COUNTER = counter  # keep it alive while installed
-    _lib.call("msha_set_rng_counter", None if counter is None else counter.data_ptr())
+        dev = counter.device.index if device is None else torch.device(device).index
+    else:
+        dev = torch.device(device).index if device is not None else None
+    if dev is None:
+        dev = torch.cuda.current_device()
+    if counter is not None and counter.device.index != dev:
+        raise ValueError(f"rng counter lives on cuda:{counter.device.index}, not cuda:{dev}")
+    prev = _RNG_COUNTERS.pop(dev, None)
+    if counter is not None:
+        _RNG_COUNTERS[dev] = counter
+    _lib.call("msha_set_rng_counter", dev, None if counter is None else counter.data_ptr())
+    return prev
+
+
+def rng_counter(device=None):
+    """The replay counter installed for ``device`` (default: current), or None."""
+    dev = torch.device(device).index if device is not None else None
+    return _RNG_COUNTERS.get(torch.cuda.current_device() if dev is None else dev)
 
 
 def _stream(t):
@@ -89,14 +107,17 @@ class _EdgeAttention(torch.autograd.Function):
         s = _stream(el)
         g = graph.desc
         u = torch.empty(n, H, F, device=dev, dtype=dt)
+        # bf16 tables under autograd: keep the rounding residual of u for the backward's
+        # D = dU . u (include/msha_gnn.h, u_lo)
+        u_lo = torch.empty_like(u) if dt == BF16 and any(ctx.needs_input_grad[:4]) else None
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)
         attd = None
         if hs is not None:
             attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
         ev = _timed("edge_attention_fwd")
         _lib.call("msha_edge_attention_fwd", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
-                  hc.data_ptr(), slope, p, seed, 0, u.data_ptr(), lse.data_ptr(),
-                  _lib.ptr(attd), s)
+                  hc.data_ptr(), slope, p, seed, 0, u.data_ptr(), _lib.ptr(u_lo),
+                  lse.data_ptr(), _lib.ptr(attd), s)
         if ev is not None:
             ev[1].record()
         v = None
@@ -105,14 +126,16 @@ class _EdgeAttention(torch.autograd.Function):
             _csc_aggregate(graph, H, F, attd, None, hs, v, None, s)
         ctx.graph, ctx.p, ctx.seed, ctx.slope = graph, p, seed, slope
         ctx.has_hs = hs is not None
-        ctx.save_for_backward(el, er, hc, hs if hs is not None else el.new_empty(0), lse, u)
+        ctx.save_for_backward(el, er, hc, hs if hs is not None else el.new_empty(0), lse, u,
+                              u_lo if u_lo is not None else el.new_empty(0))
         if v is None:
             return u
         return u, v
 
     @staticmethod
     def backward(ctx, dU, dV=None):
-        el, er, hc, hs, lse, u = ctx.saved_tensors
+        el, er, hc, hs, lse, u, u_lo = ctx.saved_tensors
+        u_lo = u_lo if u_lo.numel() else None
         graph = ctx.graph
         n, H = el.shape
         m, _, F = hc.shape
@@ -126,7 +149,7 @@ class _EdgeAttention(torch.autograd.Function):
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
         if not use_dv and FUSED_BWD:
-            return _bwd_fused(ctx, el, er, hc, lse, u, dU, d_el, hs)
+            return _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs)
         # one (de, attd) record of 2H floats per edge: the column pass reads it as one
         # 64-B segment at C4 (the CSC visits edges in random order)
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)
@@ -134,7 +157,8 @@ class _EdgeAttention(torch.autograd.Function):
         d_hs = torch.empty(n, H, F, device=dev, dtype=dt) if use_dv else None
         ev = _timed("edge_attention_bwd_rows")
         _lib.call("msha_edge_attention_bwd_rows", g, H, F, _code(dt), el.data_ptr(),
-                  er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
+                  er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), _lib.ptr(u_lo),
+                  dU.data_ptr(),
                   hs.data_ptr() if use_dv else None, _lib.ptr(dV), None, ctx.slope, ctx.p,
                   ctx.seed, 0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), 2 * H,
                   _lib.ptr(d_hs), s)
@@ -156,7 +180,7 @@ class _EdgeAttention(torch.autograd.Function):
 FUSED_BWD = True
 
 
-def _bwd_fused(ctx, el, er, hc, lse, u, dU, d_el, hs):
+def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs):
     graph = ctx.graph
     n, H = el.shape
     m, _, F = hc.shape
@@ -172,7 +196,8 @@ def _bwd_fused(ctx, el, er, hc, lse, u, dU, d_el, hs):
     d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
     ev = _timed("edge_attention_bwd_fused")
     _lib.call("msha_edge_attention_bwd_fused", g, H, F, _code(hc.dtype), el.data_ptr(),
-              er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), dU.data_ptr(),
+              er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), _lib.ptr(u_lo),
+              dU.data_ptr(),
               ctx.slope, ctx.p, ctx.seed, 0, d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
               de.data_ptr(), ws.data_ptr(), wsb, s)
     if ev is not None:
@@ -460,8 +485,9 @@ class _ProjectScores(torch.autograd.Function):
             o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
             wsb = int(_lib.load().msha_head_colsum_workspace_size(M, H, Fd))
             ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
-            _lib.call("msha_head_colsum", M, H, Fd, _code(dt), _f32c(d1).data_ptr(),
-                      _lib.ptr(_f32c(d2)), h.data_ptr(), o1.data_ptr(), _lib.ptr(o2),
+            d1, d2 = _f32c(d1), _f32c(d2)  # held until the launch (see bn_lrelu)
+            _lib.call("msha_head_colsum", M, H, Fd, _code(dt), d1.data_ptr(),
+                      _lib.ptr(d2), h.data_ptr(), o1.data_ptr(), _lib.ptr(o2),
                       ws.data_ptr(), ws.numel(), s)
             outs = [o1] + ([o2] if o2 is not None else [])
             k = 0
@@ -595,9 +621,13 @@ def bn_lrelu(x: torch.Tensor, bn: torch.nn.BatchNorm1d, slope: float,
         xc = _tc(x, dt)
         R, C = xc.shape
         y = torch.empty_like(xc)
+        # fp32 views/copies held in locals until the launch: a temporary freed after
+        # data_ptr() can be handed to the next copy by the caching allocator (bf16 models:
+        # weight and bias copies would share one block)
         rm, rv = _f32c(bn.running_mean), _f32c(bn.running_var)
-        _lib.call("msha_bn_lrelu_fwd", R, C, _code(dt), xc.data_ptr(), _lib.ptr(_f32c(bn.weight)),
-                  _lib.ptr(_f32c(bn.bias)), bn.eps, slope, 0, 0.0, rm.data_ptr(), rv.data_ptr(),
+        w32, b32 = _f32c(bn.weight), _f32c(bn.bias)
+        _lib.call("msha_bn_lrelu_fwd", R, C, _code(dt), xc.data_ptr(), _lib.ptr(w32),
+                  _lib.ptr(b32), bn.eps, slope, 0, 0.0, rm.data_ptr(), rv.data_ptr(),
                   None, None, y.data_ptr(), None, 0, _stream(xc))
         return y
     track = bn.training and bn.track_running_stats
@@ -679,6 +709,38 @@ class _PairLayer(torch.autograd.Function):
         return dx, None, dW, db, None, None, None
 
 
+class _PairHadamardSigmoid(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_i, x_j):
+        x_i, x_j = _f32c(x_i), _f32c(x_j)
+        B, Fd = x_i.shape
+        y = torch.empty_like(x_i)
+        _lib.call("msha_pair_hadamard_sigmoid", B, Fd, x_i.data_ptr(), Fd, None, x_j.data_ptr(),
+                  Fd, None, None, None, y.data_ptr(), None, _stream(x_i))
+        ctx.save_for_backward(x_i, x_j, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x_i, x_j, y = ctx.saved_tensors
+        B, Fd = x_i.shape
+        dxi, dxj = torch.empty_like(x_i), torch.empty_like(x_j)
+        _lib.call("msha_pair_hadamard_sigmoid", B, Fd, x_i.data_ptr(), Fd, None, x_j.data_ptr(),
+                  Fd, None, y.data_ptr(), _f32c(dy).data_ptr(), dxi.data_ptr(), dxj.data_ptr(),
+                  _stream(x_i))
+        return dxi, dxj
+
+
+def pair_hadamard_sigmoid(x_i, x_j):
+    """LinkPredictor with any predictor other than 'mlp' / 'inner' (LLP.py:104-115):
+    ``sigmoid(x_i * x_j)``, (B, F)."""
+    _lib.require_cuda(x_i, x_j)
+    if x_i.shape != x_j.shape or x_i.dim() != 2:
+        raise ValueError(f"pair_hadamard_sigmoid: x_i {tuple(x_i.shape)} vs x_j "
+                         f"{tuple(x_j.shape)}")
+    return _PairHadamardSigmoid.apply(x_i, x_j)
+
+
 def pair_inner(x_i, x_j):
     """'inner' LinkPredictor head: sigmoid(sum(x_i * x_j, -1))  (LLP.py:112-115)."""
     _lib.require_cuda(x_i, x_j)
@@ -748,11 +810,12 @@ class _OursAttention(torch.autograd.Function):
         s = _stream(el)
         g = graph.desc
         u_inter = torch.empty(n, H, Fd, device=dev, dtype=dt)
+        u_lo = torch.empty_like(u_inter) if dt == BF16 and any(ctx.needs_input_grad[:4]) else None
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)
         attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
         _lib.call("msha_edge_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
-                  h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(), lse.data_ptr(),
-                  attd.data_ptr(), s)
+                  h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(), _lib.ptr(u_lo),
+                  lse.data_ptr(), attd.data_ptr(), s)
         v = torch.empty(m, H, Fd, device=dev, dtype=dt)
         _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
         bstat = torch.empty(max(B, 1), H, 8, device=dev, dtype=torch.float32)
@@ -762,14 +825,16 @@ class _OursAttention(torch.autograd.Function):
                   a3s.data_ptr(), a4s.data_ptr(), el.data_ptr(), er.data_ptr(), lse.data_ptr(),
                   u_inter.data_ptr(), slope, p, seed, 0, bstat.data_ptr(), u.data_ptr(), s)
         ctx.graph, ctx.groups, ctx.p, ctx.seed, ctx.slope = graph, groups, p, seed, slope
-        ctx.save_for_backward(el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src)
+        ctx.save_for_backward(el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src,
+                              u_lo if u_lo is not None else el.new_empty(0))
         # post-dropout inter attention and batch statistics: outputs for record mode
         ctx.mark_non_differentiable(attd, bstat)
         return u, v, attd, bstat
 
     @staticmethod
     def backward(ctx, dU, dV, _attd=None, _bstat=None):
-        el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src = ctx.saved_tensors
+        el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src, u_lo = ctx.saved_tensors
+        u_lo = u_lo if u_lo.numel() else None
         graph, groups = ctx.graph, ctx.groups
         n, H = el.shape
         m, _, Fd = h1.shape
@@ -799,7 +864,7 @@ class _OursAttention(torch.autograd.Function):
         de, attd = rec[:, 0], rec[:, 1]
         d_hs = torch.empty(n, H, Fd, device=dev, dtype=dt)
         _lib.call("msha_edge_attention_bwd_rows", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
-                  h1.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), dU.data_ptr(),
+                  h1.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), _lib.ptr(u_lo), dU.data_ptr(),
                   h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p, ctx.seed,
                   0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), 2 * H, d_hs.data_ptr(), s)
         _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),

@@ -245,11 +245,12 @@ class LinkPredictor(torch.nn.Module):
     def forward(self, x_i, x_j):
         if self.predictor == "inner":
             return MF.pair_inner(x_i, x_j)
-        if self.predictor != "mlp":
-            raise NotImplementedError(f"predictor {self.predictor!r}: only 'mlp' and 'inner'")
         used = self.lins[:-1]
-        if len(used) == 0:
-            raise NotImplementedError("LinkPredictor with num_layers < 2 (no used Linear)")
+        if self.predictor != "mlp" or len(used) == 0:
+            # LLP.py:104-115: any other predictor string takes neither branch and the
+            # reference returns sigmoid(x_i * x_j), shape (B, F).  (num_layers <= 2 still
+            # builds two Linears, LLP.py:93-96, so 'mlp' always applies one.)
+            return MF.pair_hadamard_sigmoid(x_i, x_j)
         x = None
         for k, lin in enumerate(used):
             last = k == len(used) - 1
@@ -313,19 +314,35 @@ def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_a
     return _epilogues(heads, us, vs)
 
 
+class _RecordState:
+    """Where record mode leaves the whole inter attention when no ``train`` module is
+    loaded (the reference assigns it to ``train.Coeff12new``, Ours.py:93)."""
+
+    Coeff12new = None
+
+
+record_state = _RecordState()
+
+
 def _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4):
-    """Ours.py:92-96 attention dump for Explainer (record=True): the last head's
-    post-dropout inter attention (dense N x M) into Coeff12 and its intra rows into
-    Coeff3[source_index] / Coeff4[source_index] (each head overwrites, as in the
-    reference).  Off the hot path (torch scatter); dropout-free values (Record()
-    runs in eval mode, train.py:284-291)."""
+    """Ours.py:92-96 attention dump for Explainer (record=True).  As the reference:
+    the (N, M) post-dropout inter attention is assigned to ``train.Coeff12new`` (the
+    ``train`` module when one is loaded, else ``layers.record_state``); the batch rows of
+    the (B, N) city / province attention go to Coeff3[source_index] /
+    Coeff4[source_index]; the Coeff12 argument is not written.  Every head overwrites,
+    so the last head's values remain.  Off the hot path (torch scatter); Record() runs
+    in eval mode (train.py:284-291), so the values are dropout-free."""
+    import sys
+
     H = len(heads)
     dev = attd.device
     rows = torch.repeat_interleave(torch.arange(graph.n_rows, device=dev), graph.deg().long())
     dense = torch.zeros(graph.n_rows, graph.n_cols, device=dev)
     dense[rows, graph.col.long()] = attd[: graph.n_edges, H - 1]
-    if Coeff12 is not None:
-        Coeff12.copy_(dense.to(Coeff12.dtype))
+    record_state.Coeff12new = dense
+    train_mod = sys.modules.get("train")
+    if train_mod is not None:
+        train_mod.Coeff12new = dense
     (g3, _, _), (g4, _, _) = groups._keep
     for Cf, gid, col in ((Coeff3, g3, 5), (Coeff4, g4, 6)):
         if Cf is None:

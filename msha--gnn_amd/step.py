@@ -32,8 +32,11 @@ class GraphedStep:
 
     def __init__(self, body: Callable[[], torch.Tensor], device, warmup: int = 3):
         self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)
-        MF.set_rng_counter(self.counter)
+        # this step's counter replaces (and on close() restores) the device's previous one
+        self._prev = MF.set_rng_counter(self.counter)
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):  # warm caches (graph views, workspaces) off-graph
@@ -51,5 +54,12 @@ class GraphedStep:
         return self.out
 
     def close(self):
-        MF.set_rng_counter(None)
+        """Drop the graph; reinstall the counter that was installed before this step
+        (if this step's counter is still the device's), so other live steps keep drawing
+        fresh masks.  The captured kernels keep reading ``self.counter``'s memory, which
+        stays alive with this object."""
+        if self.graph is None:
+            return
+        if MF.rng_counter(self.device) is self.counter:
+            MF.set_rng_counter(self._prev, self.device)
         self.graph = None

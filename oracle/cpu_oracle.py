@@ -10,23 +10,32 @@ import numpy as np
 
 from . import build_oracle
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        path = build_oracle.LIB
+def lib(fp64=False):
+    """The fp32 restatement (CPU baseline) or, fp64=True, the same source compiled with
+    REAL = double (symbols *_f64), the checker of the full-size parity tests."""
+    if fp64 not in _libs:
+        path = build_oracle.LIB64 if fp64 else build_oracle.LIB
         if not os.path.exists(path):
-            path = build_oracle.build()
-        _lib = C.CDLL(path)
+            build_oracle.build()
+        lb = C.CDLL(path)
         P, I64, I = C.c_void_p, C.c_int64, C.c_int
-        _lib.oracle_edge_attention_fwd.argtypes = [I64, P, P, I, I, P, P, P, C.c_float, P, P]
-        _lib.oracle_edge_attention_bwd_rows.argtypes = [I64, P, P, I, I, P, P, P, P, P, P,
-                                                        C.c_float, P, P, P]
-        _lib.oracle_csc_aggregate.argtypes = [I64, P, P, P, I, I, P, P, P, P, P]
-        _lib.oracle_num_threads.restype = I
-    return _lib
+        R = C.c_double if fp64 else C.c_float
+        sfx = "_f64" if fp64 else ""
+        getattr(lb, "oracle_edge_attention_fwd" + sfx).argtypes = [I64, P, P, I, I, P, P, P, R,
+                                                                   P, P]
+        getattr(lb, "oracle_edge_attention_bwd_rows" + sfx).argtypes = [
+            I64, P, P, I, I, P, P, P, P, P, P, R, P, P, P]
+        getattr(lb, "oracle_csc_aggregate" + sfx).argtypes = [I64, P, P, P, I, I, P, P, P, P, P]
+        getattr(lb, "oracle_num_threads" + sfx).restype = I
+        _libs[fp64] = lb
+    return _libs[fp64]
+
+
+def _fn(name, fp64):
+    return getattr(lib(fp64), name + ("_f64" if fp64 else ""))
 
 
 def _p(a):
@@ -41,34 +50,38 @@ def threads():
     return lib().oracle_num_threads()
 
 
-def edge_attention_fwd(rowptr, col, el, er, hc, slope=0.2):
+def edge_attention_fwd(rowptr, col, el, er, hc, slope=0.2, fp64=False):
+    """u (n, H, F), lse (n, H) of the fused forward; fp64=True: in double precision."""
+    dt = np.float64 if fp64 else np.float32
     n, H = el.shape
     F = hc.shape[-1]
     rowptr, col = _c(rowptr, np.int32), _c(col, np.int32)
-    el, er, hc = _c(el, np.float32), _c(er, np.float32), _c(hc, np.float32)
-    u = np.empty((n, H, F), np.float32)
-    lse = np.empty((n, H), np.float32)
-    lib().oracle_edge_attention_fwd(n, _p(rowptr), _p(col), H, F, _p(el), _p(er), _p(hc), slope,
-                                    _p(u), _p(lse))
+    el, er, hc = _c(el, dt), _c(er, dt), _c(hc, dt)
+    u = np.empty((n, H, F), dt)
+    lse = np.empty((n, H), dt)
+    _fn("oracle_edge_attention_fwd", fp64)(n, _p(rowptr), _p(col), H, F, _p(el), _p(er),
+                                           _p(hc), slope, _p(u), _p(lse))
     return u, lse
 
 
 def edge_attention_bwd(rowptr, col, colptr, csc_row, csc_eid, el, er, hc, lse, u, dU,
-                       slope=0.2):
+                       slope=0.2, fp64=False):
+    """(d_el, d_er, d_hc) of the fused forward's u; fp64=True: in double precision."""
+    dt = np.float64 if fp64 else np.float32
     n, H = el.shape
     m, _, F = hc.shape
     E = len(col)
     args = [_c(x, np.int32) for x in (rowptr, col, colptr, csc_row, csc_eid)]
     rowptr, col, colptr, csc_row, csc_eid = args
-    el, er, hc, lse, u, dU = (_c(x, np.float32) for x in (el, er, hc, lse, u, dU))
-    d_el = np.empty((n, H), np.float32)
-    de = np.empty((E, H), np.float32)
-    att = np.empty((E, H), np.float32)
-    lib().oracle_edge_attention_bwd_rows(n, _p(rowptr), _p(col), H, F, _p(el), _p(er), _p(hc),
-                                         _p(lse), _p(u), _p(dU), slope, _p(d_el), _p(de),
-                                         _p(att))
-    d_hc = np.empty((m, H, F), np.float32)
-    d_er = np.empty((m, H), np.float32)
-    lib().oracle_csc_aggregate(m, _p(colptr), _p(csc_row), _p(csc_eid), H, F, _p(att), _p(de),
-                               _p(dU), _p(d_hc), _p(d_er))
+    el, er, hc, lse, u, dU = (_c(x, dt) for x in (el, er, hc, lse, u, dU))
+    d_el = np.empty((n, H), dt)
+    de = np.empty((E, H), dt)
+    att = np.empty((E, H), dt)
+    _fn("oracle_edge_attention_bwd_rows", fp64)(n, _p(rowptr), _p(col), H, F, _p(el), _p(er),
+                                                _p(hc), _p(lse), _p(u), _p(dU), slope, _p(d_el),
+                                                _p(de), _p(att))
+    d_hc = np.empty((m, H, F), dt)
+    d_er = np.empty((m, H), dt)
+    _fn("oracle_csc_aggregate", fp64)(m, _p(colptr), _p(csc_row), _p(csc_eid), H, F, _p(att),
+                                      _p(de), _p(dU), _p(d_hc), _p(d_er))
     return d_el, d_er, d_hc

@@ -9,65 +9,78 @@
  * and the autograd backward (d_el, d_er, d_hc).  Column sums use the CSC view.
  * Pinned to the reference through gnn_oracle.py (tests/test_oracle_golden.py) by
  * tests/test_oracle_c.py.
+ *
+ * Built twice (oracle/build_oracle.py): REAL = float (libmsha_oracle.so, the CPU
+ * baseline) and REAL = double with the suffix _f64 (libmsha_oracle64.so, the fp64
+ * checker of the full-size parity tests).
  */
-#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <tgmath.h>
 
-static inline float lrelu(float x, float s) { return x > 0.f ? x : x * s; }
+#ifndef REAL
+#define REAL float
+#endif
+#ifndef SFX
+#define SFX(name) name
+#endif
 
-void oracle_edge_attention_fwd(int64_t n_rows, const int32_t* rowptr, const int32_t* col, int H,
-                               int F, const float* el, const float* er, const float* hc,
-                               float slope, float* u, float* lse) {
+typedef REAL real;
+
+static inline real lrelu(real x, real s) { return x > 0 ? x : x * s; }
+
+void SFX(oracle_edge_attention_fwd)(int64_t n_rows, const int32_t* rowptr, const int32_t* col, int H,
+                               int F, const real* el, const real* er, const real* hc,
+                               real slope, real* u, real* lse) {
   const int D = H * F;
 #pragma omp parallel for schedule(dynamic, 256)
   for (int64_t i = 0; i < n_rows; ++i) {
     const int32_t a = rowptr[i], b = rowptr[i + 1];
-    float* ui = u + i * D;
-    for (int k = 0; k < D; ++k) ui[k] = 0.f;
+    real* ui = u + i * D;
+    for (int k = 0; k < D; ++k) ui[k] = (real)0;
     for (int h = 0; h < H; ++h) {
-      float m = -INFINITY;
+      real m = -(real)INFINITY;
       for (int32_t e = a; e < b; ++e) {
-        const float s = lrelu(el[i * H + h] + er[(int64_t)col[e] * H + h], slope);
+        const real s = lrelu(el[i * H + h] + er[(int64_t)col[e] * H + h], slope);
         if (s > m) m = s;
       }
-      float l = 0.f;
+      real l = (real)0;
       for (int32_t e = a; e < b; ++e) {
-        const float s = lrelu(el[i * H + h] + er[(int64_t)col[e] * H + h], slope);
-        const float p = expf(s - m);
+        const real s = lrelu(el[i * H + h] + er[(int64_t)col[e] * H + h], slope);
+        const real p = exp(s - m);
         l += p;
-        const float* hj = hc + (int64_t)col[e] * D + h * F;
+        const real* hj = hc + (int64_t)col[e] * D + h * F;
         for (int f = 0; f < F; ++f) ui[h * F + f] += p * hj[f];
       }
-      const float inv = l > 0.f ? 1.f / l : 0.f;
+      const real inv = l > (real)0 ? (real)1 / l : (real)0;
       for (int f = 0; f < F; ++f) ui[h * F + f] *= inv;
-      lse[i * H + h] = l > 0.f ? m + logf(l) : -INFINITY;
+      lse[i * H + h] = l > (real)0 ? m + log(l) : -(real)INFINITY;
     }
   }
 }
 
 /* row half of the backward: d_el, per-edge de and att (for the column half) */
-void oracle_edge_attention_bwd_rows(int64_t n_rows, const int32_t* rowptr, const int32_t* col,
-                                    int H, int F, const float* el, const float* er,
-                                    const float* hc, const float* lse, const float* u,
-                                    const float* dU, float slope, float* d_el, float* de,
-                                    float* att_out) {
+void SFX(oracle_edge_attention_bwd_rows)(int64_t n_rows, const int32_t* rowptr, const int32_t* col,
+                                    int H, int F, const real* el, const real* er,
+                                    const real* hc, const real* lse, const real* u,
+                                    const real* dU, real slope, real* d_el, real* de,
+                                    real* att_out) {
   const int D = H * F;
 #pragma omp parallel for schedule(dynamic, 256)
   for (int64_t i = 0; i < n_rows; ++i) {
     const int32_t a = rowptr[i], b = rowptr[i + 1];
     for (int h = 0; h < H; ++h) {
-      const float* dui = dU + i * D + h * F;
-      float Dh = 0.f;
+      const real* dui = dU + i * D + h * F;
+      real Dh = (real)0;
       for (int f = 0; f < F; ++f) Dh += dui[f] * u[i * D + h * F + f];
-      float acc = 0.f;
+      real acc = (real)0;
       for (int32_t e = a; e < b; ++e) {
-        const float pre = el[i * H + h] + er[(int64_t)col[e] * H + h];
-        const float att = expf(lrelu(pre, slope) - lse[i * H + h]);
-        const float* hj = hc + (int64_t)col[e] * D + h * F;
-        float g = 0.f;
+        const real pre = el[i * H + h] + er[(int64_t)col[e] * H + h];
+        const real att = exp(lrelu(pre, slope) - lse[i * H + h]);
+        const real* hj = hc + (int64_t)col[e] * D + h * F;
+        real g = (real)0;
         for (int f = 0; f < F; ++f) g += dui[f] * hj[f];
-        const float d = att * (g - Dh) * (pre > 0.f ? 1.f : slope);
+        const real d = att * (g - Dh) * (pre > (real)0 ? (real)1 : slope);
         de[(int64_t)e * H + h] = d;
         att_out[(int64_t)e * H + h] = att;
         acc += d;
@@ -78,20 +91,20 @@ void oracle_edge_attention_bwd_rows(int64_t n_rows, const int32_t* rowptr, const
 }
 
 /* column half: out[j] = sum_e w[e] table[row(e)], out_x[j] = sum_e x[e] */
-void oracle_csc_aggregate(int64_t n_cols, const int32_t* colptr, const int32_t* csc_row,
-                          const int32_t* csc_eid, int H, int F, const float* w, const float* x,
-                          const float* table, float* out, float* out_x) {
+void SFX(oracle_csc_aggregate)(int64_t n_cols, const int32_t* colptr, const int32_t* csc_row,
+                          const int32_t* csc_eid, int H, int F, const real* w, const real* x,
+                          const real* table, real* out, real* out_x) {
   const int D = H * F;
 #pragma omp parallel for schedule(dynamic, 64)
   for (int64_t j = 0; j < n_cols; ++j) {
-    float* oj = out + j * D;
-    for (int k = 0; k < D; ++k) oj[k] = 0.f;
+    real* oj = out + j * D;
+    for (int k = 0; k < D; ++k) oj[k] = (real)0;
     for (int h = 0; h < H; ++h) {
-      float xs = 0.f;
+      real xs = (real)0;
       for (int32_t s = colptr[j]; s < colptr[j + 1]; ++s) {
         const int64_t e = csc_eid[s];
-        const float* ti = table + (int64_t)csc_row[s] * D + h * F;
-        const float ww = w[e * H + h];
+        const real* ti = table + (int64_t)csc_row[s] * D + h * F;
+        const real ww = w[e * H + h];
         for (int f = 0; f < F; ++f) oj[h * F + f] += ww * ti[f];
         if (x) xs += x[e * H + h];
       }
@@ -100,7 +113,7 @@ void oracle_csc_aggregate(int64_t n_cols, const int32_t* colptr, const int32_t* 
   }
 }
 
-int oracle_num_threads(void) {
+int SFX(oracle_num_threads)(void) {
 #ifdef _OPENMP
   extern int omp_get_max_threads(void);
   return omp_get_max_threads();

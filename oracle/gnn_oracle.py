@@ -324,7 +324,8 @@ def gat_fwd(feat, head_Ws, out_W, rowptr, col):
 # ----------------------------------------------------------------------------------
 def link_predict(x_i, x_j, mode, lins=(), keep=None, p=0.0):
     """``sigmoid(relu(x_i*x_j @ W0.T + b0))`` for 'mlp' (lins[:-1] only: LLP.py:107-111,
-    the last Linear is never applied) or ``sigmoid(sum(x_i*x_j))`` for 'inner'."""
+    the last Linear is never applied), ``sigmoid(sum(x_i*x_j))`` for 'inner', and
+    ``sigmoid(x_i*x_j)`` (B, F) for any other predictor string (LLP.py:104-115)."""
     x = x_i * x_j
     if mode == "mlp":
         for li, (W, b) in enumerate(lins[:-1]):
@@ -350,6 +351,10 @@ def link_predict_bwd(x_i, x_j, mode, lins, dout):
         s = 1.0 / (1.0 + np.exp(-x.sum(axis=-1)))
         dz = dout * s * (1 - s)
         dx = dz[:, None] * np.ones_like(x)
+        return dict(dx_i=dx * x_j, dx_j=dx * x_i)
+    if mode != "mlp":  # neither branch (LLP.py:106-113): y = sigmoid(x_i * x_j)
+        s = 1.0 / (1.0 + np.exp(-x))
+        dx = dout * s * (1 - s)
         return dict(dx_i=dx * x_j, dx_j=dx * x_i)
     W, b = lins[0]
     z = x @ W.T + b

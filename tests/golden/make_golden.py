@@ -25,11 +25,14 @@ Fixtures
                   degree 65 and 80 (> one wavefront), one hot column; normalize
                   with a zero column (NaN spread) and on random counts.
   ours_small.npz  Ours.OursLayer (full MSHA with city / province attention).
+  ours_record.npz Ours.OursLayer record=True: train.Coeff12new and Coeff3 / Coeff4.
   gcn_sub512.npz  model.GCN (nfeat 64, nhid 128; adj^T @ (X W) + scalar bias) on the
                   512-source subgraph: init, train output, nll loss, grads.
   years.npz       per-year node counts, group ids and GDP (2015-2018).
 
-``python tests/golden/make_golden.py gcn`` regenerates only gcn_sub512.npz.
+``python tests/golden/make_golden.py gcn`` regenerates only gcn_sub512.npz;
+``... round2`` regenerates sub512.npz (adds the fp64 softmax outputs), link.npz (adds
+the num_layers=1 and unknown-predictor cases) and ours_record.npz.
 """
 from __future__ import annotations
 
@@ -261,6 +264,7 @@ def make_sub512(g, mask):
     assert len(r32["softmax"]) == 3, len(r32["softmax"])
     for i, name in enumerate(["h0_att", "h1_att", "gal_att"]):
         out[f"sm32.{name}"] = np32(r32["softmax"][i])
+        out[f"sm64.{name}"] = np64(r64["softmax"][i])
     np.savez_compressed(os.path.join(OUT, "sub512.npz"), **out)
     return counts, gdp_sub, flows_sub
 
@@ -296,9 +300,13 @@ def make_link():
     xi = torch.randn(256, 32, generator=g)
     xj = torch.randn(256, 32, generator=g)
     res["x_i"], res["x_j"] = xi.numpy(), xj.numpy()
-    for mode in ("mlp", "inner"):
+    # 'mlp1': num_layers=1 still builds two Linears (LLP.py:93-96), so lins[:-1] is one
+    # layer as with num_layers=2; 'other': any predictor string besides 'mlp'/'inner'
+    # skips both branches and returns sigmoid(x_i * x_j), shape (B, F) (LLP.py:104-115)
+    for mode, pred, nl in (("mlp", "mlp", 2), ("inner", "inner", 2), ("mlp1", "mlp", 1),
+                           ("other", "dot", 2)):
         torch.manual_seed(4)
-        lp = LP(mode, 32, 32, 1, 2, 0.0)
+        lp = LP(pred, 32, 32, 1, nl, 0.0)
         for k, v in lp.state_dict().items():
             res[f"{mode}.init.{k}"] = v.numpy()
         a = xi.clone().requires_grad_(True)
@@ -443,6 +451,43 @@ def make_ours_small(g):
     np.savez_compressed(os.path.join(OUT, "ours_small.npz"), **res)
 
 
+def make_ours_record(g):
+    """Ours.OursLayer with record=True (Ours.py:92-96, eval mode as Record() runs it,
+    train.py:284-291): the layer sets ``train.Coeff12new`` to the (N, M) inter attention
+    and writes the batch rows of the (B, N) city / province attention into
+    Coeff3[source_index] / Coeff4[source_index]; the Coeff12 argument is never
+    written.  Same 64-source graph as ours_small.npz."""
+    import types
+
+    sink = types.SimpleNamespace()
+    O = extract(os.path.join(REF, "Ours.py"), {"OursLayer"}, dict(train=sink))["OursLayer"]
+    z = np.load(os.path.join(OUT, "ours_small.npz"))
+    counts = torch.as_tensor(z["counts"])
+    n, m = counts.shape
+    city, prov = z["city"], z["prov"]
+    city_adj = torch.as_tensor((city[:, None] == city[None, :]).astype(np.float32))
+    prov_adj = torch.as_tensor((prov[:, None] == prov[None, :]).astype(np.float32))
+    inter = refmodel.normalize_adjacency_matrix(counts)
+    city_n = refmodel.normalize_adjacency_matrix(city_adj)
+    prov_n = refmodel.normalize_adjacency_matrix(prov_adj)
+    torch.manual_seed(10)
+    layer = O(16, 8, 0.0)
+    layer.eval()
+    S = torch.as_tensor(z["S"])
+    R = torch.as_tensor(z["R"])
+    res = {}
+    C12 = torch.full((n, m), -1.0)
+    C3 = torch.full((n, n), -1.0)
+    C4 = torch.full((n, n), -1.0)
+    for k, si in enumerate((np.arange(0, 32), np.arange(32, 64))):  # Record(): batches
+        with torch.no_grad():
+            layer(S, R, inter, city_n, prov_n, torch.as_tensor(si), True, C12, C3, C4)
+        res[f"rec.coeff12new.{k}"] = np32(sink.Coeff12new)
+    res["rec.coeff3"], res["rec.coeff4"] = np32(C3), np32(C4)
+    assert bool((C12 == -1).all())  # the argument is never written
+    np.savez_compressed(os.path.join(OUT, "ours_record.npz"), **res)
+
+
 def make_gcn():
     """model.GCN (model.py:11-64) on the sub512 graph: GraphConvolution is
     adj^T @ (X @ W) + b with a SCALAR bias (model.py:23), the second layer runs on
@@ -494,6 +539,13 @@ def main():
     if sys.argv[1:] == ["gcn"]:
         make_gcn()
         return
+    if sys.argv[1:] == ["round2"]:  # link quirks, sub512 fp64 softmax, Ours record dump
+        g = load_2015()
+        mask = (g["counts"] > 0).numpy()
+        make_sub512(g, mask)
+        make_link()
+        make_ours_record(g)
+        return
     g = load_2015()
     mask = make_r15(g)
     counts, gdp_sub, flows_sub = make_sub512(g, mask)
@@ -501,6 +553,7 @@ def main():
     make_link()
     make_edge_cases()
     make_ours_small(g)
+    make_ours_record(g)
     make_gcn()
     make_years()
     for f in sorted(os.listdir(OUT)):

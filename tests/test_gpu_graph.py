@@ -99,3 +99,44 @@ def test_graphed_train_step_matches_eager(cuda, msha):
     np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=1e-6)
     for k, p in runs[False][1].items():
         torch.testing.assert_close(runs[True][1][k], p, rtol=1e-5, atol=1e-6, msg=k)
+
+
+def test_two_graphed_steps_keep_their_counters(cuda, msha):
+    """Two live GraphedSteps on one device: each replays fresh masks from its own
+    counter; closing the newer one reinstalls the older one's counter (the library keeps
+    one slot per device, msha_set_rng_counter), closing both leaves none.  A launch from
+    a side stream of the device reads that device's counter."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+    from msha_gnn_amd.step import GraphedStep
+
+    rng = np.random.default_rng(4)
+    c = random_counts(rng, 300, 32, 20)
+    graph = Graph.from_dense(t(c, cuda))
+    el, er = t(rng.standard_normal((300, 2)), cuda), t(rng.standard_normal((32, 2)), cuda)
+    hc = t(rng.standard_normal((32, 2, 64)), cuda)
+
+    def body():
+        return MF.edge_attention(graph, el, er, hc, p=0.5, training=True, seed=9)
+
+    assert MF.rng_counter(cuda) is None
+    a = GraphedStep(body, cuda, warmup=1)
+    b = GraphedStep(body, cuda, warmup=1)
+    assert MF.rng_counter(cuda) is b.counter
+    outs_a = [a.replay().clone() for _ in range(2)]
+    outs_b = [b.replay().clone() for _ in range(2)]
+    assert not torch.equal(outs_a[0], outs_a[1]) and not torch.equal(outs_b[0], outs_b[1])
+    b.close()
+    assert MF.rng_counter(cuda) is a.counter
+    # eager draws follow the reinstalled counter (a's), also from a side stream
+    side = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(side):
+        a.counter.fill_(2)
+        eager = body()
+    side.synchronize()
+    a.counter.fill_(1)
+    a.replay()  # the graph's first node makes it 2 again
+    assert torch.equal(a.out, eager)
+    a.close()
+    assert MF.rng_counter(cuda) is None
+    assert msha._lib.load().msha_get_rng_counter(cuda.index) is None

@@ -281,7 +281,7 @@ def test_edge_attention_weights_exported(cuda):
     attd = torch.empty(E, H, device=cuda)
     tel, ter, thc = t(el, cuda), t(er, cuda), t(hc, cuda)  # keep alive across the launch
     _lib.call("msha_edge_attention_fwd", graph.desc, H, F, 0, tel.data_ptr(), ter.data_ptr(),
-              thc.data_ptr(), 0.2, 0.0, 0, 0, u.data_ptr(), lse.data_ptr(), attd.data_ptr(),
+              thc.data_ptr(), 0.2, 0.0, 0, 0, u.data_ptr(), None, lse.data_ptr(), attd.data_ptr(),
               _lib.stream_handle())
     torch.cuda.synchronize()
     att, _, _ = O.edge_softmax_fwd(rowptr, col, el, er, rowflag=empty)
@@ -468,9 +468,12 @@ def test_link_predictor_matches_reference(cuda, msha):
     from msha_gnn_amd import layers
 
     z = golden("link.npz")
-    for mode in ("mlp", "inner"):
+    # mlp1: num_layers=1 (still two Linears, one applied); other: an unknown predictor
+    # string -> sigmoid(x_i * x_j), (B, F) (LLP.py:104-115)
+    for mode, pred, nl in (("mlp", "mlp", 2), ("inner", "inner", 2), ("mlp1", "mlp", 1),
+                           ("other", "dot", 2)):
         torch.manual_seed(4)
-        lp = layers.LinkPredictor(mode, 32, 32, 1, 2, 0.0)
+        lp = layers.LinkPredictor(pred, 32, 32, 1, nl, 0.0)
         for k, v in lp.state_dict().items():  # same init as the reference (bitwise)
             assert np.array_equal(v.numpy(), z[f"{mode}.init.{k}"]), k
         lp = lp.to(cuda).train()
@@ -481,11 +484,15 @@ def test_link_predictor_matches_reference(cuda, msha):
         y.backward(t(z[f"{mode}.dout"], cuda))
         tol_close(xi.grad.cpu().numpy(), z[f"{mode}.grad.x_i"], 1e-4, 1e-5)
         tol_close(xj.grad.cpu().numpy(), z[f"{mode}.grad.x_j"], 1e-4, 1e-5)
-        if mode == "mlp":
-            tol_close(lp.lins[0].weight.grad.cpu().numpy(), z["mlp.grad.lins.0.weight"], 1e-4,
+        assert y.shape == z[f"{mode}.out"].shape
+        if pred == "mlp":
+            tol_close(lp.lins[0].weight.grad.cpu().numpy(), z[f"{mode}.grad.lins.0.weight"],
+                      1e-4, 1e-5)
+            tol_close(lp.lins[0].bias.grad.cpu().numpy(), z[f"{mode}.grad.lins.0.bias"], 1e-4,
                       1e-5)
-            tol_close(lp.lins[0].bias.grad.cpu().numpy(), z["mlp.grad.lins.0.bias"], 1e-4, 1e-5)
             assert lp.lins[1].weight.grad is None
+        if mode == "other":
+            assert all(p.grad is None for p in lp.parameters())
 
 
 def test_link_predictor_deep_and_dropout(cuda, msha):

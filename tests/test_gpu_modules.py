@@ -34,13 +34,14 @@ def test_ablation3_train_step_matches_reference(cuda, msha):
     ri = torch.as_tensor(z["recipient_index"], device=cuda)
     model.train()
     out = model(adj, None, None, si)
-    tol_close(out.detach().cpu().numpy(), z["out32"], 1e-4, 2e-5)
-    tol_close(out.detach().cpu().numpy(), z["out64"], 1e-4, 2e-5)
+    # north_star fp32 bar (1e-5) against the reference's fp64 run; the reference's own
+    # fp32 run is itself ~1e-6 from it (tests/golden: out32 vs out64)
+    tol_close(out.detach().cpu().numpy(), z["out64"], 1e-5, 1e-5)
     loss = F.nll_loss(out[si], ri)
-    assert abs(loss.item() - float(z["loss64"])) < 1e-4 * max(1.0, abs(float(z["loss64"])))
+    assert abs(loss.item() - float(z["loss64"])) < 1e-5 * max(1.0, abs(float(z["loss64"])))
     loss.backward()
     for k, p in model.named_parameters():
-        key = f"grad32.{k}"
+        key = f"grad64.{k}" if f"grad64.{k}" in z.files else f"grad32.{k}"
         if key not in z.files:
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
             continue
@@ -48,7 +49,7 @@ def test_ablation3_train_step_matches_reference(cuda, msha):
         if k.endswith(".a") and "out_att" in k:
             assert float(p.grad.abs().max()) == 0.0 and np.abs(ref).max() < 1e-5
             continue
-        tol_close(p.grad.cpu().numpy(), ref, 2e-3, 2e-4)
+        tol_close(p.grad.cpu().numpy(), ref, 1e-5, 1e-5)
     # BN running statistics advanced exactly as the reference's one train step
     sd = model.state_dict()
     for k in z.files:
@@ -67,7 +68,7 @@ def test_ablation3_eval_matches_reference(cuda, msha):
     model.eval()
     with torch.no_grad():
         out = model(adj, None, None, torch.as_tensor(z["source_index"], device=cuda))
-    tol_close(out.cpu().numpy(), z["out_eval64"], 1e-4, 2e-5)
+    tol_close(out.cpu().numpy(), z["out_eval64"], 1e-5, 1e-5)
 
 
 def test_gat_matches_reference(cuda, msha):
@@ -197,3 +198,42 @@ def test_gcn_matches_reference(cuda, msha):
             tol_close(p.grad.cpu().numpy(), z[key], 1e-3, 1e-4)
         else:
             assert p.grad is None, k
+
+
+def test_ablation3_intermediates_vs_reference_fp64(cuda, msha):
+    """Per head on sub512 (in 128, F 64): the masked-softmax attention (Ablation.py:268-270),
+    u = att @ h1 and v = att.T @ h2 (the BatchNorm inputs, :273-274) against the
+    reference's own fp64 run, 1e-5 -- the kernels' intermediates, not only the model
+    output."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import graph_for
+
+    z = golden("sub512.npz")
+    adj = torch.as_tensor(z["adj_norm"], device=cuda)
+    g = graph_for(adj)
+    S = torch.as_tensor(z["init.Sfeatures"], device=cuda)
+    R = torch.as_tensor(z["init.Rfeatures"], device=cuda)
+    rows = np.repeat(np.arange(512), np.diff(g.rowptr.cpu().numpy()))
+    cols = g.col.cpu().numpy()
+    for h in range(2):
+        W1 = torch.as_tensor(z[f"init.attention_{h}.W1"], device=cuda)
+        W2 = torch.as_tensor(z[f"init.attention_{h}.W2"], device=cuda)
+        a = torch.as_tensor(z[f"init.attention_{h}.a"], device=cuda).view(2, 64)
+        h1, er = MF.project_scores(R, W1, ar=a[0:1], heads=1)
+        h2, el = MF.project_scores(S, W2, al=a[1:2], heads=1)
+        u, v = MF.edge_attention(g, el, er, h1.view(32, 1, 64), hs=h2.view(512, 1, 64))
+        tol_close(u[:, 0].cpu().numpy(), z[f"bn64.h{h}_u_pre"], 1e-5, 1e-5)
+        tol_close(v[:, 0].cpu().numpy(), z[f"bn64.h{h}_v_pre"], 1e-5, 1e-5)
+        # the attention itself: the forward's per-edge attention output (attd)
+        u2 = torch.empty(512, 1, 64, device=cuda)
+        lse = torch.empty(512, 1, device=cuda)
+        attd = torch.empty(g.n_edges, 1, device=cuda)
+        _lib.call("msha_edge_attention_fwd", g.desc, 1, 64, 0, el.data_ptr(), er.data_ptr(),
+                  h1.data_ptr(), 0.2, 0.0, 0, 0, u2.data_ptr(), None, lse.data_ptr(), attd.data_ptr(),
+                  _lib.stream_handle(cuda))
+        dense = np.zeros((512, 32))
+        dense[rows, cols] = attd[:, 0].cpu().numpy()
+        ref = z[f"sm64.h{h}_att"]
+        tol_close(dense, ref, 1e-5, 1e-5)
+        assert np.all(ref[dense == 0] < 1e-12)  # masked entries: exp(-9e15 - max) = 0

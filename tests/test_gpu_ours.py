@@ -44,17 +44,17 @@ def test_ours_layer_matches_reference(cuda, msha, tag):
     layer.eval()
     with torch.no_grad():
         y = layer(S, R, inter, city, prov, src, False)
-    tol_close(y.cpu().numpy(), z[tag + "out_eval"], 1e-4, 1e-5)
+    tol_close(y.cpu().numpy(), z[tag + "out_eval"], 1e-5, 1e-5)
     layer.train()
     y = layer(S, R, inter, city, prov, src, False)
-    tol_close(y.detach().cpu().numpy(), z[tag + "out"], 1e-4, 1e-5)
+    tol_close(y.detach().cpu().numpy(), z[tag + "out"], 1e-5, 1e-5)
     y.backward(t(z[tag + "dout"], cuda))
-    tol_close(S.grad.cpu().numpy(), z[tag + "grad.S"], 1e-3, 1e-4)
-    tol_close(R.grad.cpu().numpy(), z[tag + "grad.R"], 1e-3, 1e-4)
+    tol_close(S.grad.cpu().numpy(), z[tag + "grad.S"], 1e-5, 1e-5)
+    tol_close(R.grad.cpu().numpy(), z[tag + "grad.R"], 1e-5, 1e-5)
     for k, p in layer.named_parameters():
         key = f"{tag}grad.{k}"
         if key in z.files:
-            tol_close(p.grad.cpu().numpy(), z[key], 1e-3, 1e-4)
+            tol_close(p.grad.cpu().numpy(), z[key], 1e-5, 1e-5)
         else:
             assert p.grad is None, k
 
@@ -180,8 +180,42 @@ def test_ours_model_record_and_train_step(cuda, msha):
     C4 = torch.zeros(n, n, device=cuda)
     with torch.no_grad():
         model(inter, city, prov, src, True, C12, C3, C4)
-    assert torch.allclose(C12.sum(1), torch.ones(n, device=cuda), atol=1e-5)
+    assert bool((C12 == 0).all())  # as Ours.py:92-96: the argument is never written
+    c12new = layers.record_state.Coeff12new
+    assert torch.allclose(c12new.sum(1), torch.ones(n, device=cuda), atol=1e-5)
     same = torch.as_tensor(z["city"][z["source_index"]][:, None] == z["city"][None, :],
                            device=cuda)
     r3 = C3[src]
     assert bool((r3[~same] == 0).all()) and bool((r3[same] > 0).all())
+
+
+def test_ours_record_dump_matches_reference(cuda, msha):
+    """Record() (train.py:284-291: eval, batches of sources) through OursLayer with
+    record=True vs the reference's own dump (ours_record.npz from Ours.OursLayer):
+    train.Coeff12new after each batch, Coeff3 / Coeff4 after both, Coeff12 untouched."""
+    import sys
+    import types
+
+    from msha_gnn_amd import layers
+
+    z, layer, inter, city, prov, S, R, _ = _layer_case(msha, cuda, "")
+    r = golden("ours_record.npz")
+    n, m = z["counts"].shape
+    layer.eval()
+    C12 = torch.full((n, m), -1.0, device=cuda)
+    C3 = torch.full((n, n), -1.0, device=cuda)
+    C4 = torch.full((n, n), -1.0, device=cuda)
+    sink = types.ModuleType("train")  # the module Ours.py:5 imports as `train`
+    sys.modules["train"] = sink
+    try:
+        for k, si in enumerate((np.arange(0, 32), np.arange(32, 64))):
+            with torch.no_grad():
+                layer(S, R, inter, city, prov, torch.as_tensor(si, device=cuda), True, C12, C3,
+                      C4)
+            tol_close(sink.Coeff12new.cpu().numpy(), r[f"rec.coeff12new.{k}"], 1e-5, 1e-6)
+            assert sink.Coeff12new is layers.record_state.Coeff12new
+    finally:
+        del sys.modules["train"]
+    assert bool((C12 == -1).all())
+    tol_close(C3.cpu().numpy(), r["rec.coeff3"], 1e-5, 1e-6)
+    tol_close(C4.cpu().numpy(), r["rec.coeff4"], 1e-5, 1e-6)

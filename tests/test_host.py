@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(msha):
     from msha_gnn_amd import _lib
 
     lib = _lib.load()  # loads without touching the GPU
-    assert lib.msha_abi_version() == 3
+    assert lib.msha_abi_version() == 4
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (msha_\w+)", out))
@@ -43,7 +43,7 @@ def test_abi_argument_errors_are_reported(msha):
 
     with pytest.raises(RuntimeError, match="graph descriptor is NULL"):
         _lib.call("msha_edge_attention_fwd", None, 8, 16, 0, None, None, None, 0.2, 0.0, 0, 0,
-                  None, None, None, None)
+                  None, None, None, None, None)
     with pytest.raises(RuntimeError, match="p must be in"):
         _lib.call("msha_dropout_keep_mask", 0, 0, 10, 1.5, 1, None)
 

@@ -149,18 +149,19 @@ def test_edge_cases_layer(tag):
 def test_link_predictor():
     z = golden("link.npz")
     xi, xj = z["x_i"], z["x_j"]
-    for mode in ("mlp", "inner"):
+    for mode, pred in (("mlp", "mlp"), ("inner", "inner"), ("mlp1", "mlp"), ("other", "dot")):
         lins = [(z[f"{mode}.init.lins.0.weight"], z[f"{mode}.init.lins.0.bias"]),
                 (z[f"{mode}.init.lins.1.weight"], z[f"{mode}.init.lins.1.bias"])]
-        y = O.link_predict(xi, xj, mode, lins)
+        y = O.link_predict(xi, xj, pred, lins)
+        assert y.shape == z[f"{mode}.out"].shape
         np.testing.assert_allclose(y, z[f"{mode}.out"], rtol=1e-6, atol=1e-6)
-        g = O.link_predict_bwd(xi, xj, mode, lins, z[f"{mode}.dout"])
+        g = O.link_predict_bwd(xi, xj, pred, lins, z[f"{mode}.dout"])
         np.testing.assert_allclose(g["dx_i"], z[f"{mode}.grad.x_i"], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(g["dx_j"], z[f"{mode}.grad.x_j"], rtol=1e-5, atol=1e-6)
-        if mode == "mlp":
-            np.testing.assert_allclose(g["dW"], z["mlp.grad.lins.0.weight"], rtol=1e-5,
+        if pred == "mlp":
+            np.testing.assert_allclose(g["dW"], z[f"{mode}.grad.lins.0.weight"], rtol=1e-5,
                                        atol=1e-6)
-            np.testing.assert_allclose(g["db"], z["mlp.grad.lins.0.bias"], rtol=1e-5,
+            np.testing.assert_allclose(g["db"], z[f"{mode}.grad.lins.0.bias"], rtol=1e-5,
                                        atol=1e-6)
 
 
@@ -231,3 +232,80 @@ def test_gcn_oracle_matches_reference():
                     float(z["init.gc1.bias"]), z["init.gc2.weight"].astype(np.float64),
                     float(z["init.gc2.bias"]), rowptr, col, vals, adj.shape[1])
     np.testing.assert_allclose(out, z["out"], rtol=1e-4, atol=1e-5)
+
+
+def _torch_heads(z, prefix, n_heads):
+    return [{k: torch.as_tensor(v) for k, v in h.items()}
+            for h in _heads(z, prefix, n_heads, np.float64)]
+
+
+def test_dense_ref_matches_reference():
+    """tests/dense_ref.py (the fp64 torch restatement the full-size GPU tests use for
+    gradients) reproduces the reference's fp64 runs: ablation3 train forward, loss and
+    parameter gradients (sub512), OursLayer train/eval outputs and gradients (ours_small
+    case B)."""
+    import dense_ref as D
+
+    z = golden("sub512.npz")
+    mask = torch.as_tensor(z["adj_norm"] > 0)
+    heads = _torch_heads(z, "init.", 2)
+    for p in heads:
+        for k in ("W1", "W2", "a", "bn1_weight", "bn1_bias", "bn2_weight", "bn2_bias"):
+            p[k].requires_grad_(True)
+    Sf = torch.as_tensor(z["init.Sfeatures"], dtype=torch.float64).requires_grad_(True)
+    Rf = torch.as_tensor(z["init.Rfeatures"], dtype=torch.float64).requires_grad_(True)
+    oW = torch.as_tensor(z["init.out_att.W"], dtype=torch.float64).requires_grad_(True)
+    out = D.model(Sf, Rf, heads, oW, mask, True)
+    np.testing.assert_allclose(out.detach().numpy(), z["out64"], rtol=1e-10, atol=1e-10)
+    si = torch.as_tensor(z["source_index"])
+    loss = torch.nn.functional.nll_loss(out[si], torch.as_tensor(z["recipient_index"]))
+    assert abs(float(loss.detach()) - float(z["loss64"])) < 1e-12
+    loss.backward()
+    np.testing.assert_allclose(Rf.grad.numpy(), z["grad64.Rfeatures"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(oW.grad.numpy(), z["grad64.out_att.W"], rtol=1e-9, atol=1e-12)
+    for h, p in enumerate(heads):
+        for k in ("W1", "W2", "a", "bn1_weight", "bn1_bias", "bn2_weight", "bn2_bias"):
+            ref = z[f"grad64.attention_{h}.{k.replace('_', '.')}"]
+            np.testing.assert_allclose(p[k].grad.numpy(), ref, rtol=1e-8,
+                                       atol=1e-10 * np.abs(ref).max())
+
+    o = golden("ours_small.npz")
+    p = {k: torch.as_tensor(o[f"init.{k}"], dtype=torch.float64).requires_grad_(True)
+         for k in ("W1", "W2", "a", "a3", "a4")}
+    for bn in ("bn1", "bn2"):
+        for k in ("weight", "bias", "running_mean", "running_var"):
+            p[f"{bn}_{k}"] = torch.as_tensor(o[f"init.{bn}.{k}"], dtype=torch.float64)
+        p[f"{bn}_weight"].requires_grad_(True)
+        p[f"{bn}_bias"].requires_grad_(True)
+    mask = torch.as_tensor(o["B.counts"] > 0)
+    city, prov = torch.as_tensor(o["city"]), torch.as_tensor(o["prov"])
+    src = torch.as_tensor(o["B.source_index"])
+    S = torch.as_tensor(o["B.S"]).requires_grad_(True)
+    R = torch.as_tensor(o["B.R"]).requires_grad_(True)
+    y = D.ours_layer(S, R, p, mask, city, prov, src, False)
+    np.testing.assert_allclose(y.detach().numpy(), o["B.out_eval"], rtol=1e-10, atol=1e-10)
+    y = D.ours_layer(S, R, p, mask, city, prov, src, True)
+    np.testing.assert_allclose(y.detach().numpy(), o["B.out"], rtol=1e-10, atol=1e-10)
+    (y * torch.as_tensor(o["B.dout"])).sum().backward()
+    np.testing.assert_allclose(S.grad.numpy(), o["B.grad.S"], rtol=1e-8, atol=1e-12)
+    np.testing.assert_allclose(R.grad.numpy(), o["B.grad.R"], rtol=1e-8, atol=1e-12)
+    for k in ("W1", "W2", "a", "a3", "a4", "bn1_weight", "bn1_bias", "bn2_weight", "bn2_bias"):
+        ref = o[f"B.grad.{k.replace('_', '.')}"]
+        np.testing.assert_allclose(p[k].grad.numpy(), ref, rtol=1e-8,
+                                   atol=1e-10 * np.abs(ref).max())
+
+
+def test_record_fixture_semantics():
+    """ours_record.npz (Ours.py:92-96 record mode, eval): train.Coeff12new is the dense
+    post-softmax inter attention (rows sum to 1 over the edges); Coeff3 / Coeff4 rows of
+    the recorded batches are the same-group masks times E/SUM (one value per row)."""
+    r = golden("ours_record.npz")
+    o = golden("ours_small.npz")
+    mask = o["counts"] > 0
+    for k in (0, 1):
+        c12 = r[f"rec.coeff12new.{k}"]
+        np.testing.assert_allclose(c12.sum(1), 1.0, rtol=1e-5)
+        assert np.all(c12[~mask] == 0)
+    same = o["city"][:, None] == o["city"][None, :]
+    c3 = r["rec.coeff3"]
+    assert np.all(c3[~same] == 0) and np.all(c3[same] > 0)
