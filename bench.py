@@ -142,7 +142,8 @@ def fwd_bytes(n, m, e, H, F, s=4):
 class Layer:
     """The benchmarked GAT layer (one replica)."""
 
-    def __init__(self, dev, rowptr, col, n, m, fin, H, F, seed, dtype=torch.float32, graph=None):
+    def __init__(self, dev, rowptr, col, n, m, fin, H, F, seed, dtype=torch.float32, graph=None,
+                 dropout=0.0):
         import msha_loader
 
         msha_loader.load()
@@ -162,6 +163,9 @@ class Layer:
         self.al = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
         self.ar = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
         self.dU = torch.randn(n, H, F, generator=g).to(dev, dtype)
+        # attention dropout of the reference's training forward (Ablation.py:271): Philox
+        # masks drawn inside the forward and regenerated by the backward
+        self.p = dropout
 
     def step(self):
         for p in (self.W, self.al, self.ar):
@@ -174,17 +178,20 @@ class Layer:
             h1, er = self.MF.project_scores(self.Xr, self.W, ar=self.ar, heads=self.H)
             _, el = self.MF.project_scores(self.X, self.W, al=self.al, heads=self.H)
             hc = h1.view(self.m, self.H, self.F)
-        u = self.MF.edge_attention(self.graph, el, er, hc)
+        u = self.MF.edge_attention(self.graph, el, er, hc, p=self.p, training=self.p > 0)
         u.backward(self.dU)
 
 
-def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup=3,
-                     hidden=128, n_pairs=4_000_000, dtype=torch.float32):
+def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=16, warmup=3,
+                     hidden=128, n_pairs=4_000_000, dtype=torch.float32, amortise=8):
     """score P = 4M pairs (2M graph edges + 2M uniform negatives,
     seed 1) against h (n x F) with LinkPredictor 'mlp' (hidden 128) and 'inner'.
     Rank r owns rows [r R, (r+1) R) of h (sharding.ShardedTable); one RCCL
     all_gather_into_tensor per batch rebuilds the full table (inside the timed
-    loop), then each rank scores its contiguous P/W slice.  pairs/s over all ranks."""
+    loop), then each rank scores its contiguous P/W slice.  pairs/s over all ranks, with
+    the all-gather once per batch (``pairs_per_sec_*``) and once per ``amortise`` batches
+    (``pairs_per_sec_*_amortised``: the table is reused by k batches, as when one
+    embedding pass is scored against many negative samples)."""
     from msha_gnn_amd import functional as MF
     from msha_gnn_amd import sharding
 
@@ -210,27 +217,32 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
     fns = {"mlp": lambda h, s_, d_: MF.score_pairs(h, s_, d_, "mlp", W, b, out=out_mlp),
            "inner": lambda h, s_, d_: MF.score_pairs(h, s_, d_, "inner", out=out_inner)}
     res = {}
+    plo_, phi_ = sharding.pair_range(n_pairs, world, rank)
     for mode in ("mlp", "inner"):
-        def one():
-            sharding.score_sharded(table, t_src, t_dst, fns[mode])
-        for _ in range(warmup):
-            one()
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            one()
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
-        if dist:
-            tt = torch.tensor([dt], device=dev)
-            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-            dt = float(tt.item())
-        res[f"pairs_per_sec_{mode}"] = n_pairs * steps / dt
-        res[f"ms_per_batch_{mode}"] = dt / steps * 1e3
+        for every, tag in ((1, ""), (amortise, "_amortised")):
+            def one(k):
+                if k % every == 0:
+                    sharding.score_sharded(table, t_src, t_dst, fns[mode])
+                else:  # the gathered table of the last all-gather is reused
+                    fns[mode](table.full[:n], t_src[plo_:phi_], t_dst[plo_:phi_])
+            for k in range(warmup):
+                one(k)
+            if dist:
+                tdist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for k in range(steps):
+                one(k)
+            if dist:
+                tdist.barrier()
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            if dist:
+                tt = torch.tensor([dt], device=dev)
+                tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+                dt = float(tt.item())
+            res[f"pairs_per_sec_{mode}{tag}"] = n_pairs * steps / dt
+            res[f"ms_per_batch_{mode}{tag}"] = dt / steps * 1e3
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -238,6 +250,7 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=10, warmup
     torch.cuda.synchronize(dev)
     res["allgather_ms"] = (time.perf_counter() - t0) / steps * 1e3
     res.update(pairs_per_batch=n_pairs, feat=F, hidden=hidden, world=world,
+               amortised_over_batches=amortise,
                dtype="bf16" if dtype == torch.bfloat16 else "f32",
                mlp_scores_dtype="bf16" if dtype == torch.bfloat16 else "f32",
                sharding="h rows all-gathered over RCCL (all_gather_into_tensor), pairs split "
@@ -395,6 +408,133 @@ def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
                        f"{el_t:.1f}s: numpy X@W + oracle/edge_attention_cpu.c (OpenMP)")
 
 
+def host_cpu():
+    """lscpu-style host description: CPU model and the threads the CPU legs use."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"model": model, "cpus_visible": os.cpu_count(), "cpus_affinity": avail,
+            "torch_threads": torch.get_num_threads()}
+
+
+def cpu_baseline_r15(budget_s=10.0, dropout=0.5):
+    """configs[1] CPU baseline: the reference's train.py iteration on the shipped 2015
+    graph (ablation3, in 128, F 64, 2 heads, dropout 0.5, nll on 64 flows, Adam) in the
+    reference's own dense formulation (oracle/dense_step.py, pinned to the reference's
+    outputs and gradients by tests/test_oracle_golden.py), on this host's cores."""
+    from oracle import dense_step as D
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    n, m = int(z["n"]), int(z["m"])
+    adj = torch.zeros(n, m)
+    rows = torch.as_tensor(np.repeat(np.arange(n), np.diff(z["rowptr"])))
+    adj[rows, torch.as_tensor(z["col"]).long()] = torch.as_tensor(z["norm"])
+    p = D.init_params(n, m)
+    opt = torch.optim.Adam(D.leaves(p), lr=1e-3, weight_decay=5e-4)
+    g = torch.Generator().manual_seed(0)
+    src, dst = torch.randint(0, n, (64,), generator=g), torch.randint(0, m, (64,), generator=g)
+    D.train_step(p, opt, adj, src, dst, dropout)  # warm-up
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 20):
+        t0 = time.perf_counter()
+        D.train_step(p, opt, adj, src, dst, dropout)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return dict(value=med, unit="s/step", higher_is_better=False, cores=torch.get_num_threads(),
+                kind="port", edges_per_sec=len(z["col"]) / med,
+                sample=f"ablation3 train step on the full 2015 graph ({n} x {m}), median of "
+                       f"{len(times)} steps: oracle/dense_step.py (the reference's dense torch "
+                       "formulation, CPU)")
+
+
+def cpu_baseline_pairs(n, F, budget_s=4.0, hidden=128, n_pairs=1_000_000):
+    """C5 CPU baseline: LinkPredictor 'mlp' (hidden 128) and 'inner' with the caller's
+    gather (LLP.py:233, :104-115) on this host's cores, over a bounded 1M-pair sample of
+    the same batch shape (oracle/dense_step.score_pairs, pinned to the reference's
+    LinkPredictor outputs by tests/test_oracle_golden.py)."""
+    from oracle import dense_step as D
+
+    g = torch.Generator().manual_seed(1)
+    h = torch.rand(n, F, generator=g)
+    src = torch.randint(0, n, (n_pairs,), generator=g)
+    dst = torch.randint(0, n, (n_pairs,), generator=g)
+    W = torch.randn(hidden, F, generator=g) * F ** -0.5
+    b = torch.randn(hidden, generator=g)
+    res = {}
+    with torch.no_grad():
+        for mode in ("mlp", "inner"):
+            D.score_pairs(h, src, dst, mode, W, b)
+            reps, t0 = 0, time.perf_counter()
+            while reps < 1 or (time.perf_counter() - t0 < budget_s / 2 and reps < 20):
+                D.score_pairs(h, src, dst, mode, W, b)
+                reps += 1
+            res[f"pairs_per_sec_{mode}"] = n_pairs * reps / (time.perf_counter() - t0)
+    res.update(unit="pairs/s", cores=torch.get_num_threads(), kind="port",
+               sample=f"{n_pairs} pairs against a ({n}, {F}) fp32 table, hidden {hidden}: "
+                      "oracle/dense_step.score_pairs (torch CPU)")
+    return res
+
+
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` without a launcher: start N ranks through torch.distributed.run
+    on 127.0.0.1 (this process never initialises the GPU) and return their exit status."""
+    import socket
+    import subprocess
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    return subprocess.call(cmd + list(argv))
+
+
+def dry_run(world, rank):
+    """CPU rehearsal of the multi-rank path (gloo): rank launch, the sharded table's
+    all-gather, the contiguous pair split and the max-over-ranks timing.  Prints one JSON
+    line on rank 0 (n_gpus = ranks that took part)."""
+    import torch.distributed as tdist
+
+    from msha_loader import load
+
+    load()
+    from msha_gnn_amd import sharding
+
+    if world > 1:
+        tdist.init_process_group("gloo")
+    n, F, P = 1001, 8, 5003
+    tab = sharding.ShardedTable(n, F, world, rank, "cpu")
+    lo, hi = sharding.row_range(n, world, rank)
+    full_ref = torch.arange(n * F, dtype=torch.float32).view(n, F)
+    tab.set_local(full_ref[lo:hi])
+    t0 = time.perf_counter()
+    ok = bool(torch.equal(tab.gather(), full_ref))
+    plo, phi = sharding.pair_range(P, world, rank)
+    dt = time.perf_counter() - t0
+    cnt = torch.tensor([phi - plo, int(ok), 1], dtype=torch.float64)
+    tt = torch.tensor([dt])
+    if world > 1:
+        tdist.all_reduce(cnt)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_reporting": int(cnt[2]),
+                          "pairs_covered": int(cnt[0]), "pairs": P,
+                          "table_ok_ranks": int(cnt[1]), "max_rank_s": float(tt)}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -408,12 +548,26 @@ def main():
     ap.add_argument("--no-bf16", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="report the eager launches (no HIP-graph replay of the timed steps)")
+    ap.add_argument("--no-dropout-leg", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: rehearse the rank launch and the sharded table exchange over "
+                         "gloo on the CPU (tests)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # one process per GPU: launch the ranks (before anything touches the GPU) and exit
+        # with their status
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if args.dry_run:
+        return dry_run(world, rank)
     if dist:
         import torch.distributed as tdist
 
@@ -522,6 +676,28 @@ def main():
               "the eager pass); roofline: HIP events around every launch over the eager timed "
               "region of the same steps" if dt_graph is not None else
               "value and roofline: eager launches, HIP events around every launch")
+    drop_leg = None
+    if not args.no_dropout_leg:
+        # the reference's training forward drops attention at p = 0.5 (Ablation.py:271):
+        # the same step with the Philox mask drawn in the forward and regenerated in the
+        # backward (no mask tensor)
+        layd = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank, graph=layer.graph,
+                     dropout=0.5)
+        dtde, kd, nd = timed(layd, args.steps, args.warmup)
+        dtdg = None if args.eager else timed_graph(layd, args.steps)
+        dtd = dtdg if dtdg is not None else dtde
+        ad = fwd_bytes(n, m, e, H, F) / (kd * 1e-3) / 1e9
+        drop_leg = {"workload": f"gat_layer_{args.workload}, attention dropout p = 0.5 "
+                                "(training forward + backward)",
+                    "value": world * e * args.steps / dtd, "unit": "edges/s",
+                    "ms_per_step": dtd / args.steps * 1e3,
+                    "ms_per_step_eager": dtde / args.steps * 1e3, "dtype": "f32",
+                    "roofline": {"kernel": "msha_edge_attention_fwd (p = 0.5)", "bound": "hbm",
+                                 "achieved": ad, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": ad / HBM_PEAK_GBS, "avg_launch_us": kd * 1e3,
+                                 "launches_timed": nd},
+                    "edge_kernels": edge_kernels(layd, 4)}
+        del layd
     bf16_leg = None
     if not args.no_bf16:
         # config C3: the same layer with bf16 tables / projection (bf16 MFMA)
@@ -577,6 +753,8 @@ def main():
                      "launches_timed": n_launch},
     }
     out["edge_kernels"] = edge_kernels(layer, 4)
+    if drop_leg is not None:
+        out["dropout_p05"] = drop_leg
     if bf16_leg is not None:
         out["bf16"] = bf16_leg
     if link is not None:
@@ -585,8 +763,9 @@ def main():
         out["train_step_configs1"] = {
             "workload": "train.py iteration: full-graph fwd + nll(64 flows) + bwd + Adam; "
                         "in 128, F 64, 2 heads, dropout 0.5, fp32",
-            "reference_cpu_s_per_step": "ablation3 @2015: 1.01-1.27 (BASELINE.md, 8-core "
-                                        "container CPU; not this box)",
+            "reference_cpu_s_per_step": "ablation3 @2015: see cpu_baseline.configs1_ablation3 "
+                                        "(this host, same run); 1.01-1.27 on the 8-core build "
+                                        "container (BASELINE.md)",
             "runs": [train_step_leg(dev, y, "Ours") for y in ("2015", "2016", "2017", "2018")]
             + [train_step_leg(dev, "2015", "ablation3")]}
         if not args.no_bf16:
@@ -597,7 +776,13 @@ def main():
                 "runs": [train_step_leg(dev, y, "Ours", dtype=torch.bfloat16)
                          for y in ("2015", "2016", "2017", "2018")]}
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
+        cb = cpu_baseline(rowptr, col, n, fin, H, F, args.cpu_budget)
+        cb["host"] = host_cpu()
+        if not args.no_r15:
+            cb["configs1_ablation3"] = cpu_baseline_r15(args.cpu_budget)
+        if link is not None:
+            cb["link_score"] = cpu_baseline_pairs(n, H * F)
+        out["cpu_baseline"] = cb
     print(json.dumps(out), flush=True)
     if dist:
         tdist.destroy_process_group()

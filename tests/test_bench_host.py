@@ -56,3 +56,31 @@ def test_pmc_traffic_reads_newest_profile():
     assert src32 is not None and src16 is not None
     assert 1.0e9 < t32 < 1.4e9
     assert 0.5e9 < t16 < 0.8e9
+
+
+def test_gpus_flag_launches_ranks():
+    """``bench.py --gpus 2`` without WORLD_SIZE starts two ranks itself (torch.distributed.run
+    on 127.0.0.1); --dry-run runs them over gloo on the CPU: both ranks report, the sharded
+    table all-gathers exactly and the pair split covers the batch."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_reporting"] == 2 and d["table_ok_ranks"] == 2
+    assert d["pairs_covered"] == d["pairs"]
+
+
+def test_gpus_flag_mismatch_fails():
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0

@@ -309,3 +309,70 @@ def test_record_fixture_semantics():
     same = o["city"][:, None] == o["city"][None, :]
     c3 = r["rec.coeff3"]
     assert np.all(c3[~same] == 0) and np.all(c3[same] > 0)
+
+
+def _dense_params(z):
+    """oracle/dense_step parameters from the sub512 fixture's initial state."""
+    t = lambda k: torch.tensor(z[k]).double().requires_grad_(True)  # noqa: E731
+    heads = []
+    for h in range(2):
+        d = {k: t(f"init.attention_{h}.{k}") for k in ("W1", "W2", "a")}
+        for bn in ("bn1", "bn2"):
+            for k in ("weight", "bias"):
+                d[f"{bn}_{k}"] = t(f"init.attention_{h}.{bn}.{k}")
+            for k in ("running_mean", "running_var"):
+                d[f"{bn}_{k}"] = torch.tensor(z[f"init.attention_{h}.{bn}.{k}"]).double()
+        heads.append(d)
+    return {"Sfeatures": t("init.Sfeatures"), "Rfeatures": t("init.Rfeatures"), "heads": heads,
+            "out_W": t("init.out_att.W"), "out_a": t("init.out_att.a")}
+
+
+def test_dense_step_matches_reference_train_step():
+    """oracle/dense_step (the CPU baseline of configs[1]) restates the reference's
+    ablation3 step: fp64 output, loss, every gradient and the BN running statistics
+    after one train forward vs the reference's own fp64 run (dropout 0)."""
+    from oracle import dense_step
+
+    z = golden("sub512.npz")
+    p = _dense_params(z)
+    adj = torch.tensor(z["adj_norm"]).double()
+    si, ri = torch.tensor(z["source_index"]), torch.tensor(z["recipient_index"])
+    out = dense_step.ablation3(p, adj, 0.0, True)
+    np.testing.assert_allclose(out.detach().numpy(), z["out64"], rtol=1e-9, atol=1e-9)
+    loss = torch.nn.functional.nll_loss(out[si], ri)
+    assert abs(float(loss.detach()) - float(z["loss64"])) < 1e-9
+    loss.backward()
+    names = {"Sfeatures": p["Sfeatures"], "Rfeatures": p["Rfeatures"], "out_att.W": p["out_W"]}
+    for h, d in enumerate(p["heads"]):
+        for k in ("W1", "W2", "a"):
+            names[f"attention_{h}.{k}"] = d[k]
+        for bn in ("bn1", "bn2"):
+            names[f"attention_{h}.{bn}.weight"] = d[f"{bn}_weight"]
+            names[f"attention_{h}.{bn}.bias"] = d[f"{bn}_bias"]
+    for k, v in names.items():
+        # the fixture holds the (512, 128) Sfeatures gradient only from the fp32 run
+        tol = 1e-7 if f"grad64.{k}" in z.files else 1e-5
+        ref = z[f"grad64.{k}"] if f"grad64.{k}" in z.files else z[f"grad32.{k}"]
+        np.testing.assert_allclose(v.grad.numpy(), ref, rtol=tol,
+                                   atol=tol * max(1e-2, np.abs(ref).max()), err_msg=k)
+    for h, d in enumerate(p["heads"]):
+        for bn in ("bn1", "bn2"):
+            for k in ("running_mean", "running_var"):
+                np.testing.assert_allclose(d[f"{bn}_{k}"].numpy(),
+                                           z[f"after64.attention_{h}.{bn}.{k}"], rtol=1e-9,
+                                           atol=1e-12)
+
+
+def test_dense_step_score_pairs_matches_reference():
+    """oracle/dense_step.score_pairs vs the reference LinkPredictor fixture (eval)."""
+    from oracle import dense_step
+
+    z = golden("link.npz")
+    h = torch.cat([torch.tensor(z["x_i"]), torch.tensor(z["x_j"])])
+    src = torch.arange(256)
+    dst = src + 256
+    for mode, pred in (("mlp", "mlp"), ("inner", "inner"), ("other", "dot")):
+        W = torch.tensor(z[f"{mode}.init.lins.0.weight"])
+        b = torch.tensor(z[f"{mode}.init.lins.0.bias"])
+        got = dense_step.score_pairs(h, src, dst, pred, W, b).numpy()
+        np.testing.assert_allclose(got, z[f"{mode}.out"], rtol=1e-6, atol=1e-7, err_msg=mode)
