@@ -642,9 +642,19 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   const int zq = threadIdx.x >> 4, cq = threadIdx.x & 15;
   const int f4 = blockIdx.x * 16 + cq;  // float4 index in the 128 x 128 tile
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int b = zq; b < nb; b += 16) {
-    const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)b * (128 * 128))[f4];
-    s = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
+  // 8 slabs' loads in flight before they are added (same order: b ascending)
+  constexpr int RB = 8;
+  for (int b0 = zq; b0 < nb; b0 += 16 * RB) {
+    float4 v[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int b = b0 + 16 * j;
+      v[j] = b < nb ? reinterpret_cast<const float4*>(slab + (int64_t)b * (128 * 128))[f4]
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+      if (b0 + 16 * j < nb) s = make_float4(s.x + v[j].x, s.y + v[j].y, s.z + v[j].z, s.w + v[j].w);
   }
   part[threadIdx.x] = s;
   __syncthreads();
