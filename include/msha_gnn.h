@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 4
+#define MSHA_ABI_VERSION 5
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -430,6 +430,61 @@ MSHA_API int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, in
                                  float* G, float* bgrad, float* row_coef, float* da3s,
                                  float* da4s, void* d_hs, void* ws, size_t ws_bytes,
                                  msha_stream_t stream);
+
+
+/* ---- Model head (Ablation.py:273-277 + :298-301, Ours.py:100-109
+ * + :163-167): for every row i of the source side
+ *   u_out_h = lrelu(bn2_h(u[:, h]))       v_out_h = lrelu(bn1_h(v[:, h]))   (per head h)
+ *   x[i]    = dropout(cat_h elu(u_out_h[i] @ v_out_h^T), p_x)               (H*M values)
+ *   out[i]  = log_softmax(elu(elu(dropout(mask_i / deg_i, p_att) * (x[i] @ W))))
+ * i.e. the heads' BatchNorm + LeakyReLU epilogue, u_out @ v_out.T, elu, the heads'
+ * concatenation, the model's dropout, the GraphAttentionLayer out_att (its score is
+ * constant along a row: attention = mask / deg, 1/M on a virtual full row), the model's
+ * elu and log_softmax, in three launches (u statistics partials, statistics finalize +
+ * the whole v side, one row pass).  u (N, H, F) and v (M, H, F) are the attention
+ * aggregates (dtype storage, fp32 arithmetic), W the out_att weight (H*M, M) fp32,
+ * out (N, M) log-probabilities (dtype).  training: batch statistics, running statistics
+ * updated as nn.BatchNorm1d (momentum, unbiased variance; num_batches_tracked is the
+ * caller's); otherwise running statistics and no dropout.  Dropout: Philox keyed on
+ * (seed_x, element i*H*M + k) and (seed_att, element i*M + j), offset 0.
+ * stats (4, H*F) fp32 out: u mean, u invstd, v mean, v invstd (the backward's input).
+ *
+ * Backward (training statistics): given dout (N, M), writes du (N, H, F), dv (M, H, F),
+ * dW (H*M, M) fp32 and the per-head BatchNorm weight / bias gradients.  Rows whose dout
+ * is all zero (train.py's nll on out[source_index] touches 64 rows) contribute only
+ * through the BatchNorm batch terms and cost one row read.  Deterministic: per-wave
+ * partials over ascending row ranges, added in wave order.
+ * Limits: heads <= 8, heads*feat <= 512, n_cols <= 256, heads*n_cols <= 512,
+ * msha_head_supported() for the LDS budget (backward row pass <= 150 KB per wave). */
+#define MSHA_HEAD_MAX_HEADS 8
+typedef struct msha_head_params {
+  int32_t heads, feat;
+  float eps, momentum, slope;                     /* BatchNorm eps / momentum, lrelu slope */
+  const float* u_weight[MSHA_HEAD_MAX_HEADS];     /* bn2 of head h (u side), feat each */
+  const float* u_bias[MSHA_HEAD_MAX_HEADS];
+  float* u_running_mean[MSHA_HEAD_MAX_HEADS];
+  float* u_running_var[MSHA_HEAD_MAX_HEADS];
+  const float* v_weight[MSHA_HEAD_MAX_HEADS];     /* bn1 of head h (v side) */
+  const float* v_bias[MSHA_HEAD_MAX_HEADS];
+  float* v_running_mean[MSHA_HEAD_MAX_HEADS];
+  float* v_running_var[MSHA_HEAD_MAX_HEADS];
+  float* du_weight[MSHA_HEAD_MAX_HEADS];          /* backward outputs (nullable) */
+  float* du_bias[MSHA_HEAD_MAX_HEADS];
+  float* dv_weight[MSHA_HEAD_MAX_HEADS];
+  float* dv_bias[MSHA_HEAD_MAX_HEADS];
+} msha_head_params;
+MSHA_API int msha_head_supported(int64_t n_cols, int32_t heads, int32_t feat);
+MSHA_API size_t msha_head_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);
+MSHA_API int msha_head_fwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
+                           const void* u, const void* v, const float* W, int32_t training,
+                           float p_x, uint64_t seed_x, float p_att, uint64_t seed_att,
+                           float* stats, void* out, void* ws, size_t ws_bytes,
+                           msha_stream_t stream);
+MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
+                           const void* u, const void* v, const float* W, float p_x,
+                           uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
+                           const void* dout, void* du, void* dv, float* dW, void* ws,
+                           size_t ws_bytes, msha_stream_t stream);
 
 #ifdef __cplusplus
 }

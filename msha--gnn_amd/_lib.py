@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 4  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 5  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -50,6 +50,22 @@ class MshaGroups(C.Structure):
 
 
 GRP = C.POINTER(MshaGroups)
+
+HEAD_MAX_HEADS = 8
+
+
+class MshaHeadParams(C.Structure):
+    """Mirror of ``struct msha_head_params`` (include/msha_gnn.h)."""
+
+    _fields_ = [("heads", C.c_int32), ("feat", C.c_int32), ("eps", C.c_float),
+                ("momentum", C.c_float), ("slope", C.c_float)] + [
+        (name, C.c_void_p * HEAD_MAX_HEADS)
+        for name in ("u_weight", "u_bias", "u_running_mean", "u_running_var", "v_weight",
+                     "v_bias", "v_running_mean", "v_running_var", "du_weight", "du_bias",
+                     "dv_weight", "dv_bias")]
+
+
+HPP = C.POINTER(MshaHeadParams)
 
 # name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
 SIGNATURES = {
@@ -109,6 +125,11 @@ SIGNATURES = {
     "msha_ours_workspace_size": (SZ, [GRP, I64, I32, I32]),
     "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, I32, F32, F32,
                                       U64, U64, P, P, P, P, P, P, P, SZ, P]),
+    "msha_head_supported": (C.c_int, [I64, I32, I32]),
+    "msha_head_workspace_size": (SZ, [GP, I32, I32]),
+    "msha_head_fwd": (C.c_int, [GP, HPP, I32, P, P, P, I32, F32, U64, F32, U64, P, P, P, SZ, P]),
+    "msha_head_bwd": (C.c_int, [GP, HPP, I32, P, P, P, F32, U64, F32, U64, P, P, P, P, P, P, SZ,
+                                P]),
 }
 
 _lib = None

@@ -21,21 +21,6 @@ constexpr int kBnRows = 256;  // rows per partial block
 #endif
 constexpr int kBnThreads = 256;
 
-struct Wf {
-  float n, mean, m2;
-};
-
-__device__ __forceinline__ Wf wf_combine(Wf a, Wf b) {
-  if (b.n == 0.f) return a;
-  if (a.n == 0.f) return b;
-  const float n = a.n + b.n;
-  const float d = b.mean - a.mean;
-  Wf r;
-  r.n = n;
-  r.mean = a.mean + d * (b.n / n);
-  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
-  return r;
-}
 
 // threads: channel c = t % CT (CT = min(C, 256) channels per column tile, blockIdx.y
 // tiles), row group rg = t / CT strides the block's rows
@@ -351,6 +336,25 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwd a, const float2
 }
 
 static int64_t bn_blocks(int64_t rows) { return (rows + kBnRows - 1) / kBnRows; }
+
+// per-channel Welford partials of a (rows, C) table, one per kBnRows-row block (the
+// model head's u statistics, head.hip); returns the number of partial blocks
+int64_t bn_stats_partials(int64_t rows, int C, bool bf, const void* x, void* part,
+                          hipStream_t s) {
+  BnArgs a{};
+  a.rows = rows;
+  a.C = C;
+  const int64_t nb = bn_blocks(rows);
+  const dim3 g((unsigned)nb, (C + kBnThreads - 1) / kBnThreads);
+  if (bf)
+    hipLaunchKernelGGL(bn_partial_kernel<bf16_t>, g, dim3(kBnThreads), 0, s, a, (const bf16_t*)x,
+                       (Wf*)part);
+  else
+    hipLaunchKernelGGL(bn_partial_kernel<float>, g, dim3(kBnThreads), 0, s, a, (const float*)x,
+                       (Wf*)part);
+  return nb;
+}
+int64_t bn_stats_blocks(int64_t rows) { return bn_blocks(rows); }
 
 }  // namespace msha
 

@@ -318,6 +318,27 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
                  const float* a, const float* de2, const float* a2, hipStream_t s);
 
+// Welford triple (count, mean, M2) and Chan's combination (bn.hip, head.hip)
+struct Wf {
+  float n, mean, m2;
+};
+
+__host__ __device__ __forceinline__ Wf wf_combine(Wf a, Wf b) {
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float n = a.n + b.n;
+  const float d = b.mean - a.mean;
+  Wf r;
+  r.n = n;
+  r.mean = a.mean + d * (b.n / n);
+  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
+  return r;
+}
+
+// bn.hip: Welford partials per 256-row block of a (rows, C) table (Wf, block-major)
+int64_t bn_stats_partials(int64_t rows, int C, bool bf, const void* x, void* part, hipStream_t s);
+int64_t bn_stats_blocks(int64_t rows);
+
 inline int grid_for(int64_t work_items, int per_block, int cap = 1 << 20) {
   int64_t g = (work_items + per_block - 1) / per_block;
   if (g < 1) g = 1;

@@ -1,0 +1,946 @@
+// Model head: everything between the attention aggregates and the log-probabilities
+// (SURVEY.md §8f #3), in three forward and three backward launches.
+//
+// Reference (per head h, then the model):
+//   Ablation.py:273-277 / Ours.py:100-109   v_out = lrelu(bn1(v)), u_out = lrelu(bn2(u)),
+//                                           elu(u_out @ v_out.T)              (N, M)
+//   Ablation.py:298-301 / Ours.py:163-167   x = dropout(cat_h(...)); elu(out_att(x, adj));
+//                                           log_softmax(dim=1)
+//   GAT.py:20-35 (out_att)                  elu(dropout(softmax(mask * const)) * (x @ W))
+//                                           = elu(dropout(mask / deg) * (x @ W))
+// Every step after the BatchNorm statistics is local to a row, so one wave computes a
+// whole row of the output from u[i] (H*F values), the tiny v side (lrelu(bn1(v)), M x F
+// per head, in LDS transposed so lanes j read consecutive banks) and W (H*M x M, LDS).
+//
+// Forward launches: u statistics partials (bn.hip), finalize (u channels, one wave each;
+// the last block does the whole v side: 32 rows), the row pass.
+// Backward: train.py's loss reads 64 rows of the (N, M) output, so dout is zero on all
+// other rows; a zero row's only gradient path is BatchNorm's batch terms.
+//   rows pass    one wave per contiguous row range: a row whose dout is zero is skipped
+//                after one 128-B read; a nonzero row recomputes its forward and
+//                accumulates dW, d v_out and the BatchNorm sums (sum dz, sum dz * xhat)
+//                in the wave's LDS partials; writes dz of the row (the BN-input side)
+//   reduce       the flagged waves' partials added in wave order (deterministic)
+//   apply        du for every row (dz of nonzero rows, the batch terms for all), and in
+//                block 0 the v side's BatchNorm backward over its M rows
+#include "common.h"
+
+namespace msha {
+
+constexpr int kHeadThreads = 256;  // forward row pass: 4 waves per block
+constexpr int kHeadBwdWaves = 1024;
+constexpr int kHeadRowsPerWave = 64;
+constexpr int kHeadVStage = 4096;  // floats of v staged in LDS by the v-side blocks
+
+struct HeadArgs {
+  int64_t N;
+  int M, H, F, HF, KX;
+  float eps, momentum, slope;
+  const int32_t* rowptr;
+  const int32_t* col;
+  const float* uw[MSHA_HEAD_MAX_HEADS];
+  const float* ub[MSHA_HEAD_MAX_HEADS];
+  float* urm[MSHA_HEAD_MAX_HEADS];
+  float* urv[MSHA_HEAD_MAX_HEADS];
+  const float* vw[MSHA_HEAD_MAX_HEADS];
+  const float* vb[MSHA_HEAD_MAX_HEADS];
+  float* vrm[MSHA_HEAD_MAX_HEADS];
+  float* vrv[MSHA_HEAD_MAX_HEADS];
+  float* duw[MSHA_HEAD_MAX_HEADS];
+  float* dub[MSHA_HEAD_MAX_HEADS];
+  float* dvw[MSHA_HEAD_MAX_HEADS];
+  float* dvb[MSHA_HEAD_MAX_HEADS];
+  const float* W;  // (KX, M)
+  Dropout dx, dg;
+  float* stats;    // [u mean | u invstd | v mean | v invstd] (HF each) | vo_t (HF x M)
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// dst[e] = src[e] for e < n by the block's threads, 8 loads in flight per thread before
+// their LDS stores (a load -> store per iteration waits out one memory latency each)
+template <typename S>
+__device__ __forceinline__ void lds_copy(float* dst, const S* __restrict__ src, int n) {
+  constexpr int U = 8;
+  if constexpr (sizeof(S) == 4) {  // fp32: 16-byte pieces when aligned
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+      const int n4 = n / 4, nt = blockDim.x;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(dst);
+      int e0 = threadIdx.x;
+      for (; e0 + (U - 1) * nt < n4; e0 += U * nt) {
+        float4 v[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) v[q] = s4[e0 + q * nt];
+#pragma unroll
+        for (int q = 0; q < U; ++q) d4[e0 + q * nt] = v[q];
+      }
+      for (; e0 < n4; e0 += nt) d4[e0] = s4[e0];
+      for (int e = 4 * n4 + threadIdx.x; e < n; e += nt) dst[e] = src[e];
+      return;
+    }
+  }
+  const int nt = blockDim.x;
+  int e0 = threadIdx.x;
+  for (; e0 + (U - 1) * nt < n; e0 += U * nt) {
+    float v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) v[q] = to_f32(src[e0 + q * nt]);
+#pragma unroll
+    for (int q = 0; q < U; ++q) dst[e0 + q * nt] = v[q];
+  }
+  for (; e0 < n; e0 += nt) dst[e0] = to_f32(src[e0]);
+}
+
+template <typename T>
+__device__ __forceinline__ float4 ld4(const T* p) {
+  if constexpr (sizeof(T) == 4) {
+    return *reinterpret_cast<const float4*>(p);
+  } else {
+    const uint2 r = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                       __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u));
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, float4 v) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = v;
+  } else {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  }
+}
+
+__device__ __forceinline__ float elu1(float z) { return z > 0.f ? z : expm1f(z); }
+__device__ __forceinline__ float delu1(float z) { return z > 0.f ? 1.f : __expf(z); }
+
+__device__ __forceinline__ float pw(const float* const* p, int c, int F, float dflt) {
+  const float* q = p[c / F];
+  return q != nullptr ? q[c % F] : dflt;
+}
+
+// ---- finalize: u channels (one wave each) from the partials; the last block: v side
+template <typename T>
+__global__ void __launch_bounds__(256) head_prep_kernel(HeadArgs a, int training, int nbu,
+                                                        const Wf* __restrict__ part,
+                                                        const T* __restrict__ v) {
+  const int HF = a.HF, F = a.F, M = a.M;
+  float* st = a.stats;
+  if (blockIdx.x + 1 < gridDim.x) {
+    const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= HF) return;
+    if (!training) {
+      if (lane == 0) {
+        st[c] = pw(a.urm, c, F, 0.f);
+        st[HF + c] = rsqrtf(pw(a.urv, c, F, 1.f) + a.eps);
+      }
+      return;
+    }
+    Wf w{0.f, 0.f, 0.f};
+    for (int b = lane; b < nbu; b += 64) w = wf_combine(w, part[(int64_t)b * HF + c]);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+      w = wf_combine(w, Wf{__shfl_xor(w.n, o), __shfl_xor(w.mean, o), __shfl_xor(w.m2, o)});
+    if (lane == 0) {
+      const float var = w.n > 0.f ? w.m2 / w.n : 0.f;
+      st[c] = w.mean;
+      st[HF + c] = rsqrtf(var + a.eps);
+      float* rm = a.urm[c / F];
+      if (rm != nullptr) {
+        float* rv = a.urv[c / F];
+        const float unb = w.n > 1.f ? w.m2 / (w.n - 1.f) : var;
+        rm[c % F] = (1.f - a.momentum) * rm[c % F] + a.momentum * w.mean;
+        rv[c % F] = (1.f - a.momentum) * rv[c % F] + a.momentum * unb;
+      }
+    }
+    return;
+  }
+  // v side: M rows (<= 256) x HF channels, one thread per channel, rows in order; v
+  // staged in LDS first when it fits (coalesced loads, all in flight)
+  __shared__ float vs[kHeadVStage];
+  const bool staged = M * HF <= kHeadVStage;
+  if (staged) {
+    lds_copy(vs, v, M * HF);
+    __syncthreads();
+  }
+  auto vat = [&](int j, int c) { return staged ? vs[j * HF + c] : to_f32(v[(int64_t)j * HF + c]); };
+  for (int c = threadIdx.x; c < HF; c += blockDim.x) {
+    float mean, inv;
+    if (training) {
+      Wf w{0.f, 0.f, 0.f};
+      for (int j = 0; j < M; ++j) {
+        const float x = vat(j, c);
+        w.n += 1.f;
+        const float d = x - w.mean;
+        w.mean += d / w.n;
+        w.m2 += d * (x - w.mean);
+      }
+      const float var = w.n > 0.f ? w.m2 / w.n : 0.f;
+      mean = w.mean;
+      inv = rsqrtf(var + a.eps);
+      float* rm = a.vrm[c / F];
+      if (rm != nullptr) {
+        float* rv = a.vrv[c / F];
+        const float unb = w.n > 1.f ? w.m2 / (w.n - 1.f) : var;
+        rm[c % F] = (1.f - a.momentum) * rm[c % F] + a.momentum * w.mean;
+        rv[c % F] = (1.f - a.momentum) * rv[c % F] + a.momentum * unb;
+      }
+    } else {
+      mean = pw(a.vrm, c, F, 0.f);
+      inv = rsqrtf(pw(a.vrv, c, F, 1.f) + a.eps);
+    }
+    st[2 * HF + c] = mean;
+    st[3 * HF + c] = inv;
+    const float g = pw(a.vw, c, F, 1.f), b = pw(a.vb, c, F, 0.f);
+    float* vo = st + 4 * HF;
+    for (int j = 0; j < M; ++j) {
+      const float z = fmaf(g * inv, vat(j, c) - mean, b);
+      vo[(int64_t)c * M + j] = z > 0.f ? z : z * a.slope;  // vo_t[c][j]
+    }
+  }
+}
+
+// block-shared tables of the row passes
+struct HeadShared {
+  float* vo;  // HF x M
+  float* W;   // KX x M
+  float* g;   // u BN weight, bias, mean, invstd (HF each)
+  float* b;
+  float* mu;
+  float* su;
+};
+
+__device__ __forceinline__ HeadShared head_shared_load(const HeadArgs& a, float* smem) {
+  HeadShared s;
+  const int HF = a.HF, M = a.M;
+  s.vo = smem;
+  s.W = s.vo + HF * M;
+  s.g = s.W + a.KX * M;
+  s.b = s.g + HF;
+  s.mu = s.b + HF;
+  s.su = s.mu + HF;
+  lds_copy(s.vo, a.stats + 4 * HF, HF * M);
+  lds_copy(s.W, a.W, a.KX * M);
+  for (int c = threadIdx.x; c < HF; c += blockDim.x) {
+    s.g[c] = pw(a.uw, c, a.F, 1.f);
+    s.b[c] = pw(a.ub, c, a.F, 0.f);
+    s.mu[c] = a.stats[c];
+    s.su[c] = a.stats[HF + c];
+  }
+  return s;
+}
+
+// forward of one row up to the log-softmax inputs (wave-cooperative).  Leaves in LDS:
+// uo (HF: lrelu(bn(u))), xs (KX: dropout(elu(c))), cp (KX: c, when non-null), fl (M:
+// row mask); returns per lane the row's y_j = elu(elu(a_j hg_j)) for j = lane + 64 q,
+// and hg_j / a_j when asked.
+template <typename T, int QM>
+__device__ __forceinline__ void head_row_fwd(const HeadArgs& a, const HeadShared& s, int64_t i,
+                                             const T* __restrict__ u, float* uo, float* xs,
+                                             float* cp, int* fl, float (&y)[QM],
+                                             float (&hgv)[QM], float (&av)[QM]) {
+  const int lane = threadIdx.x & 63;
+  const int HF = a.HF, F = a.F, M = a.M, KX = a.KX;
+  const int32_t lo = a.rowptr[i], hi = a.rowptr[i + 1];
+  const int deg = hi - lo;
+  for (int c = lane; c < HF; c += 64) {
+    const float z = fmaf(s.g[c] * s.su[c], to_f32(u[i * HF + c]) - s.mu[c], s.b[c]);
+    uo[c] = z > 0.f ? z : z * a.slope;
+  }
+  for (int j = lane; j < M; j += 64) fl[j] = 0;
+  wave_sync();
+  for (int e = lane; e < deg; e += 64) fl[a.col[lo + e]] = 1;
+  for (int k = lane; k < KX; k += 64) {
+    const int h = k / M, j = k - h * M;
+    const float* uh = uo + h * F;
+    const float* vh = s.vo + (int64_t)h * F * M + j;
+    float c = 0.f;
+#pragma unroll 8
+    for (int f = 0; f < F; ++f) c = fmaf(uh[f], vh[f * M], c);
+    if (cp != nullptr) cp[k] = c;
+    xs[k] = elu1(c) * dropout_factor(a.dx, (uint64_t)i * KX + k);
+  }
+  wave_sync();
+  const float inv = deg > 0 ? 1.f / (float)deg : 0.f;
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int j = lane + 64 * q;
+    y[q] = -INFINITY;
+    hgv[q] = 0.f;
+    av[q] = 0.f;
+    if (j < M) {
+      float hg = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < KX; ++k) hg = fmaf(xs[k], s.W[k * M + j], hg);
+      const float at = (fl[j] ? inv : 0.f) * dropout_factor(a.dg, (uint64_t)i * M + j);
+      hgv[q] = hg;
+      av[q] = at;
+      y[q] = elu1(elu1(at * hg));
+    }
+  }
+}
+
+template <int QM>
+__device__ __forceinline__ float row_lse(const float (&y)[QM]) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < QM; ++q) mx = fmaxf(mx, y[q]);
+  mx = wave_xor_max<1>(mx);
+  float sm = 0.f;
+#pragma unroll
+  for (int q = 0; q < QM; ++q) sm += y[q] == -INFINITY ? 0.f : __expf(y[q] - mx);
+  sm = wave_xor_sum<1>(sm);
+  return mx + __logf(sm);
+}
+
+template <typename T, int QM>
+__global__ void __launch_bounds__(kHeadThreads) head_fwd_kernel(HeadArgs a,
+                                                                const T* __restrict__ u,
+                                                                T* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const HeadShared s = head_shared_load(a, smem);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* scratch = s.su + a.HF + w * (a.HF + a.KX + a.M);
+  float* uo = scratch;
+  float* xs = uo + a.HF;
+  int* fl = reinterpret_cast<int*>(xs + a.KX);
+  __syncthreads();
+  const int64_t nwaves = (int64_t)gridDim.x * (kHeadThreads / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (kHeadThreads / 64) + w; i < a.N; i += nwaves) {
+    float y[QM], hg[QM], at[QM];
+    head_row_fwd<T, QM>(a, s, i, u, uo, xs, nullptr, fl, y, hg, at);
+    const float lse = row_lse<QM>(y);
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = lane + 64 * q;
+      if (j < a.M) out[i * a.M + j] = from_f32<T>(y[q] - lse);
+    }
+    wave_sync();  // this row's LDS reads done before the next row's writes
+  }
+}
+
+// Forward row pass with the small operands in registers (KX = H*M <= 64, F <= 64): lane
+// k = (h, j) holds its column of v_out_h (F values), lane j its column of W (KX values).
+// A wave takes kHeadBatch consecutive rows at a time, so the batch's rowptr, u rows and
+// edge columns are three rounds of loads in flight together (per row they were a chain
+// of dependent round trips); per row the LDS traffic is the row's uo and x vectors, read
+// as 16-byte broadcasts.
+constexpr int kHeadBatch = 16;
+#ifndef HD_DBG
+#define HD_DBG 0  // diagnostic builds only: 1 no c dots, 2 no tail, 4 no u loads, 8 no masks
+#endif
+
+template <typename T, int FV, int KXV>
+__global__ void __launch_bounds__(kHeadThreads) head_fwd_reg_kernel(HeadArgs a,
+                                                                    const T* __restrict__ u,
+                                                                    T* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int R = kHeadBatch;
+  const int HF = a.HF, M = a.M;
+  float* g = smem;
+  float* b = g + HF;
+  float* mu = b + HF;
+  float* su = mu + HF;
+  for (int c = threadIdx.x; c < HF; c += blockDim.x) {
+    g[c] = pw(a.uw, c, FV, 1.f);
+    b[c] = pw(a.ub, c, FV, 0.f);
+    mu[c] = a.stats[c];
+    su[c] = a.stats[HF + c];
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float* uo = su + HF + w * (R * HF + R * KXV + R * 64 + 32);
+  float* xs = uo + R * HF;
+  int* fl = reinterpret_cast<int*>(xs + R * KXV);  // R x M row masks
+  int* rps = fl + R * 64;                            // R + 1 rowptr entries
+  const int kh = lane < KXV ? lane / M : 0, kj = lane < KXV ? lane - kh * M : 0;
+  float vreg[FV], wreg[KXV];
+  const float* vo = a.stats + 4 * HF;
+#pragma unroll
+  for (int f = 0; f < FV; ++f) vreg[f] = lane < KXV ? vo[(int64_t)(kh * FV + f) * M + kj] : 0.f;
+  const int rpt = M <= 32 ? 2 : 1;  // rows per tail pass
+  const int half = rpt == 2 ? lane >> 5 : 0, jl = rpt == 2 ? lane & 31 : lane;
+#pragma unroll
+  for (int k = 0; k < KXV; ++k) wreg[k] = jl < M ? a.W[k * M + jl] : 0.f;
+  __syncthreads();
+  const int64_t nb = (a.N + R - 1) / R;
+  const int64_t nwaves = (int64_t)gridDim.x * (kHeadThreads / 64);
+  const int q4 = HF / 4;
+  for (int64_t bt = (int64_t)blockIdx.x * (kHeadThreads / 64) + w; bt < nb; bt += nwaves) {
+    const int64_t r0 = bt * R;
+    const int nr = (int)(a.N - r0 < R ? a.N - r0 : R);
+    if (lane <= nr) rps[lane] = a.rowptr[r0 + lane];
+    // u rows -> lrelu(bn(u)) in LDS; 8 16-byte loads per lane in flight per round
+    constexpr int UL = 8;
+    for (int eb4 = 0; eb4 < ((HD_DBG & 4) ? 0 : nr * q4); eb4 += 64 * UL) {
+      float4 xq[UL];
+#pragma unroll
+      for (int t = 0; t < UL; ++t) {
+        const int e4 = eb4 + 64 * t + lane;
+        const int r = e4 / q4, c = 4 * (e4 - r * q4);
+        xq[t] = e4 < nr * q4 ? ld4(u + (r0 + r) * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int t = 0; t < UL; ++t) {
+      const int e4 = eb4 + 64 * t + lane;
+      if (e4 >= nr * q4) break;
+      const int r = e4 / q4, c = 4 * (e4 - r * q4);
+      const float4 x = xq[t];
+      const float xv[4] = {x.x, x.y, x.z, x.w};
+      float4 o;
+      float* ov = reinterpret_cast<float*>(&o);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float z = fmaf(g[c + t] * su[c + t], xv[t] - mu[c + t], b[c + t]);
+        ov[t] = z > 0.f ? z : z * a.slope;
+      }
+      *reinterpret_cast<float4*>(uo + r * HF + c) = o;
+      }
+    }
+    for (int e = lane; e < R * M; e += 64) fl[(e / M) * 64 + e % M] = 0;
+    wave_sync();
+    const int32_t eb = rps[0], ee = rps[nr];
+    for (int32_t e = eb + lane; e < ((HD_DBG & 8) ? eb : ee); e += 64) {  // edges -> row masks
+      int r = 0;
+      while (rps[r + 1] <= e) ++r;
+      fl[r * 64 + a.col[e]] = 1;
+    }
+    if (lane < KXV && !(HD_DBG & 1)) {
+      for (int r = 0; r < nr; ++r) {
+        const float4* u4 = reinterpret_cast<const float4*>(uo + r * HF + kh * FV);
+        float c = 0.f;
+#pragma unroll
+        for (int f4 = 0; f4 < FV / 4; ++f4) {
+          const float4 q = u4[f4];
+          c = fmaf(q.x, vreg[4 * f4], c);
+          c = fmaf(q.y, vreg[4 * f4 + 1], c);
+          c = fmaf(q.z, vreg[4 * f4 + 2], c);
+          c = fmaf(q.w, vreg[4 * f4 + 3], c);
+        }
+        xs[r * KXV + lane] = elu1(c) * dropout_factor(a.dx, (uint64_t)(r0 + r) * KXV + lane);
+      }
+    }
+    wave_sync();
+    // two rows per pass when a row fits half the wave (M <= 32: lanes 32.. take row r + 1)
+    for (int r2 = 0; r2 < ((HD_DBG & 2) ? 0 : nr); r2 += rpt) {
+      const int r = r2 + half;
+      const bool act = jl < M && r < nr;
+      float y = -INFINITY;
+      if (act) {
+        const float4* x4 = reinterpret_cast<const float4*>(xs + r * KXV);
+        float hg = 0.f;
+#pragma unroll
+        for (int k4 = 0; k4 < KXV / 4; ++k4) {
+          const float4 q = x4[k4];
+          hg = fmaf(q.x, wreg[4 * k4], hg);
+          hg = fmaf(q.y, wreg[4 * k4 + 1], hg);
+          hg = fmaf(q.z, wreg[4 * k4 + 2], hg);
+          hg = fmaf(q.w, wreg[4 * k4 + 3], hg);
+        }
+        const int deg = rps[r + 1] - rps[r];
+        const float at = (fl[r * 64 + jl] ? (deg > 0 ? 1.f / (float)deg : 0.f) : 0.f) *
+                         dropout_factor(a.dg, (uint64_t)(r0 + r) * M + jl);
+        y = elu1(elu1(at * hg));
+      }
+      float mx = y;
+      for (int o = 1; o < 64 / rpt; o <<= 1) mx = fmaxf(mx, xor_shfl(mx, o));
+      float sm = act ? __expf(y - mx) : 0.f;
+      for (int o = 1; o < 64 / rpt; o <<= 1) sm += xor_shfl(sm, o);
+      const float lse = mx + __logf(sm);
+      if (act) out[(r0 + r) * M + jl] = from_f32<T>(y - lse);
+    }
+    wave_sync();  // the batch's LDS reads done before the next batch's writes
+  }
+}
+
+static size_t fwd_reg_lds(int HF, int KX) {
+  return sizeof(float) * (4 * (size_t)HF + (kHeadThreads / 64) *
+                          (size_t)(kHeadBatch * (HF + KX + 64) + 32));
+}
+
+// ---- backward
+struct HeadBwdWs {
+  float* part;     // kHeadBwdWaves x PT partials: dW (KX*M) | dvo (HF*M) | sdb (HF) | sdbx (HF)
+  int* wflag;      // kHeadBwdWaves
+  float* dz;       // N x HF: BN-input-side gradient of nonzero rows
+  uint8_t* rflag;  // N
+  float* red;      // PT reduced
+};
+
+__host__ __device__ inline int64_t head_pt(int HF, int KX, int M) { return (int64_t)KX * M + (int64_t)HF * M + 2 * HF; }
+
+template <typename T, int QM>
+__global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* __restrict__ u,
+                                                           const T* __restrict__ dout,
+                                                           HeadBwdWs ws, int64_t rows_per_wave) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x;
+  const int HF = a.HF, M = a.M, KX = a.KX, F = a.F;
+  const int64_t PT = head_pt(HF, KX, M);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wave;
+  const int64_t r1 = r0 + rows_per_wave < a.N ? r0 + rows_per_wave : a.N;
+  HeadShared s{};
+  float *uo = nullptr, *xs = nullptr, *cp = nullptr, *dcv = nullptr, *dhg = nullptr;
+  int* fl = nullptr;
+  float *P = nullptr, *PW = nullptr, *Pvo = nullptr, *Pdb = nullptr, *Pdbx = nullptr;
+  bool any = false;
+  // 64 rows per pass: each lane reads one row's dout (all loads in flight together);
+  // the nonzero rows are then processed in ascending order
+  for (int64_t base = r0; base < r1; base += 64) {
+    const int64_t ri = base + lane;
+    bool nzl = false;
+    if (ri < r1) {
+      const T* dr = dout + ri * M;
+      int nzi = 0;
+#pragma unroll 8
+      for (int j = 0; j < M; ++j) nzi |= to_f32(dr[j]) != 0.f;
+      nzl = nzi != 0;
+      ws.rflag[ri] = nzl ? 1 : 0;
+    }
+    uint64_t mask = __ballot(nzl);
+    if (mask != 0ull && !any) {  // first nonzero row of this wave: tables and partials
+      any = true;
+      s = head_shared_load(a, smem);
+      uo = s.su + HF;
+      xs = uo + HF;
+      cp = xs + KX;
+      dcv = cp + KX;
+      dhg = dcv + KX;
+      fl = reinterpret_cast<int*>(dhg + M);
+      P = reinterpret_cast<float*>(fl + M);
+      PW = P;
+      Pvo = PW + (int64_t)KX * M;
+      Pdb = Pvo + (int64_t)HF * M;
+      Pdbx = Pdb + HF;
+      for (int64_t t = lane; t < PT; t += 64) P[t] = 0.f;
+      __syncthreads();
+    }
+    while (mask != 0ull) {
+    const int bit = __builtin_ctzll(mask);
+    mask &= mask - 1ull;
+    const int64_t i = base + bit;
+    float dov[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = lane + 64 * q;
+      dov[q] = j < M ? to_f32(dout[i * M + j]) : 0.f;
+    }
+    float y[QM], hg[QM], at[QM];
+    head_row_fwd<T, QM>(a, s, i, u, uo, xs, cp, fl, y, hg, at);
+    const float lse = row_lse<QM>(y);
+    float sdo = 0.f;
+#pragma unroll
+    for (int q = 0; q < QM; ++q) sdo += dov[q];
+    sdo = wave_xor_sum<1>(sdo);
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      const int j = lane + 64 * q;
+      if (j < M) {
+        // log_softmax, elu, elu, the GAL attention scale
+        const float dy = dov[q] - __expf(y[q] - lse) * sdo;
+        const float z = at[q] * hg[q];
+        const float g = elu1(z);
+        dhg[j] = dy * delu1(g) * delu1(z) * at[q];
+      }
+    }
+    wave_sync();
+    for (int k = lane; k < KX; k += 64) {
+      float dx = 0.f;
+      const float xk = xs[k];
+#pragma unroll 8
+      for (int j = 0; j < M; ++j) {
+        const float d = dhg[j];
+        dx = fmaf(d, s.W[k * M + j], dx);
+        PW[k * M + j] = fmaf(xk, d, PW[k * M + j]);
+      }
+      const float keep = dropout_factor(a.dx, (uint64_t)i * KX + k);
+      dcv[k] = dx * keep * delu1(cp[k]);
+    }
+    wave_sync();
+    for (int c = lane; c < HF; c += 64) {
+      const int h = c / F;
+      const float* dch = dcv + h * M;
+      const float* voc = s.vo + (int64_t)c * M;
+      float* pv = Pvo + (int64_t)c * M;
+      const float uc = uo[c];
+      float duo = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < M; ++j) {
+        duo = fmaf(dch[j], voc[j], duo);
+        pv[j] = fmaf(dch[j], uc, pv[j]);
+      }
+      const float xhat = (to_f32(u[i * HF + c]) - s.mu[c]) * s.su[c];
+      const float zb = fmaf(s.g[c], xhat, s.b[c]);
+      const float dz = duo * (zb > 0.f ? 1.f : a.slope);
+      Pdb[c] += dz;
+      Pdbx[c] = fmaf(dz, xhat, Pdbx[c]);
+      ws.dz[i * HF + c] = dz;
+    }
+    wave_sync();
+    }
+  }
+  if (lane == 0) ws.wflag[blockIdx.x] = any ? 1 : 0;
+  if (any) {
+    float* dst = ws.part + (int64_t)blockIdx.x * PT;
+    for (int64_t t = lane; t < PT; t += 64) dst[t] = P[t];
+  }
+}
+
+// reduced[t] = sum over flagged waves (ascending) of part[w][t]; dW and the u-side
+// BatchNorm weight / bias gradients written out
+__global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBwdWs ws, int nw,
+                                                              float* __restrict__ dW) {
+  __shared__ int list[kHeadBwdWaves];
+  __shared__ int cnt[257];
+  // ordered compaction of the wave flags (each thread a contiguous slice of them)
+  const int per = (nw + 255) / 256;
+  const int b0 = threadIdx.x * per;
+  int c = 0;
+  for (int b = b0; b < b0 + per && b < nw; ++b) c += ws.wflag[b];
+  cnt[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int q = 0; q < 256; ++q) {
+      const int x = cnt[q];
+      cnt[q] = run;
+      run += x;
+    }
+    cnt[256] = run;
+  }
+  __syncthreads();
+  int pos = cnt[threadIdx.x];
+  for (int b = b0; b < b0 + per && b < nw; ++b)
+    if (ws.wflag[b]) list[pos++] = b;
+  __syncthreads();
+  const int nl = cnt[256];
+  const int64_t PT = head_pt(a.HF, a.KX, a.M);
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= PT) return;
+  float sum = 0.f;
+  int l = 0;
+  for (; l + 8 <= nl; l += 8) {  // 8 partials in flight, added in list order
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = ws.part[(int64_t)list[l + q] * PT + t];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sum += v[q];
+  }
+  for (; l < nl; ++l) sum += ws.part[(int64_t)list[l] * PT + t];
+  ws.red[t] = sum;
+  const int64_t nW = (int64_t)a.KX * a.M, nV = (int64_t)a.HF * a.M;
+  if (t < nW) {
+    dW[t] = sum;
+  } else if (t >= nW + nV) {
+    const int64_t r = t - nW - nV;
+    const int ch = (int)(r % a.HF);
+    float* const* dst = r < a.HF ? a.dub : a.duw;  // sdb = d bias, sdbx = d weight
+    float* d = dst[ch / a.F];
+    if (d != nullptr) d[ch % a.F] = sum;
+  }
+}
+
+// du for every row; block 0: the v side's BatchNorm backward (M rows, one thread per
+// channel, rows in order)
+// du for every row (4 channels per thread); block 0: the v side's BatchNorm backward
+// (M rows, one thread per channel, rows in order, v and d v_out staged in LDS)
+template <typename T>
+__global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T* __restrict__ u,
+                                                             const T* __restrict__ v,
+                                                             HeadBwdWs ws, T* __restrict__ du,
+                                                             T* __restrict__ dv) {
+  const int HF = a.HF, M = a.M, F = a.F;
+  const float* red = ws.red;
+  const int64_t nW = (int64_t)a.KX * M, nV = (int64_t)HF * M;
+  const float* dvo = red + nW;  // [c][j]
+  const float* sdb = red + nW + nV;
+  const float* sdbx = sdb + HF;
+  const float* st = a.stats;
+  if (blockIdx.x == 0) {
+    __shared__ float vs[kHeadVStage], gs[kHeadVStage];
+    const bool staged = M * HF <= kHeadVStage;
+    if (staged) {
+      lds_copy(vs, v, M * HF);
+      lds_copy(gs, dvo, M * HF);
+      __syncthreads();
+    }
+    for (int c = threadIdx.x; c < HF; c += blockDim.x) {
+      const float mean = st[2 * HF + c], inv = st[3 * HF + c];
+      const float g = pw(a.vw, c, F, 1.f), b = pw(a.vb, c, F, 0.f);
+      auto xv = [&](int j) { return staged ? vs[j * HF + c] : to_f32(v[(int64_t)j * HF + c]); };
+      auto gv = [&](int j) { return staged ? gs[c * M + j] : dvo[(int64_t)c * M + j]; };
+      float db = 0.f, dw = 0.f;
+      for (int j = 0; j < M; ++j) {
+        const float xh = (xv(j) - mean) * inv;
+        const float dz = gv(j) * (fmaf(g, xh, b) > 0.f ? 1.f : a.slope);
+        db += dz;
+        dw = fmaf(dz, xh, dw);
+      }
+      const float invR = 1.f / (float)M;
+      for (int j = 0; j < M; ++j) {
+        const float xh = (xv(j) - mean) * inv;
+        const float dz = gv(j) * (fmaf(g, xh, b) > 0.f ? 1.f : a.slope);
+        dv[(int64_t)j * HF + c] = from_f32<T>(g * inv * (dz - db * invR - xh * dw * invR));
+      }
+      float* dwp = a.dvw[c / F];
+      float* dbp = a.dvb[c / F];
+      if (dwp != nullptr) dwp[c % F] = dw;
+      if (dbp != nullptr) dbp[c % F] = db;
+    }
+    return;
+  }
+  // per-channel coefficients in LDS: mean, invstd, w * invstd, sum dz / N, sum dz xhat / N
+  __shared__ float cf[5 * 512];
+  const float invN = 1.f / (float)a.N;
+  for (int c = threadIdx.x; c < HF; c += blockDim.x) {
+    cf[c] = st[c];
+    cf[HF + c] = st[HF + c];
+    cf[2 * HF + c] = pw(a.uw, c, F, 1.f) * st[HF + c];
+    cf[3 * HF + c] = sdb[c] * invN;
+    cf[4 * HF + c] = sdbx[c] * invN;
+  }
+  __syncthreads();
+  const int q = HF / 4;  // float4 groups per row (HF % 4 == 0, checked by the caller)
+  const int64_t total = a.N * q;
+  const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
+  constexpr int U = 4;  // elements per thread whose loads are in flight together
+  for (int64_t e0 = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; e0 < total;
+       e0 += U * stride) {
+    float4 x[U], dz[U];
+    uint8_t nz[U];
+#pragma unroll
+    for (int t = 0; t < U; ++t) {
+      const int64_t e = e0 + t * stride;
+      const int64_t i = e < total ? e / q : 0;
+      const int c = 4 * (int)(e - i * q);
+      x[t] = e < total ? ld4(u + i * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      nz[t] = e < total ? ws.rflag[i] : 0;
+      // dz of a zero row is never written: loaded anyway (in flight with the rest) and
+      // not used
+      dz[t] = e < total ? *reinterpret_cast<const float4*>(ws.dz + i * HF + c)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int t = 0; t < U; ++t) {
+      const int64_t e = e0 + t * stride;
+      if (e >= total) break;
+      const int64_t i = e / q;
+      const int c = 4 * (int)(e - i * q);
+      const float xs[4] = {x[t].x, x[t].y, x[t].z, x[t].w};
+      const float dzs[4] = {dz[t].x, dz[t].y, dz[t].z, dz[t].w};
+      float r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ch = c + k;
+        const float xh = (xs[k] - cf[ch]) * cf[HF + ch];
+        r[k] = cf[2 * HF + ch] * ((nz[t] ? dzs[k] : 0.f) - cf[3 * HF + ch] - xh * cf[4 * HF + ch]);
+      }
+      st4(du + i * HF + c, make_float4(r[0], r[1], r[2], r[3]));
+    }
+  }
+}
+
+static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static size_t fwd_lds(int HF, int KX, int M) {
+  return sizeof(float) * ((size_t)HF * M + (size_t)KX * M + 4 * HF +
+                          (kHeadThreads / 64) * (size_t)(HF + KX + M));
+}
+static size_t bwd_lds(int HF, int KX, int M) {
+  return sizeof(float) * ((size_t)HF * M + (size_t)KX * M + 4 * HF + HF + 3 * (size_t)KX + 2 * M +
+                          (size_t)head_pt(HF, KX, M));
+}
+
+struct HeadLayout {
+  size_t part_u, part_b, wflag, dz, rflag, red, total;
+};
+
+static HeadLayout head_layout(int64_t N, int M, int H, int F) {
+  const int HF = H * F, KX = H * M;
+  HeadLayout L{};
+  size_t off = 0;
+  L.part_u = off;
+  const size_t fwd = al256((size_t)bn_stats_blocks(N) * HF * sizeof(Wf));
+  // backward regions (the forward's partials are dead by then: they alias)
+  L.part_b = 0;
+  off = al256((size_t)kHeadBwdWaves * head_pt(HF, KX, M) * sizeof(float));
+  L.wflag = off;
+  off += al256(kHeadBwdWaves * sizeof(int));
+  L.dz = off;
+  off += al256((size_t)N * HF * sizeof(float));
+  L.rflag = off;
+  off += al256((size_t)N);
+  L.red = off;
+  off += al256((size_t)head_pt(HF, KX, M) * sizeof(float));
+  L.total = off > fwd ? off : fwd;
+  return L;
+}
+
+static int head_check(const msha_graph* g, const msha_head_params* hp, int32_t dtype) {
+  MSHA_ARG_CHECK(g != nullptr && g->rowptr && g->col && hp != nullptr, "head: null graph/params");
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "head: bad dtype");
+  MSHA_ARG_CHECK(msha_head_supported(g->n_cols, hp->heads, hp->feat), "head: shape not supported");
+  MSHA_ARG_CHECK(g->n_rows > 0, "head: no rows");
+  return MSHA_OK;
+}
+
+static HeadArgs head_args(const msha_graph* g, const msha_head_params* hp, const float* W,
+                          float* stats) {
+  HeadArgs a{};
+  a.N = g->n_rows;
+  a.M = (int)g->n_cols;
+  a.H = hp->heads;
+  a.F = hp->feat;
+  a.HF = a.H * a.F;
+  a.KX = a.H * a.M;
+  a.eps = hp->eps;
+  a.momentum = hp->momentum;
+  a.slope = hp->slope;
+  a.rowptr = g->rowptr;
+  a.col = g->col;
+  for (int h = 0; h < MSHA_HEAD_MAX_HEADS; ++h) {
+    const bool on = h < hp->heads;
+    a.uw[h] = on ? hp->u_weight[h] : nullptr;
+    a.ub[h] = on ? hp->u_bias[h] : nullptr;
+    a.urm[h] = on ? hp->u_running_mean[h] : nullptr;
+    a.urv[h] = on ? hp->u_running_var[h] : nullptr;
+    a.vw[h] = on ? hp->v_weight[h] : nullptr;
+    a.vb[h] = on ? hp->v_bias[h] : nullptr;
+    a.vrm[h] = on ? hp->v_running_mean[h] : nullptr;
+    a.vrv[h] = on ? hp->v_running_var[h] : nullptr;
+    a.duw[h] = on ? hp->du_weight[h] : nullptr;
+    a.dub[h] = on ? hp->du_bias[h] : nullptr;
+    a.dvw[h] = on ? hp->dv_weight[h] : nullptr;
+    a.dvb[h] = on ? hp->dv_bias[h] : nullptr;
+  }
+  a.W = W;
+  a.stats = stats;
+  return a;
+}
+
+}  // namespace msha
+
+using namespace msha;
+
+extern "C" int msha_head_supported(int64_t n_cols, int32_t heads, int32_t feat) {
+  if (heads < 1 || heads > MSHA_HEAD_MAX_HEADS || feat < 1 || n_cols < 1) return 0;
+  const int64_t HF = (int64_t)heads * feat, KX = heads * n_cols;
+  if (HF > 512 || HF % 4 != 0 || n_cols > 256 || KX > 512) return 0;
+  return bwd_lds((int)HF, (int)KX, (int)n_cols) <= 150 * 1024 &&
+         fwd_lds((int)HF, (int)KX, (int)n_cols) <= 96 * 1024;
+}
+
+extern "C" size_t msha_head_workspace_size(const msha_graph* g, int32_t heads, int32_t feat) {
+  if (g == nullptr) return 0;
+  return head_layout(g->n_rows, (int)g->n_cols, heads, feat).total;
+}
+
+extern "C" int msha_head_fwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
+                             const void* u, const void* v, const float* W, int32_t training,
+                             float p_x, uint64_t seed_x, float p_att, uint64_t seed_att,
+                             float* stats, void* out, void* ws, size_t ws_bytes,
+                             msha_stream_t stream) {
+  if (int rc = head_check(g, hp, dtype)) return rc;
+  MSHA_ARG_CHECK(u && v && W && stats && out, "head_fwd: null pointer");
+  MSHA_ARG_CHECK(p_x >= 0.f && p_x <= 1.f && p_att >= 0.f && p_att <= 1.f, "head_fwd: bad p");
+  const HeadLayout L = head_layout(g->n_rows, (int)g->n_cols, hp->heads, hp->feat);
+  MSHA_ARG_CHECK(!training || (ws && ws_bytes >= L.total), "head_fwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  HeadArgs a = head_args(g, hp, W, stats);
+  a.dx = make_dropout(training ? p_x : 0.f, seed_x, 0, s);
+  a.dg = make_dropout(training ? p_att : 0.f, seed_att, 0, s);
+  const bool bf = dtype == MSHA_DTYPE_BF16;
+  int64_t nbu = 0;
+  Wf* part = training ? (Wf*)((char*)ws + L.part_u) : nullptr;
+  if (training) nbu = bn_stats_partials(a.N, a.HF, bf, u, part, s);
+  const dim3 gp((a.HF + 3) / 4 + 1);
+  if (bf)
+    hipLaunchKernelGGL(head_prep_kernel<bf16_t>, gp, dim3(256), 0, s, a, training, (int)nbu, part,
+                       (const bf16_t*)v);
+  else
+    hipLaunchKernelGGL(head_prep_kernel<float>, gp, dim3(256), 0, s, a, training, (int)nbu, part,
+                       (const float*)v);
+  const dim3 gr(grid_for(a.N, kHeadThreads / 64, 2048));
+  const dim3 grb(grid_for((a.N + kHeadBatch - 1) / kHeadBatch, kHeadThreads / 64, 512));
+  // register-resident path: KX = H*M of 32 or 64 and F of 16 / 32 / 64 (R15: 2 x 64, M 32)
+#define HEAD_FWD_REG(T, FV, KXV)                                                          \
+  if (a.F == FV && a.KX == KXV) {                                                         \
+    hipLaunchKernelGGL((head_fwd_reg_kernel<T, FV, KXV>), grb, dim3(kHeadThreads),        \
+                       fwd_reg_lds(a.HF, KXV), s, a, (const T*)u, (T*)out);               \
+    return check_launch("head_fwd");                                                      \
+  }
+  if (a.HF % 4 == 0 && a.HF <= 256 && a.M <= 64) {
+    if (bf) {
+      HEAD_FWD_REG(bf16_t, 64, 64) HEAD_FWD_REG(bf16_t, 32, 64) HEAD_FWD_REG(bf16_t, 16, 64)
+      HEAD_FWD_REG(bf16_t, 64, 32) HEAD_FWD_REG(bf16_t, 32, 32) HEAD_FWD_REG(bf16_t, 16, 32)
+    } else {
+      HEAD_FWD_REG(float, 64, 64) HEAD_FWD_REG(float, 32, 64) HEAD_FWD_REG(float, 16, 64)
+      HEAD_FWD_REG(float, 64, 32) HEAD_FWD_REG(float, 32, 32) HEAD_FWD_REG(float, 16, 32)
+    }
+  }
+#undef HEAD_FWD_REG
+  const size_t lds = fwd_lds(a.HF, a.KX, a.M);
+#define HEAD_FWD(T, QM)                                                                   \
+  hipLaunchKernelGGL((head_fwd_kernel<T, QM>), gr, dim3(kHeadThreads), lds, s, a,         \
+                     (const T*)u, (T*)out)
+  const int qm = (a.M + 63) / 64;
+  if (bf) {
+    if (qm == 1) HEAD_FWD(bf16_t, 1); else if (qm == 2) HEAD_FWD(bf16_t, 2); else HEAD_FWD(bf16_t, 4);
+  } else {
+    if (qm == 1) HEAD_FWD(float, 1); else if (qm == 2) HEAD_FWD(float, 2); else HEAD_FWD(float, 4);
+  }
+#undef HEAD_FWD
+  return check_launch("head_fwd");
+}
+
+extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
+                             const void* u, const void* v, const float* W, float p_x,
+                             uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
+                             const void* dout, void* du, void* dv, float* dW, void* ws,
+                             size_t ws_bytes, msha_stream_t stream) {
+  if (int rc = head_check(g, hp, dtype)) return rc;
+  MSHA_ARG_CHECK(u && v && W && stats && dout && du && dv && dW, "head_bwd: null pointer");
+  const HeadLayout L = head_layout(g->n_rows, (int)g->n_cols, hp->heads, hp->feat);
+  MSHA_ARG_CHECK(ws && ws_bytes >= L.total, "head_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  HeadArgs a = head_args(g, hp, W, const_cast<float*>(stats));
+  a.dx = make_dropout(p_x, seed_x, 0, s);
+  a.dg = make_dropout(p_att, seed_att, 0, s);
+  char* base = (char*)ws;
+  HeadBwdWs w;
+  w.part = (float*)(base + L.part_b);
+  w.wflag = (int*)(base + L.wflag);
+  w.dz = (float*)(base + L.dz);
+  w.rflag = (uint8_t*)(base + L.rflag);
+  w.red = (float*)(base + L.red);
+  int64_t rpw = (a.N + kHeadBwdWaves - 1) / kHeadBwdWaves;
+  if (rpw < kHeadRowsPerWave) rpw = kHeadRowsPerWave;
+  const int nw = (int)((a.N + rpw - 1) / rpw);
+  const bool bf = dtype == MSHA_DTYPE_BF16;
+  const size_t lds = bwd_lds(a.HF, a.KX, a.M);
+  const int qm = (a.M + 63) / 64;
+#define HEAD_BWD(T, QM)                                                                     \
+  hipLaunchKernelGGL((head_bwd_rows_kernel<T, QM>), dim3(nw), dim3(64), lds, s, a,          \
+                     (const T*)u, (const T*)dout, w, rpw)
+  if (bf) {
+    if (qm == 1) HEAD_BWD(bf16_t, 1); else if (qm == 2) HEAD_BWD(bf16_t, 2); else HEAD_BWD(bf16_t, 4);
+  } else {
+    if (qm == 1) HEAD_BWD(float, 1); else if (qm == 2) HEAD_BWD(float, 2); else HEAD_BWD(float, 4);
+  }
+#undef HEAD_BWD
+  const int64_t PT = head_pt(a.HF, a.KX, a.M);
+  hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 255) / 256)), dim3(256), 0, s, a,
+                     w, nw, dW);
+  const dim3 ga(1 + grid_for(a.N * a.HF / 4, 256 * 4, 1024));
+  if (bf)
+    hipLaunchKernelGGL(head_bwd_apply_kernel<bf16_t>, ga, dim3(256), 0, s, a, (const bf16_t*)u,
+                       (const bf16_t*)v, w, (bf16_t*)du, (bf16_t*)dv);
+  else
+    hipLaunchKernelGGL(head_bwd_apply_kernel<float>, ga, dim3(256), 0, s, a, (const float*)u,
+                       (const float*)v, w, (float*)du, (float*)dv);
+  return check_launch("head_bwd");
+}

@@ -892,3 +892,148 @@ def ours_attention(graph: Graph, groups, src, el, er, h1, h2, a3s, a4s, p: float
     u, v, attd, bstat = _OursAttention.apply(el, er, h1, h2, a3s, a4s, graph, groups, src, p,
                                              seed, slope)
     return (u, v, attd, bstat) if return_aux else (u, v)
+
+
+# ------------------------------------------------------------------ model head ---
+HEAD_TAPS = None  # tests: a list here collects each model-head forward's inputs and statistics
+def head_supported(graph: Graph, heads: int, feat: int) -> bool:
+    return bool(_lib.load().msha_head_supported(graph.n_cols, heads, feat))
+
+
+def _head_params(H, F, eps, momentum, slope, ptrs):
+    hp = _lib.MshaHeadParams()
+    hp.heads, hp.feat, hp.eps, hp.momentum, hp.slope = H, F, eps, momentum, slope
+    for name, lst in ptrs.items():
+        arr = getattr(hp, name)
+        for h in range(H):
+            arr[h] = lst[h] if lst is not None else None
+    return hp
+
+
+class _ModelHead(torch.autograd.Function):
+    """msha_head_fwd / msha_head_bwd: the heads' BatchNorm + LeakyReLU epilogues,
+    elu(u_out @ v_out.T), cat, dropout, out_att (GraphAttentionLayer), elu, log_softmax
+    (Ablation.py:273-277 + :298-301; Ours.py:100-109 + :163-167).  ``params``: the heads'
+    bn2 (u side) weights, bn2 biases, bn1 (v side) weights, bn1 biases, then out_att.a."""
+
+    @staticmethod
+    def forward(ctx, u, v, W, graph: Graph, bns, training, eps, momentum, slope, px, sx, pa,
+                sa, *params):
+        N, H, F = u.shape
+        M = graph.n_cols
+        dt = _table_dtype(u, v)
+        u, v = _tc(u, dt), _tc(v, dt)
+        W32 = _f32c(W)
+        a_out = params[4 * H]
+        p32 = [_f32c(p) for p in params[:4 * H]]  # held until the launches (see bn_lrelu)
+        dev = u.device
+        run = {}
+        copies = []
+        for side, k in (("u", 0), ("v", 1)):
+            rm, rv = [], []
+            for bu_bv in bns:
+                bn = bu_bv[k]
+                if training and bn.track_running_stats and bn.running_mean is not None:
+                    m32, v32 = _f32c(bn.running_mean), _f32c(bn.running_var)
+                    if m32.data_ptr() != bn.running_mean.data_ptr():
+                        copies.append((bn.running_mean, m32, bn.running_var, v32))
+                    rm.append(m32)
+                    rv.append(v32)
+                elif not training:
+                    rm.append(_f32c(bn.running_mean))
+                    rv.append(_f32c(bn.running_var))
+                else:
+                    rm.append(None)
+                    rv.append(None)
+            run[side] = (rm, rv)
+        ptr = lambda lst: [_lib.ptr(t) for t in lst]  # noqa: E731
+        hp = _head_params(H, F, eps, momentum, slope, {
+            "u_weight": ptr(p32[0:H]), "u_bias": ptr(p32[H:2 * H]),
+            "u_running_mean": ptr(run["u"][0]), "u_running_var": ptr(run["u"][1]),
+            "v_weight": ptr(p32[2 * H:3 * H]), "v_bias": ptr(p32[3 * H:4 * H]),
+            "v_running_mean": ptr(run["v"][0]), "v_running_var": ptr(run["v"][1])})
+        stats = torch.empty(4 * H * F + H * F * M, device=dev, dtype=torch.float32)
+        out = torch.empty(N, M, device=dev, dtype=dt)
+        g = graph.desc
+        wsb = int(_lib.load().msha_head_workspace_size(g, H, F)) if training else 0
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        _lib.call("msha_head_fwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
+                  W32.data_ptr(), int(training), px, sx, pa, sa, stats.data_ptr(),
+                  out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(u))
+        if HEAD_TAPS is not None:  # tests: the statistics that decide the LeakyReLU branches
+            HEAD_TAPS.append({"u": u.detach().clone(), "v": v.detach().clone(),
+                              "stats": stats.detach().clone(),
+                              "params": [p.detach().clone() for p in p32]})
+        for rm, m32, rv, v32 in copies:  # non-fp32 running buffers: write the update back
+            rm.copy_(m32)
+            rv.copy_(v32)
+        ctx.graph, ctx.hpar = graph, (H, F, eps, momentum, slope)
+        ctx.drop = (px, sx, pa, sa)
+        ctx.pdtypes = [p.dtype for p in params[:4 * H]]
+        ctx.wdtype = W.dtype
+        ctx.a_meta = (a_out.shape, a_out.dtype, a_out.device)
+        ctx.save_for_backward(u, v, W32, stats, *p32)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        u, v, W32, stats, *p32 = ctx.saved_tensors
+        H, F, eps, momentum, slope = ctx.hpar
+        px, sx, pa, sa = ctx.drop
+        graph = ctx.graph
+        dev = u.device
+        dt = u.dtype
+        dout = _tc(dout, dt)
+        du = torch.empty_like(u)
+        dv = torch.empty_like(v)
+        dW = torch.empty_like(W32)
+        dp = torch.empty(4, H, F, device=dev, dtype=torch.float32)
+        ptr = lambda lst: [_lib.ptr(t) for t in lst]  # noqa: E731
+        hp = _head_params(H, F, eps, momentum, slope, {
+            "u_weight": ptr(p32[0:H]), "u_bias": ptr(p32[H:2 * H]),
+            "v_weight": ptr(p32[2 * H:3 * H]), "v_bias": ptr(p32[3 * H:4 * H]),
+            "du_weight": ptr(dp[0].unbind(0)), "du_bias": ptr(dp[1].unbind(0)),
+            "dv_weight": ptr(dp[2].unbind(0)), "dv_bias": ptr(dp[3].unbind(0)),
+            "u_running_mean": None, "u_running_var": None, "v_running_mean": None,
+            "v_running_var": None})
+        g = graph.desc
+        wsb = int(_lib.load().msha_head_workspace_size(g, H, F))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        _lib.call("msha_head_bwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
+                  W32.data_ptr(), px, sx, pa, sa, stats.data_ptr(), dout.data_ptr(),
+                  du.data_ptr(), dv.data_ptr(), dW.data_ptr(), ws.data_ptr(), ws.numel(),
+                  _stream(u))
+        shape, adt, adev = ctx.a_meta
+        grads = [dp[k, h].to(ctx.pdtypes[k * H + h]) for k in range(4) for h in range(H)]
+        return (du, dv, dW.to(ctx.wdtype), None, None, None, None, None, None, None, None, None,
+                None, *grads, torch.zeros(shape, dtype=adt, device=adev))
+
+
+def C_byref(x):
+    import ctypes
+
+    return ctypes.byref(x)
+
+
+def model_head(graph: Graph, u, v, bns, out_W, out_a, p: float = 0.0, training: bool = False,
+               slope: float = 0.2):
+    """log_softmax(elu(out_att(dropout(cat_h elu(lrelu(bn2_h(u_h)) @ lrelu(bn1_h(v_h)).T)))))
+    for the (N, H, F) / (M, H, F) attention aggregates u, v; ``bns``: per head (bn2, bn1)
+    BatchNorm1d modules (u side, v side).  Training: batch statistics (running
+    statistics and num_batches_tracked advanced as nn.BatchNorm1d), dropout p on x and on
+    the out_att attention; eval: running statistics."""
+    _lib.require_cuda(u, v, out_W)
+    N, H, F = u.shape
+    bn0 = bns[0][0]
+    px = pa = float(p) if training else 0.0
+    sx = new_seed() if px > 0 else 0
+    sa = new_seed() if pa > 0 else 0
+    params = ([b[0].weight for b in bns] + [b[0].bias for b in bns] + [b[1].weight for b in bns]
+              + [b[1].bias for b in bns] + [out_a])
+    if training:
+        ctr = [bn.num_batches_tracked for b in bns for bn in b
+               if bn.track_running_stats and bn.num_batches_tracked is not None]
+        if ctr:
+            torch._foreach_add_(ctr, 1)
+    return _ModelHead.apply(u, v, out_W, graph, bns, bool(training), float(bn0.eps),
+                            float(bn0.momentum), float(slope), px, sx, pa, sa, *params)

@@ -169,9 +169,39 @@ def _score_halves(heads, name):
     return torch.stack([getattr(h, name).view(2, Fd) for h in heads])
 
 
-def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
-    """All heads of an ablation3 in one launch: projections stacked along features,
-    one (H-head) edge-attention forward/backward, per-head BN epilogues."""
+def _head_fusable(heads, graph: Graph, training) -> bool:
+    """The model head (msha_head_fwd/bwd) covers the model's tail when the shape fits its
+    LDS budget, the BatchNorms share eps / momentum (exponential average), and either
+    training (batch statistics) or no autograd (eval)."""
+    if not (training or not torch.is_grad_enabled()):
+        return False
+    bns = [bn for h in heads for bn in (h.bn1, h.bn2)]
+    if any(bn.momentum is None or bn.eps != bns[0].eps or bn.momentum != bns[0].momentum
+           or bn.training != training or not bn.affine for bn in bns):
+        return False
+    return MF.head_supported(graph, len(heads), heads[0].out_features)
+
+
+def _model_tail(model, graph: Graph, u, v):
+    """Ablation.py:273-277 per head + :298-301 (Ours.py:100-109 + :163-167) on the fused
+    model head: one row pass from the (N, H, F) / (M, H, F) aggregates to log-probs."""
+    heads = model.attentions
+    return MF.model_head(graph, u, v, [(h.bn2, h.bn1) for h in heads], model.out_att.W,
+                         model.out_att.a, model.dropout, model.training, heads[0].alpha)
+
+
+def _tail_unfused(model, graph: Graph, u, v):
+    """The same tail as per-head epilogue launches + out_att + ATen (shapes the model
+    head does not cover, eval with autograd)."""
+    outs = _epilogues(model.attentions, u.unbind(1), v.unbind(1))
+    x = torch.cat(outs, dim=1)
+    x = F.dropout(x, model.dropout, training=model.training)
+    x = F.elu(model.out_att(x, graph))
+    return F.log_softmax(x, dim=1)
+
+
+def _attention_uv3(heads, s_input, r_input, graph: Graph, training):
+    """OursLayer3 inter attention of all heads: (u (N, H, F), v (M, H, F))."""
     H = len(heads)
     Fd = heads[0].out_features
     n, m = s_input.shape[0], r_input.shape[0]
@@ -184,12 +214,17 @@ def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
     a_r, a_l = _score_halves(heads, "a").unbind(1)  # (H, F) each
     h1, er = MF.project_scores(r_input, W1, ar=a_r, heads=H)  # (M, H*F), (M, H)
     h2, el = MF.project_scores(s_input, W2, al=a_l, heads=H)  # (N, H*F), (N, H)
-    u, v = MF.edge_attention(graph, el, er, h1.view(m, H, Fd), hs=h2.view(n, H, Fd),
+    return MF.edge_attention(graph, el, er, h1.view(m, H, Fd), hs=h2.view(n, H, Fd),
                              p=heads[0].dropout, training=training)
+
+
+def fused_ours_layer3(heads, s_input, r_input, graph: Graph, training):
+    """All heads of an ablation3 in one launch: projections stacked along features,
+    one (H-head) edge-attention forward/backward, per-head BN epilogues."""
+    u, v = _attention_uv3(heads, s_input, r_input, graph, training)
     # unbind: the backward stacks the head gradients in one copy (u[:, k] selects would
     # zero-fill and copy a full (rows, H, F) gradient per head and add them)
-    us, vs = u.unbind(1), v.unbind(1)
-    return _epilogues(heads, us, vs)
+    return _epilogues(heads, u.unbind(1), v.unbind(1))
 
 
 class ablation3(nn.Module):  # noqa: N801  (reference class name)
@@ -214,11 +249,10 @@ class ablation3(nn.Module):  # noqa: N801  (reference class name)
         g = _graph(inter_adj)
         s_input = F.dropout(self.Sfeatures, self.dropout, training=self.training)
         r_input = F.dropout(self.Rfeatures, self.dropout, training=self.training)
-        x = torch.cat(fused_ours_layer3(self.attentions, s_input, r_input, g, self.training),
-                      dim=1)
-        x = F.dropout(x, self.dropout, training=self.training)
-        x = F.elu(self.out_att(x, g))
-        return F.log_softmax(x, dim=1)
+        u, v = _attention_uv3(self.attentions, s_input, r_input, g, self.training)
+        if _head_fusable(self.attentions, g, self.training):
+            return _model_tail(self, g, u, v)
+        return _tail_unfused(self, g, u, v)
 
 
 class LinkPredictor(torch.nn.Module):
@@ -287,6 +321,15 @@ class OursLayer(OursLayer3):
 def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_adj,
                      source_index, training, record=False, Coeff12=None, Coeff3=None,
                      Coeff4=None):
+    u, v = _attention_uv(heads, s_input, r_input, graph, city_adj, province_adj, source_index,
+                         training, record, Coeff12, Coeff3, Coeff4)
+    return _epilogues(heads, u.unbind(1), v.unbind(1))  # one stacked gradient copy
+
+
+def _attention_uv(heads, s_input, r_input, graph: Graph, city_adj, province_adj,
+                  source_index, training, record=False, Coeff12=None, Coeff3=None,
+                  Coeff4=None):
+    """OursLayer inter + intra attention of all heads: (u (N, H, F), v (M, H, F))."""
     H = len(heads)
     Fd = heads[0].out_features
     n, m = s_input.shape[0], r_input.shape[0]
@@ -310,8 +353,7 @@ def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_a
                                           training=training, return_aux=True)
     if record:
         _record(attd, bstat, graph, groups, src, heads, Coeff12, Coeff3, Coeff4)
-    us, vs = u.unbind(1), v.unbind(1)  # one stacked gradient copy (see fused_ours_layer3)
-    return _epilogues(heads, us, vs)
+    return u, v
 
 
 class _RecordState:
@@ -374,12 +416,11 @@ class Ours(nn.Module):
         g = _graph(inter_adj)
         s_input = F.dropout(self.Sfeatures, self.dropout, training=self.training)
         r_input = F.dropout(self.Rfeatures, self.dropout, training=self.training)
-        x = torch.cat(fused_ours_layer(self.attentions, s_input, r_input, g, city_adj,
-                                       province_adj, source_index, self.training, record,
-                                       Coeff12, Coeff3, Coeff4), dim=1)
-        x = F.dropout(x, self.dropout, training=self.training)
-        x = F.elu(self.out_att(x, g))
-        return F.log_softmax(x, dim=1)
+        u, v = _attention_uv(self.attentions, s_input, r_input, g, city_adj, province_adj,
+                             source_index, self.training, record, Coeff12, Coeff3, Coeff4)
+        if _head_fusable(self.attentions, g, self.training):
+            return _model_tail(self, g, u, v)
+        return _tail_unfused(self, g, u, v)
 
 
 class GraphConvolution(nn.Module):

@@ -1,0 +1,201 @@
+"""Model head (msha_head_fwd / msha_head_bwd) vs an fp64 torch restatement of the
+reference's tail (Ablation.py:273-277 per head + :298-301; GAT.py:20-35 for out_att),
+with the kernels' own Philox dropout masks injected into the reference.
+
+fp32 bar: 1e-5 relative to each tensor's scale (north_star); bf16 tables: 1e-2 against
+the fp64 reference evaluated on the same bf16-rounded inputs.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gpu_helpers import tol_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(n, m, seed, dev):
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(seed)
+    cnt = np.zeros((n, m), np.float32)
+    for i in range(n):
+        d = int(rng.integers(0, 6))
+        if d:
+            cnt[i, rng.choice(m, d, replace=False)] = 1
+    cnt[:3] = 0  # empty rows: virtual full rows, uniform 1/M attention
+    cnt[3] = 1   # a full row
+    g = Graph.from_dense(torch.as_tensor(cnt, device=dev))
+    mask = cnt > 0
+    mask[~mask.any(1)] = True
+    return g, torch.as_tensor(mask)
+
+
+def _bns(H, F, dev, seed):
+    gen = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(H):
+        pair = []
+        for _ in range(2):
+            bn = torch.nn.BatchNorm1d(F).to(dev)
+            with torch.no_grad():
+                bn.weight.copy_(torch.rand(F, generator=gen) + 0.5)
+                bn.bias.copy_(torch.randn(F, generator=gen) * 0.1)
+                bn.running_mean.copy_(torch.randn(F, generator=gen) * 0.1)
+                bn.running_var.copy_(torch.rand(F, generator=gen) + 0.5)
+            pair.append(bn)
+        out.append(tuple(pair))  # (bn2 u side, bn1 v side)
+    return out
+
+
+def _reference(u, v, bns, W, mask, keep_x, keep_g, p, training, dout):
+    """fp64 restatement on CPU; returns (out, grads dict) with autograd."""
+    N, H, F_ = u.shape
+    M = v.shape[0]
+    u = u.detach().double().cpu().requires_grad_(True)
+    v = v.detach().double().cpu().requires_grad_(True)
+    W = W.detach().double().cpu().requires_grad_(True)
+    prm = []
+    for bu, bv in bns:
+        prm.append([t.detach().double().cpu().requires_grad_(True)
+                    for t in (bu.weight, bu.bias, bv.weight, bv.bias)])
+    runs = [[t.detach().double().cpu().clone() for t in (bu.running_mean, bu.running_var,
+                                                          bv.running_mean, bv.running_var)]
+            for bu, bv in bns]
+    scale = 1.0 / (1.0 - p) if p > 0 else 1.0
+    cs = []
+    for h in range(H):
+        wu, bu_, wv, bv_ = prm[h]
+        rmu, rvu, rmv, rvv = runs[h]
+        uo = F.leaky_relu(F.batch_norm(u[:, h], rmu, rvu, wu, bu_, training, 0.1, 1e-5), 0.2)
+        vo = F.leaky_relu(F.batch_norm(v[:, h], rmv, rvv, wv, bv_, training, 0.1, 1e-5), 0.2)
+        cs.append(F.elu(uo @ vo.t()))
+    x = torch.cat(cs, 1)
+    if training and p > 0:
+        x = x * keep_x.double().view(N, H * M) * scale
+    hg = x @ W
+    deg = mask.sum(1, keepdim=True).double()
+    att = mask.double() / deg
+    if training and p > 0:
+        att = att * keep_g.double().view(N, M) * scale
+    out = F.log_softmax(F.elu(F.elu(att * hg)), dim=1)
+    grads = {}
+    if dout is not None:
+        out.backward(dout.double().cpu())
+        grads = {"u": u.grad, "v": v.grad, "W": W.grad,
+                 "uw": [q[0].grad for q in prm], "ub": [q[1].grad for q in prm],
+                 "vw": [q[2].grad for q in prm], "vb": [q[3].grad for q in prm]}
+    return out.detach(), grads, runs
+
+
+def _run(cuda, n, m, H, F_, p, training, dtype=torch.float32, sparse=True, seed=0):
+    from msha_gnn_amd import functional as MF
+
+    g, mask = _graph(n, m, seed, cuda)
+    gen = torch.Generator().manual_seed(seed + 1)
+    u = (torch.randn(n, H, F_, generator=gen)).to(cuda, dtype)
+    v = (torch.randn(m, H, F_, generator=gen)).to(cuda, dtype)
+    W = (torch.randn(H * m, m, generator=gen) * (H * m) ** -0.5).to(cuda)
+    a = torch.zeros(2 * m, 1, device=cuda)
+    bns = _bns(H, F_, cuda, seed + 2)
+    for pair in bns:
+        for bn in pair:
+            bn.train(training)
+    ref_bns = _bns(H, F_, cuda, seed + 2)  # same values, untouched by the kernel
+    sx, sa = 1234 + seed, 5678 + seed
+    pp = p if training else 0.0
+    u_ = u.clone().requires_grad_(True)
+    v_ = v.clone().requires_grad_(True)
+    W_ = W.clone().requires_grad_(True)
+    params = ([b[0].weight for b in bns] + [b[0].bias for b in bns] + [b[1].weight for b in bns]
+              + [b[1].bias for b in bns] + [a])
+    with torch.set_grad_enabled(training):
+        out = MF._ModelHead.apply(u_, v_, W_, g, bns, training, 1e-5, 0.1, 0.2, pp, sx, pp, sa,
+                                  *params)
+    keep_x = MF.dropout_keep_mask(n * H * m, pp, sx, cuda).cpu().bool() if pp > 0 else None
+    keep_g = MF.dropout_keep_mask(n * m, pp, sa, cuda).cpu().bool() if pp > 0 else None
+    dout = None
+    if training:
+        dout = torch.zeros(n, m)
+        rows = torch.randint(0, n, (64,), generator=gen) if sparse else torch.arange(n)
+        dout.index_put_((rows,), torch.randn(len(rows), m, generator=gen), accumulate=True)
+        out.backward(dout.to(cuda, dtype))
+    ref, grads, runs = _reference(u, v, ref_bns, W, mask, keep_x, keep_g, pp, training, dout)
+    return out, ref, grads, runs, (u_, v_, W_, bns)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.5])
+@pytest.mark.parametrize("sparse", [True, False])
+def test_head_train_matches_fp64(cuda, msha, p, sparse):
+    """R15's shape (2 heads x 64, 32 recipients) with empty / full rows: output, every
+    gradient and the BatchNorm running statistics within 1e-5."""
+    out, ref, gr, runs, (u, v, W, bns) = _run(cuda, 3000, 32, 2, 64, p, True, sparse=sparse)
+    tol_close(out.detach().cpu().numpy(), ref.numpy(), 1e-5, 1e-5)
+    tol_close(u.grad.cpu().numpy(), gr["u"].numpy(), 1e-5, 1e-5)
+    tol_close(v.grad.cpu().numpy(), gr["v"].numpy(), 1e-5, 1e-5)
+    tol_close(W.grad.cpu().numpy(), gr["W"].numpy(), 1e-5, 1e-5)
+    for h, (bu, bv) in enumerate(bns):
+        tol_close(bu.weight.grad.cpu().numpy(), gr["uw"][h].numpy(), 1e-5, 1e-5)
+        tol_close(bu.bias.grad.cpu().numpy(), gr["ub"][h].numpy(), 1e-5, 1e-5)
+        tol_close(bv.weight.grad.cpu().numpy(), gr["vw"][h].numpy(), 1e-5, 1e-5)
+        tol_close(bv.bias.grad.cpu().numpy(), gr["vb"][h].numpy(), 1e-5, 1e-5)
+        for t, r in zip((bu.running_mean, bu.running_var, bv.running_mean, bv.running_var),
+                        runs[h]):
+            tol_close(t.cpu().numpy(), r.numpy(), 1e-5, 1e-6)
+
+
+def test_head_wide_recipients(cuda, msha):
+    """80 recipients (two 64-lane column passes per row), 2 heads x 16."""
+    out, ref, gr, _, (u, v, W, _) = _run(cuda, 700, 80, 2, 16, 0.3, True, seed=3)
+    tol_close(out.detach().cpu().numpy(), ref.numpy(), 1e-5, 1e-5)
+    tol_close(u.grad.cpu().numpy(), gr["u"].numpy(), 1e-5, 1e-5)
+    tol_close(W.grad.cpu().numpy(), gr["W"].numpy(), 1e-5, 1e-5)
+
+
+def test_head_eval_running_stats(cuda, msha):
+    out, ref, _, _, _ = _run(cuda, 1000, 32, 2, 64, 0.5, False, seed=5)
+    tol_close(out.detach().cpu().numpy(), ref.numpy(), 1e-5, 1e-5)
+
+
+def test_head_bf16_vs_fp64(cuda, msha):
+    """bf16 tables (u, v, out, du, dv): 1e-2 against fp64 on the same rounded inputs."""
+    out, ref, gr, _, (u, v, W, _) = _run(cuda, 2000, 32, 2, 64, 0.0, True, torch.bfloat16,
+                                         seed=7)
+    tol_close(out.detach().float().cpu().numpy(), ref.numpy(), 1e-2, 1e-2)
+    tol_close(u.grad.float().cpu().numpy(), gr["u"].numpy(), 1e-2, 1e-2)
+    tol_close(v.grad.float().cpu().numpy(), gr["v"].numpy(), 1e-2, 1e-2)
+    tol_close(W.grad.cpu().numpy(), gr["W"].numpy(), 1e-2, 1e-2)
+
+
+def test_models_use_the_fused_head(cuda, msha):
+    """ablation3 / Ours route their tail through the model head in training and under
+    no_grad; eval with autograd takes the per-head launches."""
+    from msha_gnn_amd import layers
+
+    class Probe:
+        calls = 0
+
+    orig = layers.MF.model_head
+
+    def probe(*a, **k):
+        Probe.calls += 1
+        return orig(*a, **k)
+
+    g, _ = _graph(200, 32, 11, cuda)
+    gdp = {i: 0.1 for i in range(200)}
+    torch.manual_seed(0)
+    model = layers.ablation3(128, 64, 32, 2, 0.5, gdp, 200, 32).to(cuda)
+    layers.MF.model_head = probe
+    try:
+        model.train()
+        model(g, None, None, torch.arange(4, device=cuda)).sum().backward()
+        assert Probe.calls == 1
+        model.eval()
+        with torch.no_grad():
+            model(g, None, None, None)
+        assert Probe.calls == 2
+        model(g, None, None, None)
+        assert Probe.calls == 2
+    finally:
+        layers.MF.model_head = orig

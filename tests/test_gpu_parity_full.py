@@ -204,10 +204,34 @@ class _Branches:
             return out
 
         MF.project_scores, MF.bn_lrelu, MF.ours_attention = project_scores, bn_lrelu, ours_attention
+        MF.HEAD_TAPS = self.taps = []
         return self
 
     def __exit__(self, *exc):
         self.MF.project_scores, self.MF.bn_lrelu, self.MF.ours_attention = self._orig
+        self.MF.HEAD_TAPS = None
+
+    def _head_bn_signs(self, H):
+        """BatchNorm + LeakyReLU branches of the fused model head: z = fma(w * invstd,
+        x - mean, b) from the kernel's own statistics, evaluated exactly in fp64 from the
+        fp32 factors (the fp32 fma rounds the exact value, so the signs agree)."""
+        tap = self.taps[0]
+        st = tap["stats"].double().cpu()
+        prm = [q.double().cpu() for q in tap["params"]]
+        out = []
+        for h in range(H):
+            res = {}
+            for side, x, k0, s0 in (("u", tap["u"][:, h], 0, 0), ("v", tap["v"][:, h], 2, 2)):
+                Fd = x.shape[1]
+                w, b = prm[k0 * H + h], prm[(k0 + 1) * H + h]
+                hf = H * Fd
+                mean = st[s0 * hf + h * Fd: s0 * hf + (h + 1) * Fd].float()
+                inv = st[(s0 + 1) * hf + h * Fd: (s0 + 1) * hf + (h + 1) * Fd].float()
+                a = (w.float() * inv).double()
+                d = (x.float().cpu() - mean).double()
+                res[side] = (a * d + b) > 0
+            out.append(res)
+        return out
 
     def heads(self, H):
         """One dense_ref branch dict per head (the first forward recorded)."""
@@ -216,10 +240,14 @@ class _Branches:
         er = get("er")[0].float().cpu().numpy()
         bns = get("bn")
         bstat = get("bstat")
+        fused = self._head_bn_signs(H) if self.taps else None
         out = []
         for h in range(H):
-            d = {"edge": torch.as_tensor((el[:, h][:, None] + er[:, h][None, :]) > 0),
-                 "v": bns[2 * h].cpu() > 0, "u": bns[2 * h + 1].cpu() > 0}
+            d = {"edge": torch.as_tensor((el[:, h][:, None] + er[:, h][None, :]) > 0)}
+            if fused is not None:
+                d.update(fused[h])
+            else:
+                d.update({"v": bns[2 * h].cpu() > 0, "u": bns[2 * h + 1].cpu() > 0})
             if bstat:
                 d["p3"] = bstat[0][:, h, 0].cpu() > 0
                 d["p4"] = bstat[0][:, h, 1].cpu() > 0

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(msha):
     from msha_gnn_amd import _lib
 
     lib = _lib.load()  # loads without touching the GPU
-    assert lib.msha_abi_version() == 4
+    assert lib.msha_abi_version() == _lib.ABI_VERSION == 5
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (msha_\w+)", out))
@@ -36,6 +36,10 @@ def test_library_exports_every_header_symbol(msha):
     assert lib.msha_edge_attention_supported(8, 16) == 1
     assert lib.msha_edge_attention_supported(3, 16) == 0
     assert lib.msha_graph_workspace_size(39179, 32) > 0
+    # model head: R15's shape (2 heads x 64, 32 recipients) is covered, 9 heads are not
+    assert lib.msha_head_supported(32, 2, 64) == 1
+    assert lib.msha_head_supported(32, 9, 64) == 0
+    assert lib.msha_head_supported(300, 2, 64) == 0
 
 
 def test_abi_argument_errors_are_reported(msha):
