@@ -486,6 +486,25 @@ MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int3
                            const void* dout, void* du, void* dv, float* dW, void* ws,
                            size_t ws_bytes, msha_stream_t stream);
 
+
+/* ---- Batched segment copies: the models' per-head parameter packing (Ablation.py:262-267,
+ * Ours.py:58-75 read W1/W2/a/a3/a4 of every head; one launch stacks them, one scatters
+ * their gradients back) and the feature dropout of Sfeatures / Rfeatures
+ * (Ablation.py:296-297, Ours.py:161-162) in one launch forward and one backward.
+ * For every segment:  dst[r*ldd + c] = (a[r*lda + c] (+ b[r*ldb + c])) * keep(r*cols + c)
+ * for r < rows, c < cols; a NULL `a` writes zeros; keep is the Philox dropout factor
+ * (0 or 1/(1-p)) keyed on (seed, element, offset) when p > 0, else 1. */
+#define MSHA_MAX_SEGMENTS 32
+typedef struct msha_segment {
+  const float* a;
+  const float* b;
+  float* dst;
+  int64_t rows, cols, lda, ldb, ldd;
+  float p;
+  uint64_t seed, offset;
+} msha_segment;
+MSHA_API int msha_segments(int32_t n, const msha_segment* segs, msha_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

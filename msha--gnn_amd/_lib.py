@@ -67,6 +67,17 @@ class MshaHeadParams(C.Structure):
 
 HPP = C.POINTER(MshaHeadParams)
 
+MAX_SEGMENTS = 32
+
+
+class MshaSegment(C.Structure):
+    """Mirror of ``struct msha_segment`` (include/msha_gnn.h)."""
+
+    _fields_ = [("a", C.c_void_p), ("b", C.c_void_p), ("dst", C.c_void_p),
+                ("rows", C.c_int64), ("cols", C.c_int64), ("lda", C.c_int64),
+                ("ldb", C.c_int64), ("ldd", C.c_int64), ("p", C.c_float),
+                ("seed", C.c_uint64), ("offset", C.c_uint64)]
+
 # name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
 SIGNATURES = {
     "msha_abi_version": (C.c_int, []),
@@ -125,6 +136,7 @@ SIGNATURES = {
     "msha_ours_workspace_size": (SZ, [GRP, I64, I32, I32]),
     "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, I32, F32, F32,
                                       U64, U64, P, P, P, P, P, P, P, SZ, P]),
+    "msha_segments": (C.c_int, [I32, P, P]),
     "msha_head_supported": (C.c_int, [I64, I32, I32]),
     "msha_head_workspace_size": (SZ, [GP, I32, I32]),
     "msha_head_fwd": (C.c_int, [GP, HPP, I32, P, P, P, I32, F32, U64, F32, U64, P, P, P, SZ, P]),

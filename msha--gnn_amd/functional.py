@@ -1037,3 +1037,141 @@ def model_head(graph: Graph, u, v, bns, out_W, out_a, p: float = 0.0, training: 
             torch._foreach_add_(ctr, 1)
     return _ModelHead.apply(u, v, out_W, graph, bns, bool(training), float(bn0.eps),
                             float(bn0.momentum), float(slope), px, sx, pa, sa, *params)
+
+
+# ------------------------------------------------- parameter packing / feature dropout ---
+def _segments(segs, stream):
+    """One msha_segments launch: segs = [(a, dst, rows, cols, lda, ldd, b, ldb, p, seed)]
+    (pointers as ints, a / b may be None)."""
+    arr = (_lib.MshaSegment * len(segs))()
+    for k, (a, dst, rows, cols, lda, ldd, b, ldb, p, seed) in enumerate(segs):
+        arr[k] = _lib.MshaSegment(a, b, dst, rows, cols, lda, ldb, ldd, p, seed, 0)
+    _lib.call("msha_segments", len(segs), C_byref(arr), stream)
+
+
+class _FeatureDropout(torch.autograd.Function):
+    """dropout(Sfeatures), dropout(Rfeatures) (Ablation.py:296-297, Ours.py:161-162) in one
+    launch; the backward regenerates both Philox masks in one launch."""
+
+    @staticmethod
+    def forward(ctx, S, R, p, s_seed, r_seed):
+        S, R = S.contiguous(), R.contiguous()
+        So, Ro = torch.empty_like(S), torch.empty_like(R)
+        _segments([(S.data_ptr(), So.data_ptr(), S.shape[0], S.shape[1], S.shape[1], S.shape[1],
+                    None, 0, p, s_seed),
+                   (R.data_ptr(), Ro.data_ptr(), R.shape[0], R.shape[1], R.shape[1], R.shape[1],
+                    None, 0, p, r_seed)], _stream(S))
+        ctx.p, ctx.seeds = p, (s_seed, r_seed)
+        return So, Ro
+
+    @staticmethod
+    def backward(ctx, dSo, dRo):
+        segs, outs = [], []
+        for d, seed in ((dSo, ctx.seeds[0]), (dRo, ctx.seeds[1])):
+            if d is None:
+                outs.append(None)
+                continue
+            d = d.contiguous()
+            g = torch.empty_like(d)
+            segs.append((d.data_ptr(), g.data_ptr(), d.shape[0], d.shape[1], d.shape[1],
+                         d.shape[1], None, 0, ctx.p, seed))
+            outs.append(g)
+        if segs:
+            _segments(segs, _stream(outs[0] if outs[0] is not None else outs[1]))
+        return outs[0], outs[1], None, None, None
+
+
+def feature_dropout(S, R, p: float, training: bool):
+    """(dropout(S, p), dropout(R, p)) for the models' two feature tables: one launch each
+    way for fp32 tables (Philox masks, seeds from torch's CPU generator), F.dropout
+    otherwise."""
+    if not training or p <= 0:
+        return S, R
+    if S.dtype != torch.float32 or R.dtype != torch.float32 or S.dim() != 2 or R.dim() != 2:
+        return (torch.nn.functional.dropout(S, p, training=True),
+                torch.nn.functional.dropout(R, p, training=True))
+    _lib.require_cuda(S, R)
+    return _FeatureDropout.apply(S, R, float(p), new_seed(), new_seed())
+
+
+class _PackHeads(torch.autograd.Function):
+    """The heads' parameters as the fused launches read them (Ablation.py:262-267,
+    Ours.py:58-75): W1 / W2 concatenated along features (K, H*F), the score vector halves
+    a[:F] (recipient side) / a[F:] (source side) as (H, F), and for the full MSHA layer
+    a3[:F] + a3[F:], a4[:F] + a4[F:] -- one launch; the backward scatters the packed
+    gradients to every head's parameters in one launch."""
+
+    @staticmethod
+    def forward(ctx, H, intra, *params):
+        W1s, W2s, As = params[:H], params[H:2 * H], params[2 * H:3 * H]
+        K, Fd = W1s[0].shape
+        dev = W1s[0].device
+        W1 = torch.empty(K, H * Fd, device=dev)
+        W2 = torch.empty(K, H * Fd, device=dev)
+        ar = torch.empty(H, Fd, device=dev)
+        al = torch.empty(H, Fd, device=dev)
+        outs = [W1, W2, ar, al]
+        segs = []
+        for h in range(H):
+            segs.append((W1s[h].data_ptr(), W1.data_ptr() + 4 * h * Fd, K, Fd, Fd, H * Fd,
+                         None, 0, 0.0, 0))
+            segs.append((W2s[h].data_ptr(), W2.data_ptr() + 4 * h * Fd, K, Fd, Fd, H * Fd,
+                         None, 0, 0.0, 0))
+            pa = As[h].data_ptr()
+            segs.append((pa, ar.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+            segs.append((pa + 4 * Fd, al.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+        if intra:
+            a3s = torch.empty(H, Fd, device=dev)
+            a4s = torch.empty(H, Fd, device=dev)
+            outs += [a3s, a4s]
+            for h in range(H):
+                for src, dst in ((params[3 * H + h], a3s), (params[4 * H + h], a4s)):
+                    pa = src.data_ptr()
+                    segs.append((pa, dst.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, pa + 4 * Fd, Fd,
+                                 0.0, 0))
+        _segments(segs, _stream(W1))
+        ctx.H, ctx.intra, ctx.K, ctx.Fd = H, intra, K, Fd
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, dW1, dW2, dar, dal, da3s=None, da4s=None):
+        H, K, Fd = ctx.H, ctx.K, ctx.Fd
+        dev = (dW1 if dW1 is not None else dW2).device if (dW1 is not None or dW2 is not None) \
+            else dar.device
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        dW1, dW2, dar, dal, da3s, da4s = map(c, (dW1, dW2, dar, dal, da3s, da4s))
+        ptr = lambda t, off=0: None if t is None else t.data_ptr() + off  # noqa: E731
+        gW1 = [torch.empty(K, Fd, device=dev) for _ in range(H)]
+        gW2 = [torch.empty(K, Fd, device=dev) for _ in range(H)]
+        gA = [torch.empty(2 * Fd, 1, device=dev) for _ in range(H)]
+        segs = []
+        for h in range(H):
+            o = 4 * h * Fd
+            segs.append((ptr(dW1, o), gW1[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0))
+            segs.append((ptr(dW2, o), gW2[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0))
+            segs.append((ptr(dar, o), gA[h].data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+            segs.append((ptr(dal, o), gA[h].data_ptr() + 4 * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+        g3 = g4 = []
+        if ctx.intra:
+            g3 = [torch.empty(2 * Fd, 1, device=dev) for _ in range(H)]
+            g4 = [torch.empty(2 * Fd, 1, device=dev) for _ in range(H)]
+            for h in range(H):
+                o = 4 * h * Fd
+                for d, g in ((da3s, g3[h]), (da4s, g4[h])):  # sum backward: both halves
+                    segs.append((ptr(d, o), g.data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+                    segs.append((ptr(d, o), g.data_ptr() + 4 * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+        _segments(segs, _lib.stream_handle(dev))
+        return (None, None, *gW1, *gW2, *gA, *g3, *g4)
+
+
+def pack_heads(heads, intra: bool):
+    """(W1 (K, H*F), W2, a_r (H, F), a_l (H, F)[, a3s, a4s]) of the heads' parameters, or
+    None when the one-launch packing does not apply (non-fp32 or non-contiguous
+    parameters, more than 4 heads)."""
+    H = len(heads)
+    names = ["W1", "W2", "a"] + (["a3", "a4"] if intra else [])
+    params = [getattr(h, n) for n in names for h in heads]
+    if H > 4 or any(p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda
+                    for p in params):
+        return None
+    return _PackHeads.apply(H, intra, *params)

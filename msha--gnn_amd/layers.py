@@ -208,10 +208,14 @@ def _attention_uv3(heads, s_input, r_input, graph: Graph, training):
     if graph.n_cols != m or graph.n_rows != n:
         raise ValueError(f"inter_adj is {graph.n_rows}x{graph.n_cols}, features are {n} "
                          f"sources x {m} recipients")
-    W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
-    W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
-    # Ablation.py:262-267: a[:F] scores the recipient (column) side h1, a[F:] the source h2
-    a_r, a_l = _score_halves(heads, "a").unbind(1)  # (H, F) each
+    packed = MF.pack_heads(heads, intra=False)
+    if packed is not None:  # one launch (and one in the backward)
+        W1, W2, a_r, a_l = packed
+    else:
+        W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
+        W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
+        # Ablation.py:262-267: a[:F] scores the recipient (column) side h1, a[F:] the source
+        a_r, a_l = _score_halves(heads, "a").unbind(1)  # (H, F) each
     h1, er = MF.project_scores(r_input, W1, ar=a_r, heads=H)  # (M, H*F), (M, H)
     h2, el = MF.project_scores(s_input, W2, al=a_l, heads=H)  # (N, H*F), (N, H)
     return MF.edge_attention(graph, el, er, h1.view(m, H, Fd), hs=h2.view(n, H, Fd),
@@ -247,8 +251,8 @@ class ablation3(nn.Module):  # noqa: N801  (reference class name)
 
     def forward(self, inter_adj, city_adj, province_adj, source_index):
         g = _graph(inter_adj)
-        s_input = F.dropout(self.Sfeatures, self.dropout, training=self.training)
-        r_input = F.dropout(self.Rfeatures, self.dropout, training=self.training)
+        s_input, r_input = MF.feature_dropout(self.Sfeatures, self.Rfeatures, self.dropout,
+                                              self.training)
         u, v = _attention_uv3(self.attentions, s_input, r_input, g, self.training)
         if _head_fusable(self.attentions, g, self.training):
             return _model_tail(self, g, u, v)
@@ -337,16 +341,20 @@ def _attention_uv(heads, s_input, r_input, graph: Graph, city_adj, province_adj,
         raise ValueError(f"inter_adj is {graph.n_rows}x{graph.n_cols}, features are {n} "
                          f"sources x {m} recipients")
     groups = groups_for(city_adj, province_adj, s_input.device)
-    W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
-    W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
-    # (H, 2, F) views of the score vectors: their halves by unbind / sum, whose backward
-    # is one stack / expand kernel (two slices cost a zero-fill + copy each, and an add)
-    a_r, a_l = _score_halves(heads, "a").unbind(1)
+    # e3 = lrelu(cat(h2_b, h2_b) @ a3) = lrelu(h2_b . (a3[:F] + a3[F:]))  (Ours.py:74-75)
+    packed = MF.pack_heads(heads, intra=True)
+    if packed is not None:  # one launch (and one in the backward)
+        W1, W2, a_r, a_l, a3s, a4s = packed
+    else:
+        W1 = heads[0].W1 if H == 1 else torch.cat([h.W1 for h in heads], dim=1)
+        W2 = heads[0].W2 if H == 1 else torch.cat([h.W2 for h in heads], dim=1)
+        # (H, 2, F) views of the score vectors: their halves by unbind / sum, whose
+        # backward is one stack / expand kernel
+        a_r, a_l = _score_halves(heads, "a").unbind(1)
+        a3s = _score_halves(heads, "a3").sum(1)
+        a4s = _score_halves(heads, "a4").sum(1)
     h1, er = MF.project_scores(r_input, W1, ar=a_r, heads=H)
     h2, el = MF.project_scores(s_input, W2, al=a_l, heads=H)
-    # e3 = lrelu(cat(h2_b, h2_b) @ a3) = lrelu(h2_b . (a3[:F] + a3[F:]))  (Ours.py:74-75)
-    a3s = _score_halves(heads, "a3").sum(1)
-    a4s = _score_halves(heads, "a4").sum(1)
     src = torch.as_tensor(source_index, device=s_input.device)
     u, v, attd, bstat = MF.ours_attention(graph, groups, src, el, er, h1.view(m, H, Fd),
                                           h2.view(n, H, Fd), a3s, a4s, p=heads[0].dropout,
@@ -414,8 +422,8 @@ class Ours(nn.Module):
     def forward(self, inter_adj, city_adj, province_adj, source_index, record=False,
                 Coeff12=None, Coeff3=None, Coeff4=None):
         g = _graph(inter_adj)
-        s_input = F.dropout(self.Sfeatures, self.dropout, training=self.training)
-        r_input = F.dropout(self.Rfeatures, self.dropout, training=self.training)
+        s_input, r_input = MF.feature_dropout(self.Sfeatures, self.Rfeatures, self.dropout,
+                                              self.training)
         u, v = _attention_uv(self.attentions, s_input, r_input, g, city_adj, province_adj,
                              source_index, self.training, record, Coeff12, Coeff3, Coeff4)
         if _head_fusable(self.attentions, g, self.training):

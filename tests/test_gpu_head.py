@@ -199,3 +199,54 @@ def test_models_use_the_fused_head(cuda, msha):
         assert Probe.calls == 2
     finally:
         layers.MF.model_head = orig
+
+
+@pytest.mark.parametrize("intra", [False, True])
+def test_pack_heads_matches_cat_and_stack(cuda, msha, intra):
+    """One-launch parameter packing == torch.cat / stack / sum of the heads' parameters,
+    and its backward == autograd's gradients of that torch formulation (bit-exact: copies
+    and one add)."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd import layers
+
+    torch.manual_seed(0)
+    cls = layers.OursLayer if intra else layers.OursLayer3
+    heads = [cls(128, 64, 0.0).to(cuda) for _ in range(2)]
+    packed = MF.pack_heads(heads, intra)
+    ref = [torch.cat([h.W1 for h in heads], 1), torch.cat([h.W2 for h in heads], 1)]
+    halves = layers._score_halves(heads, "a")
+    ref += [halves[:, 0], halves[:, 1]]
+    if intra:
+        ref += [layers._score_halves(heads, "a3").sum(1), layers._score_halves(heads, "a4").sum(1)]
+    assert len(packed) == len(ref)
+    gen = torch.Generator(device=cuda).manual_seed(1)
+    ws = [torch.randn(r.shape, device=cuda, generator=gen) for r in ref]
+    for got, want in zip(packed, ref):
+        assert torch.equal(got, want)
+    params = [p for h in heads for p in h.parameters()]
+    g_ref = torch.autograd.grad(sum((r * w).sum() for r, w in zip(ref, ws)), params,
+                                allow_unused=True)
+    g_got = torch.autograd.grad(sum((r * w).sum() for r, w in zip(packed, ws)), params,
+                                allow_unused=True)
+    for a, b in zip(g_got, g_ref):
+        assert (a is None) == (b is None)
+        if a is not None:
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_feature_dropout_masks_and_grad(cuda, msha):
+    """Both feature tables dropped in one launch with the Philox masks
+    (msha_dropout_keep_mask of the same seed), gradients masked the same way."""
+    from msha_gnn_amd import functional as MF
+
+    gen = torch.Generator(device=cuda).manual_seed(2)
+    S = torch.rand(1000, 128, device=cuda, generator=gen).requires_grad_(True)
+    R = torch.rand(32, 128, device=cuda, generator=gen).requires_grad_(True)
+    So, Ro = MF._FeatureDropout.apply(S, R, 0.5, 77, 78)
+    kS = MF.dropout_keep_mask(S.numel(), 0.5, 77, cuda).view_as(S).bool()
+    kR = MF.dropout_keep_mask(R.numel(), 0.5, 78, cuda).view_as(R).bool()
+    assert torch.equal(So, torch.where(kS, S * 2.0, torch.zeros_like(S)))
+    assert torch.equal(Ro, torch.where(kR, R * 2.0, torch.zeros_like(R)))
+    (So.sum() + 3 * Ro.sum()).backward()
+    assert torch.equal(S.grad, kS.float() * 2.0)
+    assert torch.equal(R.grad, kR.float() * 6.0)
