@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 5
+#define MSHA_ABI_VERSION 6
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -450,7 +450,8 @@ MSHA_API int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, in
  * stats (4, H*F) fp32 out: u mean, u invstd, v mean, v invstd (the backward's input).
  *
  * Backward (training statistics): given dout (N, M), writes du (N, H, F), dv (M, H, F),
- * dW (H*M, M) fp32 and the per-head BatchNorm weight / bias gradients.  Rows whose dout
+ * dW (H*M, M) fp32 and the per-head BatchNorm weight / bias gradients, and zeroes
+ * dzero[0 .. n_zero) (nullable: the out_att score vector's gradient, which is exactly 0).  Rows whose dout
  * is all zero (train.py's nll on out[source_index] touches 64 rows) contribute only
  * through the BatchNorm batch terms and cost one row read.  Deterministic: per-wave
  * partials over ascending row ranges, added in wave order.
@@ -483,8 +484,8 @@ MSHA_API int msha_head_fwd(const msha_graph* g, const msha_head_params* hp, int3
 MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
                            const void* u, const void* v, const float* W, float p_x,
                            uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
-                           const void* dout, void* du, void* dv, float* dW, void* ws,
-                           size_t ws_bytes, msha_stream_t stream);
+                           const void* dout, void* du, void* dv, float* dW, float* dzero,
+                           int64_t n_zero, void* ws, size_t ws_bytes, msha_stream_t stream);
 
 
 /* ---- Batched segment copies: the models' per-head parameter packing (Ablation.py:262-267,
@@ -492,8 +493,10 @@ MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int3
  * their gradients back) and the feature dropout of Sfeatures / Rfeatures
  * (Ablation.py:296-297, Ours.py:161-162) in one launch forward and one backward.
  * For every segment:  dst[r*ldd + c] = (a[r*lda + c] (+ b[r*ldb + c])) * keep(r*cols + c)
- * for r < rows, c < cols; a NULL `a` writes zeros; keep is the Philox dropout factor
- * (0 or 1/(1-p)) keyed on (seed, element, offset) when p > 0, else 1. */
+ * for r < rows, c < cols; a NULL `a` writes zeros; keep is the dropout factor (0 or
+ * 1/(1-p)) when p > 0, else 1: element e = r*cols + c keeps iff word e % 4 of the
+ * Philox4x32-10 block (seed; counter {e / 4, offset}) is >= p * 2^32 (one generator call
+ * per four elements; msha_dropout_keep_mask4 writes the same mask). */
 #define MSHA_MAX_SEGMENTS 32
 typedef struct msha_segment {
   const float* a;
@@ -504,6 +507,26 @@ typedef struct msha_segment {
   uint64_t seed, offset;
 } msha_segment;
 MSHA_API int msha_segments(int32_t n, const msha_segment* segs, msha_stream_t stream);
+MSHA_API int msha_dropout_keep_mask4(uint64_t seed, uint64_t offset, int64_t n, float p,
+                                     uint8_t* keep, msha_stream_t stream);
+
+
+/* ---- Projection of a small node table in one workgroup (the recipient side: R15 has 32
+ * recipients; Ablation.py:262, :266-267): h = X @ W (M x N, N = heads*feat) with optional
+ * per-head score halves el = h . al, er = h . ar; backward with D = dh + d_el (x) al +
+ * d_er (x) ar: dX = D @ W^T, dW = X^T @ D, dal / dar[h, f] = sum_m d_el / d_er[m, h]
+ * h[m, h*feat + f] -- one launch each (any output pointer may be NULL).  fp32, M <= 256,
+ * K <= 128, heads*feat <= 128 (msha_project_small_supported). */
+MSHA_API int msha_project_small_supported(int64_t M, int64_t K, int32_t heads, int32_t feat);
+MSHA_API int msha_project_small(int64_t M, int64_t K, int32_t heads, int32_t feat,
+                                const float* X, const float* W, const float* al,
+                                const float* ar, float* h, float* el, float* er,
+                                msha_stream_t stream);
+MSHA_API int msha_project_small_bwd(int64_t M, int64_t K, int32_t heads, int32_t feat,
+                                    const float* X, const float* W, const float* al,
+                                    const float* ar, const float* h, const float* dh,
+                                    const float* d_el, const float* d_er, float* dX, float* dW,
+                                    float* dal, float* dar, msha_stream_t stream);
 
 #ifdef __cplusplus
 }

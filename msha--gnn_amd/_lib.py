@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 5  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 6  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -137,11 +137,16 @@ SIGNATURES = {
     "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, I32, F32, F32,
                                       U64, U64, P, P, P, P, P, P, P, SZ, P]),
     "msha_segments": (C.c_int, [I32, P, P]),
+    "msha_project_small_supported": (C.c_int, [I64, I64, I32, I32]),
+    "msha_project_small": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
+    "msha_project_small_bwd": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, P, P, P,
+                                         P]),
+    "msha_dropout_keep_mask4": (C.c_int, [U64, U64, I64, F32, P, P]),
     "msha_head_supported": (C.c_int, [I64, I32, I32]),
     "msha_head_workspace_size": (SZ, [GP, I32, I32]),
     "msha_head_fwd": (C.c_int, [GP, HPP, I32, P, P, P, I32, F32, U64, F32, U64, P, P, P, SZ, P]),
-    "msha_head_bwd": (C.c_int, [GP, HPP, I32, P, P, P, F32, U64, F32, U64, P, P, P, P, P, P, SZ,
-                                P]),
+    "msha_head_bwd": (C.c_int, [GP, HPP, I32, P, P, P, F32, U64, F32, U64, P, P, P, P, P, P, I64,
+                                P, SZ, P]),
 }
 
 _lib = None

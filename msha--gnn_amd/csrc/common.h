@@ -264,6 +264,26 @@ __host__ __device__ __forceinline__ uint32_t philox_x(uint64_t seed, uint64_t of
   return c0;
 }
 
+// all four words of the same Philox4x32-10 block: word t of block q keys element 4q + t
+// of the flat-table dropout masks (msha_segments), one generator call per 4 elements
+__host__ __device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_t q) {
+  uint32_t c0 = (uint32_t)q, c1 = (uint32_t)(q >> 32);
+  uint32_t c2 = (uint32_t)offset, c3 = (uint32_t)(offset >> 32);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
 struct Dropout {
   uint64_t seed, offset;
   uint32_t threshold;  // drop when philox < threshold

@@ -593,7 +593,11 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
 // reduced[t] = sum over flagged waves (ascending) of part[w][t]; dW and the u-side
 // BatchNorm weight / bias gradients written out
 __global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBwdWs ws, int nw,
-                                                              float* __restrict__ dW) {
+                                                              float* __restrict__ dW,
+                                                              float* __restrict__ dzero,
+                                                              int64_t n_zero) {
+  if (blockIdx.x == 0)  // the out_att score vector's (exactly zero) gradient
+    for (int64_t e = threadIdx.x; e < n_zero; e += blockDim.x) dzero[e] = 0.f;
   __shared__ int list[kHeadBwdWaves];
   __shared__ int cnt[257];
   // ordered compaction of the wave flags (each thread a contiguous slice of them)
@@ -900,8 +904,8 @@ extern "C" int msha_head_fwd(const msha_graph* g, const msha_head_params* hp, in
 extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
                              const void* u, const void* v, const float* W, float p_x,
                              uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
-                             const void* dout, void* du, void* dv, float* dW, void* ws,
-                             size_t ws_bytes, msha_stream_t stream) {
+                             const void* dout, void* du, void* dv, float* dW, float* dzero,
+                             int64_t n_zero, void* ws, size_t ws_bytes, msha_stream_t stream) {
   if (int rc = head_check(g, hp, dtype)) return rc;
   MSHA_ARG_CHECK(u && v && W && stats && dout && du && dv && dW, "head_bwd: null pointer");
   const HeadLayout L = head_layout(g->n_rows, (int)g->n_cols, hp->heads, hp->feat);
@@ -934,7 +938,7 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
 #undef HEAD_BWD
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
   hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 255) / 256)), dim3(256), 0, s, a,
-                     w, nw, dW);
+                     w, nw, dW, dzero, dzero != nullptr ? n_zero : 0);
   const dim3 ga(1 + grid_for(a.N * a.HF / 4, 256 * 4, 1024));
   if (bf)
     hipLaunchKernelGGL(head_bwd_apply_kernel<bf16_t>, ga, dim3(256), 0, s, a, (const bf16_t*)u,

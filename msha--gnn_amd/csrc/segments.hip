@@ -10,6 +10,11 @@ struct SegBatch {
   const uint64_t* ctr;  // device replay counter (dropout offsets)
 };
 
+__device__ __forceinline__ float keep4(const Dropout& d, uint64_t e, uint4 w) {
+  const uint32_t x = (e & 3) == 0 ? w.x : (e & 3) == 1 ? w.y : (e & 3) == 2 ? w.z : w.w;
+  return x >= d.threshold ? d.scale : 0.f;
+}
+
 __global__ void __launch_bounds__(256) segments_kernel(SegBatch sb) {
   const msha_segment& g = sb.s[blockIdx.y];
   const int64_t total = g.rows * g.cols;
@@ -23,16 +28,53 @@ __global__ void __launch_bounds__(256) segments_kernel(SegBatch sb) {
     d.threshold = g.p >= 1.f ? 0xFFFFFFFFu : (uint32_t)(t > 4294967295.0 ? 4294967295.0 : t);
     d.scale = g.p < 1.f ? (float)(1.0 / (1.0 - (double)g.p)) : 0.f;
   }
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  const uint64_t off = d.active ? dropout_offset(d, d.offset) : 0;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool flat = g.lda == g.cols && g.ldd == g.cols && (g.b == nullptr || g.ldb == g.cols) &&
+                    total % 4 == 0 &&
+                    (((uintptr_t)g.a | (uintptr_t)g.b | (uintptr_t)g.dst) & 15) == 0;
+  if (flat) {  // contiguous table: 4 elements per thread, one generator block per 4
+    const float4* a4 = reinterpret_cast<const float4*>(g.a);
+    const float4* b4 = reinterpret_cast<const float4*>(g.b);
+    float4* d4 = reinterpret_cast<float4*>(g.dst);
+    for (int64_t q = tid; q < total / 4; q += nthr) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (g.a != nullptr) {
+        v = a4[q];
+        if (g.b != nullptr) {
+          const float4 w = b4[q];
+          v = make_float4(v.x + w.x, v.y + w.y, v.z + w.z, v.w + w.w);
+        }
+      }
+      if (d.active) {
+        const uint4 w = philox4(d.seed, off, (uint64_t)q);
+        v = make_float4(v.x * (w.x >= d.threshold ? d.scale : 0.f),
+                        v.y * (w.y >= d.threshold ? d.scale : 0.f),
+                        v.z * (w.z >= d.threshold ? d.scale : 0.f),
+                        v.w * (w.w >= d.threshold ? d.scale : 0.f));
+      }
+      d4[q] = v;
+    }
+    return;
+  }
+  for (int64_t e = tid; e < total; e += nthr) {
     const int64_t r = e / g.cols, c = e - r * g.cols;
     float v = 0.f;
     if (g.a != nullptr) {
       v = g.a[r * g.lda + c];
       if (g.b != nullptr) v += g.b[r * g.ldb + c];
     }
-    g.dst[r * g.ldd + c] = v * dropout_factor(d, (uint64_t)e);
+    if (d.active) v *= keep4(d, (uint64_t)e, philox4(d.seed, off, (uint64_t)e >> 2));
+    g.dst[r * g.ldd + c] = v;
   }
+}
+
+__global__ void __launch_bounds__(256) keep_mask4_kernel(Dropout d, int64_t n, uint8_t* keep) {
+  const uint64_t off = dropout_offset(d, d.offset);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x)
+    keep[e] = keep4(d, (uint64_t)e, philox4(d.seed, off, (uint64_t)e >> 2)) != 0.f ? 1 : 0;
 }
 
 }  // namespace msha
@@ -57,4 +99,16 @@ extern "C" int msha_segments(int32_t n, const msha_segment* segs, msha_stream_t 
   const dim3 grid(grid_for(mx, 256 * 4, 1024), n);
   hipLaunchKernelGGL(segments_kernel, grid, dim3(256), 0, s, sb);
   return check_launch("segments");
+}
+
+extern "C" int msha_dropout_keep_mask4(uint64_t seed, uint64_t offset, int64_t n, float p,
+                                       uint8_t* keep, msha_stream_t stream) {
+  MSHA_ARG_CHECK(n >= 0 && (n == 0 || keep != nullptr), "dropout_keep_mask4: bad buffer");
+  MSHA_ARG_CHECK(p >= 0.f && p <= 1.f, "dropout_keep_mask4: p must be in [0, 1]");
+  if (n == 0) return MSHA_OK;
+  Dropout d = make_dropout(p, seed, offset, (hipStream_t)stream);
+  d.active = true;
+  hipLaunchKernelGGL(keep_mask4_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, d, n, keep);
+  return check_launch("dropout_keep_mask4");
 }

@@ -285,10 +285,13 @@ def gal(graph: Graph, h, p: float = 0.0, training: bool = False, seed: int | Non
     return _GAL.apply(h, zero_grad_of, graph, p, seed)
 
 
-def dropout_keep_mask(n: int, p: float, seed: int, device, offset: int = 0) -> torch.Tensor:
+def dropout_keep_mask(n: int, p: float, seed: int, device, offset: int = 0,
+                      flat4: bool = False) -> torch.Tensor:
+    """The kernels' Philox keep mask of n elements (uint8); flat4: the four-words-per-call
+    mask of the flat-table dropout (msha_segments, feature dropout)."""
     keep = torch.empty(n, dtype=torch.uint8, device=device)
-    _lib.call("msha_dropout_keep_mask", seed, offset, n, p, keep.data_ptr(),
-              _lib.stream_handle(device))
+    _lib.call("msha_dropout_keep_mask4" if flat4 else "msha_dropout_keep_mask", seed, offset, n,
+              p, keep.data_ptr(), _lib.stream_handle(device))
     return keep
 
 
@@ -432,7 +435,11 @@ class _ProjectScores(torch.autograd.Function):
         h = torch.empty(M, heads * feat, device=dev, dtype=dt)
         el = torch.empty(M, heads, device=dev, dtype=torch.float32) if al is not None else None
         er = torch.empty(M, heads, device=dev, dtype=torch.float32) if ar is not None else None
-        fn = "msha_project_scores_bf16" if dt == BF16 else "msha_project_scores"
+        # a small table (the 32 recipients of R15): one single-workgroup launch each way
+        ctx.small = dt == torch.float32 and bool(
+            _lib.load().msha_project_small_supported(M, K, heads, feat))
+        fn = ("msha_project_small" if ctx.small else
+              "msha_project_scores_bf16" if dt == BF16 else "msha_project_scores")
         _lib.call(fn, M, K, heads, feat, X.data_ptr(), W.data_ptr(), _lib.ptr(al), _lib.ptr(ar),
                   h.data_ptr(), _lib.ptr(el), _lib.ptr(er), _stream(X))
         ctx.heads, ctx.feat = heads, feat
@@ -456,6 +463,20 @@ class _ProjectScores(torch.autograd.Function):
         it = iter(dscores)
         d_el = next(it) if al is not None else None
         d_er = next(it) if ar is not None else None
+        if ctx.small:
+            d_el, d_er = _f32c(d_el), _f32c(d_er)
+            dh = None if dh is None else _tc(dh, dt)
+            dX = torch.empty_like(X) if ctx.needs_input_grad[0] else None
+            dW = torch.empty_like(W) if ctx.needs_input_grad[1] else None
+            dal = torch.empty(H, Fd, device=dev) if d_el is not None and ctx.needs_input_grad[2] \
+                else None
+            dar = torch.empty(H, Fd, device=dev) if d_er is not None and ctx.needs_input_grad[3] \
+                else None
+            _lib.call("msha_project_small_bwd", M, X.shape[1], H, Fd, X.data_ptr(), W.data_ptr(),
+                      _lib.ptr(al), _lib.ptr(ar), h.data_ptr(), _lib.ptr(dh), _lib.ptr(d_el),
+                      _lib.ptr(d_er), _lib.ptr(dX), _lib.ptr(dW), _lib.ptr(dal), _lib.ptr(dar), s)
+            return (dX, dW, None if dal is None else dal.reshape(al.shape).to(aldt),
+                    None if dar is None else dar.reshape(ar.shape).to(ardt), None, None)
         dh = torch.zeros_like(h) if dh is None else _tc(dh, dt)
         terms = [(d, a) for d, a in ((d_el, al), (d_er, ar)) if d is not None]
         dX = dW = dal = dar = None
@@ -829,6 +850,7 @@ class _OursAttention(torch.autograd.Function):
                               u_lo if u_lo is not None else el.new_empty(0))
         # post-dropout inter attention and batch statistics: outputs for record mode
         ctx.mark_non_differentiable(attd, bstat)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for attd / bstat
         return u, v, attd, bstat
 
     @staticmethod
@@ -999,14 +1021,15 @@ class _ModelHead(torch.autograd.Function):
         g = graph.desc
         wsb = int(_lib.load().msha_head_workspace_size(g, H, F))
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        shape, adt, adev = ctx.a_meta
+        da = torch.empty(shape, dtype=torch.float32, device=adev)  # zeroed by the reduce
         _lib.call("msha_head_bwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
                   W32.data_ptr(), px, sx, pa, sa, stats.data_ptr(), dout.data_ptr(),
-                  du.data_ptr(), dv.data_ptr(), dW.data_ptr(), ws.data_ptr(), ws.numel(),
-                  _stream(u))
-        shape, adt, adev = ctx.a_meta
+                  du.data_ptr(), dv.data_ptr(), dW.data_ptr(), da.data_ptr(), da.numel(),
+                  ws.data_ptr(), ws.numel(), _stream(u))
         grads = [dp[k, h].to(ctx.pdtypes[k * H + h]) for k in range(4) for h in range(H)]
         return (du, dv, dW.to(ctx.wdtype), None, None, None, None, None, None, None, None, None,
-                None, *grads, torch.zeros(shape, dtype=adt, device=adev))
+                None, *grads, da.to(adt))
 
 
 def C_byref(x):

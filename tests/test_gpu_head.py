@@ -243,10 +243,44 @@ def test_feature_dropout_masks_and_grad(cuda, msha):
     S = torch.rand(1000, 128, device=cuda, generator=gen).requires_grad_(True)
     R = torch.rand(32, 128, device=cuda, generator=gen).requires_grad_(True)
     So, Ro = MF._FeatureDropout.apply(S, R, 0.5, 77, 78)
-    kS = MF.dropout_keep_mask(S.numel(), 0.5, 77, cuda).view_as(S).bool()
-    kR = MF.dropout_keep_mask(R.numel(), 0.5, 78, cuda).view_as(R).bool()
+    kS = MF.dropout_keep_mask(S.numel(), 0.5, 77, cuda, flat4=True).view_as(S).bool()
+    kR = MF.dropout_keep_mask(R.numel(), 0.5, 78, cuda, flat4=True).view_as(R).bool()
+    assert 0.45 < kS.float().mean() < 0.55
+    # word 0 of block q is the per-element generator at index q
+    assert torch.equal(kS.view(-1)[::4], MF.dropout_keep_mask(S.numel() // 4, 0.5, 77, cuda)
+                       .bool())
     assert torch.equal(So, torch.where(kS, S * 2.0, torch.zeros_like(S)))
     assert torch.equal(Ro, torch.where(kR, R * 2.0, torch.zeros_like(R)))
     (So.sum() + 3 * Ro.sum()).backward()
     assert torch.equal(S.grad, kS.float() * 2.0)
     assert torch.equal(R.grad, kR.float() * 6.0)
+
+
+@pytest.mark.parametrize("M,K,H,F_", [(32, 128, 2, 64), (200, 64, 1, 128), (7, 128, 8, 16)])
+def test_project_small_vs_fp64(cuda, msha, M, K, H, F_):
+    """The recipient-side projection (msha_project_small / _bwd, one launch each way):
+    h, el, er and every gradient (dX, dW, dal, dar) vs fp64 torch within 1e-5."""
+    from msha_gnn_amd import functional as MF
+
+    assert msha._lib.load().msha_project_small_supported(M, K, H, F_) == 1
+    gen = torch.Generator().manual_seed(M)
+    X = torch.randn(M, K, generator=gen)
+    W = torch.randn(K, H * F_, generator=gen) / K ** 0.5
+    al = torch.randn(H, F_, generator=gen)
+    ar = torch.randn(H, F_, generator=gen)
+    dh = torch.randn(M, H * F_, generator=gen)
+    dl = torch.randn(M, H, generator=gen)
+    dr = torch.randn(M, H, generator=gen)
+    ts = [t.to(cuda).requires_grad_(True) for t in (X, W, al, ar)]
+    h, el, er = MF.project_scores(*ts, heads=H)
+    torch.autograd.backward([h, el, er], [dh.to(cuda), dl.to(cuda), dr.to(cuda)])
+    r = [t.double().requires_grad_(True) for t in (X, W, al, ar)]
+    h64 = r[0] @ r[1]
+    hv = h64.view(M, H, F_)
+    el64 = (hv * r[2]).sum(-1)
+    er64 = (hv * r[3]).sum(-1)
+    torch.autograd.backward([h64, el64, er64], [dh.double(), dl.double(), dr.double()])
+    for got, want in ((h, h64), (el, el64), (er, er64)):
+        tol_close(got.detach().cpu().numpy(), want.detach().numpy(), 1e-5, 1e-5)
+    for got, want in zip(ts, r):
+        tol_close(got.grad.cpu().numpy(), want.grad.numpy(), 1e-5, 1e-5)
