@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 6
+#define MSHA_ABI_VERSION 7
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -444,8 +444,8 @@ MSHA_API int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, in
  * the whole v side, one row pass).  u (N, H, F) and v (M, H, F) are the attention
  * aggregates (dtype storage, fp32 arithmetic), W the out_att weight (H*M, M) fp32,
  * out (N, M) log-probabilities (dtype).  training: batch statistics, running statistics
- * updated as nn.BatchNorm1d (momentum, unbiased variance; num_batches_tracked is the
- * caller's); otherwise running statistics and no dropout.  Dropout: Philox keyed on
+ * updated as nn.BatchNorm1d (momentum, unbiased variance; the num_batches_tracked
+ * counters given are advanced on the device); otherwise running statistics and no dropout.  Dropout: Philox keyed on
  * (seed_x, element i*H*M + k) and (seed_att, element i*M + j), offset 0.
  * stats (4, H*F) fp32 out: u mean, u invstd, v mean, v invstd (the backward's input).
  *
@@ -473,6 +473,7 @@ typedef struct msha_head_params {
   float* du_bias[MSHA_HEAD_MAX_HEADS];
   float* dv_weight[MSHA_HEAD_MAX_HEADS];
   float* dv_bias[MSHA_HEAD_MAX_HEADS];
+  int64_t* num_batches_tracked[2 * MSHA_HEAD_MAX_HEADS]; /* nullable; +1 per training forward */
 } msha_head_params;
 MSHA_API int msha_head_supported(int64_t n_cols, int32_t heads, int32_t feat);
 MSHA_API size_t msha_head_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 6  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 7  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -62,7 +62,8 @@ class MshaHeadParams(C.Structure):
         (name, C.c_void_p * HEAD_MAX_HEADS)
         for name in ("u_weight", "u_bias", "u_running_mean", "u_running_var", "v_weight",
                      "v_bias", "v_running_mean", "v_running_var", "du_weight", "du_bias",
-                     "dv_weight", "dv_bias")]
+                     "dv_weight", "dv_bias")] + [
+        ("num_batches_tracked", C.c_void_p * (2 * HEAD_MAX_HEADS))]
 
 
 HPP = C.POINTER(MshaHeadParams)

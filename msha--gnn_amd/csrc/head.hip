@@ -28,8 +28,8 @@
 namespace msha {
 
 constexpr int kHeadThreads = 256;  // forward row pass: 4 waves per block
-constexpr int kHeadBwdWaves = 1024;
-constexpr int kHeadRowsPerWave = 64;
+constexpr int kHeadBwdWaves = 4096;
+constexpr int kHeadRowsPerWave = 16;
 constexpr int kHeadVStage = 4096;  // floats of v staged in LDS by the v-side blocks
 
 struct HeadArgs {
@@ -50,6 +50,7 @@ struct HeadArgs {
   float* dub[MSHA_HEAD_MAX_HEADS];
   float* dvw[MSHA_HEAD_MAX_HEADS];
   float* dvb[MSHA_HEAD_MAX_HEADS];
+  int64_t* nbt[2 * MSHA_HEAD_MAX_HEADS];
   const float* W;  // (KX, M)
   Dropout dx, dg;
   float* stats;    // [u mean | u invstd | v mean | v invstd] (HF each) | vo_t (HF x M)
@@ -115,6 +116,17 @@ __device__ __forceinline__ void st4(T* p, float4 v) {
   }
 }
 
+// v of lane ^ o for the row reductions; offset 4 as two DPP moves (row_half_mirror gives
+// lane ^ 7 within 8 lanes, quad_perm [3,2,1,0] then ^ 3) instead of an LDS permute
+__device__ __forceinline__ float xor_red(float v, int o) {
+  if (o == 4) {
+    const int x = __builtin_bit_cast(int, v);
+    const int m = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true);
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, true));
+  }
+  return xor_shfl(v, o);
+}
+
 __device__ __forceinline__ float elu1(float z) { return z > 0.f ? z : expm1f(z); }
 __device__ __forceinline__ float delu1(float z) { return z > 0.f ? 1.f : __expf(z); }
 
@@ -123,14 +135,21 @@ __device__ __forceinline__ float pw(const float* const* p, int c, int F, float d
   return q != nullptr ? q[c % F] : dflt;
 }
 
-// ---- finalize: u channels (one wave each) from the partials; the last block: v side
+// ---- finalize: u channels (one wave each) from the partials (blocks [0, nub)); the v
+// side (blocks [nub, ...)): 32 channels per block, 8 lanes per channel splitting the M
+// rows (Welford per lane, Chan-combined over the 8 lanes in a fixed xor tree), then
+// v_out = lrelu(bn1(v)) transposed into stats; block 0 thread 0 advances the BatchNorms'
+// num_batches_tracked (training)
 template <typename T>
 __global__ void __launch_bounds__(256) head_prep_kernel(HeadArgs a, int training, int nbu,
                                                         const Wf* __restrict__ part,
-                                                        const T* __restrict__ v) {
+                                                        const T* __restrict__ v, int nub) {
   const int HF = a.HF, F = a.F, M = a.M;
   float* st = a.stats;
-  if (blockIdx.x + 1 < gridDim.x) {
+  if (training && blockIdx.x == 0 && threadIdx.x == 0)
+    for (int k = 0; k < 2 * MSHA_HEAD_MAX_HEADS; ++k)
+      if (a.nbt[k] != nullptr) *a.nbt[k] += 1;
+  if ((int)blockIdx.x < nub) {
     const int c = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const int lane = threadIdx.x & 63;
     if (c >= HF) return;
@@ -160,29 +179,27 @@ __global__ void __launch_bounds__(256) head_prep_kernel(HeadArgs a, int training
     }
     return;
   }
-  // v side: M rows (<= 256) x HF channels, one thread per channel, rows in order; v
-  // staged in LDS first when it fits (coalesced loads, all in flight)
-  __shared__ float vs[kHeadVStage];
-  const bool staged = M * HF <= kHeadVStage;
-  if (staged) {
-    lds_copy(vs, v, M * HF);
-    __syncthreads();
-  }
-  auto vat = [&](int j, int c) { return staged ? vs[j * HF + c] : to_f32(v[(int64_t)j * HF + c]); };
-  for (int c = threadIdx.x; c < HF; c += blockDim.x) {
-    float mean, inv;
-    if (training) {
-      Wf w{0.f, 0.f, 0.f};
-      for (int j = 0; j < M; ++j) {
-        const float x = vat(j, c);
+  const int c = ((int)blockIdx.x - nub) * 32 + (threadIdx.x >> 3);
+  const int g = threadIdx.x & 7;
+  const bool live = c < HF;
+  float mean = 0.f, inv = 1.f;
+  if (training) {
+    Wf w{0.f, 0.f, 0.f};
+    if (live)
+      for (int j = g; j < M; j += 8) {
+        const float x = to_f32(v[(int64_t)j * HF + c]);
         w.n += 1.f;
         const float d = x - w.mean;
         w.mean += d / w.n;
         w.m2 += d * (x - w.mean);
       }
-      const float var = w.n > 0.f ? w.m2 / w.n : 0.f;
-      mean = w.mean;
-      inv = rsqrtf(var + a.eps);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1)
+      w = wf_combine(w, Wf{__shfl_xor(w.n, o), __shfl_xor(w.mean, o), __shfl_xor(w.m2, o)});
+    const float var = w.n > 0.f ? w.m2 / w.n : 0.f;
+    mean = w.mean;
+    inv = rsqrtf(var + a.eps);
+    if (live && g == 0) {
       float* rm = a.vrm[c / F];
       if (rm != nullptr) {
         float* rv = a.vrv[c / F];
@@ -190,18 +207,21 @@ __global__ void __launch_bounds__(256) head_prep_kernel(HeadArgs a, int training
         rm[c % F] = (1.f - a.momentum) * rm[c % F] + a.momentum * w.mean;
         rv[c % F] = (1.f - a.momentum) * rv[c % F] + a.momentum * unb;
       }
-    } else {
-      mean = pw(a.vrm, c, F, 0.f);
-      inv = rsqrtf(pw(a.vrv, c, F, 1.f) + a.eps);
     }
+  } else if (live) {
+    mean = pw(a.vrm, c, F, 0.f);
+    inv = rsqrtf(pw(a.vrv, c, F, 1.f) + a.eps);
+  }
+  if (!live) return;
+  if (g == 0) {
     st[2 * HF + c] = mean;
     st[3 * HF + c] = inv;
-    const float g = pw(a.vw, c, F, 1.f), b = pw(a.vb, c, F, 0.f);
-    float* vo = st + 4 * HF;
-    for (int j = 0; j < M; ++j) {
-      const float z = fmaf(g * inv, vat(j, c) - mean, b);
-      vo[(int64_t)c * M + j] = z > 0.f ? z : z * a.slope;  // vo_t[c][j]
-    }
+  }
+  const float gm = pw(a.vw, c, F, 1.f), bt = pw(a.vb, c, F, 0.f);
+  float* vo = st + 4 * HF;
+  for (int j = g; j < M; j += 8) {
+    const float z = fmaf(gm * inv, to_f32(v[(int64_t)j * HF + c]) - mean, bt);
+    vo[(int64_t)c * M + j] = z > 0.f ? z : z * a.slope;  // vo_t[c][j]
   }
 }
 
@@ -447,14 +467,180 @@ __global__ void __launch_bounds__(kHeadThreads) head_fwd_reg_kernel(HeadArgs a,
         y = elu1(elu1(at * hg));
       }
       float mx = y;
-      for (int o = 1; o < 64 / rpt; o <<= 1) mx = fmaxf(mx, xor_shfl(mx, o));
+      for (int o = 1; o < 64 / rpt; o <<= 1) mx = fmaxf(mx, xor_red(mx, o));
       float sm = act ? __expf(y - mx) : 0.f;
-      for (int o = 1; o < 64 / rpt; o <<= 1) sm += xor_shfl(sm, o);
+      for (int o = 1; o < 64 / rpt; o <<= 1) sm += xor_red(sm, o);
       const float lse = mx + __logf(sm);
       if (act) out[(r0 + r) * M + jl] = from_f32<T>(y - lse);
     }
     wave_sync();  // the batch's LDS reads done before the next batch's writes
   }
+}
+
+// Forward row pass on the matrix cores for the R15 shape family (H heads x F, M = 16 MB
+// recipients): a wave takes 16 rows; both products run transposed so the first one's
+// accumulators ARE the second one's B operand (no LDS round trip between them):
+//   C_h^T (M x 16) = v_out_h (M x F) @ uo_h^T (F x 16)    A = v_out_h: registers, B = uo (LDS)
+//   x^T = dropout(elu(C^T))                                in the accumulators, k = h M + j
+//   hg^T (M x 16) = W^T (M x KX) @ x^T (KX x 16)           A = W^T: registers
+// v_mfma_f32_16x16x4_f32 (exact fp32).  The second product walks k in the order the first
+// one's accumulators hold it (step (c, q): lane group g supplies k = 16 c + 4 g + q), with
+// W^T's A operand loaded in the same order.  Each lane then holds 8 of its row's M = 32
+// logits (hg^T rows 16 jb + 4 g + q): GAL scale, elu, elu and the row's log_softmax
+// (max / sum over its 8 values, then across the 4 lane groups by xor 16 / 32).
+template <typename T, int H, int F, int M>
+__global__ void __launch_bounds__(kHeadThreads) head_fwd_mfma_kernel(HeadArgs a,
+                                                                     const T* __restrict__ u,
+                                                                     T* __restrict__ out) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int HF = H * F, KX = H * M, MB = M / 16, KB = KX / 16, R = 16;
+  constexpr int UP = HF + 1;  // padded uo pitch: lanes r16 read rows UP floats apart
+  static_assert(M % 16 == 0 && F % 4 == 0, "head mfma shape");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* g_ = smem;
+  float* b_ = g_ + HF;
+  float* mu = b_ + HF;
+  float* su = mu + HF;
+  for (int c = threadIdx.x; c < HF; c += blockDim.x) {
+    g_[c] = pw(a.uw, c, F, 1.f);
+    b_[c] = pw(a.ub, c, F, 0.f);
+    mu[c] = a.stats[c];
+    su[c] = a.stats[HF + c];
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4, r16 = lane & 15;
+  float* uo = su + HF + w * (R * UP + R * M + 32);
+  int* fl = reinterpret_cast<int*>(uo + R * UP);  // R x M row masks
+  int* rps = fl + R * M;                            // R + 1 rowptr entries
+  // A operands (constant): v_out_h rows 16 jb + r16 at f = 4 s + g; W rows k = 16 c + 4 g + q
+  // at column 16 jb + r16
+  const float* vo = a.stats + 4 * HF;
+  float A1[H][MB][F / 4], A2[MB][KB][4];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int jb = 0; jb < MB; ++jb)
+#pragma unroll
+      for (int s4 = 0; s4 < F / 4; ++s4)
+        A1[h][jb][s4] = vo[(h * F + 4 * s4 + g) * M + 16 * jb + r16];
+#pragma unroll
+  for (int jb = 0; jb < MB; ++jb)
+#pragma unroll
+    for (int c = 0; c < KB; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) A2[jb][c][q] = a.W[(16 * c + 4 * g + q) * M + 16 * jb + r16];
+  __syncthreads();
+  const int64_t nb = (a.N + R - 1) / R;
+  const int64_t nwaves = (int64_t)gridDim.x * (kHeadThreads / 64);
+  for (int64_t bt = (int64_t)blockIdx.x * (kHeadThreads / 64) + w; bt < nb; bt += nwaves) {
+    const int64_t r0 = bt * R;
+    const int nr = (int)(a.N - r0 < R ? a.N - r0 : R);
+    if (lane <= nr) rps[lane] = a.rowptr[r0 + lane];
+    // u rows -> lrelu(bn(u)) (padded rows; rows past the batch are zero)
+    constexpr int Q4 = HF / 4;
+    constexpr int UL = (R * Q4 + 63) / 64;
+    float4 xq[UL];
+#pragma unroll
+    for (int t = 0; t < UL; ++t) {
+      const int e4 = 64 * t + lane;
+      const int r = e4 / Q4, c = 4 * (e4 - r * Q4);
+      xq[t] = r < nr ? ld4(u + (r0 + r) * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int t = 0; t < UL; ++t) {
+      const int e4 = 64 * t + lane;
+      if (e4 >= R * Q4) break;
+      const int r = e4 / Q4, c = 4 * (e4 - r * Q4);
+      const float xv[4] = {xq[t].x, xq[t].y, xq[t].z, xq[t].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float z = fmaf(g_[c + k] * su[c + k], xv[k] - mu[c + k], b_[c + k]);
+        uo[r * UP + c + k] = r < nr ? (z > 0.f ? z : z * a.slope) : 0.f;
+      }
+    }
+    for (int e = lane; e < R * M; e += 64) fl[e] = 0;
+    wave_sync();
+    const int32_t eb = rps[0], ee = rps[nr];
+    for (int32_t e = eb + lane; e < ee; e += 64) {
+      int r = 0;
+      while (rps[r + 1] <= e) ++r;
+      fl[r * M + a.col[e]] = 1;
+    }
+    // C_h^T = v_out_h @ uo_h^T
+    f32x4 xc[H][MB];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+#pragma unroll
+      for (int jb = 0; jb < MB; ++jb) xc[h][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < F / 4; ++s4) {
+        const float bv = uo[r16 * UP + h * F + 4 * s4 + g];
+#pragma unroll
+        for (int jb = 0; jb < MB; ++jb)
+          xc[h][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[h][jb][s4], bv, xc[h][jb], 0, 0, 0);
+      }
+    }
+    // x^T = dropout(elu(C^T)); element (row r0 + r16, k = h M + 16 jb + 4 g + q)
+    const uint64_t row = (uint64_t)(r0 + r16);
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int jb = 0; jb < MB; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          xc[h][jb][q] = elu1(xc[h][jb][q]) *
+                         dropout_factor(a.dx, row * KX + h * M + 16 * jb + 4 * g + q);
+    // hg^T = W^T @ x^T, k in the accumulators' order
+    f32x4 hg[MB];
+#pragma unroll
+    for (int jb = 0; jb < MB; ++jb) hg[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KB; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jb = 0; jb < MB; ++jb)
+          hg[jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A2[jb][c][q], xc[c / MB][c % MB][q],
+                                                        hg[jb], 0, 0, 0);
+    // GAL scale, elu, elu, log_softmax over the row's M logits
+    const bool rv = r16 < nr;
+    const int deg = rv ? rps[r16 + 1] - rps[r16] : 1;
+    const float inv = deg > 0 ? 1.f / (float)deg : 0.f;
+    float y[MB][4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int jb = 0; jb < MB; ++jb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 16 * jb + 4 * g + q;
+        const float at = (rv && fl[r16 * M + j] ? inv : 0.f) *
+                         dropout_factor(a.dg, row * M + j);
+        y[jb][q] = elu1(elu1(at * hg[jb][q]));
+        mx = fmaxf(mx, y[jb][q]);
+      }
+    mx = fmaxf(mx, xor_shfl(mx, 16));
+    mx = fmaxf(mx, xor_shfl(mx, 32));
+    float sm = 0.f;
+#pragma unroll
+    for (int jb = 0; jb < MB; ++jb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sm += __expf(y[jb][q] - mx);
+    sm += xor_shfl(sm, 16);
+    sm += xor_shfl(sm, 32);
+    const float lse = mx + __logf(sm);
+    if (rv) {
+#pragma unroll
+      for (int jb = 0; jb < MB; ++jb)
+        st4(out + (r0 + r16) * M + 16 * jb + 4 * g,
+            make_float4(y[jb][0] - lse, y[jb][1] - lse, y[jb][2] - lse, y[jb][3] - lse));
+    }
+    wave_sync();  // the batch's LDS reads done before the next batch's writes
+  }
+}
+
+static size_t fwd_mfma_lds(int HF, int M) {
+  return sizeof(float) * (4 * (size_t)HF + (kHeadThreads / 64) *
+                          (size_t)(16 * (HF + 1) + 16 * M + 32));
 }
 
 static size_t fwd_reg_lds(int HF, int KX) {
@@ -496,8 +682,24 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
     if (ri < r1) {
       const T* dr = dout + ri * M;
       int nzi = 0;
+      if (M % 4 == 0) {  // 16-byte pieces of the row, 8 in flight
+        int j = 0;
+        for (; j + 32 <= M; j += 32) {
+          float4 q[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) q[t] = ld4(dr + j + 4 * t);
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            nzi |= (q[t].x != 0.f) | (q[t].y != 0.f) | (q[t].z != 0.f) | (q[t].w != 0.f);
+        }
+        for (; j < M; j += 4) {
+          const float4 q = ld4(dr + j);
+          nzi |= (q.x != 0.f) | (q.y != 0.f) | (q.z != 0.f) | (q.w != 0.f);
+        }
+      } else {
 #pragma unroll 8
-      for (int j = 0; j < M; ++j) nzi |= to_f32(dr[j]) != 0.f;
+        for (int j = 0; j < M; ++j) nzi |= to_f32(dr[j]) != 0.f;
+      }
       nzl = nzi != 0;
       ws.rflag[ri] = nzl ? 1 : 0;
     }
@@ -820,6 +1022,8 @@ static HeadArgs head_args(const msha_graph* g, const msha_head_params* hp, const
     a.dub[h] = on ? hp->du_bias[h] : nullptr;
     a.dvw[h] = on ? hp->dv_weight[h] : nullptr;
     a.dvb[h] = on ? hp->dv_bias[h] : nullptr;
+    a.nbt[2 * h] = on ? hp->num_batches_tracked[2 * h] : nullptr;
+    a.nbt[2 * h + 1] = on ? hp->num_batches_tracked[2 * h + 1] : nullptr;
   }
   a.W = W;
   a.stats = stats;
@@ -861,16 +1065,32 @@ extern "C" int msha_head_fwd(const msha_graph* g, const msha_head_params* hp, in
   int64_t nbu = 0;
   Wf* part = training ? (Wf*)((char*)ws + L.part_u) : nullptr;
   if (training) nbu = bn_stats_partials(a.N, a.HF, bf, u, part, s);
-  const dim3 gp((a.HF + 3) / 4 + 1);
+  const int nub = (a.HF + 3) / 4;
+  const dim3 gp(nub + (a.HF + 31) / 32);
   if (bf)
     hipLaunchKernelGGL(head_prep_kernel<bf16_t>, gp, dim3(256), 0, s, a, training, (int)nbu, part,
-                       (const bf16_t*)v);
+                       (const bf16_t*)v, nub);
   else
     hipLaunchKernelGGL(head_prep_kernel<float>, gp, dim3(256), 0, s, a, training, (int)nbu, part,
-                       (const float*)v);
+                       (const float*)v, nub);
   const dim3 gr(grid_for(a.N, kHeadThreads / 64, 2048));
   const dim3 grb(grid_for((a.N + kHeadBatch - 1) / kHeadBatch, kHeadThreads / 64, 512));
-  // register-resident path: KX = H*M of 32 or 64 and F of 16 / 32 / 64 (R15: 2 x 64, M 32)
+  // matrix-core path: R15's shape (2 heads x 64, 32 recipients)
+#define HEAD_FWD_MFMA(T, H_, F_, M_)                                                      \
+  if (a.H == H_ && a.F == F_ && a.M == M_) {                                              \
+    hipLaunchKernelGGL((head_fwd_mfma_kernel<T, H_, F_, M_>), grb, dim3(kHeadThreads),    \
+                       fwd_mfma_lds(H_ * F_, M_), s, a, (const T*)u, (T*)out);            \
+    return check_launch("head_fwd");                                                      \
+  }
+  if (getenv("MSHA_HEAD_MFMA") == nullptr || atoi(getenv("MSHA_HEAD_MFMA")) != 0) {
+    if (bf) {
+      HEAD_FWD_MFMA(bf16_t, 2, 64, 32)
+    } else {
+      HEAD_FWD_MFMA(float, 2, 64, 32)
+    }
+  }
+#undef HEAD_FWD_MFMA
+  // register-resident path: KX = H*M of 32 or 64 and F of 16 / 32 / 64
 #define HEAD_FWD_REG(T, FV, KXV)                                                          \
   if (a.F == FV && a.KX == KXV) {                                                         \
     hipLaunchKernelGGL((head_fwd_reg_kernel<T, FV, KXV>), grb, dim3(kHeadThreads),        \

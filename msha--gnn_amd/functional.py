@@ -927,7 +927,7 @@ def _head_params(H, F, eps, momentum, slope, ptrs):
     hp.heads, hp.feat, hp.eps, hp.momentum, hp.slope = H, F, eps, momentum, slope
     for name, lst in ptrs.items():
         arr = getattr(hp, name)
-        for h in range(H):
+        for h in range(len(lst) if lst is not None else H):
             arr[h] = lst[h] if lst is not None else None
     return hp
 
@@ -973,7 +973,13 @@ class _ModelHead(torch.autograd.Function):
             "u_weight": ptr(p32[0:H]), "u_bias": ptr(p32[H:2 * H]),
             "u_running_mean": ptr(run["u"][0]), "u_running_var": ptr(run["u"][1]),
             "v_weight": ptr(p32[2 * H:3 * H]), "v_bias": ptr(p32[3 * H:4 * H]),
-            "v_running_mean": ptr(run["v"][0]), "v_running_var": ptr(run["v"][1])})
+            "v_running_mean": ptr(run["v"][0]), "v_running_var": ptr(run["v"][1]),
+            # the kernel advances the BatchNorms' step counters (nn.BatchNorm1d's +1)
+            "num_batches_tracked": [
+                _lib.ptr(bn.num_batches_tracked)
+                if training and bn.track_running_stats and bn.num_batches_tracked is not None
+                and bn.num_batches_tracked.is_cuda else None
+                for pair in bns for bn in pair]})
         stats = torch.empty(4 * H * F + H * F * M, device=dev, dtype=torch.float32)
         out = torch.empty(N, M, device=dev, dtype=dt)
         g = graph.desc
@@ -1053,11 +1059,6 @@ def model_head(graph: Graph, u, v, bns, out_W, out_a, p: float = 0.0, training: 
     sa = new_seed() if pa > 0 else 0
     params = ([b[0].weight for b in bns] + [b[0].bias for b in bns] + [b[1].weight for b in bns]
               + [b[1].bias for b in bns] + [out_a])
-    if training:
-        ctr = [bn.num_batches_tracked for b in bns for bn in b
-               if bn.track_running_stats and bn.num_batches_tracked is not None]
-        if ctr:
-            torch._foreach_add_(ctr, 1)
     return _ModelHead.apply(u, v, out_W, graph, bns, bool(training), float(bn0.eps),
                             float(bn0.momentum), float(slope), px, sx, pa, sa, *params)
 

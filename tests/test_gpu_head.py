@@ -143,6 +143,8 @@ def test_head_train_matches_fp64(cuda, msha, p, sparse):
         for t, r in zip((bu.running_mean, bu.running_var, bv.running_mean, bv.running_var),
                         runs[h]):
             tol_close(t.cpu().numpy(), r.numpy(), 1e-5, 1e-6)
+        # the kernel advanced every BatchNorm's step counter once (nn.BatchNorm1d's +1)
+        assert int(bu.num_batches_tracked) == 1 and int(bv.num_batches_tracked) == 1
 
 
 def test_head_wide_recipients(cuda, msha):
