@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 7
+#define MSHA_ABI_VERSION 8
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -500,12 +500,16 @@ MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int3
  * per four elements; msha_dropout_keep_mask4 writes the same mask). */
 #define MSHA_MAX_SEGMENTS 32
 typedef struct msha_segment {
-  const float* a;
-  const float* b;
-  float* dst;
+  const void* a;
+  const void* b;
+  void* dst;
   int64_t rows, cols, lda, ldb, ldd;
   float p;
   uint64_t seed, offset;
+  /* storage types (MSHA_DTYPE_*) of a and b (shared) and of dst; arithmetic is fp32 and
+   * a bf16 dst is rounded once (nearest-even), so a segment is also a dtype cast (the
+   * bf16 models' parameter / gradient / running-statistics conversions, ABI 8) */
+  int32_t a_dtype, dst_dtype;
 } msha_segment;
 MSHA_API int msha_segments(int32_t n, const msha_segment* segs, msha_stream_t stream);
 MSHA_API int msha_dropout_keep_mask4(uint64_t seed, uint64_t offset, int64_t n, float p,

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 7  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 8  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -77,7 +77,8 @@ class MshaSegment(C.Structure):
     _fields_ = [("a", C.c_void_p), ("b", C.c_void_p), ("dst", C.c_void_p),
                 ("rows", C.c_int64), ("cols", C.c_int64), ("lda", C.c_int64),
                 ("ldb", C.c_int64), ("ldd", C.c_int64), ("p", C.c_float),
-                ("seed", C.c_uint64), ("offset", C.c_uint64)]
+                ("seed", C.c_uint64), ("offset", C.c_uint64), ("a_dtype", C.c_int32),
+                ("dst_dtype", C.c_int32)]
 
 # name -> (restype, argtypes); every symbol here is declared in include/msha_gnn.h
 SIGNATURES = {

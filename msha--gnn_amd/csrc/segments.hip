@@ -1,6 +1,7 @@
 // Batched 2-D segment copies (include/msha_gnn.h msha_segments): the per-head parameter
-// packing of the MSHA layers and the models' feature dropout, each one launch where
-// torch issued a cat / stack / sum / contiguous copy or a dropout per tensor.
+// packing of the MSHA layers, the models' feature dropout and the bf16 models' dtype
+// casts, each one launch where torch issued a cat / stack / sum / contiguous copy, a
+// dropout or a .to(dtype) per tensor.
 #include "common.h"
 
 namespace msha {
@@ -15,9 +16,37 @@ __device__ __forceinline__ float keep4(const Dropout& d, uint64_t e, uint4 w) {
   return x >= d.threshold ? d.scale : 0.f;
 }
 
+// element loads / stores in a segment's storage type (fp32 arithmetic, bf16 rounded once)
+__device__ __forceinline__ float seg_ld(const void* p, int dt, int64_t i) {
+  return dt == MSHA_DTYPE_BF16 ? (float)reinterpret_cast<const bf16_t*>(p)[i]
+                               : reinterpret_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void seg_st(void* p, int dt, int64_t i, float v) {
+  if (dt == MSHA_DTYPE_BF16)
+    reinterpret_cast<bf16_t*>(p)[i] = (bf16_t)v;
+  else
+    reinterpret_cast<float*>(p)[i] = v;
+}
+// 4 consecutive elements (element 4q .. 4q + 3): 16 B fp32 / 8 B bf16
+__device__ __forceinline__ float4 seg_ld4(const void* p, int dt, int64_t q) {
+  if (dt == MSHA_DTYPE_BF16) {
+    const uint2 w = reinterpret_cast<const uint2*>(p)[q];
+    return make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                       __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+  }
+  return reinterpret_cast<const float4*>(p)[q];
+}
+__device__ __forceinline__ void seg_st4(void* p, int dt, int64_t q, float4 v) {
+  if (dt == MSHA_DTYPE_BF16)
+    reinterpret_cast<uint2*>(p)[q] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  else
+    reinterpret_cast<float4*>(p)[q] = v;
+}
+
 __global__ void __launch_bounds__(256) segments_kernel(SegBatch sb) {
   const msha_segment& g = sb.s[blockIdx.y];
   const int64_t total = g.rows * g.cols;
+  const int adt = g.a_dtype, ddt = g.dst_dtype;
   Dropout d{};
   d.active = g.p > 0.f;
   if (d.active) {
@@ -31,19 +60,18 @@ __global__ void __launch_bounds__(256) segments_kernel(SegBatch sb) {
   const uint64_t off = d.active ? dropout_offset(d, d.offset) : 0;
   const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // 4-element pieces: 16 B (fp32) / 8 B (bf16) aligned in every operand
+  const uintptr_t amask = adt == MSHA_DTYPE_BF16 ? 7 : 15, dmask = ddt == MSHA_DTYPE_BF16 ? 7 : 15;
   const bool flat = g.lda == g.cols && g.ldd == g.cols && (g.b == nullptr || g.ldb == g.cols) &&
-                    total % 4 == 0 &&
-                    (((uintptr_t)g.a | (uintptr_t)g.b | (uintptr_t)g.dst) & 15) == 0;
+                    total % 4 == 0 && (((uintptr_t)g.a | (uintptr_t)g.b) & amask) == 0 &&
+                    ((uintptr_t)g.dst & dmask) == 0;
   if (flat) {  // contiguous table: 4 elements per thread, one generator block per 4
-    const float4* a4 = reinterpret_cast<const float4*>(g.a);
-    const float4* b4 = reinterpret_cast<const float4*>(g.b);
-    float4* d4 = reinterpret_cast<float4*>(g.dst);
     for (int64_t q = tid; q < total / 4; q += nthr) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (g.a != nullptr) {
-        v = a4[q];
+        v = seg_ld4(g.a, adt, q);
         if (g.b != nullptr) {
-          const float4 w = b4[q];
+          const float4 w = seg_ld4(g.b, adt, q);
           v = make_float4(v.x + w.x, v.y + w.y, v.z + w.z, v.w + w.w);
         }
       }
@@ -54,7 +82,7 @@ __global__ void __launch_bounds__(256) segments_kernel(SegBatch sb) {
                         v.z * (w.z >= d.threshold ? d.scale : 0.f),
                         v.w * (w.w >= d.threshold ? d.scale : 0.f));
       }
-      d4[q] = v;
+      seg_st4(g.dst, ddt, q, v);
     }
     return;
   }
@@ -62,11 +90,11 @@ __global__ void __launch_bounds__(256) segments_kernel(SegBatch sb) {
     const int64_t r = e / g.cols, c = e - r * g.cols;
     float v = 0.f;
     if (g.a != nullptr) {
-      v = g.a[r * g.lda + c];
-      if (g.b != nullptr) v += g.b[r * g.ldb + c];
+      v = seg_ld(g.a, adt, r * g.lda + c);
+      if (g.b != nullptr) v += seg_ld(g.b, adt, r * g.ldb + c);
     }
     if (d.active) v *= keep4(d, (uint64_t)e, philox4(d.seed, off, (uint64_t)e >> 2));
-    g.dst[r * g.ldd + c] = v;
+    seg_st(g.dst, ddt, r * g.ldd + c, v);
   }
 }
 
@@ -91,6 +119,9 @@ extern "C" int msha_segments(int32_t n, const msha_segment* segs, msha_stream_t 
     const msha_segment& g = segs[i];
     MSHA_ARG_CHECK(g.dst != nullptr && g.rows >= 0 && g.cols >= 0, "segments: bad segment");
     MSHA_ARG_CHECK(g.p >= 0.f && g.p <= 1.f, "segments: p must be in [0, 1]");
+    MSHA_ARG_CHECK((g.a_dtype == MSHA_DTYPE_F32 || g.a_dtype == MSHA_DTYPE_BF16) &&
+                       (g.dst_dtype == MSHA_DTYPE_F32 || g.dst_dtype == MSHA_DTYPE_BF16),
+                   "segments: dtypes must be MSHA_DTYPE_F32 or MSHA_DTYPE_BF16");
     sb.s[i] = g;
     if (g.rows * g.cols > mx) mx = g.rows * g.cols;
   }

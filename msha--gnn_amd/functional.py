@@ -945,29 +945,42 @@ class _ModelHead(torch.autograd.Function):
         M = graph.n_cols
         dt = _table_dtype(u, v)
         u, v = _tc(u, dt), _tc(v, dt)
-        W32 = _f32c(W)
         a_out = params[4 * H]
-        p32 = [_f32c(p) for p in params[:4 * H]]  # held until the launches (see bn_lrelu)
         dev = u.device
+        s = _stream(u)
+        # fp32 views of W, the BatchNorm affine parameters and running statistics: the
+        # tensors themselves when fp32, else fp32 copies made in ONE cast launch (and the
+        # updated running statistics cast back in one launch after the head)
+        cast_in, cast_out = [], []
+
+        def f32_of(t):
+            if t.dtype == torch.float32 and t.is_contiguous():
+                return t
+            c = torch.empty(t.shape, device=t.device, dtype=torch.float32)
+            cast_in.append((t.contiguous(), c))
+            return c
+
+        W32 = f32_of(W)
+        p32 = [f32_of(p) for p in params[:4 * H]]  # held until the launches (see bn_lrelu)
         run = {}
-        copies = []
         for side, k in (("u", 0), ("v", 1)):
             rm, rv = [], []
             for bu_bv in bns:
                 bn = bu_bv[k]
                 if training and bn.track_running_stats and bn.running_mean is not None:
-                    m32, v32 = _f32c(bn.running_mean), _f32c(bn.running_var)
-                    if m32.data_ptr() != bn.running_mean.data_ptr():
-                        copies.append((bn.running_mean, m32, bn.running_var, v32))
-                    rm.append(m32)
-                    rv.append(v32)
+                    for buf, lst in ((bn.running_mean, rm), (bn.running_var, rv)):
+                        b32 = f32_of(buf)
+                        if b32 is not buf:
+                            cast_out.append((b32, buf))
+                        lst.append(b32)
                 elif not training:
-                    rm.append(_f32c(bn.running_mean))
-                    rv.append(_f32c(bn.running_var))
+                    rm.append(f32_of(bn.running_mean))
+                    rv.append(f32_of(bn.running_var))
                 else:
                     rm.append(None)
                     rv.append(None)
             run[side] = (rm, rv)
+        _cast_many(cast_in, s)
         ptr = lambda lst: [_lib.ptr(t) for t in lst]  # noqa: E731
         hp = _head_params(H, F, eps, momentum, slope, {
             "u_weight": ptr(p32[0:H]), "u_bias": ptr(p32[H:2 * H]),
@@ -987,14 +1000,12 @@ class _ModelHead(torch.autograd.Function):
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
         _lib.call("msha_head_fwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
                   W32.data_ptr(), int(training), px, sx, pa, sa, stats.data_ptr(),
-                  out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(u))
+                  out.data_ptr(), ws.data_ptr(), ws.numel(), s)
         if HEAD_TAPS is not None:  # tests: the statistics that decide the LeakyReLU branches
             HEAD_TAPS.append({"u": u.detach().clone(), "v": v.detach().clone(),
                               "stats": stats.detach().clone(),
                               "params": [p.detach().clone() for p in p32]})
-        for rm, m32, rv, v32 in copies:  # non-fp32 running buffers: write the update back
-            rm.copy_(m32)
-            rv.copy_(v32)
+        _cast_many(cast_out, s)  # non-fp32 running buffers: write the update back
         ctx.graph, ctx.hpar = graph, (H, F, eps, momentum, slope)
         ctx.drop = (px, sx, pa, sa)
         ctx.pdtypes = [p.dtype for p in params[:4 * H]]
@@ -1033,9 +1044,21 @@ class _ModelHead(torch.autograd.Function):
                   W32.data_ptr(), px, sx, pa, sa, stats.data_ptr(), dout.data_ptr(),
                   du.data_ptr(), dv.data_ptr(), dW.data_ptr(), da.data_ptr(), da.numel(),
                   ws.data_ptr(), ws.numel(), _stream(u))
-        grads = [dp[k, h].to(ctx.pdtypes[k * H + h]) for k in range(4) for h in range(H)]
-        return (du, dv, dW.to(ctx.wdtype), None, None, None, None, None, None, None, None, None,
-                None, *grads, da.to(adt))
+        # gradients in the parameters' dtypes: one cast launch for every non-fp32 one
+        casts = []
+
+        def as_dtype(g, dtype):
+            if g.dtype == dtype:
+                return g
+            c = torch.empty(g.shape, device=g.device, dtype=dtype)
+            casts.append((g, c))
+            return c
+
+        grads = [as_dtype(dp[k, h], ctx.pdtypes[k * H + h]) for k in range(4) for h in range(H)]
+        dW, da = as_dtype(dW, ctx.wdtype), as_dtype(da, adt)
+        _cast_many(casts, _stream(u))
+        return (du, dv, dW, None, None, None, None, None, None, None, None, None,
+                None, *grads, da)
 
 
 def C_byref(x):
@@ -1065,12 +1088,33 @@ def model_head(graph: Graph, u, v, bns, out_W, out_a, p: float = 0.0, training: 
 
 # ------------------------------------------------- parameter packing / feature dropout ---
 def _segments(segs, stream):
-    """One msha_segments launch: segs = [(a, dst, rows, cols, lda, ldd, b, ldb, p, seed)]
-    (pointers as ints, a / b may be None)."""
-    arr = (_lib.MshaSegment * len(segs))()
-    for k, (a, dst, rows, cols, lda, ldd, b, ldb, p, seed) in enumerate(segs):
-        arr[k] = _lib.MshaSegment(a, b, dst, rows, cols, lda, ldb, ldd, p, seed, 0)
-    _lib.call("msha_segments", len(segs), C_byref(arr), stream)
+    """msha_segments launches: segs = [(a, dst, rows, cols, lda, ldd, b, ldb, p, seed
+    [, a_dtype, dst_dtype])] (pointers as ints, a / b may be None; dtypes as torch dtypes,
+    fp32 when omitted), MSHA_MAX_SEGMENTS per launch."""
+    for lo in range(0, len(segs), _lib.MAX_SEGMENTS):
+        part = segs[lo:lo + _lib.MAX_SEGMENTS]
+        arr = (_lib.MshaSegment * len(part))()
+        for k, sg in enumerate(part):
+            a, dst, rows, cols, lda, ldd, b, ldb, p, seed = sg[:10]
+            adt, ddt = (sg[10], sg[11]) if len(sg) > 10 else (torch.float32, torch.float32)
+            arr[k] = _lib.MshaSegment(a, b, dst, rows, cols, lda, ldb, ldd, p, seed, 0,
+                                      _code(adt), _code(ddt))
+        _lib.call("msha_segments", len(part), C_byref(arr), stream)
+
+
+def _cast_segs(pairs):
+    """Segments writing dst = src (cast to dst's dtype) for contiguous same-numel pairs."""
+    return [(a.data_ptr(), d.data_ptr(), 1, a.numel(), a.numel(), a.numel(), None, 0, 0.0, 0,
+             a.dtype, d.dtype) for a, d in pairs if a.numel() > 0]
+
+
+def _cast_many(pairs, stream):
+    """Every (src, dst) pair of contiguous same-numel tensors copied with a dtype cast in
+    one launch (the bf16 models' small parameters, gradients and BatchNorm buffers: one
+    launch where ``.to(dtype)`` issued one per tensor)."""
+    segs = _cast_segs(pairs)
+    if segs:
+        _segments(segs, stream)
 
 
 class _FeatureDropout(torch.autograd.Function):
@@ -1082,9 +1126,9 @@ class _FeatureDropout(torch.autograd.Function):
         S, R = S.contiguous(), R.contiguous()
         So, Ro = torch.empty_like(S), torch.empty_like(R)
         _segments([(S.data_ptr(), So.data_ptr(), S.shape[0], S.shape[1], S.shape[1], S.shape[1],
-                    None, 0, p, s_seed),
+                    None, 0, p, s_seed, S.dtype, S.dtype),
                    (R.data_ptr(), Ro.data_ptr(), R.shape[0], R.shape[1], R.shape[1], R.shape[1],
-                    None, 0, p, r_seed)], _stream(S))
+                    None, 0, p, r_seed, R.dtype, R.dtype)], _stream(S))
         ctx.p, ctx.seeds = p, (s_seed, r_seed)
         return So, Ro
 
@@ -1098,7 +1142,7 @@ class _FeatureDropout(torch.autograd.Function):
             d = d.contiguous()
             g = torch.empty_like(d)
             segs.append((d.data_ptr(), g.data_ptr(), d.shape[0], d.shape[1], d.shape[1],
-                         d.shape[1], None, 0, ctx.p, seed))
+                         d.shape[1], None, 0, ctx.p, seed, d.dtype, d.dtype))
             outs.append(g)
         if segs:
             _segments(segs, _stream(outs[0] if outs[0] is not None else outs[1]))
@@ -1107,11 +1151,12 @@ class _FeatureDropout(torch.autograd.Function):
 
 def feature_dropout(S, R, p: float, training: bool):
     """(dropout(S, p), dropout(R, p)) for the models' two feature tables: one launch each
-    way for fp32 tables (Philox masks, seeds from torch's CPU generator), F.dropout
-    otherwise."""
+    way for fp32 / bf16 tables (Philox masks, seeds from torch's CPU generator; bf16
+    outputs rounded once from the fp32 product), F.dropout otherwise."""
     if not training or p <= 0:
         return S, R
-    if S.dtype != torch.float32 or R.dtype != torch.float32 or S.dim() != 2 or R.dim() != 2:
+    ok = (torch.float32, BF16)
+    if S.dtype not in ok or R.dtype not in ok or S.dim() != 2 or R.dim() != 2:
         return (torch.nn.functional.dropout(S, p, training=True),
                 torch.nn.functional.dropout(R, p, training=True))
     _lib.require_cuda(S, R)
@@ -1120,30 +1165,35 @@ def feature_dropout(S, R, p: float, training: bool):
 
 class _PackHeads(torch.autograd.Function):
     """The heads' parameters as the fused launches read them (Ablation.py:262-267,
-    Ours.py:58-75): W1 / W2 concatenated along features (K, H*F), the score vector halves
-    a[:F] (recipient side) / a[F:] (source side) as (H, F), and for the full MSHA layer
-    a3[:F] + a3[F:], a4[:F] + a4[F:] -- one launch; the backward scatters the packed
-    gradients to every head's parameters in one launch."""
+    Ours.py:58-75): W1 / W2 concatenated along features (K, H*F) in the parameters'
+    dtype, the score vector halves a[:F] (recipient side) / a[F:] (source side) as fp32
+    (H, F), and for the full MSHA layer a3[:F] + a3[F:], a4[:F] + a4[F:] -- one launch;
+    the backward scatters the packed gradients to every head's parameters (cast to their
+    dtype) in one launch.  fp32 or bf16 parameters (the scores are fp32 either way)."""
 
     @staticmethod
     def forward(ctx, H, intra, *params):
         W1s, W2s, As = params[:H], params[H:2 * H], params[2 * H:3 * H]
         K, Fd = W1s[0].shape
         dev = W1s[0].device
-        W1 = torch.empty(K, H * Fd, device=dev)
-        W2 = torch.empty(K, H * Fd, device=dev)
+        pdt = W1s[0].dtype
+        es = W1s[0].element_size()
+        W1 = torch.empty(K, H * Fd, device=dev, dtype=pdt)
+        W2 = torch.empty(K, H * Fd, device=dev, dtype=pdt)
         ar = torch.empty(H, Fd, device=dev)
         al = torch.empty(H, Fd, device=dev)
         outs = [W1, W2, ar, al]
+        f32 = torch.float32
         segs = []
         for h in range(H):
-            segs.append((W1s[h].data_ptr(), W1.data_ptr() + 4 * h * Fd, K, Fd, Fd, H * Fd,
-                         None, 0, 0.0, 0))
-            segs.append((W2s[h].data_ptr(), W2.data_ptr() + 4 * h * Fd, K, Fd, Fd, H * Fd,
-                         None, 0, 0.0, 0))
+            segs.append((W1s[h].data_ptr(), W1.data_ptr() + es * h * Fd, K, Fd, Fd, H * Fd,
+                         None, 0, 0.0, 0, pdt, pdt))
+            segs.append((W2s[h].data_ptr(), W2.data_ptr() + es * h * Fd, K, Fd, Fd, H * Fd,
+                         None, 0, 0.0, 0, pdt, pdt))
             pa = As[h].data_ptr()
-            segs.append((pa, ar.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
-            segs.append((pa + 4 * Fd, al.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+            segs.append((pa, ar.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0, pdt, f32))
+            segs.append((pa + es * Fd, al.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                         pdt, f32))
         if intra:
             a3s = torch.empty(H, Fd, device=dev)
             a4s = torch.empty(H, Fd, device=dev)
@@ -1151,51 +1201,61 @@ class _PackHeads(torch.autograd.Function):
             for h in range(H):
                 for src, dst in ((params[3 * H + h], a3s), (params[4 * H + h], a4s)):
                     pa = src.data_ptr()
-                    segs.append((pa, dst.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, pa + 4 * Fd, Fd,
-                                 0.0, 0))
+                    segs.append((pa, dst.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, pa + es * Fd, Fd,
+                                 0.0, 0, pdt, f32))
         _segments(segs, _stream(W1))
-        ctx.H, ctx.intra, ctx.K, ctx.Fd = H, intra, K, Fd
+        ctx.H, ctx.intra, ctx.K, ctx.Fd, ctx.pdt = H, intra, K, Fd, pdt
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, dW1, dW2, dar, dal, da3s=None, da4s=None):
-        H, K, Fd = ctx.H, ctx.K, ctx.Fd
+        H, K, Fd, pdt = ctx.H, ctx.K, ctx.Fd, ctx.pdt
         dev = (dW1 if dW1 is not None else dW2).device if (dW1 is not None or dW2 is not None) \
             else dar.device
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
         dW1, dW2, dar, dal, da3s, da4s = map(c, (dW1, dW2, dar, dal, da3s, da4s))
-        ptr = lambda t, off=0: None if t is None else t.data_ptr() + off  # noqa: E731
-        gW1 = [torch.empty(K, Fd, device=dev) for _ in range(H)]
-        gW2 = [torch.empty(K, Fd, device=dev) for _ in range(H)]
-        gA = [torch.empty(2 * Fd, 1, device=dev) for _ in range(H)]
+        # a missing gradient writes zeros (NULL a); its dtype code is then irrelevant
+        dty = lambda t: pdt if t is None else t.dtype  # noqa: E731
+        ptr = lambda t, off=0: None if t is None else t.data_ptr() + off * t.element_size()  # noqa: E731
+        gW1 = [torch.empty(K, Fd, device=dev, dtype=pdt) for _ in range(H)]
+        gW2 = [torch.empty(K, Fd, device=dev, dtype=pdt) for _ in range(H)]
+        gA = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
+        ge = gA[0].element_size()
         segs = []
         for h in range(H):
-            o = 4 * h * Fd
-            segs.append((ptr(dW1, o), gW1[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0))
-            segs.append((ptr(dW2, o), gW2[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0))
-            segs.append((ptr(dar, o), gA[h].data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0))
-            segs.append((ptr(dal, o), gA[h].data_ptr() + 4 * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+            o = h * Fd
+            segs.append((ptr(dW1, o), gW1[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0,
+                         dty(dW1), pdt))
+            segs.append((ptr(dW2, o), gW2[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0,
+                         dty(dW2), pdt))
+            segs.append((ptr(dar, o), gA[h].data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                         dty(dar), pdt))
+            segs.append((ptr(dal, o), gA[h].data_ptr() + ge * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                         dty(dal), pdt))
         g3 = g4 = []
         if ctx.intra:
-            g3 = [torch.empty(2 * Fd, 1, device=dev) for _ in range(H)]
-            g4 = [torch.empty(2 * Fd, 1, device=dev) for _ in range(H)]
+            g3 = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
+            g4 = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
             for h in range(H):
-                o = 4 * h * Fd
+                o = h * Fd
                 for d, g in ((da3s, g3[h]), (da4s, g4[h])):  # sum backward: both halves
-                    segs.append((ptr(d, o), g.data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0))
-                    segs.append((ptr(d, o), g.data_ptr() + 4 * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0))
+                    segs.append((ptr(d, o), g.data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                                 dty(d), pdt))
+                    segs.append((ptr(d, o), g.data_ptr() + ge * Fd, 1, Fd, Fd, Fd, None, 0, 0.0,
+                                 0, dty(d), pdt))
         _segments(segs, _lib.stream_handle(dev))
         return (None, None, *gW1, *gW2, *gA, *g3, *g4)
 
 
 def pack_heads(heads, intra: bool):
     """(W1 (K, H*F), W2, a_r (H, F), a_l (H, F)[, a3s, a4s]) of the heads' parameters, or
-    None when the one-launch packing does not apply (non-fp32 or non-contiguous
-    parameters, more than 4 heads)."""
+    None when the one-launch packing does not apply (mixed or non-fp32/bf16 dtypes,
+    non-contiguous parameters, more than 4 heads)."""
     H = len(heads)
     names = ["W1", "W2", "a"] + (["a3", "a4"] if intra else [])
     params = [getattr(h, n) for n in names for h in heads]
-    if H > 4 or any(p.dtype != torch.float32 or not p.is_contiguous() or not p.is_cuda
-                    for p in params):
+    pdt = params[0].dtype
+    if H > 4 or pdt not in (torch.float32, BF16) or any(
+            p.dtype != pdt or not p.is_contiguous() or not p.is_cuda for p in params):
         return None
     return _PackHeads.apply(H, intra, *params)

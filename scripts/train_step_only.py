@@ -10,4 +10,5 @@ import bench  # noqa: E402
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "Ours"
 year = sys.argv[2] if len(sys.argv) > 2 else "2015"
-print(json.dumps(bench.train_step_leg(torch.device("cuda:0"), year, kind)))
+dtype = getattr(torch, sys.argv[3]) if len(sys.argv) > 3 else torch.float32
+print(json.dumps(bench.train_step_leg(torch.device("cuda:0"), year, kind, dtype=dtype)))

@@ -203,23 +203,27 @@ def test_models_use_the_fused_head(cuda, msha):
         layers.MF.model_head = orig
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
 @pytest.mark.parametrize("intra", [False, True])
-def test_pack_heads_matches_cat_and_stack(cuda, msha, intra):
+def test_pack_heads_matches_cat_and_stack(cuda, msha, intra, dtype):
     """One-launch parameter packing == torch.cat / stack / sum of the heads' parameters,
     and its backward == autograd's gradients of that torch formulation (bit-exact: copies
-    and one add)."""
+    and one add).  bf16 parameters: W packed in bf16, score halves (and the a3/a4 half
+    sums) in fp32, gradients cast back to bf16 in the same launch."""
     from msha_gnn_amd import functional as MF
     from msha_gnn_amd import layers
 
     torch.manual_seed(0)
     cls = layers.OursLayer if intra else layers.OursLayer3
-    heads = [cls(128, 64, 0.0).to(cuda) for _ in range(2)]
+    heads = [cls(128, 64, 0.0).to(cuda, dtype) for _ in range(2)]
     packed = MF.pack_heads(heads, intra)
     ref = [torch.cat([h.W1 for h in heads], 1), torch.cat([h.W2 for h in heads], 1)]
-    halves = layers._score_halves(heads, "a")
+    halves = layers._score_halves(heads, "a").float()
     ref += [halves[:, 0], halves[:, 1]]
     if intra:
-        ref += [layers._score_halves(heads, "a3").sum(1), layers._score_halves(heads, "a4").sum(1)]
+        ref += [layers._score_halves(heads, "a3").float().sum(1),
+                layers._score_halves(heads, "a4").float().sum(1)]
+    assert [t.dtype for t in packed] == [dtype] * 2 + [torch.float32] * (len(packed) - 2)
     assert len(packed) == len(ref)
     gen = torch.Generator(device=cuda).manual_seed(1)
     ws = [torch.randn(r.shape, device=cuda, generator=gen) for r in ref]
@@ -236,14 +240,16 @@ def test_pack_heads_matches_cat_and_stack(cuda, msha, intra):
             torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
-def test_feature_dropout_masks_and_grad(cuda, msha):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_feature_dropout_masks_and_grad(cuda, msha, dtype):
     """Both feature tables dropped in one launch with the Philox masks
-    (msha_dropout_keep_mask of the same seed), gradients masked the same way."""
+    (msha_dropout_keep_mask of the same seed), gradients masked the same way (bf16
+    tables: the same masks, x * 2 exact in bf16)."""
     from msha_gnn_amd import functional as MF
 
     gen = torch.Generator(device=cuda).manual_seed(2)
-    S = torch.rand(1000, 128, device=cuda, generator=gen).requires_grad_(True)
-    R = torch.rand(32, 128, device=cuda, generator=gen).requires_grad_(True)
+    S = torch.rand(1000, 128, device=cuda, generator=gen).to(dtype).requires_grad_(True)
+    R = torch.rand(32, 128, device=cuda, generator=gen).to(dtype).requires_grad_(True)
     So, Ro = MF._FeatureDropout.apply(S, R, 0.5, 77, 78)
     kS = MF.dropout_keep_mask(S.numel(), 0.5, 77, cuda, flat4=True).view_as(S).bool()
     kR = MF.dropout_keep_mask(R.numel(), 0.5, 78, cuda, flat4=True).view_as(R).bool()
@@ -254,8 +260,29 @@ def test_feature_dropout_masks_and_grad(cuda, msha):
     assert torch.equal(So, torch.where(kS, S * 2.0, torch.zeros_like(S)))
     assert torch.equal(Ro, torch.where(kR, R * 2.0, torch.zeros_like(R)))
     (So.sum() + 3 * Ro.sum()).backward()
-    assert torch.equal(S.grad, kS.float() * 2.0)
-    assert torch.equal(R.grad, kR.float() * 6.0)
+    assert S.grad.dtype == dtype and So.dtype == dtype
+    assert torch.equal(S.grad, (kS.float() * 2.0).to(dtype))
+    assert torch.equal(R.grad, (kR.float() * 6.0).to(dtype))
+
+
+def test_cast_segments_round_to_nearest_even(cuda, msha):
+    """msha_segments as a dtype cast (ABI 8): fp32 -> bf16 rounds like torch's .to(),
+    bf16 -> fp32 is exact, strided rows, and several pairs in one launch."""
+    from msha_gnn_amd import functional as MF
+
+    gen = torch.Generator(device=cuda).manual_seed(3)
+    a = torch.randn(37, 129, device=cuda, generator=gen) * 1e3
+    b = torch.randn(4096, device=cuda, generator=gen).to(torch.bfloat16)
+    a16 = torch.empty(a.shape, device=cuda, dtype=torch.bfloat16)
+    b32 = torch.empty(b.shape, device=cuda)
+    MF._cast_many([(a, a16), (b, b32)], torch.cuda.current_stream(cuda).cuda_stream)
+    assert torch.equal(a16, a.to(torch.bfloat16))
+    assert torch.equal(b32, b.float())
+    # strided (non-flat) segment path: the first 65 columns of each row of a
+    out = torch.zeros(37, 65, device=cuda, dtype=torch.bfloat16)
+    MF._segments([(a.data_ptr(), out.data_ptr(), 37, 65, 129, 65, None, 0, 0.0, 0,
+                   torch.float32, torch.bfloat16)], torch.cuda.current_stream(cuda).cuda_stream)
+    assert torch.equal(out, a[:, :65].to(torch.bfloat16))
 
 
 @pytest.mark.parametrize("M,K,H,F_", [(32, 128, 2, 64), (200, 64, 1, 128), (7, 128, 8, 16)])
