@@ -118,25 +118,32 @@ def csc_bytes(m, e, H, F, n_chunks, s=4):
     return e * (8 + 8 * H + s * D) + m * (s * D + 4 * H) + 12 * n_chunks + 4 * (m + 1)
 
 
-def bwd_fused_bytes(n, m, e, H, F, n_chunks, s=4):
+def bwd_fused_bytes(n, m, e, H, F, n_chunks, s=4, rowterms=False):
     """Algorithmic bytes of msha_edge_attention_bwd_fused (its three launches):
     row stats (dU, u, el, lse in; the 3H-float row record out); the column pass (per
     CSC slot row + eid + the record gather + s*D dU gather + de write; per column hc,
-    er in, d_hc, d_er out; the chunk plan); the row sum (rowptr, slot map, de, d_el)."""
+    er in, d_hc, d_er out; the chunk plan); the row sum (rowptr, slot map, de, d_el).
+    rowterms (msha_edge_attention_bwd_fused_ex with uc, qc; large graphs): the row
+    stats also read uc (fp32 D floats), qc and the row flag and write d_el; the column
+    pass writes no de; no row sum."""
     D = H * F
     stats = n * (2 * s * D + 8 * H + 12 * H)
-    cols = e * (8 + 12 * H + s * D + 4 * H) + m * (2 * s * D + 8 * H) + 12 * n_chunks \
-        + 4 * (m + 1)
+    cols = e * (8 + 12 * H + s * D) + m * (2 * s * D + 8 * H) + 12 * n_chunks + 4 * (m + 1)
+    if rowterms:
+        return stats + n * (4 * D + 4 * H + 1 + 4 * H) + cols
     slot_map = 4 if e * 4 * H >= 192 << 20 else 0  # de in slot order (edge_attention.hip)
     rsum = 4 * (n + 1) + e * (4 * H + slot_map) + n * 4 * H
-    return stats + cols + rsum
+    return stats + cols + e * 4 * H + rsum
 
 
-def fwd_bytes(n, m, e, H, F, s=4):
+def fwd_bytes(n, m, e, H, F, s=4, rowterms=False):
     """Algorithmic bytes of one msha_edge_attention_fwd launch:
     rowptr + col + er gather + el + h gather (s*HF per edge) + u write + lse write;
-    s = bytes per table element (4 fp32, 2 bf16)."""
-    return 4 * (n + 1) + 4 * e + 4 * e * H + 4 * n * H + s * e * H * F + s * n * H * F + 4 * n * H
+    s = bytes per table element (4 fp32, 2 bf16); rowterms: + the uc (fp32) and qc
+    writes of msha_edge_attention_fwd_ex."""
+    rt = 4 * n * H * F + 4 * n * H if rowterms else 0
+    return (4 * (n + 1) + 4 * e + 4 * e * H + 4 * n * H + s * e * H * F + s * n * H * F
+            + 4 * n * H + rt)
 
 
 class Layer:
@@ -166,6 +173,13 @@ class Layer:
         # attention dropout of the reference's training forward (Ablation.py:271): Philox
         # masks drawn inside the forward and regenerated by the backward
         self.p = dropout
+        # the u-only fused backward takes the forward's row terms on large graphs
+        # (msha_edge_attention_rowterms_preferred): their bytes enter the rooflines
+        from msha_gnn_amd import _lib
+
+        code = 1 if dtype == torch.bfloat16 else 0
+        self.rowterms = bool(MF.ROWTERMS and MF.FUSED_BWD and _lib.load()
+                             .msha_edge_attention_rowterms_preferred(self.graph.desc, H, F, code))
 
     def step(self):
         for p in (self.W, self.al, self.ar):
@@ -654,19 +668,22 @@ def main():
         """Rooflines of the edge kernels of the step (HIP events, same run): the forward
         and either the fused backward or bwd_rows + csc_aggregate."""
         nch = lay.graph._plan["n_chunks"]
+        rt = lay.rowterms
         out = []
-        for name, nbytes in (("msha_edge_attention_fwd", fwd_bytes(n, m, e, H, F, s)),
+        for name, nbytes in (("msha_edge_attention_fwd", fwd_bytes(n, m, e, H, F, s, rt)),
                              ("msha_edge_attention_bwd_rows", bwd_rows_bytes(n, m, e, H, F, s)),
                              ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s)),
                              ("msha_edge_attention_bwd_fused",
-                              bwd_fused_bytes(n, m, e, H, F, nch, s))):
+                              bwd_fused_bytes(n, m, e, H, F, nch, s, rt))):
             key = name[len("msha_"):]
             if key not in lay.kernel_ms:
                 continue
             us = lay.kernel_ms[key] * 1e3
             gbs = nbytes / (us * 1e-6) / 1e9
             out.append({"kernel": name, "algorithmic_bytes": nbytes, "avg_us": us,
-                        "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
+                        "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
+                        **({"rowterms": True} if rt and "rows" not in name
+                           and "csc" not in name else {})})
         return out
 
     dt_eager, k_ms, n_launch = timed(layer, args.steps, args.warmup)
@@ -686,7 +703,7 @@ def main():
         dtde, kd, nd = timed(layd, args.steps, args.warmup)
         dtdg = None if args.eager else timed_graph(layd, args.steps)
         dtd = dtdg if dtdg is not None else dtde
-        ad = fwd_bytes(n, m, e, H, F) / (kd * 1e-3) / 1e9
+        ad = fwd_bytes(n, m, e, H, F, 4, layd.rowterms) / (kd * 1e-3) / 1e9
         drop_leg = {"workload": f"gat_layer_{args.workload}, attention dropout p = 0.5 "
                                 "(training forward + backward)",
                     "value": world * e * args.steps / dtd, "unit": "edges/s",
@@ -706,7 +723,7 @@ def main():
         dt16e, k16, n16 = timed(lay16, args.steps, args.warmup)
         dt16g = None if args.eager else timed_graph(lay16, args.steps)
         dt16 = dt16g if dt16g is not None else dt16e
-        fb16 = fwd_bytes(n, m, e, H, F, s=2)
+        fb16 = fwd_bytes(n, m, e, H, F, 2, lay16.rowterms)
         a16 = fb16 / (k16 * 1e-3) / 1e9
         tr16, src16 = pmc_traffic(H, F, True, args.workload)
         bf16_leg = {"workload": f"gat_layer_{args.workload} (config C3: bf16 tables, bf16 MFMA "
@@ -733,7 +750,7 @@ def main():
         return
     ms_per_step = dt / args.steps * 1e3
     value = world * e * args.steps / dt
-    fb = fwd_bytes(n, m, e, H, F)
+    fb = fwd_bytes(n, m, e, H, F, 4, layer.rowterms)
     achieved = fb / (k_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(H, F, False, args.workload)
     out = {

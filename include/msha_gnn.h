@@ -171,6 +171,23 @@ MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t
                                      const void* hc, float neg_slope, float drop_p,
                                      uint64_t seed, uint64_t offset, void* u, void* u_lo,
                                      float* lse, float* attd, msha_stream_t stream);
+/* The same forward that also writes the row terms of the fused backward (ABI 8), with
+ * c_ij = lrelu'(el_i + er_j) (1 when > 0, else neg_slope):
+ *   uc (n_rows, heads, feat) fp32 = sum_j c_ij attd_ij hc[j]   (attd: post-dropout)
+ *   qc (n_rows, heads)       fp32 = sum_j c_ij att_ij          (att: pre-dropout)
+ * so d_el_i = dU_i . uc_i - D_i qc_i (D_i = dU_i . u_i) needs no per-edge de in CSR
+ * order.  uc and qc together or both NULL (= msha_edge_attention_fwd).  Needs the
+ * batched forward (MSHA_ERR_UNSUPPORTED otherwise); msha_edge_attention_rowterms_preferred
+ * says whether a graph should use them (1: the graph is large enough that the per-edge
+ * de of msha_edge_attention_bwd_fused would leave the Infinity Cache). */
+MSHA_API int msha_edge_attention_rowterms_preferred(const msha_graph* g, int32_t heads,
+                                                    int32_t feat, int32_t dtype);
+MSHA_API int msha_edge_attention_fwd_ex(const msha_graph* g, int32_t heads, int32_t feat,
+                                        int32_t dtype, const float* el, const float* er,
+                                        const void* hc, float neg_slope, float drop_p,
+                                        uint64_t seed, uint64_t offset, void* u, void* u_lo,
+                                        float* lse, float* attd, float* uc, float* qc,
+                                        msha_stream_t stream);
 
 /* Row half of the backward (autograd of the chain above; Ablation.py:266-274):
  *   g_e  = dU[i]·hc[j] (+ dV[j]·hs[i] when dV != NULL: the v = att^T @ h2 branch,
@@ -230,6 +247,15 @@ MSHA_API int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads, i
                                            uint64_t seed, uint64_t offset, float* d_el,
                                            float* d_er, void* d_hc, float* de, void* ws,
                                            size_t ws_bytes, msha_stream_t stream);
+/* The same with the forward's row terms (uc, qc from msha_edge_attention_fwd_ex, same
+ * dropout seed/offset): d_el is finished in the row-statistics pass, the column pass
+ * stores no de and no row sum runs (de may be NULL).  uc = qc = NULL: the call above. */
+MSHA_API int msha_edge_attention_bwd_fused_ex(
+    const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype, const float* el,
+    const float* er, const void* hc, const float* lse, const void* u, const void* u_lo,
+    const void* dU, float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
+    const float* uc, const float* qc, float* d_el, float* d_er, void* d_hc, float* de, void* ws,
+    size_t ws_bytes, msha_stream_t stream);
 
 /* ----------------------------------------------- GraphAttentionLayer (GAL) --- */
 /* GAT.py:20-35 / Ablation.py:100-115.  The layer's score is constant along a row

@@ -95,6 +95,11 @@ SIGNATURES = {
     "msha_edge_attention_supported": (C.c_int, [I32, I32]),
     "msha_edge_attention_fwd": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P, P,
                                           P, P, P]),
+    "msha_edge_attention_rowterms_preferred": (C.c_int, [GP, I32, I32, I32]),
+    "msha_edge_attention_fwd_ex": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P,
+                                             P, P, P, P, P, P]),
+    "msha_edge_attention_bwd_fused_ex": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,
+                                                   F32, U64, U64, P, P, P, P, P, P, P, SZ, P]),
     "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, P,
                                                F32, F32, U64, U64, P, P, P, I32, P, P]),
     "msha_edge_attention_bwd_fused_workspace_size": (SZ, [GP, I32, I32]),

@@ -333,6 +333,9 @@ int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int6
                             const int64_t* gi, const void* G2, int64_t ldg2, const int64_t* gj,
                             const void* W, const float* bias, int act, const Dropout& dp,
                             void* out, bool out_bf16, hipStream_t s);
+int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, float* C,
+              int hH, int hF, const float* d1, const float* a1, const float* d2, const float* a2,
+              hipStream_t s);
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,

@@ -233,17 +233,24 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 // issued a chunk earlier, so it runs while the gathers are in flight.
 // Row bounds are wave-uniform (readfirstlane): scalar loads and scalar loop control.
 // Needs every table below 2 GiB (the dispatcher checks and otherwise runs the above).
+//
+// RT (row terms for the backward's d_el, large graphs): with c_ij = lrelu'(el_i + er_j)
+// (1 or slope), the kernel also accumulates uc_i = sum_j c_ij attd_ij hc_j (fp32, N x D)
+// and qc_i = sum_j c_ij att_ij (N x H, pre-dropout probabilities), by the same online
+// rescale as u and l.  Then d_el_i = dU_i . uc_i - D_i qc_i per head (D_i = dU_i . u_i),
+// which is sum_j de_ij rearranged: the fused backward needs no per-edge de crossing
+// from CSC to CSR order (bwd_row_stats_kernel<RT> finishes d_el in its row pass).
 #ifndef FWD_WPE
 #define FWD_WPE 1
 #endif
-template <int H, int F, typename T, int EPL>
+template <int H, int F, typename T, int EPL, bool RT = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
 edge_attn_fwd_bat_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
     const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
     float slope, Dropout dp, T* __restrict__ u, T* __restrict__ u_lo, float* __restrict__ lse,
-    float* __restrict__ attd) {
+    float* __restrict__ attd, float* __restrict__ uc, float* __restrict__ qc) {
   using G = Geo<H, F, T>;
   static_assert(G::QPL == 1, "batched forward: one 16-byte piece per lane");
   constexpr int CEL = EPL * G::CE;    // edges per chunk
@@ -275,8 +282,8 @@ edge_attn_fwd_bat_kernel(
     for (int t = 0; t < EPL; ++t)
       erv[t] = buf_f32(r_er, start + t * G::CE + e_s < end
                                  ? (uint32_t)j0[t] * (4u * H) + 4u * h_s : kOOB);
-    float m = -INFINITY, l = 0.f;
-    Pk<T> acc = pk_zero<T>();
+    float m = -INFINITY, l = 0.f, lc = 0.f;
+    Pk<T> acc = pk_zero<T>(), accc = pk_zero<T>();
     float sc_keep[EPL];  // the last chunk's scores (record mode, one-chunk rows)
     for (int32_t cs = start; cs < end; cs += CEL) {
       const int nvalid = min(CEL, (int)(end - cs));
@@ -302,28 +309,36 @@ edge_attn_fwd_bat_kernel(
         j2[t] = buf_i32(r_col, e2 < end ? (uint32_t)e2 * 4u : kOOB);
       }
       // (3) the chunk's online softmax (score layout), while the gathers fly
-      float sc[EPL], smax = -INFINITY;
+      float sc[EPL], cf[EPL], smax = -INFINITY;
+      uint64_t cpos[EPL];  // RT: ballot of pre > 0 over the score lanes (edge * H + head)
       bool valid[EPL];
 #pragma unroll
       for (int t = 0; t < EPL; ++t) {
         valid[t] = cs + t * G::CE + e_s < end;
-        sc[t] = valid[t] ? (virt ? 0.f : lrelu(elh + erv[t], slope)) : -INFINITY;
+        const float pre = elh + erv[t];
+        sc[t] = valid[t] ? (virt ? 0.f : lrelu(pre, slope)) : -INFINITY;
+        cf[t] = pre > 0.f ? 1.f : slope;  // the column pass's lrelu' (virtual rows: unused)
+        if (RT) cpos[t] = __ballot(pre > 0.f);
         smax = fmaxf(smax, sc[t]);
         sc_keep[t] = sc[t];
       }
       const float mn = fmaxf(m, wave_xor_max<H>(smax));
       const float alpha = __expf(m - mn);
-      float w[EPL], psum = 0.f;
+      float w[EPL], psum = 0.f, pcsum = 0.f;
 #pragma unroll
       for (int t = 0; t < EPL; ++t) {
         const float pe = valid[t] ? __expf(sc[t] - mn) : 0.f;
         psum += pe;
+        if (RT) pcsum = fmaf(pe, cf[t], pcsum);
         w[t] = valid[t] ? pe * dropout_factor(dp, (uint64_t)(cs + t * G::CE + e_s) * H + h_s)
                         : 0.f;
       }
       l = fmaf(l, alpha, wave_xor_sum<H>(psum));
+      if (RT) lc = fmaf(lc, alpha, wave_xor_sum<H>(pcsum));
       m = mn;
-      acc = pk_scale(acc, __shfl(alpha, q / G::QH));
+      const float alpha_q = __shfl(alpha, q / G::QH);
+      acc = pk_scale(acc, alpha_q);
+      if (RT) accc = pk_scale(accc, alpha_q);
       // (4) accumulate in gather order (masked lanes carry w = 0 and a zero row)
 #pragma unroll
       for (int gi = 0; gi < NGI; ++gi) {
@@ -331,7 +346,12 @@ edge_attn_fwd_bat_kernel(
         const int t = g / G::CE;
         const int ei = g % G::CE + g_e;
         const float wq = __shfl(w[t], ei * H + q / G::QH);
-        acc = pk_fma(wq, pk_from_raw(raw[gi], (T*)nullptr), acc);
+        const Pk<T> xr = pk_from_raw(raw[gi], (T*)nullptr);
+        acc = pk_fma(wq, xr, acc);
+        if (RT) {  // lrelu' of this gather lane's (edge, head) from the ballot: no shuffle
+          const float c = (cpos[t] >> (ei * H + q / G::QH)) & 1ull ? 1.f : slope;
+          accc = pk_fma(wq * c, xr, accc);
+        }
       }
 #pragma unroll
       for (int t = 0; t < EPL; ++t) {
@@ -343,6 +363,10 @@ edge_attn_fwd_bat_kernel(
     if (G::EPI > 1) {
 #pragma unroll
       for (int o = G::NQ; o < 64; o <<= 1) acc = pk_xor_add(acc, o);
+      if (RT) {
+#pragma unroll
+        for (int o = G::NQ; o < 64; o <<= 1) accc = pk_xor_add(accc, o);
+      }
     }
     const float lk = __shfl(l, q / G::QH);
     const float inv = lk > 0.f ? 1.f / lk : 0.f;
@@ -352,9 +376,17 @@ edge_attn_fwd_bat_kernel(
       // bf16 tables: the rounding residual too, so the backward's D = dU . u is exact
       if (sizeof(T) == 2 && u_lo != nullptr)
         pk_store(u_lo + (int64_t)row * G::D + G::V * q, pk_residual(uk));
+      if (RT) {  // uc in fp32 for either table type
+        const Pk<T> ck = pk_scale(accc, inv);
+        float* dst = uc + (int64_t)row * G::D + G::V * q;
+#pragma unroll
+        for (int v = 0; v < G::V; v += 4)
+          *reinterpret_cast<float4*>(dst + v) = make_float4(ck.v[v], ck.v[v + 1], ck.v[v + 2], ck.v[v + 3]);
+      }
     }
     const float lse_h = l > 0.f ? m + __logf(l) : -INFINITY;
     if (lane < H) lse[(int64_t)row * H + lane] = lse_h;
+    if (RT && lane < H) qc[(int64_t)row * H + lane] = l > 0.f ? lc / l : 0.f;
     if (attd != nullptr && end - start <= CEL) {
       // one chunk (every R15 row): its scores are still in registers -- the same values
       // the reload below would recompute, without the col -> er round trips
@@ -379,6 +411,13 @@ edge_attn_fwd_bat_kernel(
 }
 
 // --------------------------------------------------------------- backward rows ---
+// The gather-group loops unroll fully for fp32 and by BWR_UNR_BF16 for bf16 tables: the
+// kernel is latency-bound (R15 rows hold ~2.3 edges, so the first group is usually the
+// only one), and the fully unrolled bf16 v-branch variant held 129 VGPRs (3 waves/SIMD,
+// 2x the fp32 time) for groups it rarely runs.
+#ifndef BWR_UNR_BF16
+#define BWR_UNR_BF16 2
+#endif
 template <int H, int F, typename T, bool DV>
 __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
@@ -390,6 +429,7 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
     float* __restrict__ d_el, float* __restrict__ de, float* __restrict__ attd, int ld,
     T* __restrict__ d_hs) {
   using G = Geo<H, F, T>;
+  constexpr int UNR = sizeof(T) == 2 ? BWR_UNR_BF16 : G::CE / G::EPI;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
   const int g_e = G::QPL == 1 ? lane / G::NQ : 0;
@@ -440,7 +480,7 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
           w = __expf(s - lseh) * dropout_factor(dp, (uint64_t)e * H + h_s);
         }
         const int nvalid = min(G::CE, (int)(end - cs));
-#pragma unroll
+#pragma unroll UNR
         for (int g = 0; g < G::CE; g += G::EPI) {
           if (g >= nvalid) break;
           const int ei = g + g_e;
@@ -504,7 +544,7 @@ __global__ void __launch_bounds__(256) edge_attn_bwd_rows_kernel(
       }
       const int nvalid = min(G::CE, (int)(end - cs));
       float gsum = 0.f;
-#pragma unroll
+#pragma unroll UNR
       for (int g = 0; g < G::CE; g += G::EPI) {
         if (g >= nvalid) break;
         const int ei = g + g_e;
@@ -709,11 +749,15 @@ __host__ __device__ constexpr int rec_stride(int H) {
   return REC_PAD ? s : 3 * H;
 }
 
-template <int H, int F, typename T>
+// RT: the forward's row terms are given (uc, qc; see edge_attn_fwd_bat_kernel), so the
+// same pass also finishes d_el_i = dU_i . uc_i - D_i qc_i (0 on virtual rows) and the
+// column pass stores no per-edge de (no row sum follows).
+template <int H, int F, typename T, bool RT = false>
 __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
     int64_t n_rows, const float* __restrict__ el, const float* __restrict__ lse,
     const T* __restrict__ u, const T* __restrict__ u_lo, const T* __restrict__ dU,
-    float* __restrict__ rec) {
+    float* __restrict__ rec, const float* __restrict__ uc, const float* __restrict__ qc,
+    const uint8_t* __restrict__ rowflag, float* __restrict__ d_el) {
   using G = Geo<H, F, T>;
   constexpr int UNR = G::QPL == 1 ? 4 : 1;        // load groups per trip
   constexpr int RPW = G::EPI * UNR;               // rows per trip
@@ -746,6 +790,21 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
           dot += pk_dot(a[g][k], pk_load(u_lo + rr * G::D + G::V * q));
         }
         const float dk = group_sum<G::QH>(dot);
+        float dc = 0.f;
+        if (RT) {  // dU_i . uc_i over the head's pieces (uc is fp32 for either table type)
+          const int64_t rr = min(row, n_rows - 1);
+          const float* cp = uc + rr * G::D + G::V * q;
+          float cv = 0.f;
+#pragma unroll
+          for (int v = G::V - 4; v >= 0; v -= 4) {
+            const float4 c4 = *reinterpret_cast<const float4*>(cp + v);
+            cv = fmaf(a[g][k].v[v + 3], c4.w, cv);
+            cv = fmaf(a[g][k].v[v + 2], c4.z, cv);
+            cv = fmaf(a[g][k].v[v + 1], c4.y, cv);
+            cv = fmaf(a[g][k].v[v], c4.x, cv);
+          }
+          dc = group_sum<G::QH>(cv);
+        }
         // the head's first chunk lane writes D; el and lse ride along
         if (q % G::QH == 0 && row < n_rows) {
           const int h = q / G::QH;
@@ -753,6 +812,10 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
           r[h] = el[row * H + h];
           r[H + h] = lse[row * H + h];
           r[2 * H + h] = dk;
+          if (RT) {
+            const bool virt = rowflag != nullptr && rowflag[row] != 0;
+            d_el[row * H + h] = virt ? 0.f : fmaf(-dk, qc[row * H + h], dc);
+          }
         }
       }
     }
@@ -895,7 +958,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
       if (valid) {
         const float ds = att * (gsum * dropf - Dsi);
         const float dev = virt ? 0.f : ds * (pre > 0.f ? 1.f : slope);
-        de[(slot_de ? (int64_t)slot : eid) * H + h_s] = dev;
+        if (de != nullptr) de[(slot_de ? (int64_t)slot : eid) * H + h_s] = dev;
         xacc += dev;
       }
       i0 = i1;
@@ -1184,43 +1247,78 @@ static bool dtype_ok(int32_t dtype, int32_t feat) {
   return dtype == MSHA_DTYPE_F32 || (dtype == MSHA_DTYPE_BF16 && feat % 8 == 0);
 }
 
+// the batched-gather forward applies: one piece per lane, every table addressable by
+// 32-bit offsets
+static bool fwd_bat_ok(const msha_graph* g, int heads, int feat, int32_t dtype) {
+  const int64_t lim = (int64_t)1 << 31;
+  const int64_t esz = dtype == MSHA_DTYPE_BF16 ? 2 : 4;
+  return env_int("MSHA_FWD_BAT", 1) != 0 && (int64_t)heads * feat * esz <= 1024 &&
+         g->n_rows < lim && g->n_edges * 4 < lim && g->n_cols * 4 * heads < lim &&
+         g->n_cols * heads * feat * esz < lim;
+}
+
+extern "C" int msha_edge_attention_rowterms_preferred(const msha_graph* g, int32_t heads,
+                                                      int32_t feat, int32_t dtype) {
+  if (g == nullptr || !shape_supported(heads, feat) || !dtype_ok(dtype, feat)) return 0;
+  if (!fwd_bat_ok(g, heads, feat, dtype)) return 0;
+  // MSHA_ROWTERMS: 1 = always, 0 = never, default: once the per-edge de would leave the
+  // Infinity Cache (the regime where its CSC -> CSR crossing costs ~4x its bytes)
+  const int knob = env_int("MSHA_ROWTERMS", -1);
+  if (knob >= 0) return knob != 0;
+  return g->n_edges * 4 * (int64_t)heads >= DE_SLOT_MIN_BYTES ? 1 : 0;
+}
+
 extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
                                        int32_t dtype, const float* el, const float* er,
                                        const void* hc, float neg_slope, float drop_p,
                                        uint64_t seed, uint64_t offset, void* u, void* u_lo,
                                        float* lse, float* attd, msha_stream_t stream) {
+  return msha_edge_attention_fwd_ex(g, heads, feat, dtype, el, er, hc, neg_slope, drop_p, seed,
+                                    offset, u, u_lo, lse, attd, nullptr, nullptr, stream);
+}
+
+extern "C" int msha_edge_attention_fwd_ex(const msha_graph* g, int32_t heads, int32_t feat,
+                                          int32_t dtype, const float* el, const float* er,
+                                          const void* hc, float neg_slope, float drop_p,
+                                          uint64_t seed, uint64_t offset, void* u, void* u_lo,
+                                          float* lse, float* attd, float* uc, float* qc,
+                                          msha_stream_t stream) {
   if (int rc = check_graph(g, false)) return rc;
   MSHA_ARG_CHECK(el && er && hc && u && lse, "edge_attention_fwd: null pointer");
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_fwd: p must be in [0,1]");
+  MSHA_ARG_CHECK((uc == nullptr) == (qc == nullptr), "edge_attention_fwd: uc and qc go together");
   if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: unsupported (heads, feat, dtype)");
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
-  // batched-gather kernel: one piece per lane and every table addressable by 32-bit offsets
-  const int64_t lim = (int64_t)1 << 31;
-  const int64_t esz = dtype == MSHA_DTYPE_BF16 ? 2 : 4;
-  const bool bat = env_int("MSHA_FWD_BAT", 1) != 0 && (int64_t)heads * feat * esz <= 1024 &&
-                   g->n_rows < lim && g->n_edges * 4 < lim && g->n_cols * 4 * heads < lim &&
-                   g->n_cols * heads * feat * esz < lim;
+  const bool bat = fwd_bat_ok(g, heads, feat, dtype);
+  if (uc != nullptr && !bat)
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: row terms need the batched forward");
   if (bat) {
     const int64_t cap = env_int("MSHA_FWD_WAVES", 0);
     const dim3 grid = wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
 #define XB(h, f)                                                                               \
     if (heads == h && feat == f) {                                                             \
       if (dtype == MSHA_DTYPE_BF16) {                                                          \
-        if constexpr (f % 8 == 0 && h * f * 2 <= 1024)                                         \
-          hipLaunchKernelGGL((edge_attn_fwd_bat_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>()>), \
-                             grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,             \
+        if constexpr (f % 8 == 0 && h * f * 2 <= 1024) {                                       \
+          auto kern = uc != nullptr                                                            \
+              ? edge_attn_fwd_bat_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>(), true>          \
+              : edge_attn_fwd_bat_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>(), false>;        \
+          hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,       \
                              (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,  \
-                             er, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u,             \
-                             (bf16_t*)u_lo, lse, attd);                                        \
+                             er, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u,                 \
+                             (bf16_t*)u_lo, lse, attd, uc, qc);                                \
+        }                                                                                      \
       } else {                                                                                 \
-        if constexpr (h * f * 4 <= 1024)                                                       \
-          hipLaunchKernelGGL((edge_attn_fwd_bat_kernel<h, f, float, fwd_epl<h, f, float>()>),  \
-                             grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,             \
+        if constexpr (h * f * 4 <= 1024) {                                                     \
+          auto kern = uc != nullptr                                                            \
+              ? edge_attn_fwd_bat_kernel<h, f, float, fwd_epl<h, f, float>(), true>            \
+              : edge_attn_fwd_bat_kernel<h, f, float, fwd_epl<h, f, float>(), false>;          \
+          hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,       \
                              (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,  \
-                             er, (const float*)hc, neg_slope, dp, (float*)u, (float*)nullptr, \
-                             lse, attd);                                                       \
+                             er, (const float*)hc, neg_slope, dp, (float*)u, (float*)nullptr,  \
+                             lse, attd, uc, qc);                                               \
+        }                                                                                      \
       }                                                                                        \
     }
     MSHA_FOR_EACH_SHAPE(XB)
@@ -1383,7 +1481,9 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
                              const float* er, const void* hc, const float* lse, const void* u,
                              const void* u_lo, const void* dU, float neg_slope, const Dropout& dp, float* d_el,
                              float* d_er, void* d_hc, float* de, float* rec, float* part,
-                             float* part_x, hipStream_t s) {
+                             float* part_x, const float* uc, const float* qc, hipStream_t s) {
+  const bool rt = uc != nullptr;  // row terms: d_el in the row pass, no de, no row sum
+  if (rt) de = nullptr;
   // the buffer-descriptor kernel addresses each table with 32-bit byte offsets
   const int64_t lim = (int64_t)1 << 31;
   // de in CSC slot order (contiguous writes, gathered by the row sum) once it outgrows
@@ -1396,8 +1496,12 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
 #define X(h, f)                                                                                \
   if (heads == h && feat == f) {                                                               \
     if constexpr (f % Pk<T>::V == 0) {                                                         \
-      hipLaunchKernelGGL((bwd_row_stats_kernel<h, f, T>), wave_grid(g->n_rows / 8 + 1), dim3(256), 0,  \
-                         s, g->n_rows, el, lse, (const T*)u, (const T*)u_lo, (const T*)dU, rec); \
+      auto row_stats = rt ? bwd_row_stats_kernel<h, f, T, true>                                \
+                          : bwd_row_stats_kernel<h, f, T, false>;                              \
+      hipLaunchKernelGGL(row_stats,                                                            \
+                         wave_grid(g->n_rows / 8 + 1), dim3(256), 0, s, g->n_rows, el, lse,   \
+                         (const T*)u, (const T*)u_lo, (const T*)dU, rec, uc, qc, g->rowflag,  \
+                         d_el);                                                                \
       if (f * sizeof(T) <= 64 && COLS_EH && buf_ok)                                            \
         hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
@@ -1415,8 +1519,9 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
                            de, (T*)d_hc, d_er,                                                 \
                            part, part_x);                                                      \
       }                                                                                        \
-      hipLaunchKernelGGL((bwd_row_sum_kernel<h>), wave_grid(g->n_rows), dim3(256), 0, s,       \
-                         g->rowptr, g->n_rows, de, slot_de ? g->csr_slot : nullptr, d_el);    \
+      if (!rt)                                                                                 \
+        hipLaunchKernelGGL((bwd_row_sum_kernel<h>), wave_grid(g->n_rows), dim3(256), 0, s,     \
+                           g->rowptr, g->n_rows, de, slot_de ? g->csr_slot : nullptr, d_el);  \
     }                                                                                          \
   }
   MSHA_FOR_EACH_SHAPE(X)
@@ -1437,11 +1542,23 @@ extern "C" int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads,
                                              uint64_t seed, uint64_t offset, float* d_el,
                                              float* d_er, void* d_hc, float* de, void* ws,
                                              size_t ws_bytes, msha_stream_t stream) {
+  return msha_edge_attention_bwd_fused_ex(g, heads, feat, dtype, el, er, hc, lse, u, u_lo, dU,
+                                          neg_slope, drop_p, seed, offset, nullptr, nullptr,
+                                          d_el, d_er, d_hc, de, ws, ws_bytes, stream);
+}
+
+extern "C" int msha_edge_attention_bwd_fused_ex(
+    const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype, const float* el,
+    const float* er, const void* hc, const float* lse, const void* u, const void* u_lo,
+    const void* dU, float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
+    const float* uc, const float* qc, float* d_el, float* d_er, void* d_hc, float* de, void* ws,
+    size_t ws_bytes, msha_stream_t stream) {
   if (int rc = check_graph(g, true)) return rc;
   MSHA_ARG_CHECK(el && er && hc && lse && u && dU && d_el && d_er && d_hc,
                  "edge_attention_bwd_fused: null pointer");
-  MSHA_ARG_CHECK(g->n_edges == 0 || (de && g->csc_eid),
-                 "edge_attention_bwd_fused: needs de scratch and csc_eid");
+  MSHA_ARG_CHECK((uc == nullptr) == (qc == nullptr), "edge_attention_bwd_fused: uc and qc go together");
+  MSHA_ARG_CHECK(g->n_edges == 0 || ((de || uc) && g->csc_eid),
+                 "edge_attention_bwd_fused: needs de scratch (or row terms) and csc_eid");
   MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_bwd_fused: p must be in [0,1]");
   if (!shape_supported(heads, feat) || !dtype_ok(dtype, feat))
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_fused: unsupported (heads, feat, dtype)");
@@ -1457,9 +1574,9 @@ extern "C" int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads,
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
   if (dtype == MSHA_DTYPE_BF16)
     launch_bwd_fused<bf16_t>(g, heads, feat, el, er, hc, lse, u, u_lo, dU, neg_slope, dp, d_el, d_er,
-                             d_hc, de, rec, part, part_x, s);
+                             d_hc, de, rec, part, part_x, uc, qc, s);
   else
     launch_bwd_fused<float>(g, heads, feat, el, er, hc, lse, u, nullptr, dU, neg_slope, dp, d_el, d_er,
-                            d_hc, de, rec, part, part_x, s);
+                            d_hc, de, rec, part, part_x, uc, qc, s);
   return check_launch("edge_attention_bwd_fused");
 }

@@ -690,6 +690,11 @@ static void launch_ho(const GemmArgs& p, int splits, hipStream_t s) {
 static int gemm_run(GemmArgs& p, int ho, float beta, int32_t splits, void* ws, size_t ws_bytes,
                     hipStream_t s) {
   const int64_t M = p.M, N = p.N, K = p.K;
+  // dX = (dh + de (x) a) W^T with W^T given as W (N, K) row-major: resident-W kernel
+  if (ho == HO_A && beta == 0.f && p.sAk == 1 && p.sAm == K && p.sBk == 1 && p.sBn == K &&
+      p.ldc == N &&
+      skinny_dx(M, N, K, p.A, p.B, p.C, p.hH, p.hF, p.de, p.ha, p.de2, p.ha2, s))
+    return check_launch("gemm_f32");
   if (ho != HO_A && p.slab == nullptr &&
       skinny_wgrad(M, N, K, p.A, p.sAm, p.sAk, p.B, p.sBk, p.sBn, p.C, p.ldc, beta, splits, ws,
                    ws_bytes, p.hH, p.hF, ho == HO_B ? p.de : nullptr, p.ha, p.de2, p.ha2, s))

@@ -169,10 +169,15 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 // in chunk order: one wave per (b, kind, chunk) keeps thousands of members in flight.
 constexpr int kGatherChunk = 64;  // one member per lane for the keep-bit draw
 
+// bf16 tables: a lane takes two adjacent elements per 4-byte load (EL = 2), so a wave
+// reads a 128-element row slice per instruction as the fp32 kernel does; every element's
+// sum over the members keeps its order (same bits as one element per lane).
 template <typename T, int KD>
 __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
                                                               const T* __restrict__ dU,
                                                               int nck, float* __restrict__ Gp) {
+  constexpr int EL = (sizeof(T) == 2 && KD > 1) ? 2 : 1;  // elements per lane per slot
+  constexpr int KE = KD / EL;                              // slots per lane
   const int lane = lane_id();
   const int D = a.H * a.F;
   const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -187,9 +192,11 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
   const int32_t grp = kind == 0 ? a.gid3[i] : a.gid4[i];
   const int32_t m0 = gptr[grp] + c * kGatherChunk;
   const int32_t m1 = min(gptr[grp + 1], m0 + kGatherChunk);
-  float acc[KD];
+  float acc[KE][EL];
 #pragma unroll
-  for (int k = 0; k < KD; ++k) acc[k] = 0.f;
+  for (int k = 0; k < KE; ++k)
+#pragma unroll
+    for (int e = 0; e < EL; ++e) acc[k][e] = 0.f;
   // members of this chunk: lane j draws the keep bits of (b, member j) for every head
   const int cnt = m1 - m0;  // <= kGatherChunk == 64
   const int64_t nj = lane < cnt ? (int64_t)gmem[m0 + lane] : 0;
@@ -203,7 +210,7 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
   // at a time): GU gathers in flight per wave instead of one
   constexpr int GU = 8;
   for (int t0 = 0; t0 < cnt; t0 += GU) {
-    float v[GU][KD];
+    float v[GU][KE][EL];
     int64_t nn[GU];
     uint32_t kk[GU];
 #pragma unroll
@@ -211,33 +218,44 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
       nn[u] = __shfl(nj, t0 + u);  // lanes past cnt hold member 0: a valid row, unused
       kk[u] = __shfl(kbits, t0 + u);
 #pragma unroll
-      for (int k = 0; k < KD; ++k) {
-        const int d = lane + 64 * k;
-        v[u][k] = d < D ? to_f32(dU[nn[u] * D + d]) : 0.f;
+      for (int k = 0; k < KE; ++k) {
+        const int d = (lane + 64 * k) * EL;
+        if constexpr (EL == 2) {
+          const uint32_t w = d < D ? *reinterpret_cast<const uint32_t*>(dU + nn[u] * D + d) : 0u;
+          v[u][k][0] = __uint_as_float(w << 16);
+          v[u][k][1] = __uint_as_float(w & 0xffff0000u);
+        } else {
+          v[u][k][0] = d < D ? to_f32(dU[nn[u] * D + d]) : 0.f;
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < GU; ++u) {
       if (t0 + u >= cnt) break;
 #pragma unroll
-      for (int k = 0; k < KD; ++k) {
-        const int d = lane + 64 * k;
-        if (d < D) {
-          const int h = d / a.F;
-          float drop = 1.f;
-          if (a.dp.active)
-            drop = h < 32 ? (((kk[u] >> h) & 1u) ? a.dp.scale : 0.f)
-                          : intra_drop(a.dp, kind, h, (uint64_t)b * a.N + nn[u]);
-          acc[k] = fmaf(drop, v[u][k], acc[k]);
+      for (int k = 0; k < KE; ++k) {
+#pragma unroll
+        for (int e = 0; e < EL; ++e) {
+          const int d = (lane + 64 * k) * EL + e;
+          if (d < D) {
+            const int h = d / a.F;
+            float drop = 1.f;
+            if (a.dp.active)
+              drop = h < 32 ? (((kk[u] >> h) & 1u) ? a.dp.scale : 0.f)
+                            : intra_drop(a.dp, kind, h, (uint64_t)b * a.N + nn[u]);
+            acc[k][e] = fmaf(drop, v[u][k][e], acc[k][e]);
+          }
         }
       }
     }
   }
 #pragma unroll
-  for (int k = 0; k < KD; ++k) {
-    const int d = lane + 64 * k;
-    if (d < D) Gp[(bk * nck + c) * D + d] = acc[k];
-  }
+  for (int k = 0; k < KE; ++k)
+#pragma unroll
+    for (int e = 0; e < EL; ++e) {
+      const int d = (lane + 64 * k) * EL + e;
+      if (d < D) Gp[(bk * nck + c) * D + d] = acc[k][e];
+    }
 }
 
 __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, int D, int nck,

@@ -488,6 +488,125 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_bf16_kernel(
   }
 }
 
+// ------------------------------------------------ input gradient of the projection ---
+// dX = (dh + d1 (x) a1 [+ d2 (x) a2]) W^T (msha_gemm_f32_head_outer, operand 0; the
+// backward of Ablation.py:262 / Ours.py:58 for the source table): the projection's
+// structure with W^T resident (W (N, K) row-major transposed at the fill, as pair_kernel
+// does with nn.Linear's weight) and the head-outer term folded into the A operand at the
+// MFMA step, in the tiled kernel's fma order fma(d2, a2, fma(d1, a1, x)).  a1 / a2 sit in
+// LDS; a lane's KL contiguous columns span at most two heads (hF >= KL / 2), whose d1 /
+// d2 values load with the tile.  Tiles, prefetch and epilogue as proj_kernel.
+template <int K, int N>
+__global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
+    int M, const float* __restrict__ Dh, const float* __restrict__ Wt,
+    const float* __restrict__ d1, const float* __restrict__ a1, const float* __restrict__ d2,
+    const float* __restrict__ a2, int hH, int hF, float* __restrict__ out) {
+  using Gm = ProjGeo<float, K, N>;
+  __shared__ __attribute__((aligned(16))) char smem[Gm::WBYTES + kProjWaves * Gm::SBYTES + 8 * K];
+  float* Wl = reinterpret_cast<float*>(smem);
+  float* a1s = reinterpret_cast<float*>(smem + Gm::WBYTES + kProjWaves * Gm::SBYTES);
+  float* a2s = a1s + K;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // B[k][n] = W[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL
+  for (int idx = tid; idx < K * N; idx += 64 * kProjWaves) {
+    const int n = idx / K, k = idx % K;
+    Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = Wt[idx];
+  }
+  for (int k = tid; k < K; k += 64 * kProjWaves) {
+    a1s[k] = a1[k];
+    a2s[k] = a2 != nullptr ? a2[k] : 0.f;
+  }
+  __syncthreads();
+
+  float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
+  const int cl = (lane % Gm::LPR) * Gm::EPL;
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kProjWaves;
+  const int tiles = (M + 15) / 16;
+  if (gw >= tiles) return;
+
+  const rsrc_t r_x = make_rsrc(Dh, (uint32_t)((int64_t)M * K * 4));
+  const rsrc_t r_d1 = make_rsrc(d1, (uint32_t)((int64_t)M * hH * 4));
+  const rsrc_t r_d2 = make_rsrc(d2, d2 != nullptr ? (uint32_t)((int64_t)M * hH * 4) : 0u);
+  const int h0 = (g * Gm::KL) / hF;  // first head of this lane's columns
+  struct Tile {
+    u32x4_t x[Gm::NLD];
+    float e1[2], e2[2];
+  };
+  auto load_tile = [&](int t, Tile& b) {
+    const int row = t * 16 + r16;
+    const uint32_t off = row < M ? (uint32_t)row * (K * 4u) + (uint32_t)(g * Gm::KL * 4) : kOOB;
+#pragma unroll
+    for (int i = 0; i < Gm::NLD; ++i) b.x[i] = buf_b128(r_x, off + 16u * i);
+    const uint32_t eo = row < M ? (uint32_t)row * (uint32_t)hH * 4u + 4u * h0 : kOOB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // a second head only when hF < KL (reads 0 otherwise)
+      const uint32_t o = (j == 0 || hF < Gm::KL) ? eo + 4u * j : kOOB;
+      b.e1[j] = buf_f32(r_d1, o);
+      b.e2[j] = buf_f32(r_d2, o);
+    }
+  };
+  auto tile = [&](int t, const Tile& cur) {
+    f32x4 acc[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* Wf = Wl + g * Gm::PW + r16;
+    const float* a1l = a1s + g * Gm::KL;
+    const float* a2l = a2s + g * Gm::KL;
+    float bc[Gm::NB], bn[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) bc[c] = Wf[c * 16];
+#pragma unroll
+    for (int s = 0; s < Gm::S; ++s) {
+      if (s + 1 < Gm::S) {
+#pragma unroll
+        for (int c = 0; c < Gm::NB; ++c) bn[c] = Wf[4 * (s + 1) * Gm::PW + c * 16];
+      }
+      const int hi = s >= hF ? 1 : 0;
+      const float av1 = a1l[s], av2 = a2l[s];
+      __builtin_amdgcn_sched_barrier(0);
+      const float x = __uint_as_float(cur.x[s >> 2][s & 3]);
+      const float a = fmaf(cur.e2[hi], av2, fmaf(cur.e1[hi], av1, x));
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c) bc[c] = bn[c];
+    }
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * Gm::TPS + c * 16 + r16] = acc[c][i];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int pass = 0; pass < 16 / Gm::RPP; ++pass) {
+      const int rr = pass * Gm::RPP + lane / Gm::LPR;
+      const int row = t * 16 + rr;
+      const float4 v = *reinterpret_cast<const float4*>(Tw + rr * Gm::TPS + cl);
+      if (row < M) *reinterpret_cast<float4*>(out + (int64_t)row * N + cl) = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  };
+  Tile ta, tb;
+  load_tile(gw, ta);
+  for (int t = gw; t < tiles; t += 2 * nw) {
+    load_tile(t + nw, tb);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t, ta);
+    if (t + nw >= tiles) break;
+    load_tile(t + 2 * nw, ta);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(t + nw, tb);
+  }
+}
+
 // ------------------------------------------------------------- weight gradient ---
 // dW[a, n] = sum_r X[r, a] * (D[r, n] + d1[r, n / hF] a1[n] + d2[r, n / hF] a2[n]),
 // a, n < 128.  A wave owns one column half nh (64 columns) of dW for a row range:
@@ -774,6 +893,28 @@ int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int6
   }
   SKPB(128, 128) SKPB(64, 128) SKPB(128, 64) SKPB(64, 64)
 #undef SKPB
+  return 0;
+}
+
+// dX (M x N) = (dh + d1 (x) a1 [+ d2 (x) a2]) W^T with W (N, K) row-major (the
+// projection's input gradient): K, N in {64, 128}, hF >= 16 dividing K, C row-major
+// (ldc = N); 0 = not covered (the caller runs the tiled head-outer GEMM)
+int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, float* C,
+              int hH, int hF, const float* d1, const float* a1, const float* d2, const float* a2,
+              hipStream_t s) {
+  if (!skinny_enabled() || M < 1024 || M * K * 4 >= (1ll << 31) || M * hH * 4 >= (1ll << 31))
+    return 0;
+  if (hF < 16 || K % hF != 0 || (int64_t)hH * hF != K || d1 == nullptr || a1 == nullptr) return 0;
+  if (((uintptr_t)Dh | (uintptr_t)C) & 15) return 0;
+  const dim3 grid(proj_grid(M)), block(64 * sk::kProjWaves);
+#define SKDX(k, n)                                                                              \
+  if (K == k && N == n) {                                                                       \
+    hipLaunchKernelGGL((sk::dx_kernel<k, n>), grid, block, 0, s, (int)M, Dh, W, d1, a1, d2, a2, \
+                       hH, hF, C);                                                              \
+    return 1;                                                                                   \
+  }
+  SKDX(128, 128) SKDX(64, 128) SKDX(128, 64) SKDX(64, 64)
+#undef SKDX
   return 0;
 }
 

@@ -114,10 +114,17 @@ class _EdgeAttention(torch.autograd.Function):
         attd = None
         if hs is not None:
             attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
+        # row terms for the u-only fused backward on large graphs (include/msha_gnn.h
+        # msha_edge_attention_fwd_ex): d_el without a per-edge de crossing CSC -> CSR
+        uc = qc = None
+        if (hs is None and FUSED_BWD and ctx.needs_input_grad[0] and ROWTERMS
+                and _lib.load().msha_edge_attention_rowterms_preferred(g, H, F, _code(dt))):
+            uc = torch.empty(n, H, F, device=dev, dtype=torch.float32)
+            qc = torch.empty(n, H, device=dev, dtype=torch.float32)
         ev = _timed("edge_attention_fwd")
-        _lib.call("msha_edge_attention_fwd", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
+        _lib.call("msha_edge_attention_fwd_ex", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
                   hc.data_ptr(), slope, p, seed, 0, u.data_ptr(), _lib.ptr(u_lo),
-                  lse.data_ptr(), _lib.ptr(attd), s)
+                  lse.data_ptr(), _lib.ptr(attd), _lib.ptr(uc), _lib.ptr(qc), s)
         if ev is not None:
             ev[1].record()
         v = None
@@ -126,15 +133,17 @@ class _EdgeAttention(torch.autograd.Function):
             _csc_aggregate(graph, H, F, attd, None, hs, v, None, s)
         ctx.graph, ctx.p, ctx.seed, ctx.slope = graph, p, seed, slope
         ctx.has_hs = hs is not None
+        ctx.rowterms = uc is not None
         ctx.save_for_backward(el, er, hc, hs if hs is not None else el.new_empty(0), lse, u,
-                              u_lo if u_lo is not None else el.new_empty(0))
+                              u_lo if u_lo is not None else el.new_empty(0),
+                              *((uc, qc) if uc is not None else ()))
         if v is None:
             return u
         return u, v
 
     @staticmethod
     def backward(ctx, dU, dV=None):
-        el, er, hc, hs, lse, u, u_lo = ctx.saved_tensors
+        el, er, hc, hs, lse, u, u_lo, *rowterms = ctx.saved_tensors
         u_lo = u_lo if u_lo.numel() else None
         graph = ctx.graph
         n, H = el.shape
@@ -149,7 +158,7 @@ class _EdgeAttention(torch.autograd.Function):
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
         if not use_dv and FUSED_BWD:
-            return _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs)
+            return _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms)
         # one (de, attd) record of 2H floats per edge: the column pass reads it as one
         # 64-B segment at C4 (the CSC visits edges in random order)
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)
@@ -178,9 +187,12 @@ class _EdgeAttention(torch.autograd.Function):
 # u-only backward as one column pass (msha_edge_attention_bwd_fused) instead of
 # bwd_rows + csc_aggregate; same bits.  Module switch for A/B measurements.
 FUSED_BWD = True
+# row terms (uc, qc) from the forward where the library prefers them (large graphs);
+# module switch for A/B measurements
+ROWTERMS = True
 
 
-def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs):
+def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms=()):
     graph = ctx.graph
     n, H = el.shape
     m, _, F = hc.shape
@@ -189,17 +201,19 @@ def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs):
     g = graph.desc
     if not graph.has_csc:
         raise RuntimeError("graph has no CSC view (build it with_csc=True)")
-    de = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
+    uc, qc = rowterms if rowterms else (None, None)
+    de = None if uc is not None else torch.empty(max(graph.n_edges, 1), H, device=dev,
+                                                 dtype=torch.float32)
     wsb = int(_lib.load().msha_edge_attention_bwd_fused_workspace_size(g, H, F))
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     d_hc = torch.empty(m, H, F, device=dev, dtype=hc.dtype)
     d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
     ev = _timed("edge_attention_bwd_fused")
-    _lib.call("msha_edge_attention_bwd_fused", g, H, F, _code(hc.dtype), el.data_ptr(),
+    _lib.call("msha_edge_attention_bwd_fused_ex", g, H, F, _code(hc.dtype), el.data_ptr(),
               er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), _lib.ptr(u_lo),
-              dU.data_ptr(),
-              ctx.slope, ctx.p, ctx.seed, 0, d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
-              de.data_ptr(), ws.data_ptr(), wsb, s)
+              dU.data_ptr(), ctx.slope, ctx.p, ctx.seed, 0, _lib.ptr(uc), _lib.ptr(qc),
+              d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(), _lib.ptr(de), ws.data_ptr(),
+              wsb, s)
     if ev is not None:
         ev[1].record()
     d_hs = torch.zeros_like(hs) if ctx.has_hs else None

@@ -46,6 +46,15 @@ def test_algorithmic_bytes_match_design():
         return stats + cols + 4 * (n + 1) + E * (4 * H + slot) + n * 4 * H
     assert b == by_hand(e, 0)
     assert bench.bwd_fused_bytes(n, m, 40 * e, H, F, nch) == by_hand(40 * e, 4)
+    # with the forward's row terms: no de write, no row sum; the row stats read uc, qc
+    # and the row flag and write d_el; the forward writes uc and qc
+    D = H * F
+    rt = bench.bwd_fused_bytes(n, m, 40 * e, H, F, nch, rowterms=True)
+    assert rt == by_hand(40 * e, 4) - 40 * e * 4 * H - (4 * (n + 1) + 40 * e * (4 * H + 4)
+                                                        + n * 4 * H) \
+        + n * (4 * D + 4 * H + 1 + 4 * H)
+    assert bench.fwd_bytes(n, m, e, H, F, 4, True) - bench.fwd_bytes(n, m, e, H, F) == \
+        n * (4 * D + 4 * H)
 
 
 def test_pmc_traffic_reads_newest_profile():

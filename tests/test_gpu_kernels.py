@@ -4,6 +4,8 @@ Index/graph outputs are checked bit-exact; attention weights to 1e-5 absolute an
 embeddings / gradients to 1e-5 relative (fp32, BASELINE.json north_star), with a
 scale-relative absolute floor where magnitudes are large.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -156,8 +158,12 @@ def test_edge_attention_fwd_bwd(cuda, msha, case, p):
     tol_close(ths.grad.cpu().numpy(), bw["d_hs"], EMB_RTOL, 1e-5)
 
 
-def _u_only_grads(MF, graph, el, er, hc, dU, p, seed, dev, dtype, fused):
+def _u_only_grads(MF, graph, el, er, hc, dU, p, seed, dev, dtype, fused, rowterms=None):
+    """rowterms: True / False force the fused backward's row terms on / off
+    (MSHA_ROWTERMS), None leaves the library's per-graph choice."""
     MF.FUSED_BWD = fused
+    if rowterms is not None:
+        os.environ["MSHA_ROWTERMS"] = "1" if rowterms else "0"
     try:
         tel, ter = (t(x, dev).requires_grad_(True) for x in (el, er))
         thc = t(hc, dev, dtype).requires_grad_(True)
@@ -166,6 +172,7 @@ def _u_only_grads(MF, graph, el, er, hc, dU, p, seed, dev, dtype, fused):
         return u.detach(), tel.grad, ter.grad, thc.grad
     finally:
         MF.FUSED_BWD = True
+        os.environ.pop("MSHA_ROWTERMS", None)
 
 
 def _same_as_split(got, split, dtype=torch.float32):
@@ -205,6 +212,38 @@ def test_edge_attention_fused_backward(cuda, msha, case, p):
     tol_close(got[1].cpu().numpy(), bw["d_el"], 1e-4, 1e-5)
     tol_close(got[2].cpu().numpy(), bw["d_er"], 1e-4, 1e-5)
     tol_close(got[3].cpu().numpy(), bw["d_hc"], EMB_RTOL, 1e-5)
+    # row terms forced on (the large-graph path: d_el = dU . uc - D qc in the row pass,
+    # no per-edge de): u, d_er, d_hc are the same bits, d_el matches the oracle
+    rt = _u_only_grads(MF, graph, el, er, hc, dU, p, seed, cuda, torch.float32, True,
+                       rowterms=True)
+    for a, b, name in zip(rt, got, ("u", "d_el", "d_er", "d_hc")):
+        if name != "d_el":
+            assert torch.equal(a, b), name
+    tol_close(rt[1].cpu().numpy(), bw["d_el"], 1e-4, 1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_rowterms_multichunk_and_virtual_rows(cuda, msha, dtype):
+    """Row terms on the full 2015 graph (multi-chunk columns, virtual rows) with dropout:
+    d_el from (uc, qc) within the north_star bar of the de row sum; everything else the
+    same bits."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    g, c = _r15_counts()
+    rng = np.random.default_rng(12)
+    n, m, H, F = int(g["n"]), 32, 2, 64
+    graph = Graph.from_dense(t(c, cuda))
+    el = rng.standard_normal((n, H)).astype(np.float32)
+    er = rng.standard_normal((m, H)).astype(np.float32)
+    hc = rng.standard_normal((m, H, F)).astype(np.float32)
+    dU = rng.standard_normal((n, H, F)).astype(np.float32)
+    base = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True)
+    rt = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True, rowterms=True)
+    for a, b, name in zip(rt, base, ("u", "d_el", "d_er", "d_hc")):
+        if name != "d_el":
+            assert torch.equal(a, b), name
+    tol_close(rt[1].cpu().numpy(), base[1].cpu().numpy(), 1e-5, 1e-5)
 
 
 def test_edge_attention_fused_backward_bf16_multichunk(cuda, msha):
@@ -399,10 +438,15 @@ def test_project_scores_fwd_bwd(cuda, M, K, H, F):
                                                  (1, 5000, 2, 64, 96, False),
                                                  (1, 50015, 2, 64, 128, True),
                                                  (0, 3000, 8, 16, 128, True),
+                                                 (0, 39179, 2, 64, 128, True),
+                                                 (0, 4096, 4, 32, 64, False),
+                                                 (0, 2048, 1, 64, 64, True),
                                                  (0, 517, 1, 8, 40, False)])
 def test_gemm_head_outer(cuda, operand, M, H, F, K, two):
     """dX = (dh + de (x) a) W^T (operand 0) and dW = X^T (dh + de (x) a) (operand 1)
-    with the sum folded into the operand loads, vs torch fp64."""
+    with the sum folded into the operand loads, vs torch fp64.  Operand 0 with M >= 1024,
+    D and the output width in {64, 128} runs the resident-W kernel (skinny.hip
+    dx_kernel; one or two heads per lane's 32 columns), the rest the tiled GEMM."""
     from msha_gnn_amd import functional as MF
 
     rng = np.random.default_rng(M + operand)
@@ -621,10 +665,12 @@ def test_spmm_both_directions(cuda, msha, n, m, D, dt):
 
 
 def test_edge_attention_fused_backward_slot_order(cuda, msha):
-    """A graph whose de scratch (E x H fp32) exceeds 192 MB: the fused backward keeps
-    de in CSC slot order (written contiguously, gathered through graph.csr_slot by the
-    row sum).  Same bits as the split backward for u, d_el, d_er; d_hc within the
-    reordered-sum bound."""
+    """A graph whose de scratch (E x H fp32) exceeds 192 MB: with row terms off, the
+    fused backward keeps de in CSC slot order (written contiguously, gathered through
+    graph.csr_slot by the row sum): same bits as the split backward for u, d_el, d_er;
+    d_hc within the reordered-sum bound.  With the library's default at this size (row
+    terms on): u, d_er, d_hc the same bits as that, d_el within the fp32 bar of the
+    split backward's row sum (it is exactly 0 where the row sum leaves rounding noise)."""
     import bench
     from msha_gnn_amd import functional as MF
     from msha_gnn_amd.graph import Graph
@@ -641,9 +687,16 @@ def test_edge_attention_fused_backward_slot_order(cuda, msha):
     er = rng.standard_normal((n, H)).astype(np.float32)
     hc = rng.standard_normal((n, H, F)).astype(np.float32)
     dU = rng.standard_normal((n, H, F)).astype(np.float32)
-    got = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, True)
+    assert MF._lib.load().msha_edge_attention_rowterms_preferred(graph.desc, H, F, 0) == 1
+    got = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, True,
+                        rowterms=False)
     split = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, False)
     _same_as_split(got, split)
+    rt = _u_only_grads(MF, graph, el, er, hc, dU, 0.2, 5, cuda, torch.float32, True)
+    for a, b, name in zip(rt, got, ("u", "d_el", "d_er", "d_hc")):
+        if name != "d_el":
+            assert torch.equal(a, b), name
+    tol_close(rt[1].cpu().numpy(), split[1].cpu().numpy(), 1e-5, 1e-5)
 
 
 @pytest.mark.parametrize("K,N", [(128, 128), (64, 128), (128, 64)])

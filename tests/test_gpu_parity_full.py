@@ -108,6 +108,18 @@ def test_c4_forward_backward_every_row(cuda, c4, dt):
     tol_close(_np64(el_l.grad), d_el_ref, tol, tol)
     tol_close(_np64(er_l.grad), d_er_ref, tol, tol)
     tol_close(_np64(hc_l.grad), d_hc_ref, tol, tol)
+    # the large-graph backward (row terms from the forward, no per-edge de; C4's de is
+    # below the switch-over, so force it): d_el against the same fp64 reference, d_er and
+    # d_hc the same bits as above
+    os.environ["MSHA_ROWTERMS"] = "1"
+    try:
+        el_r, er_r = (x.detach().clone().requires_grad_(True) for x in (el, er))
+        hc_r = h.detach().view(n, H, Fd).clone().requires_grad_(True)
+        MF.edge_attention(graph, el_r, er_r, hc_r).backward(dU)
+    finally:
+        os.environ.pop("MSHA_ROWTERMS")
+    tol_close(_np64(el_r.grad), d_el_ref, tol, tol)
+    assert torch.equal(er_r.grad, er_l.grad) and torch.equal(hc_r.grad, hc_l.grad)
 
     # end-to-end gradients: h is both the gathered table and the score source
     dh_ref = d_hc_ref + d_el_ref[:, :, None] * al64[None] + d_er_ref[:, :, None] * ar64[None]
