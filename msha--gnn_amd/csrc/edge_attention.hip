@@ -1261,10 +1261,13 @@ extern "C" int msha_edge_attention_rowterms_preferred(const msha_graph* g, int32
                                                       int32_t feat, int32_t dtype) {
   if (g == nullptr || !shape_supported(heads, feat) || !dtype_ok(dtype, feat)) return 0;
   if (!fwd_bat_ok(g, heads, feat, dtype)) return 0;
-  // MSHA_ROWTERMS: 1 = always, 0 = never, default: once the per-edge de would leave the
-  // Infinity Cache (the regime where its CSC -> CSR crossing costs ~4x its bytes)
+  // MSHA_ROWTERMS: 1 = always, 0 = never.  Default: fp32 tables always (C4: step 0.507 ->
+  // 0.494 ms, syn2m 11.70 -> 10.94 ms); bf16 tables once the per-edge de would leave the
+  // Infinity Cache (the fp32 uc doubles the bf16 forward's output bytes: neutral at C4,
+  // 7.34 -> 7.04 ms at syn2m)
   const int knob = env_int("MSHA_ROWTERMS", -1);
   if (knob >= 0) return knob != 0;
+  if (dtype == MSHA_DTYPE_F32) return 1;
   return g->n_edges * 4 * (int64_t)heads >= DE_SLOT_MIN_BYTES ? 1 : 0;
 }
 

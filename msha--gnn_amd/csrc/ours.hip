@@ -400,7 +400,9 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       }
     }
   } else {
-    for (int64_t t = threadIdx.x; t < B * D; t += blockDim.x) {
+    // mode 1 runs on a grid: block k takes items [k, k + gridDim.x, ...) * blockDim.x
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < B * D;
+         t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t b = t / D;
       const int d = (int)(t % D);
       const int h = d / F;
@@ -515,7 +517,10 @@ static void launch_bwd(const OursArgs& a, int stage, int64_t B, int nck, int hea
     hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(1), dim3(1024), 0, s, a, 0, bstat,
                        (const float*)G, bgrad, row_coef, da3s, da4s, (T*)nullptr);
   } else {
-    hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(1), dim3(1024), 0, s, a, 1, bstat,
+    // mode 1 (d_hs of the batch rows) is independent per (b, d): one thread per item
+    // on a grid (single workgroup: ~20 us, grid: 13 us at B = 64, D = 128)
+    hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(grid_for(B * heads * feat, 1024, 256)),
+                       dim3(1024), 0, s, a, 1, bstat,
                        (const float*)G, bgrad, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, (T*)d_hs);
   }

@@ -203,7 +203,8 @@ def test_edge_attention_fused_backward(cuda, msha, case, p):
     c, rowptr, col, empty, el, er, hc, hs, dU, dV = _edge_case(rng, n, m, H, F, max_deg, **kw)
     graph = Graph.from_dense(t(c, cuda))
     seed = 7
-    got = _u_only_grads(MF, graph, el, er, hc, dU, p, seed, cuda, torch.float32, True)
+    got = _u_only_grads(MF, graph, el, er, hc, dU, p, seed, cuda, torch.float32, True,
+                        rowterms=False)
     split = _u_only_grads(MF, graph, el, er, hc, dU, p, seed, cuda, torch.float32, False)
     _same_as_split(got, split)
     keep = _keep_mask(graph.n_edges, H, p, seed, cuda)
@@ -238,7 +239,7 @@ def test_rowterms_multichunk_and_virtual_rows(cuda, msha, dtype):
     er = rng.standard_normal((m, H)).astype(np.float32)
     hc = rng.standard_normal((m, H, F)).astype(np.float32)
     dU = rng.standard_normal((n, H, F)).astype(np.float32)
-    base = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True)
+    base = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True, rowterms=False)
     rt = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True, rowterms=True)
     for a, b, name in zip(rt, base, ("u", "d_el", "d_er", "d_hc")):
         if name != "d_el":
@@ -261,7 +262,7 @@ def test_edge_attention_fused_backward_bf16_multichunk(cuda, msha):
     hc = rng.standard_normal((m, H, F)).astype(np.float32)
     dU = rng.standard_normal((n, H, F)).astype(np.float32)
     for dtype in (torch.float32, torch.bfloat16):
-        got = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True)
+        got = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, True, rowterms=False)
         split = _u_only_grads(MF, graph, el, er, hc, dU, 0.5, 3, cuda, dtype, False)
         _same_as_split(got, split, dtype)
 
@@ -293,7 +294,7 @@ def test_edge_attention_fused_backward_wide_rows(cuda, msha, H, F, dtype):
     assert graph._plan["n_multi"] > 0  # some column spans more than one chunk
     tdt = torch.float32 if dtype == "f32" else torch.bfloat16
     for p in (0.0, 0.4):
-        got = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, True)
+        got = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, True, rowterms=False)
         split = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, False)
         _same_as_split(got, split, tdt)
         if dtype == "f32":

@@ -100,26 +100,30 @@ def test_c4_forward_backward_every_row(cuda, c4, dt):
     assert torch.equal(u2, u)  # the op is exactly this launch
     tol_close(_np64(lse), lse_ref, F32_TOL, F32_TOL)  # fp32 statistic in both paths
 
-    u.backward(dU)
-    # the edge-kernel gradients themselves (leaves at el, er, hc)
-    el_l, er_l = el.detach().clone().requires_grad_(True), er.detach().clone().requires_grad_(True)
-    hc_l = h.detach().view(n, H, Fd).clone().requires_grad_(True)
-    MF.edge_attention(graph, el_l, er_l, hc_l).backward(dU)
-    tol_close(_np64(el_l.grad), d_el_ref, tol, tol)
-    tol_close(_np64(er_l.grad), d_er_ref, tol, tol)
-    tol_close(_np64(hc_l.grad), d_hc_ref, tol, tol)
-    # the large-graph backward (row terms from the forward, no per-edge de; C4's de is
-    # below the switch-over, so force it): d_el against the same fp64 reference, d_er and
-    # d_hc the same bits as above
-    os.environ["MSHA_ROWTERMS"] = "1"
-    try:
-        el_r, er_r = (x.detach().clone().requires_grad_(True) for x in (el, er))
-        hc_r = h.detach().view(n, H, Fd).clone().requires_grad_(True)
-        MF.edge_attention(graph, el_r, er_r, hc_r).backward(dU)
-    finally:
-        os.environ.pop("MSHA_ROWTERMS")
-    tol_close(_np64(el_r.grad), d_el_ref, tol, tol)
-    assert torch.equal(er_r.grad, er_l.grad) and torch.equal(hc_r.grad, hc_l.grad)
+    u.backward(dU)  # the library's default backward (fp32: with the row terms)
+
+    # the edge-kernel gradients themselves (leaves at el, er, hc), both fused backwards:
+    # the per-edge de summed over rows (row terms off) and d_el from the forward's row
+    # terms (no per-edge de), each against the fp64 reference; d_er, d_hc the same bits
+    def leaf_grads(rowterms):
+        os.environ["MSHA_ROWTERMS"] = rowterms
+        try:
+            el_l, er_l = (x.detach().clone().requires_grad_(True) for x in (el, er))
+            hc_l = h.detach().view(n, H, Fd).clone().requires_grad_(True)
+            MF.edge_attention(graph, el_l, er_l, hc_l).backward(dU)
+        finally:
+            os.environ.pop("MSHA_ROWTERMS")
+        return el_l.grad, er_l.grad, hc_l.grad
+
+    g_off, g_on = leaf_grads("0"), leaf_grads("1")
+    for got in (g_off, g_on):
+        tol_close(_np64(got[0]), d_el_ref, tol, tol)
+        tol_close(_np64(got[1]), d_er_ref, tol, tol)
+        tol_close(_np64(got[2]), d_hc_ref, tol, tol)
+    assert torch.equal(g_on[1], g_off[1]) and torch.equal(g_on[2], g_off[2])
+    code = 1 if dt == torch.bfloat16 else 0
+    g_def = g_on if _lib.load().msha_edge_attention_rowterms_preferred(graph.desc, H, Fd, code) \
+        else g_off  # what u.backward above ran
 
     # end-to-end gradients: h is both the gathered table and the score source
     dh_ref = d_hc_ref + d_el_ref[:, :, None] * al64[None] + d_er_ref[:, :, None] * ar64[None]
@@ -132,8 +136,8 @@ def test_c4_forward_backward_every_row(cuda, c4, dt):
         # bf16: the weight-gradient GEMM reads dh = d_hc + d_el (x) al + d_er (x) ar as a
         # bf16 MFMA operand (as a bf16 torch model's autograd would hold it), so the
         # kernel is checked on that operand at the bf16 bar ...
-        dh_q = (hc_l.grad.float() + el_l.grad[:, :, None] * al.detach()[None]
-                + er_l.grad[:, :, None] * ar.detach()[None]).to(torch.bfloat16)
+        dh_q = (g_def[2].float() + g_def[0][:, :, None] * al.detach()[None]
+                + g_def[1][:, :, None] * ar.detach()[None]).to(torch.bfloat16)
         tol_close(_np64(W.grad), X64.T @ _np64(dh_q).reshape(n, H * Fd), tol, tol)
         # ... and end to end, where the 100k-row reduction of bf16-rounded dh (2^-9
         # relative per element) lands within 2e-2 of the fp64 value (a weight gradient:
