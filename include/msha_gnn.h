@@ -540,6 +540,11 @@ typedef struct msha_segment {
 MSHA_API int msha_segments(int32_t n, const msha_segment* segs, msha_stream_t stream);
 MSHA_API int msha_dropout_keep_mask4(uint64_t seed, uint64_t offset, int64_t n, float p,
                                      uint8_t* keep, msha_stream_t stream);
+/* keep[i] = word `word` (0..3) of the Philox4x32-10 block (seed; counter {i, offset}) >=
+ * p * 2^32: the Ours intra masks (att3 / att4 of head h, batch entry b, node n: offset
+ * drop_offset + 1 + h / 2, word 2 (h % 2) + kind, i = b * n_nodes + n), for tests. */
+MSHA_API int msha_dropout_keep_mask_word(uint64_t seed, uint64_t offset, int64_t n, float p,
+                                         int32_t word, uint8_t* keep, msha_stream_t stream);
 
 
 /* ---- Projection of a small node table in one workgroup (the recipient side: R15 has 32

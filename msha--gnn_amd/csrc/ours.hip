@@ -23,6 +23,7 @@
 namespace msha {
 
 constexpr int kMaxD = 512;  // heads * feat
+constexpr int kOursMB = 4;  // forward: batch matches whose loads are in flight together
 
 struct OursArgs {
   int64_t B, N, M;
@@ -38,7 +39,7 @@ struct OursArgs {
   const float* a3s;  // (H, F) = a3[:F] + a3[F:]
   const float* a4s;
   float slope;
-  Dropout dp;  // edge dropout: offset; intra att3/att4 use offset + 1 + 2h / + 2 + 2h
+  Dropout dp;  // edge dropout: offset; intra att3/att4: see intra_keep_bits
 };
 
 enum { BS_PRE3 = 0, BS_PRE4, BS_E3, BS_E4, BS_SUM, BS_W3, BS_W4, BS_I, BS_N };
@@ -48,11 +49,33 @@ __device__ __forceinline__ float ldt(const void* p, int64_t i) {
   return to_f32(reinterpret_cast<const T*>(p)[i]);
 }
 
+// Intra dropout of (batch entry b, node n), idx = b * N + n: one Philox4x32-10 block per
+// head pair j = h / 2, keyed (seed; counter {idx, offset + 1 + j}); word 2 (h % 2) + kind
+// keeps att3 (kind 0) / att4 (kind 1) of head h.  One generator call covers both kinds of
+// two heads (msha_dropout_keep_mask_word exports the words for tests).
+__device__ __forceinline__ uint32_t intra_word(const uint4& w, int h, int kind) {
+  const int t = 2 * (h & 1) + kind;
+  return t == 0 ? w.x : t == 1 ? w.y : t == 2 ? w.z : w.w;
+}
 __device__ __forceinline__ float intra_drop(const Dropout& d, int kind, int h, uint64_t idx) {
   if (!d.active) return 1.f;
-  return philox_x(d.seed, dropout_offset(d, d.offset + 1 + 2 * (uint64_t)h + (uint64_t)kind), idx) >=
-                 d.threshold
-             ? d.scale : 0.f;
+  const uint4 w = philox4(d.seed, dropout_offset(d, d.offset + 1 + (uint64_t)(h >> 1)), idx);
+  return intra_word(w, h, kind) >= d.threshold ? d.scale : 0.f;
+}
+// keep bits (bit h) of both kinds for heads h < min(H, 32)
+__device__ __forceinline__ void intra_keep_bits(const Dropout& d, int H, uint64_t idx,
+                                                uint32_t& kb3, uint32_t& kb4) {
+  kb3 = kb4 = 0u;
+  const uint64_t off = dropout_offset(d, d.offset + 1);
+  for (int h = 0; h < H && h < 32; h += 2) {
+    const uint4 w = philox4(d.seed, off + (uint64_t)(h >> 1), idx);
+    kb3 |= (w.x >= d.threshold ? 1u : 0u) << h;
+    kb4 |= (w.y >= d.threshold ? 1u : 0u) << h;
+    if (h + 1 < H) {
+      kb3 |= (w.z >= d.threshold ? 1u : 0u) << (h + 1);
+      kb4 |= (w.w >= d.threshold ? 1u : 0u) << (h + 1);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------- prep ---
@@ -109,6 +132,100 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
   const int D = a.H * a.F;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  if (a.B <= 64) {
+    // one batch chunk (train.py's 64 flows): lane b's source and its groups load once per
+    // wave; a wave walks nodes n, n + nwaves, ... with the next node's group ids and u_in
+    // loaded before this node's matches are gathered.  Same sums in the same order.
+    const bool bvalid = lane < a.B;
+    const int64_t ib = bvalid ? a.src[lane] : 0;
+    const int32_t bg3 = bvalid ? a.gid3[ib] : 0, bg4 = bvalid ? a.gid4[ib] : 0;
+    int64_t n = wave;
+    if (n >= a.N) return;
+    int32_t g3 = a.gid3[n], g4 = a.gid4[n];
+    float uin[KD];
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = lane + 64 * k;
+      uin[k] = d < D ? to_f32(u_in[n * D + d]) : 0.f;
+    }
+    while (true) {
+      const int64_t nn = n + nwaves;
+      const bool has_next = nn < a.N;
+      int32_t ng3 = 0, ng4 = 0;
+      float nuin[KD];
+      if (has_next) {
+        ng3 = a.gid3[nn];
+        ng4 = a.gid4[nn];
+      }
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        nuin[k] = has_next && d < D ? to_f32(u_in[nn * D + d]) : 0.f;
+      }
+      float acc3[KD], acc4[KD];
+#pragma unroll
+      for (int k = 0; k < KD; ++k) acc3[k] = acc4[k] = 0.f;
+      const uint64_t bal3 = __ballot(bvalid && bg3 == g3);
+      const uint64_t bal4 = __ballot(bvalid && bg4 == g4);
+      uint32_t kb3 = 0xffffffffu, kb4 = 0xffffffffu;
+      if (a.dp.active && (bal3 | bal4)) intra_keep_bits(a.dp, a.H, (uint64_t)lane * a.N + n, kb3, kb4);
+      // matches in bit order, kOursMB at a time: the batch's weight and h2 loads leave
+      // together (an unused slot repeats the first match's addresses), then the fmas run
+      // in bit order for the used slots only
+      constexpr int MB = kOursMB;
+      for (int kind = 0; kind < 2; ++kind) {
+        uint64_t bal = kind == 0 ? bal3 : bal4;
+        const uint32_t kbk = kind == 0 ? kb3 : kb4;
+        while (bal) {
+          int bits[MB];
+#pragma unroll
+          for (int q = 0; q < MB; ++q) {
+            bits[q] = bal ? __ffsll((long long)bal) - 1 : -1;
+            bal &= bal - 1;
+          }
+          float wv[MB][KD], xv[MB][KD];
+#pragma unroll
+          for (int q = 0; q < MB; ++q) {
+            const int bit = bits[q] >= 0 ? bits[q] : bits[0];
+            const int64_t ibb = __shfl(ib, bit);
+            const uint32_t kbits = __shfl(kbk, bit);
+#pragma unroll
+            for (int k = 0; k < KD; ++k) {
+              const int d = min(lane + 64 * k, D - 1);
+              const int h = d / a.F;
+              float drop = 1.f;
+              if (a.dp.active)
+                drop = h < 32 ? (((kbits >> h) & 1u) ? a.dp.scale : 0.f)
+                              : intra_drop(a.dp, kind, h, (uint64_t)bit * a.N + n);
+              wv[q][k] = bstat[((int64_t)bit * a.H + h) * BS_N + (kind == 0 ? BS_W3 : BS_W4)] * drop;
+              xv[q][k] = ldt<T>(a.h2, ibb * D + d);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < MB; ++q) {
+            if (bits[q] < 0) break;
+#pragma unroll
+            for (int k = 0; k < KD; ++k) {
+              if (kind == 0) acc3[k] = fmaf(wv[q][k], xv[q][k], acc3[k]);
+              else acc4[k] = fmaf(wv[q][k], xv[q][k], acc4[k]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        if (d < D) u_out[n * D + d] = from_f32<T>(uin[k] + (acc3[k] + acc4[k]));
+      }
+      if (!has_next) break;
+      n = nn;
+      g3 = ng3;
+      g4 = ng4;
+#pragma unroll
+      for (int k = 0; k < KD; ++k) uin[k] = nuin[k];
+    }
+    return;
+  }
   for (int64_t n = wave; n < a.N; n += nwaves) {
     const int32_t g3 = a.gid3[n], g4 = a.gid4[n];
     float acc3[KD], acc4[KD];
@@ -123,13 +240,7 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
       // keep bits of (b = base + lane, n) for every head, drawn lane-parallel once per
       // chunk (bit h of kb3 / kb4); heads >= 32 fall back to a per-use draw
       uint32_t kb3 = 0xffffffffu, kb4 = 0xffffffffu;
-      if (a.dp.active && (bal3 | bal4)) {
-        kb3 = kb4 = 0u;
-        for (int h = 0; h < a.H && h < 32; ++h) {
-          kb3 |= (intra_drop(a.dp, 0, h, (uint64_t)b * a.N + n) != 0.f ? 1u : 0u) << h;
-          kb4 |= (intra_drop(a.dp, 1, h, (uint64_t)b * a.N + n) != 0.f ? 1u : 0u) << h;
-        }
-      }
+      if (a.dp.active && (bal3 | bal4)) intra_keep_bits(a.dp, a.H, (uint64_t)b * a.N + n, kb3, kb4);
       for (int kind = 0; kind < 2; ++kind) {
         uint64_t bal = kind == 0 ? bal3 : bal4;
         while (bal) {
@@ -202,9 +313,9 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
   const int64_t nj = lane < cnt ? (int64_t)gmem[m0 + lane] : 0;
   uint32_t kbits = 0xffffffffu;
   if (a.dp.active) {
-    kbits = 0u;
-    for (int h = 0; h < a.H && h < 32; ++h)
-      kbits |= (intra_drop(a.dp, kind, h, (uint64_t)b * a.N + nj) != 0.f ? 1u : 0u) << h;
+    uint32_t k3, k4;
+    intra_keep_bits(a.dp, a.H, (uint64_t)b * a.N + nj, k3, k4);
+    kbits = kind == 0 ? k3 : k4;
   }
   // GU members' rows are loaded before they are accumulated (in member order, as one
   // at a time): GU gathers in flight per wave instead of one
@@ -456,7 +567,9 @@ static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const 
   if (B > 0)
     hipLaunchKernelGGL(ours_prep_kernel<T>, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
                        g->col, g->rowflag, el, er, lse, bstat);
-  const dim3 grid(grid_for(g->n_rows, 4, 1 << 16));
+  // B <= 64: waves walk ~4 nodes each (the batch's groups load once per wave, the next
+  // node's loads overlap this node's gathers); otherwise one node per wave
+  const dim3 grid(grid_for(g->n_rows, 4, B <= 64 ? 2048 : 1 << 16));
   const int D = a.H * a.F;
 #define FWD(kd) hipLaunchKernelGGL((ours_fwd_kernel<T, kd>), grid, dim3(256), 0, s, a, \
                                    (const float*)bstat, (const T*)u_inter, (T*)u_out)

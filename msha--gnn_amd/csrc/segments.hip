@@ -105,6 +105,17 @@ __global__ void __launch_bounds__(256) keep_mask4_kernel(Dropout d, int64_t n, u
     keep[e] = keep4(d, (uint64_t)e, philox4(d.seed, off, (uint64_t)e >> 2)) != 0.f ? 1 : 0;
 }
 
+__global__ void __launch_bounds__(256) keep_mask_word_kernel(Dropout d, int64_t n, int word,
+                                                             uint8_t* keep) {
+  const uint64_t off = dropout_offset(d, d.offset);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 w = philox4(d.seed, off, (uint64_t)e);
+    const uint32_t x = word == 0 ? w.x : word == 1 ? w.y : word == 2 ? w.z : w.w;
+    keep[e] = x >= d.threshold ? 1 : 0;
+  }
+}
+
 }  // namespace msha
 
 using namespace msha;
@@ -142,4 +153,17 @@ extern "C" int msha_dropout_keep_mask4(uint64_t seed, uint64_t offset, int64_t n
   hipLaunchKernelGGL(keep_mask4_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, d, n, keep);
   return check_launch("dropout_keep_mask4");
+}
+
+extern "C" int msha_dropout_keep_mask_word(uint64_t seed, uint64_t offset, int64_t n, float p,
+                                           int32_t word, uint8_t* keep, msha_stream_t stream) {
+  MSHA_ARG_CHECK(n >= 0 && (n == 0 || keep != nullptr), "dropout_keep_mask_word: bad buffer");
+  MSHA_ARG_CHECK(p >= 0.f && p <= 1.f, "dropout_keep_mask_word: p must be in [0, 1]");
+  MSHA_ARG_CHECK(word >= 0 && word < 4, "dropout_keep_mask_word: word must be 0..3");
+  if (n == 0) return MSHA_OK;
+  Dropout d = make_dropout(p, seed, offset, (hipStream_t)stream);
+  d.active = true;
+  hipLaunchKernelGGL(keep_mask_word_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, d, n, word, keep);
+  return check_launch("dropout_keep_mask_word");
 }

@@ -300,10 +300,15 @@ def gal(graph: Graph, h, p: float = 0.0, training: bool = False, seed: int | Non
 
 
 def dropout_keep_mask(n: int, p: float, seed: int, device, offset: int = 0,
-                      flat4: bool = False) -> torch.Tensor:
+                      flat4: bool = False, word: int | None = None) -> torch.Tensor:
     """The kernels' Philox keep mask of n elements (uint8); flat4: the four-words-per-call
-    mask of the flat-table dropout (msha_segments, feature dropout)."""
+    mask of the flat-table dropout (msha_segments, feature dropout); word: word `word` of
+    the block keyed on each element (the Ours intra masks)."""
     keep = torch.empty(n, dtype=torch.uint8, device=device)
+    if word is not None:
+        _lib.call("msha_dropout_keep_mask_word", seed, offset, n, p, word, keep.data_ptr(),
+                  _lib.stream_handle(device))
+        return keep
     _lib.call("msha_dropout_keep_mask4" if flat4 else "msha_dropout_keep_mask", seed, offset, n,
               p, keep.data_ptr(), _lib.stream_handle(device))
     return keep

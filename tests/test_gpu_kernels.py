@@ -98,6 +98,16 @@ def test_dropout_mask_statistics(cuda):
     k3 = MF.dropout_keep_mask(1 << 20, 0.5, 1235, cuda).cpu().numpy()
     assert abs((k == k3).mean() - 0.5) < 3e-3
     assert MF.dropout_keep_mask(4096, 0.0, 7, cuda).cpu().numpy().all()
+    # word masks (the Ours intra masks): word 0 of the block keyed on each element is the
+    # per-element mask; the four words are distinct streams of the right rate
+    w = [MF.dropout_keep_mask(1 << 20, 0.5, 1234, cuda, offset=3, word=t).cpu().numpy()
+         for t in range(4)]
+    assert np.array_equal(w[0], MF.dropout_keep_mask(1 << 20, 0.5, 1234, cuda, offset=3)
+                          .cpu().numpy())
+    for t in range(4):
+        assert abs(w[t].mean() - 0.5) < 3e-3
+        for u in range(t):
+            assert abs((w[t] == w[u]).mean() - 0.5) < 3e-3
 
 
 # ------------------------------------------------------------- edge attention

@@ -136,9 +136,12 @@ def test_ours_attention_kernels_vs_dense(cuda, msha, p):
         if p > 0:
             ke = torch.zeros(n, m, dtype=torch.float64)
             ke[rows, cols] = torch.as_tensor(keep_all[:, h], dtype=torch.float64)
-            k3 = torch.as_tensor(MF.dropout_keep_mask(B * n, p, seed, cuda, offset=1 + 2 * h)
+            # intra masks: head pair h // 2 at offset 1 + h // 2, word 2 (h % 2) + kind
+            k3 = torch.as_tensor(MF.dropout_keep_mask(B * n, p, seed, cuda, offset=1 + h // 2,
+                                                      word=2 * (h % 2))
                                  .cpu().numpy().reshape(B, n), dtype=torch.float64)
-            k4 = torch.as_tensor(MF.dropout_keep_mask(B * n, p, seed, cuda, offset=2 + 2 * h)
+            k4 = torch.as_tensor(MF.dropout_keep_mask(B * n, p, seed, cuda, offset=1 + h // 2,
+                                                      word=2 * (h % 2) + 1)
                                  .cpu().numpy().reshape(B, n), dtype=torch.float64)
         ru, rv = _dense_ours_core(*rs, ra3, ra4, torch.as_tensor(counts > 0), torch.as_tensor(city),
                                   torch.as_tensor(prov), torch.as_tensor(src), ke, k3, k4, p)
