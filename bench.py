@@ -305,6 +305,7 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
     import msha_loader
 
     msha = msha_loader.load()
+    from msha_gnn_amd import functional as MF
     from msha_gnn_amd import layers
     from msha_gnn_amd.data import GroupAdjacency
 
@@ -341,7 +342,9 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
         def body():
             opt.zero_grad(set_to_none=True)
             out = model(adj, cadj, padj, si_s)
-            loss = torch.nn.functional.nll_loss(out[si_s].float(), ri_s)
+            # train.py:229 F.nll_loss(output[source_index], recipient_index) as one launch
+            # each way (msha_nll_rows_fwd/_bwd) instead of ~12 ATen launches
+            loss = MF.nll_loss_rows(out, si_s, ri_s)
             loss.backward()
             opt.step()
             return loss

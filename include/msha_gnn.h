@@ -515,6 +515,19 @@ MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int3
                            int64_t n_zero, void* ws, size_t ws_bytes, msha_stream_t stream);
 
 
+/* ---- Training loss on gathered rows (train.py:227-229): F.nll_loss(logp[rows], cols),
+ * mean reduction, and its backward, one launch each (ABI 8).  logp (N, M) row stride ld,
+ * fp32 or bf16 (dtype); rows, cols int64 (B).
+ *   msha_nll_rows_fwd: loss[0] = -(1/B) sum_b logp[rows[b], cols[b]]  (fp32)
+ *   msha_nll_rows_bwd: dlogp = 0 except dlogp[rows[b], cols[b]] += -gloss[0] / B for b in
+ *                      order (repeated pairs accumulate); gloss is a device scalar. */
+MSHA_API int msha_nll_rows_fwd(int64_t B, const int64_t* rows, const int64_t* cols,
+                               int32_t dtype, const void* logp, int64_t ld, float* loss,
+                               msha_stream_t stream);
+MSHA_API int msha_nll_rows_bwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                               const int64_t* cols, const float* gloss, int32_t dtype,
+                               void* dlogp, int64_t ld, msha_stream_t stream);
+
 /* ---- Batched segment copies: the models' per-head parameter packing (Ablation.py:262-267,
  * Ours.py:58-75 read W1/W2/a/a3/a4 of every head; one launch stacks them, one scatters
  * their gradients back) and the feature dropout of Sfeatures / Rfeatures

@@ -1,0 +1,96 @@
+// The training loss on gathered rows (train.py:227-229: F.nll_loss(output[source_index],
+// recipient_index), mean reduction) and its backward, in one launch each.  In torch this
+// is a row gather, the nll forward, and in the backward a ones fill, the nll backward, a
+// zero fill of the (N, M) gradient and an index backward (sort + scatter-add): ~12
+// launches around a 64-row batch.
+//
+//   forward   loss = -(1/B) sum_b logp[rows[b], cols[b]]   (b ascending, fp32)
+//   backward  dlogp = 0 except dlogp[rows[b], cols[b]] += -g / B   (b ascending; repeated
+//             (row, col) pairs accumulate as index backward does)
+// The backward zero-fills row ranges per block; each block then adds the batch entries
+// that fall in its own rows in batch order (one lane), so the result is deterministic
+// and no two blocks touch the same row.
+#include "common.h"
+
+namespace msha {
+
+constexpr int kLossThreads = 256;
+constexpr int kLossRowsPerBlock = 64;
+
+template <typename T>
+__global__ void __launch_bounds__(kLossThreads) nll_rows_fwd_kernel(
+    int64_t B, const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
+    const T* __restrict__ logp, int64_t ld, float* __restrict__ loss) {
+  __shared__ float part[kLossThreads];
+  float s = 0.f;
+  // thread t adds entries t, t + 256, ... in order; the partials then add in a fixed tree
+  for (int64_t b = threadIdx.x; b < B; b += kLossThreads)
+    s += to_f32(logp[rows[b] * ld + cols[b]]);
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = kLossThreads / 2; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = B > 0 ? -part[0] / (float)B : 0.f;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
+    int64_t N, int64_t M, int64_t B, const int64_t* __restrict__ rows,
+    const int64_t* __restrict__ cols, const float* __restrict__ gloss, T* __restrict__ dlogp,
+    int64_t ld) {
+  const int64_t r0 = (int64_t)blockIdx.x * kLossRowsPerBlock;
+  const int64_t r1 = min(N, r0 + kLossRowsPerBlock);
+  for (int64_t e = threadIdx.x; e < (r1 - r0) * M; e += kLossThreads) {
+    const int64_t r = r0 + e / M, c = e % M;
+    dlogp[r * ld + c] = from_f32<T>(0.f);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && B > 0) {
+    const float v = -gloss[0] / (float)B;
+    for (int64_t b = 0; b < B; ++b) {
+      const int64_t r = rows[b];
+      if (r < r0 || r >= r1) continue;
+      T* p = dlogp + r * ld + cols[b];
+      *p = from_f32<T>(to_f32(*p) + v);
+    }
+  }
+}
+
+}  // namespace msha
+
+using namespace msha;
+
+extern "C" int msha_nll_rows_fwd(int64_t B, const int64_t* rows, const int64_t* cols,
+                                 int32_t dtype, const void* logp, int64_t ld, float* loss,
+                                 msha_stream_t stream) {
+  MSHA_ARG_CHECK(B >= 0 && loss != nullptr && (B == 0 || (rows && cols && logp)),
+                 "nll_rows_fwd: null pointer");
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "nll_rows_fwd: bad dtype");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MSHA_DTYPE_BF16)
+    hipLaunchKernelGGL(nll_rows_fwd_kernel<bf16_t>, dim3(1), dim3(kLossThreads), 0, s, B, rows,
+                       cols, (const bf16_t*)logp, ld, loss);
+  else
+    hipLaunchKernelGGL(nll_rows_fwd_kernel<float>, dim3(1), dim3(kLossThreads), 0, s, B, rows,
+                       cols, (const float*)logp, ld, loss);
+  return check_launch("nll_rows_fwd");
+}
+
+extern "C" int msha_nll_rows_bwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                                 const int64_t* cols, const float* gloss, int32_t dtype,
+                                 void* dlogp, int64_t ld, msha_stream_t stream) {
+  MSHA_ARG_CHECK(N > 0 && M > 0 && B >= 0 && ld >= M, "nll_rows_bwd: bad sizes");
+  MSHA_ARG_CHECK(dlogp && gloss && (B == 0 || (rows && cols)), "nll_rows_bwd: null pointer");
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "nll_rows_bwd: bad dtype");
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((N + kLossRowsPerBlock - 1) / kLossRowsPerBlock));
+  if (dtype == MSHA_DTYPE_BF16)
+    hipLaunchKernelGGL(nll_rows_bwd_kernel<bf16_t>, grid, dim3(kLossThreads), 0, s, N, M, B,
+                       rows, cols, gloss, (bf16_t*)dlogp, ld);
+  else
+    hipLaunchKernelGGL(nll_rows_bwd_kernel<float>, grid, dim3(kLossThreads), 0, s, N, M, B, rows,
+                       cols, gloss, (float*)dlogp, ld);
+  return check_launch("nll_rows_bwd");
+}

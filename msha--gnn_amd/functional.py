@@ -1278,3 +1278,42 @@ def pack_heads(heads, intra: bool):
             p.dtype != pdt or not p.is_contiguous() or not p.is_cuda for p in params):
         return None
     return _PackHeads.apply(H, intra, *params)
+
+
+# ------------------------------------------------------------- loss on gathered rows ---
+class _NllRows(torch.autograd.Function):
+    """F.nll_loss(logp[rows], cols) (mean) and its backward, one launch each
+    (msha_nll_rows_fwd / _bwd): replaces the row gather, nll forward/backward, the zero
+    fill of the (N, M) gradient and the index backward of train.py:227-229."""
+
+    @staticmethod
+    def forward(ctx, logp, rows, cols):
+        dt = _table_dtype(logp)
+        logp = _tc(logp, dt)
+        rows = rows.to(torch.int64).contiguous()
+        cols = cols.to(torch.int64).contiguous()
+        loss = torch.empty((), device=logp.device, dtype=torch.float32)
+        _lib.call("msha_nll_rows_fwd", rows.numel(), rows.data_ptr(), cols.data_ptr(), _code(dt),
+                  logp.data_ptr(), logp.stride(0), loss.data_ptr(), _stream(logp))
+        ctx.save_for_backward(rows, cols)
+        ctx.shape, ctx.dt = tuple(logp.shape), dt
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        rows, cols = ctx.saved_tensors
+        N, M = ctx.shape
+        g = _f32c(gloss.reshape(1))
+        d = torch.empty(N, M, device=rows.device, dtype=ctx.dt)
+        _lib.call("msha_nll_rows_bwd", N, M, rows.numel(), rows.data_ptr(), cols.data_ptr(),
+                  g.data_ptr(), _code(ctx.dt), d.data_ptr(), M, _stream(d))
+        return d, None, None
+
+
+def nll_loss_rows(logp, rows, cols):
+    """``F.nll_loss(logp[rows].float(), cols)`` (mean reduction) for the (N, M) log-probs
+    of a model head, train.py:227-229's loss, as one launch forward and one backward."""
+    _lib.require_cuda(logp, rows, cols)
+    if logp.dim() != 2 or rows.shape != cols.shape:
+        raise ValueError("nll_loss_rows: logp (N, M), rows and cols of the same length")
+    return _NllRows.apply(logp, rows, cols)

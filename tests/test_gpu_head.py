@@ -313,3 +313,29 @@ def test_project_small_vs_fp64(cuda, msha, M, K, H, F_):
         tol_close(got.detach().cpu().numpy(), want.detach().numpy(), 1e-5, 1e-5)
     for got, want in zip(ts, r):
         tol_close(got.grad.cpu().numpy(), want.grad.numpy(), 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_nll_loss_rows_matches_torch(cuda, msha, dtype):
+    """msha_nll_rows_fwd/_bwd == F.nll_loss(logp[rows].float(), cols) and its autograd,
+    with repeated (row, col) pairs (accumulated, as index backward does) and a row
+    repeated with another column."""
+    from msha_gnn_amd import functional as MF
+
+    gen = torch.Generator(device=cuda).manual_seed(4)
+    N, M, B = 39179, 32, 64
+    logp = torch.log_softmax(torch.randn(N, M, device=cuda, generator=gen), 1).to(dtype)
+    rows = torch.randint(0, N, (B,), device=cuda, generator=gen)
+    cols = torch.randint(0, M, (B,), device=cuda, generator=gen)
+    rows[5], cols[5] = rows[3], cols[3]  # a repeated pair
+    rows[9] = rows[3]                    # same row, another column
+    a = logp.detach().clone().requires_grad_(True)
+    b = logp.detach().clone().requires_grad_(True)
+    got = MF.nll_loss_rows(a, rows, cols)
+    ref = torch.nn.functional.nll_loss(b[rows].float(), cols)
+    tol = 1e-6 if dtype == torch.float32 else 1e-3
+    assert abs(float(got) - float(ref)) <= tol * abs(float(ref))
+    (3.0 * got).backward()
+    (3.0 * ref).backward()
+    assert a.grad.dtype == dtype
+    assert torch.equal(a.grad, b.grad)
