@@ -85,7 +85,7 @@ def pmc_traffic(H, F, bf16=False, workload="syn100k"):
     import re
 
     pat = (re.compile(rf"edge_attn_fwd(?:_bat)?_kernelILi{H}ELi{F}EDF16b") if bf16 else
-           re.compile(rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?>"))
+           re.compile(rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?(, (true|false))?>"))
 
     def newest_first(path):  # round1_syn100k_v10 after _v9: compare the numbers
         tag = os.path.basename(os.path.dirname(path))

@@ -243,6 +243,12 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 #ifndef FWD_WPE
 #define FWD_WPE 1
 #endif
+#ifndef FWD_SHORT_DEG
+#define FWD_SHORT_DEG 8
+#endif
+#ifndef FWD_SHORT_RPW
+#define FWD_SHORT_RPW 1  // rows per wave on short-row graphs (A/B: MSHA_FWD_WAVES)
+#endif
 template <int H, int F, typename T, int EPL, bool RT = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
 edge_attn_fwd_bat_kernel(
@@ -265,19 +271,24 @@ edge_attn_fwd_bat_kernel(
   const int wave0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const int nwaves = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
 
-  for (int row = wave0; row < n_rows; row += nwaves) {
-    const int32_t start = __builtin_amdgcn_readfirstlane(rowptr[row]);
-    const int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
-    const bool virt = rowflag != nullptr && rowflag[row] != 0;
-    const float elh = el[(int64_t)row * H + h_s];
-    int32_t j0[EPL], j1[EPL];
-    float erv[EPL];
+  // a wave walks rows row, row + nwaves, ... (one row when the grid covers them all);
+  // the next row's bounds, flag, el and first columns load before this row's epilogue,
+  // unconditionally (the last row reloads its own: no branch around the loads)
+  int row = wave0;
+  if (row >= n_rows) return;
+  int32_t start = __builtin_amdgcn_readfirstlane(rowptr[row]);
+  int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
+  bool virt = rowflag != nullptr && rowflag[row] != 0;
+  float elh = el[(int64_t)row * H + h_s];
+  int32_t j0[EPL], j1[EPL];
 #pragma unroll
-    for (int t = 0; t < EPL; ++t) {
-      const int32_t e0 = start + t * G::CE + e_s, e1 = e0 + CEL;
-      j0[t] = buf_i32(r_col, e0 < end ? (uint32_t)e0 * 4u : kOOB);
-      j1[t] = buf_i32(r_col, e1 < end ? (uint32_t)e1 * 4u : kOOB);
-    }
+  for (int t = 0; t < EPL; ++t) {
+    const int32_t e0 = start + t * G::CE + e_s, e1 = e0 + CEL;
+    j0[t] = buf_i32(r_col, e0 < end ? (uint32_t)e0 * 4u : kOOB);
+    j1[t] = buf_i32(r_col, e1 < end ? (uint32_t)e1 * 4u : kOOB);
+  }
+  while (true) {
+    float erv[EPL];
 #pragma unroll
     for (int t = 0; t < EPL; ++t)
       erv[t] = buf_f32(r_er, start + t * G::CE + e_s < end
@@ -360,6 +371,20 @@ edge_attn_fwd_bat_kernel(
         erv[t] = ern[t];
       }
     }
+    const int nrow_raw = row + nwaves;
+    const bool has_next = nrow_raw < n_rows;
+    const int nrow = has_next ? nrow_raw : row;
+    const int32_t nstart = __builtin_amdgcn_readfirstlane(rowptr[nrow]);
+    const int32_t nend = __builtin_amdgcn_readfirstlane(rowptr[nrow + 1]);
+    const bool nvirt = rowflag != nullptr && rowflag[nrow] != 0;
+    const float nelh = el[(int64_t)nrow * H + h_s];
+    int32_t nj0[EPL], nj1[EPL];
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      const int32_t e0 = nstart + t * G::CE + e_s, e1 = e0 + CEL;
+      nj0[t] = buf_i32(r_col, e0 < nend ? (uint32_t)e0 * 4u : kOOB);
+      nj1[t] = buf_i32(r_col, e1 < nend ? (uint32_t)e1 * 4u : kOOB);
+    }
     if (G::EPI > 1) {
 #pragma unroll
       for (int o = G::NQ; o < 64; o <<= 1) acc = pk_xor_add(acc, o);
@@ -406,6 +431,17 @@ edge_attn_fwd_bat_kernel(
               __expf(sv - lse_h) * dropout_factor(dp, (uint64_t)e * H + h_s);
         }
       }
+    }
+    if (!has_next) break;
+    row = nrow;
+    start = nstart;
+    end = nend;
+    virt = nvirt;
+    elh = nelh;
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      j0[t] = nj0[t];
+      j1[t] = nj1[t];
     }
   }
 }
@@ -1298,7 +1334,11 @@ extern "C" int msha_edge_attention_fwd_ex(const msha_graph* g, int32_t heads, in
   if (uc != nullptr && !bat)
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: row terms need the batched forward");
   if (bat) {
-    const int64_t cap = env_int("MSHA_FWD_WAVES", 0);
+    // MSHA_FWD_WAVES caps the grid (waves then walk rows with the next row prefetched);
+    // default: short rows (mean degree <= FWD_SHORT_DEG) walk ~FWD_SHORT_RPW rows per wave
+    int64_t cap = env_int("MSHA_FWD_WAVES", -1);
+    if (cap < 0)
+      cap = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows ? g->n_rows / FWD_SHORT_RPW : 0;
     const dim3 grid = wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
 #define XB(h, f)                                                                               \
     if (heads == h && feat == f) {                                                             \
