@@ -178,8 +178,9 @@ MSHA_API int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t
  * so d_el_i = dU_i . uc_i - D_i qc_i (D_i = dU_i . u_i) needs no per-edge de in CSR
  * order.  uc and qc together or both NULL (= msha_edge_attention_fwd).  Needs the
  * batched forward (MSHA_ERR_UNSUPPORTED otherwise); msha_edge_attention_rowterms_preferred
- * says whether a graph should use them (fp32 tables: always; bf16 tables: once the
- * per-edge de of msha_edge_attention_bwd_fused would leave the Infinity Cache). */
+ * says whether a graph should use them (once the per-edge de of
+ * msha_edge_attention_bwd_fused would leave the Infinity Cache, and for fp32 tables on
+ * graphs whose rows average >= 8 edges). */
 MSHA_API int msha_edge_attention_rowterms_preferred(const msha_graph* g, int32_t heads,
                                                     int32_t feat, int32_t dtype);
 MSHA_API int msha_edge_attention_fwd_ex(const msha_graph* g, int32_t heads, int32_t feat,

@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 #define FWD_SHORT_DEG 8
 #endif
 #ifndef FWD_SHORT_RPW
-#define FWD_SHORT_RPW 1  // rows per wave on short-row graphs (A/B: MSHA_FWD_WAVES)
+#define FWD_SHORT_RPW 5  // rows per wave on short-row graphs (A/B: MSHA_FWD_WAVES)
 #endif
 template <int H, int F, typename T, int EPL, bool RT = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
@@ -1297,14 +1297,15 @@ extern "C" int msha_edge_attention_rowterms_preferred(const msha_graph* g, int32
                                                       int32_t feat, int32_t dtype) {
   if (g == nullptr || !shape_supported(heads, feat) || !dtype_ok(dtype, feat)) return 0;
   if (!fwd_bat_ok(g, heads, feat, dtype)) return 0;
-  // MSHA_ROWTERMS: 1 = always, 0 = never.  Default: fp32 tables always (C4: step 0.507 ->
-  // 0.494 ms, syn2m 11.70 -> 10.94 ms); bf16 tables once the per-edge de would leave the
-  // Infinity Cache (the fp32 uc doubles the bf16 forward's output bytes: neutral at C4,
-  // 7.34 -> 7.04 ms at syn2m)
+  // MSHA_ROWTERMS: 1 = always, 0 = never.  Default: once the per-edge de would leave the
+  // Infinity Cache (syn2m: fp32 step 11.70 -> 10.94 ms, bf16 7.34 -> 7.04 ms), and for
+  // fp32 tables also on graphs whose rows average >= FWD_SHORT_DEG edges (C4: 0.507 ->
+  // 0.494 ms).  Short rows (R15, ~2.3 edges) keep the de row sum: there the row terms'
+  // extra forward work costs more (forward 48 -> 68 us) than the row sum they save.
   const int knob = env_int("MSHA_ROWTERMS", -1);
   if (knob >= 0) return knob != 0;
-  if (dtype == MSHA_DTYPE_F32) return 1;
-  return g->n_edges * 4 * (int64_t)heads >= DE_SLOT_MIN_BYTES ? 1 : 0;
+  if (g->n_edges * 4 * (int64_t)heads >= DE_SLOT_MIN_BYTES) return 1;
+  return dtype == MSHA_DTYPE_F32 && g->n_edges >= (int64_t)FWD_SHORT_DEG * g->n_rows ? 1 : 0;
 }
 
 extern "C" int msha_edge_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
