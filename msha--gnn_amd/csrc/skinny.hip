@@ -24,6 +24,7 @@
 // Both are deterministic (fixed summation orders); numerics are the fp32 MFMA's exact
 // fma chain (fp32) or fp32 accumulation of bf16 products (bf16).
 #include <cstring>
+#include <type_traits>
 
 #include "common.h"
 
@@ -57,28 +58,104 @@ struct ProjGeo {
   static_assert(64 % LPR == 0, "a row must map onto whole lanes");
 };
 
+// proj_kernel's block: PROJ_WPS waves per SIMD when the resident W and one staging
+// tile per wave fit the 160 KB of LDS, the staging tile narrowed to column halves when
+// the whole-width one would not fit (a head must not straddle the halves), else 2.
+// 2, 3 and 4 waves per SIMD measured the same at C4 (42.5 / 43.6 / 46.5 us fp32).
+#ifndef PROJ_WPS
+#define PROJ_WPS 2
+#endif
 template <typename T, int K, int N, int FE>
-__global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
+struct ProjStage {
+  using G = ProjGeo<T, K, N>;
+  static constexpr int kLds = 160 * 1024;
+  static constexpr int bytes(int waves, int sw) { return G::WBYTES + waves * 16 * (sw + 4) * 4 + 8 * N; }
+  static constexpr bool HALF_OK = (FE == 0 || FE <= N / 2) && (N / 2) % (16 / (int)sizeof(T)) == 0 &&
+                                  64 % ((N / 2) / (16 / (int)sizeof(T))) == 0;
+  static constexpr int W3 = 4 * PROJ_WPS;
+  static constexpr bool FULL3 = bytes(W3, N) <= kLds;
+  static constexpr bool HALF3 = !FULL3 && HALF_OK && bytes(W3, N / 2) <= kLds;
+  static constexpr int WAVES = FULL3 || HALF3 ? W3 : kProjWaves;
+  static constexpr int SW = HALF3 ? N / 2 : N;          // staged columns per pass
+  static constexpr int TPS = SW + 4;
+  static constexpr int SBYTES = 16 * TPS * 4;
+  static constexpr int LPR = SW / G::EPL;                // lanes per staged row
+  static constexpr int RPP = 64 / LPR;                   // rows per store pass
+  // column parts per tail tile: 4, or fewer when a head (FE columns) would straddle them
+  // or a part's staged row would cover fewer than 4 lanes
+  static constexpr bool part_ok(int pt) { return N / pt >= 4 * G::EPL && (FE == 0 || FE <= N / pt); }
+  static constexpr int PT = part_ok(4) ? 4 : part_ok(2) ? 2 : 1;
+  static_assert(bytes(WAVES, SW) <= kLds, "proj_kernel LDS");
+};
+
+template <typename T, int K, int N, int FE>
+__global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_kernel(
     int M, const T* __restrict__ X, const T* __restrict__ W, const float* __restrict__ al,
     const float* __restrict__ ar, T* __restrict__ h, float* __restrict__ el,
     float* __restrict__ er, int H) {
   using G = ProjGeo<T, K, N>;
-  __shared__ __attribute__((aligned(16))) char smem[G::WBYTES + kProjWaves * G::SBYTES];
+  using S = ProjStage<T, K, N, FE>;
+  constexpr int kWaves = S::WAVES;
+  // W image | per-wave staging tiles | score vectors al, ar (read in the epilogue)
+  __shared__ __attribute__((aligned(16))) char smem[G::WBYTES + kWaves * S::SBYTES + 8 * N];
   T* Wl = reinterpret_cast<T*>(smem);
+  float* als = reinterpret_cast<float*>(smem + G::WBYTES + kWaves * S::SBYTES);
+  float* ars = als + N;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int g = lane >> 4, r16 = lane & 15;
 
+  // Work items of a wave, in order: whole 16-row tiles gw, gw + nw, ... for the R rounds
+  // every wave completes, then the tail: the L tiles left over are cut into PT column
+  // parts each (PT L items), one per wave in the same SIMD-spreading order, so the last
+  // round costs 1 / PT of a tile instead of leaving 1 - L / (SIMDs) of the SIMDs idle.
+  // The first pass of waves covers every SIMD once (wave w & 3 of each block) before
+  // any SIMD takes a second wave's share.
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kWaves;
+  const int tiles = (M + 15) / 16;
+  constexpr int PT = S::PT;
+  const int R = tiles / nw;
+  const int units = PT * (tiles - R * nw);
+  const int n_items = R + (gw < units ? (units - gw + nw - 1) / nw : 0);
+  // item k -> (tile, first column block)
+  auto item_tile = [&](int k) -> int { return k < R ? gw + k * nw : R * nw + (gw + (k - R) * nw) / PT; };
+  auto item_cb = [&](int k) -> int { return k < R ? 0 : ((gw + (k - R) * nw) % PT) * (G::NB / PT); };
+
+  // buffer-descriptor loads: a row past M (or an item past the last) reads 0 without a
+  // branch, so the prefetch is unconditional and the waits on it stay exact (a load
+  // under "if (t + nw < tiles)" made the join wait on the tile just issued)
+  const rsrc_t r_x = make_rsrc(X, (uint32_t)((int64_t)M * K * sizeof(T)));
+  auto tile_off = [&](int t) -> uint32_t {
+    const int row = t * 16 + r16;
+    return row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) + (uint32_t)(g * G::KL * sizeof(T))
+                   : kOOB;
+  };
+  // the first item's rows leave before the W copy, so their latency hides under it
+  u32x4_t buf[G::NLD];
+  {
+    const uint32_t off = n_items > 0 ? tile_off(item_tile(0)) : kOOB;
+#pragma unroll
+    for (int i = 0; i < G::NLD; ++i) buf[i] = buf_b128(r_x, off + 16u * i);
+  }
+
   // ---- W -> LDS once per block
+  if (FE > 0) {
+    for (int n = tid; n < N; n += 64 * kWaves) {
+      als[n] = al != nullptr ? al[n] : 0.f;
+      ars[n] = ar != nullptr ? ar[n] : 0.f;
+    }
+  }
   if (G::F32) {
-    for (int idx = tid; idx < K * N / 4; idx += 64 * kProjWaves) {
+    for (int idx = tid; idx < K * N / 4; idx += 64 * kWaves) {
       const int k = idx / (N / 4), n4 = idx % (N / 4);
       const float4 v = *reinterpret_cast<const float4*>(W + k * N + 4 * n4);
       const int kr = 4 * (k % G::KL) + k / G::KL;
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(Wl) + kr * G::PW + 4 * n4) = v;
     }
   } else {
-    for (int idx = tid; idx < K * N / 8; idx += 64 * kProjWaves) {
+    for (int idx = tid; idx < K * N / 8; idx += 64 * kWaves) {
       const int k = idx / (N / 8), n8 = idx % (N / 8);
       const uint4 v = *reinterpret_cast<const uint4*>(W + k * N + 8 * n8);
       const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
@@ -89,146 +166,138 @@ __global__ void __launch_bounds__(64 * kProjWaves) proj_kernel(
     }
   }
   __syncthreads();
+  if (n_items == 0) return;
 
-  float* Tw = reinterpret_cast<float*>(smem + G::WBYTES) + w * 16 * G::TPS;
-  const int cl = (lane % G::LPR) * G::EPL;  // first output column of this lane
-  float alv[G::EPL], arv[G::EPL];
+  float* Tw = reinterpret_cast<float*>(smem + G::WBYTES) + w * 16 * S::TPS;
+  // A register i of a tile feeds steps [i SPL, (i + 1) SPL): once they have issued, it is
+  // reloaded with the next item's (one register buffer, a whole tile of lead time)
+  constexpr int SPL = G::S / G::NLD;
+  // one item: NBP column blocks from cb0 -- MFMAs over the resident W (B operands of
+  // step s + 1 read from LDS while step s's MFMAs issue), then the epilogue.  A column
+  // block's accumulation and a head's score dot are the same operations in the same
+  // order whichever item holds them, so a part's values are the whole tile's bits.
+  auto tile = [&](auto nbp_c, int t, int cb0, u32x4_t* cur, uint32_t noff) {
+    constexpr int NBP = decltype(nbp_c)::value;
+    f32x4 acc[NBP];
 #pragma unroll
-  for (int u = 0; u < G::EPL; ++u) {
-    alv[u] = FE > 0 && al != nullptr ? al[cl + u] : 0.f;
-    arv[u] = FE > 0 && ar != nullptr ? ar[cl + u] : 0.f;
-  }
-
-  // tiles: the first pass of waves covers every SIMD once (wave w & 3 of each block)
-  // before any SIMD takes a second wave's share, so the tail tiles spread out
-  const int nblk = gridDim.x;
-  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
-  const int nw = nblk * kProjWaves;
-  const int tiles = (M + 15) / 16;
-  if (gw >= tiles) return;
-
-  // buffer-descriptor loads: a row past M (or a tile past the last) reads 0 without a
-  // branch, so the prefetch is unconditional and the waits on it stay exact (a load
-  // under "if (t + nw < tiles)" made the join wait on the tile just issued)
-  const rsrc_t r_x = make_rsrc(X, (uint32_t)((int64_t)M * K * sizeof(T)));
-  auto load_tile = [&](int t, u32x4_t* raw) {
-    const int row = t * 16 + r16;
-    const uint32_t off = row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) +
-                                       (uint32_t)(g * G::KL * sizeof(T)) : kOOB;
-#pragma unroll
-    for (int i = 0; i < G::NLD; ++i) raw[i] = buf_b128(r_x, off + 16u * i);
-  };
-  // one tile: MFMAs over the resident W (B operands of step s + 1 read from LDS while
-  // step s's MFMAs issue), then the epilogue
-  auto tile = [&](int t, const u32x4_t* cur) {
-    f32x4 acc[G::NB];
-#pragma unroll
-    for (int c = 0; c < G::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < NBP; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (G::F32) {
-      const float* Wf = reinterpret_cast<const float*>(Wl) + g * G::PW + r16;
-      float bc[G::NB], bn[G::NB];
+      const float* Wf = reinterpret_cast<const float*>(Wl) + g * G::PW + r16 + cb0 * 16;
+      float bc[NBP], bn[NBP];
 #pragma unroll
-      for (int c = 0; c < G::NB; ++c) bc[c] = Wf[c * 16];
+      for (int c = 0; c < NBP; ++c) bc[c] = Wf[c * 16];
 #pragma unroll
       for (int s = 0; s < G::S; ++s) {
         if (s + 1 < G::S) {
 #pragma unroll
-          for (int c = 0; c < G::NB; ++c) bn[c] = Wf[4 * (s + 1) * G::PW + c * 16];
+          for (int c = 0; c < NBP; ++c) bn[c] = Wf[4 * (s + 1) * G::PW + c * 16];
         }
         // keep step s + 1's LDS reads ahead of step s's MFMAs (the scheduler would
         // otherwise sink each read to just before its MFMA and wait on it there)
         __builtin_amdgcn_sched_barrier(0);
         const float a = __uint_as_float(cur[s >> 2][s & 3]);
 #pragma unroll
-        for (int c = 0; c < G::NB; ++c)
+        for (int c = 0; c < NBP; ++c)
           acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+        if ((s + 1) % SPL == 0) cur[s / SPL] = buf_b128(r_x, noff + 16u * (s / SPL));
 #pragma unroll
-        for (int c = 0; c < G::NB; ++c) bc[c] = bn[c];
+        for (int c = 0; c < NBP; ++c) bc[c] = bn[c];
       }
     } else {
-      const bf16_t* Wb = reinterpret_cast<const bf16_t*>(Wl) + r16 * G::PW + g * G::KL;
-      bf16x8 bc[G::NB], bn[G::NB];
+      const bf16_t* Wb = reinterpret_cast<const bf16_t*>(Wl) + (r16 + cb0 * 16) * G::PW + g * G::KL;
+      bf16x8 bc[NBP], bn[NBP];
 #pragma unroll
-      for (int c = 0; c < G::NB; ++c) bc[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW);
+      for (int c = 0; c < NBP; ++c) bc[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW);
 #pragma unroll
       for (int s = 0; s < G::S; ++s) {
         if (s + 1 < G::S) {
 #pragma unroll
-          for (int c = 0; c < G::NB; ++c)
+          for (int c = 0; c < NBP; ++c)
             bn[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW + 8 * (s + 1));
         }
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8 a = __builtin_bit_cast(bf16x8, cur[s]);
 #pragma unroll
-        for (int c = 0; c < G::NB; ++c)
+        for (int c = 0; c < NBP; ++c)
           acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bc[c], acc[c], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+        if ((s + 1) % SPL == 0) cur[s / SPL] = buf_b128(r_x, noff + 16u * (s / SPL));
 #pragma unroll
-        for (int c = 0; c < G::NB; ++c) bc[c] = bn[c];
+        for (int c = 0; c < NBP; ++c) bc[c] = bn[c];
       }
     }
-    // ---- epilogue: stage the 16 x N tile (MFMA C layout: col = lane & 15, row =
-    // 4 (lane >> 4) + reg), then whole-row segments per wave store + score dots
+    // ---- epilogue: stage the 16 x 16 NBP item (MFMA C layout: col = lane & 15, row =
+    // 4 (lane >> 4) + reg), SWE columns at a time, then whole-row segments per wave
+    // store + score dots
+    constexpr int SWE = NBP * 16 < S::SW ? NBP * 16 : S::SW;
+    constexpr int LPR = SWE / G::EPL, RPP = 64 / LPR, TPS = SWE + 4;
+    static_assert(64 % LPR == 0 && 16 % RPP == 0 && (FE == 0 || SWE % FE == 0), "proj staging");
+    const int cl = (lane % LPR) * G::EPL;  // first staged column of this lane
 #pragma unroll
-    for (int c = 0; c < G::NB; ++c)
+    for (int hf = 0; hf < NBP * 16 / SWE; ++hf) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * G::TPS + c * 16 + r16] = acc[c][i];
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
-    __builtin_amdgcn_wave_barrier();
+      for (int c = 0; c < SWE / 16; ++c)
 #pragma unroll
-    for (int pass = 0; pass < 16 / G::RPP; ++pass) {
-      const int rr = pass * G::RPP + lane / G::LPR;
-      const int row = t * 16 + rr;
-      float e[G::EPL];
+        for (int i = 0; i < 4; ++i)
+          Tw[(4 * g + i) * TPS + c * 16 + r16] = acc[hf * (SWE / 16) + c][i];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int col = cb0 * 16 + hf * SWE + cl;
 #pragma unroll
-      for (int u = 0; u < G::EPL; u += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(Tw + rr * G::TPS + cl + u);
-        e[u] = v.x; e[u + 1] = v.y; e[u + 2] = v.z; e[u + 3] = v.w;
-      }
-      if (row < M) {
-        if constexpr (G::F32) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(h) + (int64_t)row * N + cl) =
-              make_float4(e[0], e[1], e[2], e[3]);
-        } else {
-          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(h) + (int64_t)row * N + cl) =
-              make_uint4(pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]),
-                         pack_bf16x2(e[4], e[5]), pack_bf16x2(e[6], e[7]));
+      for (int pass = 0; pass < 16 / RPP; ++pass) {
+        const int rr = pass * RPP + lane / LPR;
+        const int row = t * 16 + rr;
+        float e[G::EPL];
+#pragma unroll
+        for (int u = 0; u < G::EPL; u += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(Tw + rr * TPS + cl + u);
+          e[u] = v.x; e[u + 1] = v.y; e[u + 2] = v.z; e[u + 3] = v.w;
+        }
+        if (row < M) {
+          if constexpr (G::F32) {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(h) + (int64_t)row * N + col) =
+                make_float4(e[0], e[1], e[2], e[3]);
+          } else {
+            *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(h) + (int64_t)row * N + col) =
+                make_uint4(pack_bf16x2(e[0], e[1]), pack_bf16x2(e[2], e[3]),
+                           pack_bf16x2(e[4], e[5]), pack_bf16x2(e[6], e[7]));
+          }
+        }
+        if constexpr (FE > 0) {
+          float sl = 0.f, sr = 0.f;
+#pragma unroll
+          for (int u = 0; u < G::EPL; u += 4) {
+            const float4 a4 = *reinterpret_cast<const float4*>(als + col + u);
+            const float4 r4 = *reinterpret_cast<const float4*>(ars + col + u);
+            const float av[4] = {a4.x, a4.y, a4.z, a4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              sl = fmaf(e[u + j], av[j], sl);
+              sr = fmaf(e[u + j], rv[j], sr);
+            }
+          }
+#pragma unroll
+          for (int o = 1; o < FE / G::EPL; o <<= 1) {
+            sl += __shfl_xor(sl, o);
+            sr += __shfl_xor(sr, o);
+          }
+          if (col % FE == 0 && row < M) {
+            if (el != nullptr) el[(int64_t)row * H + col / FE] = sl;
+            if (er != nullptr) er[(int64_t)row * H + col / FE] = sr;
+          }
         }
       }
-      if constexpr (FE > 0) {
-        float sl = 0.f, sr = 0.f;
-#pragma unroll
-        for (int u = 0; u < G::EPL; ++u) {
-          sl = fmaf(e[u], alv[u], sl);
-          sr = fmaf(e[u], arv[u], sr);
-        }
-#pragma unroll
-        for (int o = 1; o < FE / G::EPL; o <<= 1) {
-          sl += __shfl_xor(sl, o);
-          sr += __shfl_xor(sr, o);
-        }
-        if (cl % FE == 0 && row < M) {
-          if (el != nullptr) el[(int64_t)row * H + cl / FE] = sl;
-          if (er != nullptr) er[(int64_t)row * H + cl / FE] = sr;
-        }
-      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // staging reads done before the next writes
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // staging reads done before the next tile's writes
-    __builtin_amdgcn_wave_barrier();
   };
-  // two register buffers, alternating: tile t + nw's loads fly during tile t
-  u32x4_t bufA[G::NLD], bufB[G::NLD];
-  load_tile(gw, bufA);
-  for (int t = gw; t < tiles; t += 2 * nw) {
-    load_tile(t + nw, bufB);
-    __builtin_amdgcn_sched_barrier(0);
-    tile(t, bufA);
-    if (t + nw >= tiles) break;
-    load_tile(t + 2 * nw, bufA);
-    __builtin_amdgcn_sched_barrier(0);
-    tile(t + nw, bufB);
-  }
+  // past the last item the prefetch reads 0 (kOOB)
+  auto next_off = [&](int k) -> uint32_t { return k + 1 < n_items ? tile_off(item_tile(k + 1)) : kOOB; };
+  for (int k = 0; k < R; ++k)
+    tile(std::integral_constant<int, G::NB>{}, item_tile(k), 0, buf, next_off(k));
+  for (int k = R; k < n_items; ++k)
+    tile(std::integral_constant<int, G::NB / PT>{}, item_tile(k), item_cb(k), buf, next_off(k));
 }
 
 // ------------------------------------------------------ pair linear (LLP 'mlp') ---
@@ -522,12 +591,18 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
   __syncthreads();
 
   float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
-  const int cl = (lane % Gm::LPR) * Gm::EPL;
+  // items as proj_kernel: R whole-tile rounds, then the leftover tiles in PT column parts
+  constexpr int PT = 4;
   const int nblk = gridDim.x;
   const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
   const int nw = nblk * kProjWaves;
   const int tiles = (M + 15) / 16;
-  if (gw >= tiles) return;
+  const int R = tiles / nw;
+  const int units = PT * (tiles - R * nw);
+  const int n_items = R + (gw < units ? (units - gw + nw - 1) / nw : 0);
+  if (n_items == 0) return;
+  auto item_tile = [&](int k) -> int { return k < R ? gw + k * nw : R * nw + (gw + (k - R) * nw) / PT; };
+  auto item_cb = [&](int k) -> int { return k < R ? 0 : ((gw + (k - R) * nw) % PT) * (Gm::NB / PT); };
 
   const rsrc_t r_x = make_rsrc(Dh, (uint32_t)((int64_t)M * K * 4));
   const rsrc_t r_d1 = make_rsrc(d1, (uint32_t)((int64_t)M * hH * 4));
@@ -550,21 +625,22 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
       b.e2[j] = buf_f32(r_d2, o);
     }
   };
-  auto tile = [&](int t, const Tile& cur) {
-    f32x4 acc[Gm::NB];
+  auto tile = [&](auto nbp_c, int t, int cb0, const Tile& cur) {
+    constexpr int NBP = decltype(nbp_c)::value;
+    f32x4 acc[NBP];
 #pragma unroll
-    for (int c = 0; c < Gm::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float* Wf = Wl + g * Gm::PW + r16;
+    for (int c = 0; c < NBP; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* Wf = Wl + g * Gm::PW + r16 + cb0 * 16;
     const float* a1l = a1s + g * Gm::KL;
     const float* a2l = a2s + g * Gm::KL;
-    float bc[Gm::NB], bn[Gm::NB];
+    float bc[NBP], bn[NBP];
 #pragma unroll
-    for (int c = 0; c < Gm::NB; ++c) bc[c] = Wf[c * 16];
+    for (int c = 0; c < NBP; ++c) bc[c] = Wf[c * 16];
 #pragma unroll
     for (int s = 0; s < Gm::S; ++s) {
       if (s + 1 < Gm::S) {
 #pragma unroll
-        for (int c = 0; c < Gm::NB; ++c) bn[c] = Wf[4 * (s + 1) * Gm::PW + c * 16];
+        for (int c = 0; c < NBP; ++c) bn[c] = Wf[4 * (s + 1) * Gm::PW + c * 16];
       }
       const int hi = s >= hF ? 1 : 0;
       const float av1 = a1l[s], av2 = a2l[s];
@@ -572,38 +648,50 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
       const float x = __uint_as_float(cur.x[s >> 2][s & 3]);
       const float a = fmaf(cur.e2[hi], av2, fmaf(cur.e1[hi], av1, x));
 #pragma unroll
-      for (int c = 0; c < Gm::NB; ++c)
+      for (int c = 0; c < NBP; ++c)
         acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int c = 0; c < Gm::NB; ++c) bc[c] = bn[c];
+      for (int c = 0; c < NBP; ++c) bc[c] = bn[c];
     }
+    constexpr int SWE = NBP * 16, LPR = SWE / 4, RPP = 64 / LPR, TPS = SWE + 4;
+    static_assert(64 % LPR == 0 && 16 % RPP == 0, "dx staging");
+    const int cl = (lane % LPR) * 4;
 #pragma unroll
-    for (int c = 0; c < Gm::NB; ++c)
+    for (int c = 0; c < NBP; ++c)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * Gm::TPS + c * 16 + r16] = acc[c][i];
+      for (int i = 0; i < 4; ++i) Tw[(4 * g + i) * TPS + c * 16 + r16] = acc[c][i];
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int pass = 0; pass < 16 / Gm::RPP; ++pass) {
-      const int rr = pass * Gm::RPP + lane / Gm::LPR;
+    for (int pass = 0; pass < 16 / RPP; ++pass) {
+      const int rr = pass * RPP + lane / LPR;
       const int row = t * 16 + rr;
-      const float4 v = *reinterpret_cast<const float4*>(Tw + rr * Gm::TPS + cl);
-      if (row < M) *reinterpret_cast<float4*>(out + (int64_t)row * N + cl) = v;
+      const float4 v = *reinterpret_cast<const float4*>(Tw + rr * TPS + cl);
+      if (row < M) *reinterpret_cast<float4*>(out + (int64_t)row * N + cb0 * 16 + cl) = v;
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
   };
+  // two tile buffers, alternating: item k + 1's loads fly during item k (past the last
+  // item they read 0)
+  auto run = [&](int k, Tile& cur) {
+    if (k < R)
+      tile(std::integral_constant<int, Gm::NB>{}, item_tile(k), 0, cur);
+    else
+      tile(std::integral_constant<int, Gm::NB / PT>{}, item_tile(k), item_cb(k), cur);
+  };
+  auto next_tile = [&](int k) -> int { return k < n_items ? item_tile(k) : tiles; };
   Tile ta, tb;
-  load_tile(gw, ta);
-  for (int t = gw; t < tiles; t += 2 * nw) {
-    load_tile(t + nw, tb);
+  load_tile(item_tile(0), ta);
+  for (int k = 0; k < n_items; k += 2) {
+    load_tile(next_tile(k + 1), tb);
     __builtin_amdgcn_sched_barrier(0);
-    tile(t, ta);
-    if (t + nw >= tiles) break;
-    load_tile(t + 2 * nw, ta);
+    run(k, ta);
+    if (k + 1 >= n_items) break;
+    load_tile(next_tile(k + 2), ta);
     __builtin_amdgcn_sched_barrier(0);
-    tile(t + nw, tb);
+    run(k + 1, tb);
   }
 }
 
@@ -811,9 +899,9 @@ static bool skinny_enabled() {
   return on != 0;
 }
 
-static int proj_grid(int64_t M) {
+static int proj_grid(int64_t M, int waves = sk::kProjWaves) {
   const int64_t tiles = (M + 15) / 16;
-  const int64_t blocks = (tiles + sk::kProjWaves - 1) / sk::kProjWaves;
+  const int64_t blocks = (tiles + waves - 1) / waves;
   return (int)(blocks < 256 ? blocks : 256);  // one 8-wave block per CU
 }
 
@@ -828,11 +916,11 @@ int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, con
   const bool score = al != nullptr || ar != nullptr;
   const int minfe = 16 / (int)sizeof(T);
   if (score && (feat < minfe || N % feat != 0)) return 0;
-  const dim3 grid(proj_grid(M)), block(64 * sk::kProjWaves);
 #define SKP(k, n, fe)                                                                           \
   if (K == k && N == n && (score ? feat == fe : fe == 0)) {                                    \
-    hipLaunchKernelGGL((sk::proj_kernel<T, k, n, fe>), grid, block, 0, s, (int)M,              \
-                       (const T*)X, (const T*)W, al, ar, (T*)h, el, er, heads);                 \
+    constexpr int wv = sk::ProjStage<T, k, n, fe>::WAVES;                                      \
+    hipLaunchKernelGGL((sk::proj_kernel<T, k, n, fe>), dim3(proj_grid(M, wv)), dim3(64 * wv),  \
+                       0, s, (int)M, (const T*)X, (const T*)W, al, ar, (T*)h, el, er, heads);   \
     return 1;                                                                                   \
   }
 #define SKP_N(k, n) SKP(k, n, 0) SKP(k, n, 16) SKP(k, n, 32) SKP(k, n, 64) SKP(k, n, n)
