@@ -430,20 +430,26 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_kernel(
 // is rounded to bf16 before the MFMA, as a bf16 x_i * x_j is in PyTorch (and as the
 // tiled bf16 GEMM's gather-hadamard loader does); nn.Linear's (N, K) weight is already
 // the [n][k] image the bf16 B operand reads.  Scores out in fp32 or bf16 (OB).
+// 3 waves per SIMD: 588 -> 540 us per 4M pairs (gather-bound: more loads in flight); a
+// one-register-set rolling reload measured slower (576 us at 3, 631 at 2 waves per SIMD)
+#ifndef PAIR_WPS
+#define PAIR_WPS 3
+#endif
+constexpr int kPairWaves = 4 * PAIR_WPS;  // pair_bf16_kernel block (waves per SIMD x 4)
 template <int K, int N, bool OB>
-__global__ void __launch_bounds__(64 * kProjWaves) pair_bf16_kernel(
+__global__ void __launch_bounds__(64 * kPairWaves) pair_bf16_kernel(
     int M, const bf16_t* __restrict__ G, int64_t ldg, const int64_t* __restrict__ gi,
     const bf16_t* __restrict__ G2, int64_t ldg2, const int64_t* __restrict__ gj,
     const bf16_t* __restrict__ Wlin, const float* __restrict__ bias, int act, Dropout dp,
     void* __restrict__ out) {
   using Gm = ProjGeo<bf16_t, K, N>;
-  __shared__ __attribute__((aligned(16))) char smem[Gm::WBYTES + kProjWaves * Gm::SBYTES];
+  __shared__ __attribute__((aligned(16))) char smem[Gm::WBYTES + kPairWaves * Gm::SBYTES];
   bf16_t* Wl = reinterpret_cast<bf16_t*>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
 
-  for (int idx = tid; idx < N * K / 8; idx += 64 * kProjWaves) {
+  for (int idx = tid; idx < N * K / 8; idx += 64 * kPairWaves) {
     const int n = idx / (K / 8), k8 = idx % (K / 8);
     *reinterpret_cast<uint4*>(Wl + n * Gm::PW + 8 * k8) =
         *reinterpret_cast<const uint4*>(Wlin + (int64_t)n * K + 8 * k8);
@@ -459,7 +465,7 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_bf16_kernel(
 
   const int nblk = gridDim.x;
   const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
-  const int nw = nblk * kProjWaves;
+  const int nw = nblk * kPairWaves;
   const int tiles = (M + 15) / 16;
   if (gw >= tiles) return;
 
@@ -966,7 +972,7 @@ int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int6
   if (G2 == nullptr) { G2 = G; ldg2 = ldg; }
   if (ldg % 8 || ldg2 % 8 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)W | (uintptr_t)out) & 15))
     return 0;
-  const dim3 grid(proj_grid(P)), block(64 * sk::kProjWaves);
+  const dim3 grid(proj_grid(P, sk::kPairWaves)), block(64 * sk::kPairWaves);
 #define SKPB(k, n)                                                                              \
   if (K == k && N == n) {                                                                       \
     if (out_bf16)                                                                               \
