@@ -46,11 +46,27 @@ def main():
         us_p = timeit(lambda: MF.project_scores(X, W, al, ar, heads=H))
         us_w = timeit(lambda: MF.gemm_head_outer(X.t(), dh, 1, outer))
         flop = 2.0 * M * K * D
+        if os.environ.get("GEMM_AB_SAVE") and dt == torch.float32:  # bitwise A/B of the outputs
+            torch.save({"h": MF.project_scores(X, W, al, ar, heads=H),
+                        "dw": MF.gemm_head_outer(X.t(), dh, 1, outer),
+                        "dw0": MF.gemm(X.t(), dh)}, os.environ["GEMM_AB_SAVE"])
         print(json.dumps({"skinny": os.environ.get("MSHA_SKINNY", "1"), "dtype": str(dt)[6:],
                           "proj_us": round(us_p, 1), "proj_TFs": round(flop / us_p / 1e6, 1),
                           "wgrad_us": round(us_w, 1), "wgrad_TFs": round(flop / us_w / 1e6, 1)}),
               flush=True)
 
 
+def cmp(a, b):
+    x, y = torch.load(a), torch.load(b)
+    for k in x:
+        xa = x[k][0] if isinstance(x[k], tuple) else x[k]
+        ya = y[k][0] if isinstance(y[k], tuple) else y[k]
+        print(json.dumps({"out": k, "bit_identical": bool(torch.equal(xa, ya)),
+                          "max_abs_diff": float((xa - ya).abs().max())}))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "cmp":
+        cmp(sys.argv[2], sys.argv[3])
+    else:
+        main()
