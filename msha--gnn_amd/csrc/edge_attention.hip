@@ -20,6 +20,8 @@
 // pass needs no second sweep over the gathered rows.
 #include <stdlib.h>
 
+#include <cstdlib>
+
 #include "common.h"
 
 #ifndef COLS_EH
@@ -929,7 +931,8 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
 #pragma unroll
         for (int g0 = 0; g0 < G::CE; g0 += UG * G::EPI) {
           if (g0 >= nvalid) break;
-          Pk<T> dl[UG][G::QPL];
+          // raw 16-B pieces in flight (a bf16 piece widens to 8 floats only at its use)
+          u32x4_t dl[UG][G::QPL];
 #pragma unroll
           for (int u = 0; u < UG; ++u) {
             const int g = g0 + u * G::EPI;
@@ -942,7 +945,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
               const uint32_t off = ei < nvalid
                   ? (uint32_t)iq * (uint32_t)(G::D * sizeof(T)) + (uint32_t)(G::V * q * sizeof(T))
                   : kOOB;
-              dl[u][k] = pk_load_buf(r_dU, off, (T*)nullptr);
+              dl[u][k] = buf_b128(r_dU, off);
             }
           }
 #pragma unroll
@@ -957,8 +960,9 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
             for (int k = 0; k < G::QPL; ++k) {
               const int q = quad_of<G>(lane, k);
               const float wq = __shfl(wv, ei * H + q / G::QH);
-              acc[k] = pk_fma(wq, dl[u][k], acc[k]);
-              float t = pk_dot(dl[u][k], hcq[k]);
+              const Pk<T> dUi = pk_from_raw(dl[u][k], (T*)nullptr);
+              acc[k] = pk_fma(wq, dUi, acc[k]);
+              float t = pk_dot(dUi, hcq[k]);
               t = group_sum<G::QH>(t);
               const float cand = __shfl(t, srcl);
               if (mine && (G::QPL == 1 || k == dsrc_k)) gsum = cand;
@@ -1535,7 +1539,11 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
   // the CSR-order row sum reads it contiguously (measured: syn100k's 64 MB de is faster
   // in edge order, syn2m's 1.28 GB in slot order)
   const bool slot_de = g->csr_slot != nullptr && g->n_edges * 4 * (int64_t)heads >= DE_SLOT_MIN_BYTES;
-  const bool buf_ok = g->n_rows * (int64_t)heads * feat * (int64_t)sizeof(T) < lim &&
+  // MSHA_COLS_NOBUF=1 forces the pointer-load column pass (what tables of 2 GiB or more
+  // take) so tests cover it at small sizes; read per call, so a test can flip it
+  const char* nobuf = getenv("MSHA_COLS_NOBUF");
+  const bool buf_ok = !(nobuf != nullptr && *nobuf == '1') &&
+                      g->n_rows * (int64_t)heads * feat * (int64_t)sizeof(T) < lim &&
                       g->n_edges * 4 * (int64_t)heads < lim && g->n_rows * 4 * rec_stride(heads) < lim;
 #define X(h, f)                                                                                \
   if (heads == h && feat == f) {                                                               \

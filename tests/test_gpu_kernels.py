@@ -316,6 +316,38 @@ def test_edge_attention_fused_backward_wide_rows(cuda, msha, H, F, dtype):
             tol_close(got[3].cpu().numpy(), bw["d_hc"], EMB_RTOL, 1e-5)
 
 
+@pytest.mark.parametrize("H,F", [(8, 16), (2, 64), (8, 64)], ids=lambda v: str(v))
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_edge_attention_fused_backward_pointer_loads(cuda, msha, H, F, dtype):
+    """The column pass that tables of 2 GiB or more take (plain pointer loads, no buffer
+    descriptors; forced here with MSHA_COLS_NOBUF=1): fused == split and fp32 == oracle,
+    with ragged slot groups, an empty row and a column split over chunks."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(17 * H + F)
+    n, m = 700, 48
+    c, rowptr, col, empty, el, er, hc, hs, dU, dV = _edge_case(
+        rng, n, m, H, F, 9, empty_rows=(2,), hot_col=7)
+    graph = Graph.from_dense(t(c, cuda))
+    tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+    p = 0.4
+    os.environ["MSHA_COLS_NOBUF"] = "1"
+    try:
+        got = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, True, rowterms=False)
+    finally:
+        os.environ.pop("MSHA_COLS_NOBUF", None)
+    split = _u_only_grads(MF, graph, el, er, hc, dU, p, 5, cuda, tdt, False)
+    _same_as_split(got, split, tdt)
+    if dtype == "f32":
+        keep = _keep_mask(graph.n_edges, H, p, 5, cuda)
+        ref = O.edge_aggregate_fwd(rowptr, col, el, er, hc, keep=keep, p=p, rowflag=empty)
+        bw = O.edge_aggregate_bwd(rowptr, col, ref, hc, dU, keep=keep, p=p)
+        tol_close(got[1].cpu().numpy(), bw["d_el"], 1e-4, 1e-5)
+        tol_close(got[2].cpu().numpy(), bw["d_er"], 1e-4, 1e-5)
+        tol_close(got[3].cpu().numpy(), bw["d_hc"], EMB_RTOL, 1e-5)
+
+
 def test_edge_attention_weights_exported(cuda):
     """attd output of the forward vs oracle attention (absolute 1e-5)."""
     from msha_gnn_amd import _lib
