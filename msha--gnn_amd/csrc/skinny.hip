@@ -58,6 +58,27 @@ struct ProjGeo {
   static_assert(64 % LPR == 0, "a row must map onto whole lanes");
 };
 
+// Fill the fp32 W image [k'][n] (k' = 4 (k % KL) + k / KL, pitch PW) from a row-major
+// (N, K) matrix M[n][k] (B[k][n] = M[n][k]).  A lane reads 16 B of one row n (4
+// consecutive k) and writes them to 4 image rows: a wave's 64 stores of one element
+// index fall in 8 banks (8-way).  One element per lane in M's order (k fastest) put every
+// lane of a wave on 2 banks (32-way), ~7 us of LDS time per block at K = N = 128.
+template <int K, int N>
+__device__ __forceinline__ void transpose_fill(float* Wl, const float* __restrict__ M, int tid,
+                                               int nthreads) {
+  using Gm = ProjGeo<float, K, N>;
+  for (int idx = tid; idx < K * N / 4; idx += nthreads) {
+    const int n = idx / (K / 4), k4 = idx % (K / 4);
+    const float4 v = *reinterpret_cast<const float4*>(M + n * K + 4 * k4);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 4 * k4 + j;
+      Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = e[j];
+    }
+  }
+}
+
 // proj_kernel's block: PROJ_WPS waves per SIMD when the resident W and one staging
 // tile per wave fit the 160 KB of LDS, the staging tile narrowed to column halves when
 // the whole-width one would not fit (a head must not straddle the halves), else 2.
@@ -324,10 +345,7 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_kernel(
   const int g = lane >> 4, r16 = lane & 15;
 
   // ---- B[k][n] = Wlin[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL
-  for (int idx = tid; idx < K * N; idx += 64 * kProjWaves) {
-    const int n = idx / K, k = idx % K;
-    Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = Wlin[idx];
-  }
+  transpose_fill<K, N>(Wl, Wlin, tid, 64 * kProjWaves);
   __syncthreads();
 
   float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
@@ -586,10 +604,7 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
   const int g = lane >> 4, r16 = lane & 15;
 
   // B[k][n] = W[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL
-  for (int idx = tid; idx < K * N; idx += 64 * kProjWaves) {
-    const int n = idx / K, k = idx % K;
-    Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = Wt[idx];
-  }
+  transpose_fill<K, N>(Wl, Wt, tid, 64 * kProjWaves);
   for (int k = tid; k < K; k += 64 * kProjWaves) {
     a1s[k] = a1[k];
     a2s[k] = a2 != nullptr ? a2[k] : 0.f;
@@ -951,7 +966,8 @@ int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t 
                        hipStream_t s) {
   if (!skinny_enabled() || P < 1024 || P >= (1ll << 31) || gi == nullptr || gj == nullptr) return 0;
   if (G2 == nullptr) { G2 = G; ldg2 = ldg; }
-  if (ldg % 4 || ldg2 % 4 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)out) & 15)) return 0;
+  if (ldg % 4 || ldg2 % 4 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)out | (uintptr_t)W) & 15))
+    return 0;
   const dim3 grid(proj_grid(P)), block(64 * sk::kProjWaves);
 #define SKPL(k, n)                                                                              \
   if (K == k && N == n) {                                                                       \
@@ -999,7 +1015,7 @@ int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, 
   if (!skinny_enabled() || M < 1024 || M * K * 4 >= (1ll << 31) || M * hH * 4 >= (1ll << 31))
     return 0;
   if (hF < 16 || K % hF != 0 || (int64_t)hH * hF != K || d1 == nullptr || a1 == nullptr) return 0;
-  if (((uintptr_t)Dh | (uintptr_t)C) & 15) return 0;
+  if (((uintptr_t)Dh | (uintptr_t)C | (uintptr_t)W) & 15) return 0;
   const dim3 grid(proj_grid(M)), block(64 * sk::kProjWaves);
 #define SKDX(k, n)                                                                              \
   if (K == k && N == n) {                                                                       \

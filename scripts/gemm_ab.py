@@ -32,7 +32,11 @@ def timeit(fn, reps=int(os.environ.get("GEMM_AB_REPS", 50)), warm=2):
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    M, K, H, F = 100000, 128, 8, 16
+    for shape in ((100000, 128, 8, 16), (39179, 128, 2, 64)):  # C4, R15 (configs[1])
+        run_shape(dev, g, *shape)
+
+
+def run_shape(dev, g, M, K, H, F):
     D = H * F
     for dt in (torch.float32, torch.bfloat16):
         X = torch.rand(M, K, device=dev, generator=g).to(dt)
@@ -45,18 +49,26 @@ def main():
         outer = (H, F, de, al, de2, ar)
         us_p = timeit(lambda: MF.project_scores(X, W, al, ar, heads=H))
         us_w = timeit(lambda: MF.gemm_head_outer(X.t(), dh, 1, outer))
+        us_x = timeit(lambda: MF.gemm_head_outer(dh, W.t(), 0, outer)) if dt == torch.float32 else 0.0
         flop = 2.0 * M * K * D
         if os.environ.get("GEMM_AB_SAVE") and dt == torch.float32:  # bitwise A/B of the outputs
             torch.save({"h": MF.project_scores(X, W, al, ar, heads=H),
                         "dw": MF.gemm_head_outer(X.t(), dh, 1, outer),
-                        "dw0": MF.gemm(X.t(), dh)}, os.environ["GEMM_AB_SAVE"])
-        print(json.dumps({"skinny": os.environ.get("MSHA_SKINNY", "1"), "dtype": str(dt)[6:],
+                        "dx": MF.gemm_head_outer(dh, W.t(), 0, outer),
+                        "dw0": MF.gemm(X.t(), dh)}, os.environ["GEMM_AB_SAVE"] + f".{M}")
+        print(json.dumps({"M": M, "heads": H, "dx_us": round(us_x, 1),
+                          "skinny": os.environ.get("MSHA_SKINNY", "1"), "dtype": str(dt)[6:],
                           "proj_us": round(us_p, 1), "proj_TFs": round(flop / us_p / 1e6, 1),
                           "wgrad_us": round(us_w, 1), "wgrad_TFs": round(flop / us_w / 1e6, 1)}),
               flush=True)
 
 
 def cmp(a, b):
+    for M in (100000, 39179):
+        cmp1(f"{a}.{M}", f"{b}.{M}")
+
+
+def cmp1(a, b):
     x, y = torch.load(a), torch.load(b)
     for k in x:
         xa = x[k][0] if isinstance(x[k], tuple) else x[k]

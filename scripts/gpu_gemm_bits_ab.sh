@@ -8,5 +8,5 @@ for A in ${ALTS:-}; do
   MSHA_GNN_LIB=msha--gnn_amd/lib/alt/$A.so GEMM_AB_SAVE=gpurun_out/g_$A.pt timeout -k 10 200 python -u scripts/gemm_ab.py >> gpurun_out/gemm_bits_ab.log 2>&1 || { tail -20 gpurun_out/gemm_bits_ab.log; exit 1; }
   timeout -k 10 100 python -u scripts/gemm_ab.py cmp gpurun_out/g_0.pt gpurun_out/g_$A.pt >> gpurun_out/gemm_bits_ab.log 2>&1
 done
-rm -f gpurun_out/g_*.pt
+rm -f gpurun_out/g_*.pt.*
 grep -v amdgpu.ids gpurun_out/gemm_bits_ab.log
