@@ -1,6 +1,6 @@
 """Benchmark: GAT layer forward+backward edges/s on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syn100k|r15]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syn100k|r15|...]
 
 One step = one full GAT attention layer forward + backward over the whole graph
 (SURVEY.md §8d, config C4 "synthetic CSR graph 100k nodes / 2M edges, 128-dim
@@ -8,10 +8,10 @@ features, 8 heads"):
     h = X @ W                     (100k x 128 @ 128 x 128, fp32)
     el, er = h . a_l, h . a_r     (per head, 8 heads x 16)
     u = softmax_row(lrelu(el_i + er_j)) @ h      <- msha_edge_attention_fwd (dominant)
-    backward of all of it (msha_edge_attention_bwd_rows + msha_csc_aggregate + GEMMs)
-Inputs are resident in HBM before the timed region.  For N > 1 GPUs the path
-does not shard (SURVEY.md §8e "replicas only"): every rank runs its own replica
-and value = total edges over all ranks / max-over-ranks time ("scaling": "weak").
+    backward of all of it (fused backward + GEMMs)
+Inputs are resident in HBM before the timed region.  For N > 1 GPUs the layer does
+not shard (SURVEY.md §8e "replicas only"): every rank runs its own replica and value
+= total edges over all ranks / max-over-ranks time ("scaling": "weak").
 
 The K timed steps run twice: eagerly, with HIP events around every edge-kernel launch
 (the rooflines), then as ONE replay of a HIP graph that holds exactly those K steps
@@ -19,9 +19,19 @@ The K timed steps run twice: eagerly, with HIP events around every edge-kernel l
 autograd; ``--eager`` reports the eager pass instead).  Both are bracketed by a
 barrier + synchronize and maxed over ranks.
 
-Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP
-events around every launch of it inside the eager timed region) and the CPU baseline
-(the oracle's C restatement, timed on this host's cores, rank 0, N=1 only).
+Further legs in the same JSON line (same timing rules):
+  * ``bf16``    config C3 at C4 (bf16 tables, bf16 MFMA projection);
+  * ``syn2m``   the cache-busting variant (2M nodes, 40M edges: a 1 GB fp32 table
+                outside the 256 MB Infinity Cache), fp32 and bf16;
+  * ``bip1m``   the repo's adjacency shape at scale: 1M sources x 32 recipients with
+                the 2015 degree law and column weights, the OursLayer3 core (in 128,
+                2 heads x 64, u = att @ h1 AND v = att.T @ h2, Ablation.py:260-277);
+  * ``link_score`` config C5: 4M pairs against a 100k x 128 table through the RCCL
+                all-gather of ShardedTable (a world-1 group on one GPU);
+  * ``train_step_configs1/2`` the train.py iteration on the shipped graphs.
+Rank 0 prints ONE JSON line with the roofline of the dominant kernel (HIP events
+around every launch of it inside the eager timed region) and the CPU baseline (the
+oracle's C restatement, timed on this host's cores, rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -39,11 +49,15 @@ sys.path.insert(0, ROOT)
 
 METRIC = "edges/sec GAT fwd+bwd @1 GPU; link-score pairs/sec; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_TFLOPS = 157.3  # exact-fp32 matrix peak (v_mfma_f32_*x*_f32), MI355X_MICROARCH.md
+BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 FUSED_ADAM = os.environ.get("MSHA_FUSED_ADAM", "1") != "0"
 
 
 def synth_graph(n, e, seed=0):
-    """C4 generator: e unique (row, col) pairs, rows sorted, cols uniform, deg >= 1."""
+    """C4 generator: e unique (row, col) pairs, rows sorted, cols uniform, deg >= 1.
+    numpy's PCG64 stream (seed 0), not the torch.Generator SURVEY §8d names: the graph's
+    law is the one §8d specifies, the exact edges are this generator's."""
     rng = np.random.default_rng(seed)
     keys = np.arange(n, dtype=np.int64) * n + rng.integers(0, n, n)  # one edge per row
     while len(keys) < e:
@@ -69,38 +83,80 @@ def r15_graph():
     return g["rowptr"].astype(np.int64), g["col"].astype(np.int64), int(g["n"]), int(g["m"])
 
 
+def bip_graph(n=1_000_000, seed=1015):
+    """SURVEY.md §8d C4's repo-shape bipartite generator: n sources x 32 recipients,
+    per-source degree from the shipped 2015 degree histogram, recipients drawn without
+    replacement in proportion to the 2015 column nnz (data.synthetic_csr)."""
+    import msha_loader
+
+    msha_loader.load()
+    from msha_gnn_amd.data import synthetic_csr
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    m = int(z["m"])
+    deg_hist = np.bincount(np.diff(z["rowptr"]))
+    col_w = np.bincount(z["col"].astype(np.int64), minlength=m).astype(np.float64)
+    rowptr, col = synthetic_csr(n, m, deg_hist, col_w, seed)
+    return rowptr, col, n, m
+
+
 WORKLOADS = {
     "syn100k": dict(n=100_000, e=2_000_000, fin=128, heads=8, feat=16),
     "syn100k_f128": dict(n=100_000, e=2_000_000, fin=128, heads=8, feat=128),
     "syn2m": dict(n=2_000_000, e=40_000_000, fin=128, heads=8, feat=16),  # cache-busting
+    "bip1m": dict(n=1_000_000, fin=128, heads=2, feat=64),  # repo shape: 1M x 32
 }
 
 
-def pmc_traffic(H, F, bf16=False, workload="syn100k"):
-    """HBM bytes per launch of the forward edge kernel from the newest committed PMC
-    summary of this workload (profiles/*/pmc_summary.json, written by
-    scripts/profile.sh + summarize_profile.py from separate rocprofv3 --pmc passes:
-    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  None if absent."""
+def _newest_first(path):  # round1_syn100k_v10 after _v9: compare the numbers
+    import re
+
+    tag = os.path.basename(os.path.dirname(path))
+    return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
+
+
+def pmc_lookup(patterns, glob_pat):
+    """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) summed over
+    the kernels matching ``patterns`` (regexes; each must match one kernel of the same
+    summary) in the newest committed profile matching ``glob_pat``
+    (profiles/<glob>/pmc_summary.json, written by scripts/summarize_profile.py from
+    separate rocprofv3 --pmc passes).  (None, None) if absent."""
     import glob
     import re
 
-    pat = (re.compile(rf"edge_attn_fwd(?:_bat)?_kernelILi{H}ELi{F}EDF16b") if bf16 else
-           re.compile(rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?(, (true|false))?>"))
-
-    def newest_first(path):  # round1_syn100k_v10 after _v9: compare the numbers
-        tag = os.path.basename(os.path.dirname(path))
-        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
-
-    paths = glob.glob(os.path.join(ROOT, "profiles", f"*{workload}_v*", "pmc_summary.json"))
-    for path in sorted(paths, key=newest_first, reverse=True):
+    pats = [re.compile(p) for p in patterns]
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", glob_pat, "pmc_summary.json")),
+                       key=_newest_first, reverse=True):
         try:
             summ = json.load(open(path))
         except (OSError, ValueError):
             continue
-        for k, v in summ.items():
-            if pat.search(k) and v.get("hbm_bytes_per_launch_corrected"):
-                return float(v["hbm_bytes_per_launch_corrected"]), os.path.relpath(path, ROOT)
+        tot, ok = 0.0, True
+        for p in pats:
+            hit = [v for k, v in summ.items() if p.search(k)
+                   and v.get("hbm_bytes_per_launch_corrected")]
+            if not hit:
+                ok = False
+                break
+            tot += float(hit[0]["hbm_bytes_per_launch_corrected"])
+        if ok:
+            return tot, os.path.relpath(path, ROOT)
     return None, None
+
+
+def fwd_kernel_pattern(H, F, bf16, row_scores):
+    """rocprofv3 name of the forward edge kernel (demangled or mangled)."""
+    if row_scores:
+        return (rf"edge_attn_fwd_rs_kernelILi{H}ELi{F}EDF16b" if bf16 else
+                rf"edge_attn_fwd_rs_kernel<{H}, {F}, float")
+    return (rf"edge_attn_fwd(?:_bat)?_kernelILi{H}ELi{F}EDF16b" if bf16 else
+            rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?(, (true|false))?>")
+
+
+def pmc_traffic(H, F, bf16=False, workload="syn100k", row_scores=False):
+    """HBM bytes per launch of the forward edge kernel from the newest committed PMC
+    summary of this workload (None if absent)."""
+    return pmc_lookup([fwd_kernel_pattern(H, F, bf16, row_scores)], f"*{workload}_v*")
 
 
 def bwd_rows_bytes(n, m, e, H, F, s=4):
@@ -125,7 +181,8 @@ def bwd_fused_bytes(n, m, e, H, F, n_chunks, s=4, rowterms=False):
     er in, d_hc, d_er out; the chunk plan); the row sum (rowptr, slot map, de, d_el).
     rowterms (msha_edge_attention_bwd_fused_ex with uc, qc; large graphs): the row
     stats also read uc (fp32 D floats), qc and the row flag and write d_el; the column
-    pass writes no de; no row sum."""
+    pass writes no de; no row sum.  (With row scores the column pass reads a_r instead
+    of er_j: the same 4H bytes per column.)"""
     D = H * F
     stats = n * (2 * s * D + 8 * H + 12 * H)
     cols = e * (8 + 12 * H + s * D) + m * (2 * s * D + 8 * H) + 12 * n_chunks + 4 * (m + 1)
@@ -136,24 +193,30 @@ def bwd_fused_bytes(n, m, e, H, F, n_chunks, s=4, rowterms=False):
     return stats + cols + e * 4 * H + rsum
 
 
-def fwd_bytes(n, m, e, H, F, s=4, rowterms=False):
-    """Algorithmic bytes of one msha_edge_attention_fwd launch:
+def fwd_bytes(n, m, e, H, F, s=4, rowterms=False, row_scores=False, attd=False):
+    """Algorithmic bytes of one forward edge-kernel launch:
     rowptr + col + er gather + el + h gather (s*HF per edge) + u write + lse write;
     s = bytes per table element (4 fp32, 2 bf16); rowterms: + the uc (fp32) and qc
-    writes of msha_edge_attention_fwd_ex."""
+    writes; row_scores (msha_edge_attention_fwd_rs): no er gather (er_j comes from the
+    gathered row); attd: + the (E, H) post-dropout attention write (v-branch path)."""
     rt = 4 * n * H * F + 4 * n * H if rowterms else 0
-    return (4 * (n + 1) + 4 * e + 4 * e * H + 4 * n * H + s * e * H * F + s * n * H * F
-            + 4 * n * H + rt)
+    er = 0 if row_scores else 4 * e * H
+    return (4 * (n + 1) + 4 * e + er + 4 * n * H + s * e * H * F + s * n * H * F
+            + 4 * n * H + rt + (4 * e * H if attd else 0))
 
 
 class Layer:
-    """The benchmarked GAT layer (one replica)."""
+    """The benchmarked GAT layer (one replica).  Square graphs (C4, syn2m): h = X W is
+    both the gathered table and the score source (u-only).  Bipartite graphs (R15,
+    bip1m): the OursLayer3 core, h1 = R W (recipients, gathered), h2 = S W (sources);
+    ``v_branch`` also aggregates v = att.T @ h2 (Ablation.py:273)."""
 
     def __init__(self, dev, rowptr, col, n, m, fin, H, F, seed, dtype=torch.float32, graph=None,
-                 dropout=0.0):
+                 dropout=0.0, v_branch=False):
         import msha_loader
 
         msha_loader.load()
+        from msha_gnn_amd import _lib
         from msha_gnn_amd import functional as MF
         from msha_gnn_amd.graph import Graph
 
@@ -170,16 +233,22 @@ class Layer:
         self.al = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
         self.ar = torch.randn(H, F, generator=g).to(dev).requires_grad_(True)
         self.dU = torch.randn(n, H, F, generator=g).to(dev, dtype)
+        self.v_branch = bool(v_branch and self.Xr is not None)
+        self.dV = torch.randn(m, H, F, generator=g).to(dev, dtype) if self.v_branch else None
         # attention dropout of the reference's training forward (Ablation.py:271): Philox
         # masks drawn inside the forward and regenerated by the backward
         self.p = dropout
-        # the u-only fused backward takes the forward's row terms on large graphs
-        # (msha_edge_attention_rowterms_preferred): their bytes enter the rooflines
-        from msha_gnn_amd import _lib
-
         code = 1 if dtype == torch.bfloat16 else 0
-        self.rowterms = bool(MF.ROWTERMS and MF.FUSED_BWD and _lib.load()
-                             .msha_edge_attention_rowterms_preferred(self.graph.desc, H, F, code))
+        lib = _lib.load()
+        # the u-only fused backward takes the forward's row terms on large graphs
+        # (msha_edge_attention_rowterms_preferred), and its scores come from the gathered
+        # rows (msha_edge_attention_fwd_rs): both enter the rooflines' byte counts
+        self.rowterms = bool(not self.v_branch and MF.ROWTERMS and MF.FUSED_BWD
+                             and lib.msha_edge_attention_rowterms_preferred(self.graph.desc, H,
+                                                                            F, code))
+        self.row_scores = bool(not self.v_branch and MF.ROW_SCORES and MF.FUSED_BWD
+                               and lib.msha_edge_attention_row_scores_supported(self.graph.desc,
+                                                                                H, F, code))
 
     def step(self):
         for p in (self.W, self.al, self.ar):
@@ -188,24 +257,196 @@ class Layer:
         if self.Xr is None:
             h, el, er = self.MF.project_scores(self.X, self.W, self.al, self.ar, heads=self.H)
             hc = h.view(self.n, self.H, self.F)
+            hs = None
         else:  # OursLayer3 shape (Ablation.py:262-274): h1 = R W (recipients), h2 = S W
             h1, er = self.MF.project_scores(self.Xr, self.W, ar=self.ar, heads=self.H)
-            _, el = self.MF.project_scores(self.X, self.W, al=self.al, heads=self.H)
+            h2, el = self.MF.project_scores(self.X, self.W, al=self.al, heads=self.H)
             hc = h1.view(self.m, self.H, self.F)
-        u = self.MF.edge_attention(self.graph, el, er, hc, p=self.p, training=self.p > 0)
-        u.backward(self.dU)
+            hs = h2.view(self.n, self.H, self.F) if self.v_branch else None
+        # er = hc . a_r: the u-only kernels recompute it from the rows they gather
+        out = self.MF.edge_attention(self.graph, el, er, hc, hs=hs, p=self.p,
+                                     training=self.p > 0, ar=self.ar)
+        if hs is None:
+            out.backward(self.dU)
+        else:
+            torch.autograd.backward(list(out), [self.dU, self.dV])
 
 
-def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=16, warmup=3,
+class Clock:
+    """Barrier + synchronize bracketing and max-over-ranks reduction (one per run)."""
+
+    def __init__(self, dev, dist):
+        self.dev, self.dist = dev, dist
+        if dist:
+            import torch.distributed as tdist
+
+            self.tdist = tdist
+
+    def barrier(self):
+        if self.dist:
+            self.tdist.barrier()
+        torch.cuda.synchronize(self.dev)
+
+    def max_over_ranks(self, x):
+        if self.dist:
+            tt = torch.tensor([x], device=self.dev)
+            self.tdist.all_reduce(tt, op=self.tdist.ReduceOp.MAX)
+            x = float(tt.item())
+        return x
+
+    def timed_graph(self, lay, steps):
+        """Max-over-ranks seconds of ONE replay of a HIP graph holding exactly `steps`
+        steps (captured after the eager pass, which warmed every cache; one untimed
+        replay first).  Same kernels, same work as the eager steps without the host
+        launch gaps (~2-10 us per launch, Python autograd).  None if capture fails."""
+        ok, g = 1, None
+        try:
+            g = torch.cuda.CUDAGraph()
+            # thread_local: a communicator's watchdog thread (N > 1) may query its events
+            # while this thread captures
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for _ in range(steps):
+                    lay.step()
+            g.replay()
+        except RuntimeError as ex:  # report the eager number instead
+            print(f"graph capture failed: {ex}", file=sys.stderr)
+            ok = 0
+        if self.dist:  # every rank falls back together (no rank left waiting in a barrier)
+            t_ok = torch.tensor([ok], device=self.dev)
+            self.tdist.all_reduce(t_ok, op=self.tdist.ReduceOp.MIN)
+            ok = int(t_ok.item())
+        if not ok:
+            return None
+        self.barrier()
+        t0 = time.perf_counter()
+        g.replay()
+        self.barrier()
+        dt_ = self.max_over_ranks(time.perf_counter() - t0)
+        del g
+        return dt_
+
+    def timed(self, lay, steps, warmup):
+        """(max-over-ranks seconds for `steps` eager steps, mean fwd-kernel ms, launches);
+        lay.kernel_ms: mean HIP-event ms of every bracketed edge-kernel launch."""
+        for _ in range(warmup):
+            lay.step()
+        self.barrier()
+        lay.MF.KERNEL_EVENTS = {}
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            lay.step()
+        self.barrier()
+        dt_ = time.perf_counter() - t0
+        evs = lay.MF.KERNEL_EVENTS
+        lay.MF.KERNEL_EVENTS = None
+        ms = {name: float(np.mean([a.elapsed_time(b) for a, b in lst]))
+              for name, lst in evs.items() if lst}
+        events = evs.get("edge_attention_fwd", [])
+        k = ms.get("edge_attention_fwd", float("nan"))
+        dt_ = self.max_over_ranks(dt_)
+        lay.kernel_ms = ms
+        return dt_, k, len(events)
+
+
+def edge_kernels(lay, n, m, e, H, F, s, workload=None):
+    """Rooflines of the edge kernels of the step (HIP events, same run): the forward and
+    either the fused backward or bwd_rows + csc_aggregate; PMC traffic per launch from
+    the newest committed profile of ``workload`` where one covers the kernel."""
+    nch = lay.graph._plan["n_chunks"]
+    rt, rs = lay.rowterms, lay.row_scores
+    bf = s == 2
+    # rocprofv3 leaves bf16 instantiations mangled (DF16b), fp32 ones demangled
+    tmpl = (lambda k: rf"{k}ILi{H}ELi{F}EDF16b") if bf else (lambda k: rf"{k}<{H}, {F}, float")
+    pats = {
+        "msha_edge_attention_fwd": [fwd_kernel_pattern(H, F, bf, rs)],
+        "msha_edge_attention_bwd_fused": [tmpl("bwd_row_stats_kernel"),
+                                          tmpl("bwd_cols(_eh)?_kernel")]
+        + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
+    }
+    out = []
+    v = lay.v_branch
+    for name, nbytes in (("msha_edge_attention_fwd",
+                          fwd_bytes(n, m, e, H, F, s, rt, rs, attd=v)),
+                         ("msha_edge_attention_bwd_rows", bwd_rows_bytes(n, m, e, H, F, s)),
+                         ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s)),
+                         ("msha_edge_attention_bwd_fused",
+                          bwd_fused_bytes(n, m, e, H, F, nch, s, rt))):
+        key = name[len("msha_"):]
+        if key not in lay.kernel_ms:
+            continue
+        us = lay.kernel_ms[key] * 1e3
+        gbs = nbytes / (us * 1e-6) / 1e9
+        row = {"kernel": name, "algorithmic_bytes": nbytes, "avg_us": us,
+               "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
+        if rt and "rows" not in name and "csc" not in name:
+            row["rowterms"] = True
+        if rs and name != "msha_csc_aggregate" and "rows" not in name:
+            row["row_scores"] = True
+        if workload and name in pats:
+            tr, src = pmc_lookup(pats[name], f"*{workload}_v*")
+            if tr is not None:
+                row["traffic"], row["traffic_source"] = tr, src
+        out.append(row)
+    return out
+
+
+def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, world, eager,
+              dtype=torch.float32, graph=None, dropout=0.0, v_branch=False, workload=None):
+    """One timed layer configuration: edges/s (HIP-graph replay unless eager), the forward
+    kernel's roofline and the edge-kernel table.  Returns (dict, layer's graph)."""
+    e = len(col)
+    s = 2 if dtype == torch.bfloat16 else 4
+    lay = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1, dtype=dtype, graph=graph,
+                dropout=dropout, v_branch=v_branch)
+    dte, k_ms, nl = clock.timed(lay, steps, warmup)
+    dtg = None if eager else clock.timed_graph(lay, steps)
+    dt = dtg if dtg is not None else dte
+    fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
+    ach = fb / (k_ms * 1e-3) / 1e9
+    tr, src = (pmc_traffic(H, F, s == 2, workload, lay.row_scores) if workload
+               else (None, None))
+    res = {"workload": label, "value": world * e * steps / dt, "unit": "edges/s",
+           "ms_per_step": dt / steps * 1e3, "ms_per_step_eager": dte / steps * 1e3,
+           "dtype": "bf16" if s == 2 else "f32",
+           "config": {"nodes": n, "cols": m, "edges": e, "in_features": fin, "heads": H,
+                      "feat": F},
+           "roofline": {"kernel": "msha_edge_attention_fwd" + ("_rs" if lay.row_scores else ""),
+                        "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS, "traffic": tr,
+                        "traffic_unit": "bytes per launch (rocprofv3 PMC)",
+                        "traffic_source": src, "algorithmic_bytes_per_launch": fb,
+                        "avg_launch_us": k_ms * 1e3, "launches_timed": nl},
+           "edge_kernels": edge_kernels(lay, n, m, e, H, F, s, workload)}
+    g = lay.graph
+    del lay
+    return res, g
+
+
+def pair_bytes(F, s, mode, hidden):
+    """Algorithmic bytes per scored pair: two int64 indices, the two
+    gathered rows, the score(s) written (fp32 inner; mlp: hidden scores in the table's
+    dtype)."""
+    out = 4 if mode == "inner" else s * hidden
+    return 16 + 2 * s * F + out
+
+
+def link_score_bench(dev, rowptr, col, n, F, world, rank, group_ok, steps=16, warmup=3,
                      hidden=128, n_pairs=4_000_000, dtype=torch.float32, amortise=8):
     """score P = 4M pairs (2M graph edges + 2M uniform negatives,
     seed 1) against h (n x F) with LinkPredictor 'mlp' (hidden 128) and 'inner'.
     Rank r owns rows [r R, (r+1) R) of h (sharding.ShardedTable); one RCCL
-    all_gather_into_tensor per batch rebuilds the full table (inside the timed
-    loop), then each rank scores its contiguous P/W slice.  pairs/s over all ranks, with
-    the all-gather once per batch (``pairs_per_sec_*``) and once per ``amortise`` batches
-    (``pairs_per_sec_*_amortised``: the table is reused by k batches, as when one
-    embedding pass is scored against many negative samples)."""
+    all_gather_into_tensor per batch rebuilds the full table (inside the timed loop;
+    a world-1 group on one GPU, so the collective path is the one measured), then each
+    rank scores its contiguous P/W slice.  pairs/s over all ranks:
+      pairs_per_sec_*             gather, then score, per batch;
+      pairs_per_sec_*_overlapped  sharding.PipelinedScorer: batch k+1's all-gather on
+                                  the communicator's stream while batch k is scored;
+      pairs_per_sec_*_amortised   one gather per ``amortise`` batches (the table reused,
+                                  as when one embedding pass is scored against many
+                                  negative samples).
+    ``roofline``: the pair kernel alone (HIP events on its stream), fp32 'mlp' against
+    the exact-fp32 MFMA peak, the rest against HBM, with PMC traffic from the newest
+    committed profiles/*link*/ summary."""
     from msha_gnn_amd import functional as MF
     from msha_gnn_amd import sharding
 
@@ -216,7 +457,7 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=16, warmup
     dst = np.concatenate([col[pick], torch.randint(0, n, (n_pairs // 2,), generator=g).numpy()])
     t_src = torch.as_tensor(src, device=dev)
     t_dst = torch.as_tensor(dst, device=dev)
-    table = sharding.ShardedTable(n, F, world, rank, dev, dtype=dtype)
+    table = sharding.ShardedTable(n, F, world, rank, dev, dtype=dtype, buffers=2)
     lo, hi = sharding.row_range(n, world, rank)
     table.set_local(torch.rand(hi - lo, F, generator=torch.Generator().manual_seed(10 + rank))
                     .to(dev, dtype))
@@ -224,39 +465,93 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=16, warmup
     b = torch.randn(hidden, generator=g).to(dev)
     plo, phi = sharding.pair_range(n_pairs, world, rank)
     # a bf16 LinkPredictor returns bf16 scores (torch semantics); fp32 table: fp32
-    out_mlp = torch.empty(phi - plo, hidden, device=dev, dtype=dtype)
-    out_inner = torch.empty(phi - plo, device=dev)
-    if dist:
+    outs = {m_: [torch.empty(phi - plo, hidden, device=dev, dtype=dtype),
+                 torch.empty(phi - plo, hidden, device=dev, dtype=dtype)] if m_ == "mlp" else
+            [torch.empty(phi - plo, device=dev), torch.empty(phi - plo, device=dev)]
+            for m_ in ("mlp", "inner")}
+    if group_ok:
         import torch.distributed as tdist
-    fns = {"mlp": lambda h, s_, d_: MF.score_pairs(h, s_, d_, "mlp", W, b, out=out_mlp),
-           "inner": lambda h, s_, d_: MF.score_pairs(h, s_, d_, "inner", out=out_inner)}
+    calls = [0]
+
+    def fn(mode):
+        def score(h, s_, d_):  # alternate output buffers (the pipelined scorer keeps two)
+            o = outs[mode][calls[0] % 2]
+            calls[0] += 1
+            if mode == "mlp":
+                return MF.score_pairs(h, s_, d_, "mlp", W, b, out=o)
+            return MF.score_pairs(h, s_, d_, "inner", out=o)
+        return score
+
+    def sync_all():
+        if group_ok:
+            tdist.barrier()
+        torch.cuda.synchronize(dev)
+
     res = {}
-    plo_, phi_ = sharding.pair_range(n_pairs, world, rank)
+    s = 2 if dtype == torch.bfloat16 else 4
     for mode in ("mlp", "inner"):
-        for every, tag in ((1, ""), (amortise, "_amortised")):
-            def one(k):
-                if k % every == 0:
-                    sharding.score_sharded(table, t_src, t_dst, fns[mode])
-                else:  # the gathered table of the last all-gather is reused
-                    fns[mode](table.full[:n], t_src[plo_:phi_], t_dst[plo_:phi_])
-            for k in range(warmup):
-                one(k)
-            if dist:
-                tdist.barrier()
-            torch.cuda.synchronize(dev)
+        f = fn(mode)
+        for variant in ("", "_overlapped", "_amortised"):
+            if variant == "_overlapped":
+                pipe = sharding.PipelinedScorer(table, f)
+                batches = [(t_src, t_dst)] * (steps)
+
+                def run(k_steps):
+                    pipe.run(batches[:k_steps])
+            else:
+                every = amortise if variant == "_amortised" else 1
+
+                def run(k_steps, every=every):
+                    for k in range(k_steps):
+                        if k % every == 0:
+                            sharding.score_sharded(table, t_src, t_dst, f)
+                        else:  # the gathered table of the last all-gather is reused
+                            f(table.full[:n], t_src[plo:phi], t_dst[plo:phi])
+            run(warmup)
+            sync_all()
             t0 = time.perf_counter()
-            for k in range(steps):
-                one(k)
-            if dist:
-                tdist.barrier()
-            torch.cuda.synchronize(dev)
+            run(steps)
+            sync_all()
             dt = time.perf_counter() - t0
-            if dist:
+            if group_ok and world > 1:
                 tt = torch.tensor([dt], device=dev)
                 tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
                 dt = float(tt.item())
-            res[f"pairs_per_sec_{mode}{tag}"] = n_pairs * steps / dt
-            res[f"ms_per_batch_{mode}{tag}"] = dt / steps * 1e3
+            res[f"pairs_per_sec_{mode}{variant}"] = n_pairs * steps / dt
+            res[f"ms_per_batch_{mode}{variant}"] = dt / steps * 1e3
+        # the pair kernel alone: HIP events on the stream it is launched on
+        full = table.full[:n]
+        evs = []
+        st = torch.cuda.current_stream(dev)
+        for k in range(warmup + steps):
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            f(full, t_src[plo:phi], t_dst[plo:phi])
+            z.record(st)
+            if k >= warmup:
+                evs.append((a, z))
+        torch.cuda.synchronize(dev)
+        us = float(np.mean([a.elapsed_time(z) for a, z in evs])) * 1e3
+        P = phi - plo
+        nbytes = P * pair_bytes(F, s, mode, hidden)
+        flops = P * (2 * F * hidden + F) if mode == "mlp" else P * 2 * F
+        kname = ("pair_kernel" if mode == "mlp" else "pair_inner")
+        tr, src_ = pmc_lookup([_pair_pattern(mode, s == 2)], "*link*")
+        if mode == "mlp" and s == 4:
+            ach = flops / (us * 1e-6) / 1e12
+            roof = {"kernel": kname, "bound": "mfma", "achieved": ach, "peak": F32_MFMA_TFLOPS,
+                    "unit": "TFLOP/s", "frac": ach / F32_MFMA_TFLOPS}
+        else:
+            ach = nbytes / (us * 1e-6) / 1e9
+            roof = {"kernel": kname, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": ach / HBM_PEAK_GBS}
+        roof.update(avg_launch_us=us, pairs_per_launch=P, algorithmic_bytes_per_launch=nbytes,
+                    flops_per_launch=flops, kernel_pairs_per_sec=P / (us * 1e-6),
+                    traffic=tr, traffic_source=src_,
+                    traffic_note="rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch: L2->fabric "
+                                 "bytes incl. Infinity-Cache hits (each table row is gathered "
+                                 f"~{2 * n_pairs // max(n, 1)}x per batch)")
+        res[f"roofline_{mode}"] = roof
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -267,9 +562,17 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, dist, steps=16, warmup
                amortised_over_batches=amortise,
                dtype="bf16" if dtype == torch.bfloat16 else "f32",
                mlp_scores_dtype="bf16" if dtype == torch.bfloat16 else "f32",
-               sharding="h rows all-gathered over RCCL (all_gather_into_tensor), pairs split "
-               "contiguously per rank" if dist else "single GPU (no collective)")
+               sharding=(f"h rows all-gathered over RCCL (all_gather_into_tensor, world "
+                         f"{world}), pairs split contiguously per rank"
+                         if table.path() == "rccl" else f"{table.path()} (no RCCL group)"))
     return res
+
+
+def _pair_pattern(mode, bf16):
+    """rocprofv3 names of the pair kernels (skinny.hip pair_kernel, scorer.hip inner)."""
+    if mode == "mlp":
+        return r"pair_kernel.*bf16|pair_kernel.*DF16b" if bf16 else r"pair_kernel(?!.*(bf16|DF16b))"
+    return r"pair_inner.*(bf16|DF16b)" if bf16 else r"pair_inner(?!.*(bf16|DF16b))"
 
 
 def _year_graph(year):
@@ -384,6 +687,34 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
     return res
 
 
+def cpu_share():
+    """CPUs this process may use: its affinity, capped by the cgroup's CPU quota (the GPU
+    box grants each GPU a share of a large host; os.cpu_count() reports the host)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            avail = min(avail, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+class _Threads:
+    """torch CPU threads = the process's CPU share for the duration of a CPU leg."""
+
+    def __enter__(self):
+        self.prev = torch.get_num_threads()
+        torch.set_num_threads(cpu_share())
+        return self
+
+    def __exit__(self, *a):
+        torch.set_num_threads(self.prev)
+
+
 def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
     """Oracle C restatement of the same step (projection via numpy BLAS + edge-softmax
     aggregate fwd/bwd), whole graph, repeated for ~budget_s."""
@@ -422,7 +753,8 @@ def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
     return dict(value=len(col) * reps / el_t, unit="edges/s", cores=cpu_oracle.threads(),
                 kind="port",
                 sample=f"whole graph ({n} rows, {len(col)} edges), {reps} fwd+bwd steps in "
-                       f"{el_t:.1f}s: numpy X@W + oracle/edge_attention_cpu.c (OpenMP)")
+                       f"{el_t:.1f}s: numpy X@W + oracle/edge_attention_cpu.c (OpenMP, "
+                       f"{cpu_oracle.threads()} threads = OMP_NUM_THREADS)")
 
 
 def host_cpu():
@@ -440,7 +772,8 @@ def host_cpu():
     except AttributeError:
         avail = os.cpu_count()
     return {"model": model, "cpus_visible": os.cpu_count(), "cpus_affinity": avail,
-            "torch_threads": torch.get_num_threads()}
+            "cpu_share": cpu_share(), "torch_threads_cpu_legs": cpu_share(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline_r15(budget_s=10.0, dropout=0.5):
@@ -459,19 +792,22 @@ def cpu_baseline_r15(budget_s=10.0, dropout=0.5):
     opt = torch.optim.Adam(D.leaves(p), lr=1e-3, weight_decay=5e-4)
     g = torch.Generator().manual_seed(0)
     src, dst = torch.randint(0, n, (64,), generator=g), torch.randint(0, m, (64,), generator=g)
-    D.train_step(p, opt, adj, src, dst, dropout)  # warm-up
-    times = []
-    t_end = time.perf_counter() + budget_s
-    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 20):
-        t0 = time.perf_counter()
+    with _Threads():
+        D.train_step(p, opt, adj, src, dst, dropout)  # warm-up
         D.train_step(p, opt, adj, src, dst, dropout)
-        times.append(time.perf_counter() - t0)
+        times = []
+        t_end = time.perf_counter() + budget_s
+        while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 20):
+            t0 = time.perf_counter()
+            D.train_step(p, opt, adj, src, dst, dropout)
+            times.append(time.perf_counter() - t0)
+        cores = torch.get_num_threads()
     med = float(np.median(times))
-    return dict(value=med, unit="s/step", higher_is_better=False, cores=torch.get_num_threads(),
+    return dict(value=med, unit="s/step", higher_is_better=False, cores=cores,
                 kind="port", edges_per_sec=len(z["col"]) / med,
                 sample=f"ablation3 train step on the full 2015 graph ({n} x {m}), median of "
-                       f"{len(times)} steps: oracle/dense_step.py (the reference's dense torch "
-                       "formulation, CPU)")
+                       f"{len(times)} steps after 2 warm-up: oracle/dense_step.py (the "
+                       "reference's dense torch formulation, CPU)")
 
 
 def cpu_baseline_pairs(n, F, budget_s=4.0, hidden=128, n_pairs=1_000_000):
@@ -488,7 +824,7 @@ def cpu_baseline_pairs(n, F, budget_s=4.0, hidden=128, n_pairs=1_000_000):
     W = torch.randn(hidden, F, generator=g) * F ** -0.5
     b = torch.randn(hidden, generator=g)
     res = {}
-    with torch.no_grad():
+    with torch.no_grad(), _Threads():
         for mode in ("mlp", "inner"):
             D.score_pairs(h, src, dst, mode, W, b)
             reps, t0 = 0, time.perf_counter()
@@ -496,7 +832,8 @@ def cpu_baseline_pairs(n, F, budget_s=4.0, hidden=128, n_pairs=1_000_000):
                 D.score_pairs(h, src, dst, mode, W, b)
                 reps += 1
             res[f"pairs_per_sec_{mode}"] = n_pairs * reps / (time.perf_counter() - t0)
-    res.update(unit="pairs/s", cores=torch.get_num_threads(), kind="port",
+        cores = torch.get_num_threads()
+    res.update(unit="pairs/s", cores=cores, kind="port",
                sample=f"{n_pairs} pairs against a ({n}, {F}) fp32 table, hidden {hidden}: "
                       "oracle/dense_step.score_pairs (torch CPU)")
     return res
@@ -519,8 +856,9 @@ def launch_ranks(n, argv):
 
 def dry_run(world, rank):
     """CPU rehearsal of the multi-rank path (gloo): rank launch, the sharded table's
-    all-gather, the contiguous pair split and the max-over-ranks timing.  Prints one JSON
-    line on rank 0 (n_gpus = ranks that took part)."""
+    all-gather (serial and double-buffered), the contiguous pair split and the
+    max-over-ranks timing.  Prints one JSON line on rank 0 (n_gpus = ranks that took
+    part)."""
     import torch.distributed as tdist
 
     from msha_loader import load
@@ -531,13 +869,16 @@ def dry_run(world, rank):
     if world > 1:
         tdist.init_process_group("gloo")
     n, F, P = 1001, 8, 5003
-    tab = sharding.ShardedTable(n, F, world, rank, "cpu")
+    tab = sharding.ShardedTable(n, F, world, rank, "cpu", buffers=2)
     lo, hi = sharding.row_range(n, world, rank)
     full_ref = torch.arange(n * F, dtype=torch.float32).view(n, F)
     tab.set_local(full_ref[lo:hi])
     t0 = time.perf_counter()
     ok = bool(torch.equal(tab.gather(), full_ref))
+    src = torch.arange(P) % n
+    outs = sharding.PipelinedScorer(tab, lambda h, s_, d_: h[s_].sum(1)).run([(src, src)] * 3)
     plo, phi = sharding.pair_range(P, world, rank)
+    ok = ok and all(torch.equal(o[2], full_ref[src[plo:phi]].sum(1)) for o in outs)
     dt = time.perf_counter() - t0
     cnt = torch.tensor([phi - plo, int(ok), 1], dtype=torch.float64)
     tt = torch.tensor([dt])
@@ -547,9 +888,35 @@ def dry_run(world, rank):
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_reporting": int(cnt[2]),
                           "pairs_covered": int(cnt[0]), "pairs": P,
-                          "table_ok_ranks": int(cnt[1]), "max_rank_s": float(tt)}), flush=True)
+                          "table_ok_ranks": int(cnt[1]), "max_rank_s": float(tt),
+                          "exchange": tab.path()}), flush=True)
     if world > 1:
         tdist.destroy_process_group()
+
+
+def _world1_group(dev):
+    """An in-process world-1 RCCL group (FileStore rendezvous) so the link scorer's
+    all-gather runs the collective on a single GPU too.  Returns a cleanup callable, or
+    None when RCCL is unavailable."""
+    import tempfile
+
+    import torch.distributed as tdist
+
+    fd, path = tempfile.mkstemp(prefix="msha_bench_rccl_")
+    os.close(fd)
+    os.unlink(path)
+    try:
+        tdist.init_process_group("nccl", store=tdist.FileStore(path, 1), rank=0, world_size=1,
+                                 device_id=dev)
+    except Exception as ex:  # noqa: BLE001 - report, fall back to the copy path
+        print(f"world-1 RCCL group failed: {ex}", file=sys.stderr)
+        return None
+
+    def done():
+        tdist.destroy_process_group()
+        if os.path.exists(path):
+            os.unlink(path)
+    return done
 
 
 def main():
@@ -563,6 +930,8 @@ def main():
     ap.add_argument("--no-link-score", action="store_true")
     ap.add_argument("--no-r15", action="store_true")
     ap.add_argument("--no-bf16", action="store_true")
+    ap.add_argument("--no-syn2m", action="store_true")
+    ap.add_argument("--no-bip1m", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="report the eager launches (no HIP-graph replay of the timed steps)")
     ap.add_argument("--no-dropout-leg", action="store_true")
@@ -591,192 +960,107 @@ def main():
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl")
     dev = torch.device("cuda", local)
+    clock = Clock(dev, dist)
 
-    if args.workload == "r15":
+    wl = args.workload
+    if wl == "r15":
         rowptr, col, n, m = r15_graph()
         fin, H, F = 128, 2, 64
+    elif wl == "bip1m":
+        rowptr, col, n, m = bip_graph()
+        fin, H, F = 128, 2, 64
     else:
-        w = WORKLOADS[args.workload]
+        w = WORKLOADS[wl]
         n, fin, H, F = w["n"], w["fin"], w["heads"], w["feat"]
         m = n
         rowptr, col = synth_graph(n, w["e"], seed=0)
     e = len(col)
-    layer = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank)
-
-    def barrier():
-        if dist:
-            tdist.barrier()
-        torch.cuda.synchronize(dev)
-
-    def max_over_ranks(x):
-        if dist:
-            tt = torch.tensor([x], device=dev)
-            tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-            x = float(tt.item())
-        return x
-
-    def timed_graph(lay, steps):
-        """Max-over-ranks seconds of ONE replay of a HIP graph holding exactly `steps`
-        steps (captured after the eager pass, which warmed every cache; one untimed
-        replay first).  Same kernels, same work as the eager steps without the host
-        launch gaps (~2-10 us per launch, Python autograd).  None if capture fails."""
-        ok, g = 1, None
-        try:
-            g = torch.cuda.CUDAGraph()
-            # thread_local: a communicator's watchdog thread (N > 1) may query its events
-            # while this thread captures
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                for _ in range(steps):
-                    lay.step()
-            g.replay()
-        except RuntimeError as ex:  # report the eager number instead
-            print(f"graph capture failed: {ex}", file=sys.stderr)
-            ok = 0
-        if dist:  # every rank falls back together (no rank left waiting in a barrier)
-            t_ok = torch.tensor([ok], device=dev)
-            tdist.all_reduce(t_ok, op=tdist.ReduceOp.MIN)
-            ok = int(t_ok.item())
-        if not ok:
-            return None
-        barrier()
-        t0 = time.perf_counter()
-        g.replay()
-        barrier()
-        dt_ = max_over_ranks(time.perf_counter() - t0)
-        del g
-        return dt_
-
-    def timed(lay, steps, warmup):
-        """(max-over-ranks seconds for `steps` steps, mean fwd-kernel ms, launches)"""
-        for _ in range(warmup):
-            lay.step()
-        barrier()
-        lay.MF.KERNEL_EVENTS = {}
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            lay.step()
-        barrier()
-        dt_ = time.perf_counter() - t0
-        evs = lay.MF.KERNEL_EVENTS
-        lay.MF.KERNEL_EVENTS = None
-        ms = {name: float(np.mean([a.elapsed_time(b) for a, b in lst]))
-              for name, lst in evs.items() if lst}
-        events = evs.get("edge_attention_fwd", [])
-        k = ms.get("edge_attention_fwd", float("nan"))
-        dt_ = max_over_ranks(dt_)
-        lay.kernel_ms = ms
-        return dt_, k, len(events)
-
-    def edge_kernels(lay, s):
-        """Rooflines of the edge kernels of the step (HIP events, same run): the forward
-        and either the fused backward or bwd_rows + csc_aggregate."""
-        nch = lay.graph._plan["n_chunks"]
-        rt = lay.rowterms
-        out = []
-        for name, nbytes in (("msha_edge_attention_fwd", fwd_bytes(n, m, e, H, F, s, rt)),
-                             ("msha_edge_attention_bwd_rows", bwd_rows_bytes(n, m, e, H, F, s)),
-                             ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s)),
-                             ("msha_edge_attention_bwd_fused",
-                              bwd_fused_bytes(n, m, e, H, F, nch, s, rt))):
-            key = name[len("msha_"):]
-            if key not in lay.kernel_ms:
-                continue
-            us = lay.kernel_ms[key] * 1e3
-            gbs = nbytes / (us * 1e-6) / 1e9
-            out.append({"kernel": name, "algorithmic_bytes": nbytes, "avg_us": us,
-                        "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
-                        **({"rowterms": True} if rt and "rows" not in name
-                           and "csc" not in name else {})})
-        return out
-
-    dt_eager, k_ms, n_launch = timed(layer, args.steps, args.warmup)
-    dt_graph = None if args.eager else timed_graph(layer, args.steps)
-    dt = dt_graph if dt_graph is not None else dt_eager
-    timing = ("value: one replay of a HIP graph holding exactly `steps` steps (captured after "
-              "the eager pass); roofline: HIP events around every launch over the eager timed "
-              "region of the same steps" if dt_graph is not None else
-              "value and roofline: eager launches, HIP events around every launch")
+    K, Wu = args.steps, args.warmup
+    head, graph = layer_leg(clock, dev, f"gat_layer_{wl}", rowptr, col, n, m, fin, H, F, K, Wu,
+                            world, args.eager, workload=wl)
     drop_leg = None
     if not args.no_dropout_leg:
         # the reference's training forward drops attention at p = 0.5 (Ablation.py:271):
         # the same step with the Philox mask drawn in the forward and regenerated in the
         # backward (no mask tensor)
-        layd = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank, graph=layer.graph,
-                     dropout=0.5)
-        dtde, kd, nd = timed(layd, args.steps, args.warmup)
-        dtdg = None if args.eager else timed_graph(layd, args.steps)
-        dtd = dtdg if dtdg is not None else dtde
-        ad = fwd_bytes(n, m, e, H, F, 4, layd.rowterms) / (kd * 1e-3) / 1e9
-        drop_leg = {"workload": f"gat_layer_{args.workload}, attention dropout p = 0.5 "
-                                "(training forward + backward)",
-                    "value": world * e * args.steps / dtd, "unit": "edges/s",
-                    "ms_per_step": dtd / args.steps * 1e3,
-                    "ms_per_step_eager": dtde / args.steps * 1e3, "dtype": "f32",
-                    "roofline": {"kernel": "msha_edge_attention_fwd (p = 0.5)", "bound": "hbm",
-                                 "achieved": ad, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": ad / HBM_PEAK_GBS, "avg_launch_us": kd * 1e3,
-                                 "launches_timed": nd},
-                    "edge_kernels": edge_kernels(layd, 4)}
-        del layd
+        drop_leg, _ = layer_leg(clock, dev, f"gat_layer_{wl}, attention dropout p = 0.5 "
+                                "(training forward + backward)", rowptr, col, n, m, fin, H, F,
+                                K, Wu, world, args.eager, graph=graph, dropout=0.5)
     bf16_leg = None
     if not args.no_bf16:
         # config C3: the same layer with bf16 tables / projection (bf16 MFMA)
-        lay16 = Layer(dev, rowptr, col, n, m, fin, H, F, seed=1 + rank, dtype=torch.bfloat16,
-                      graph=layer.graph)
-        dt16e, k16, n16 = timed(lay16, args.steps, args.warmup)
-        dt16g = None if args.eager else timed_graph(lay16, args.steps)
-        dt16 = dt16g if dt16g is not None else dt16e
-        fb16 = fwd_bytes(n, m, e, H, F, 2, lay16.rowterms)
-        a16 = fb16 / (k16 * 1e-3) / 1e9
-        tr16, src16 = pmc_traffic(H, F, True, args.workload)
-        bf16_leg = {"workload": f"gat_layer_{args.workload} (config C3: bf16 tables, bf16 MFMA "
-                                "projection, fp32 scores/softmax)",
-                    "value": world * e * args.steps / dt16, "unit": "edges/s",
-                    "ms_per_step": dt16 / args.steps * 1e3,
-                    "ms_per_step_eager": dt16e / args.steps * 1e3, "dtype": "bf16",
-                    "roofline": {"kernel": "msha_edge_attention_fwd<bf16>", "bound": "hbm",
-                                 "achieved": a16, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": a16 / HBM_PEAK_GBS, "traffic": tr16,
-                                 "traffic_source": src16, "algorithmic_bytes_per_launch": fb16,
-                                 "avg_launch_us": k16 * 1e3, "launches_timed": n16}}
-        bf16_leg["edge_kernels"] = edge_kernels(lay16, 2)
-        del lay16
+        bf16_leg, _ = layer_leg(clock, dev, f"gat_layer_{wl} (config C3: bf16 tables, bf16 "
+                                "MFMA projection, fp32 scores/softmax)", rowptr, col, n, m, fin,
+                                H, F, K, Wu, world, args.eager, dtype=torch.bfloat16,
+                                graph=graph, workload=wl)
     link = None
-    if not args.no_link_score and args.workload != "r15":
-        link = link_score_bench(dev, rowptr, col, n, H * F, world, rank, dist)
+    if not args.no_link_score and wl not in ("r15", "bip1m"):
+        done = None if dist else _world1_group(dev)
+        group_ok = dist or done is not None
+        link = link_score_bench(dev, rowptr, col, n, H * F, world, rank, group_ok)
         if not args.no_bf16:  # C5 names a bf16 table
-            link["bf16"] = link_score_bench(dev, rowptr, col, n, H * F, world, rank, dist,
+            link["bf16"] = link_score_bench(dev, rowptr, col, n, H * F, world, rank, group_ok,
                                             dtype=torch.bfloat16)
+        if done is not None:
+            done()
+    del graph
+    torch.cuda.empty_cache()
+    syn2m = bip1m = None
+    if wl == "syn100k" and not args.no_syn2m:
+        # the cache-busting variant: a 1 GB fp32 table outside the 256 MB Infinity Cache
+        w2 = WORKLOADS["syn2m"]
+        rp2, c2 = synth_graph(w2["n"], w2["e"], seed=0)
+        syn2m = {}
+        g2 = None
+        for dt_, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            if dt_ == torch.bfloat16 and args.no_bf16:
+                continue
+            syn2m[tag], g2 = layer_leg(clock, dev, "gat_layer_syn2m", rp2, c2, w2["n"], w2["n"],
+                                       w2["fin"], w2["heads"], w2["feat"], K, Wu, world,
+                                       args.eager, dtype=dt_, graph=g2, workload="syn2m")
+        del g2, rp2, c2
+        torch.cuda.empty_cache()
+    if wl == "syn100k" and not args.no_bip1m:
+        # the repo's adjacency shape at scale: 1M sources x 32 recipients, OursLayer3 core
+        rpb, cb, nb, mb = bip_graph()
+        bip1m = {}
+        gb = None
+        for dt_, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            if dt_ == torch.bfloat16 and args.no_bf16:
+                continue
+            bip1m[tag], gb = layer_leg(clock, dev, "ourslayer3_bip1m (u and v aggregates)", rpb,
+                                       cb, nb, mb, 128, 2, 64, K, Wu, world, args.eager,
+                                       dtype=dt_, graph=gb, v_branch=True, workload="bip1m")
+        del gb
+        torch.cuda.empty_cache()
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
         return
-    ms_per_step = dt / args.steps * 1e3
-    value = world * e * args.steps / dt
-    fb = fwd_bytes(n, m, e, H, F, 4, layer.rowterms)
-    achieved = fb / (k_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(H, F, False, args.workload)
+    ms_per_step = head["ms_per_step"]
     out = {
-        "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "ms_per_step_eager": dt_eager / args.steps * 1e3, "timing": timing,
+        "metric": METRIC, "value": head["value"], "unit": "edges/s", "n_gpus": world,
+        "steps": K, "warmup": Wu, "ms_per_step": ms_per_step,
+        "ms_per_step_eager": head["ms_per_step_eager"],
+        "timing": ("value: one replay of a HIP graph holding exactly `steps` steps (captured "
+                   "after the eager pass); roofline: HIP events around every launch over the "
+                   "eager timed region of the same steps" if not args.eager else
+                   "value and roofline: eager launches, HIP events around every launch"),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"gat_layer_{args.workload}", "nodes": n, "cols": m, "edges": e,
+        "config": {"workload": f"gat_layer_{wl}", "nodes": n, "cols": m, "edges": e,
                    "in_features": fin, "heads": H, "feat": F, "parallelism": f"replicas{world}"},
-        "roofline": {"kernel": "msha_edge_attention_fwd", "bound": "hbm",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "bytes per launch (rocprofv3 PMC, same command)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": fb, "avg_launch_us": k_ms * 1e3,
-                     "launches_timed": n_launch},
+        "roofline": head["roofline"],
+        "edge_kernels": head["edge_kernels"],
     }
-    out["edge_kernels"] = edge_kernels(layer, 4)
     if drop_leg is not None:
         out["dropout_p05"] = drop_leg
     if bf16_leg is not None:
         out["bf16"] = bf16_leg
+    if syn2m:
+        out["syn2m"] = syn2m
+    if bip1m:
+        out["bip1m"] = bip1m
     if link is not None:
         out["link_score"] = link
     if world == 1 and not args.no_r15:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 8
+#define MSHA_ABI_VERSION 9
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -254,6 +254,32 @@ MSHA_API int msha_edge_attention_bwd_fused(const msha_graph* g, int32_t heads, i
 MSHA_API int msha_edge_attention_bwd_fused_ex(
     const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype, const float* el,
     const float* er, const void* hc, const float* lse, const void* u, const void* u_lo,
+    const void* dU, float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
+    const float* uc, const float* qc, float* d_el, float* d_er, void* d_hc, float* de, void* ws,
+    size_t ws_bytes, msha_stream_t stream);
+
+/* Scores from the gathered row (ABI 9).  Every caller of the u = att @ hc path scores
+ * the gathered table itself: er[j,h] = hc[j,h,:] . a_r[h,:] (Ablation.py:266-267 --
+ * a[:F] against h1_j, the rows u aggregates).  Given a_r ((heads, feat) fp32, 16-byte
+ * aligned) instead of er, the forward computes er_j from the row its gather lanes hold
+ * (no per-edge er gather: a 4*heads-byte piece that costs a cache line per edge once
+ * the er table leaves L2) and the fused backward's column pass recomputes it from hc_j
+ * in the same order, so both passes see the same scores bit for bit.  The outputs and
+ * their meaning are those of msha_edge_attention_fwd_ex (without attd) and
+ * msha_edge_attention_bwd_fused_ex; d_er is still the gradient w.r.t. er (the caller
+ * routes it to whatever produced er = hc . a_r).  Supported where
+ * msha_edge_attention_row_scores_supported says so (one 16-byte piece per lane:
+ * heads*feat*sizeof <= 1024 B; tables under 2 GiB); MSHA_ERR_UNSUPPORTED otherwise. */
+MSHA_API int msha_edge_attention_row_scores_supported(const msha_graph* g, int32_t heads,
+                                                      int32_t feat, int32_t dtype);
+MSHA_API int msha_edge_attention_fwd_rs(const msha_graph* g, int32_t heads, int32_t feat,
+                                        int32_t dtype, const float* el, const float* ar,
+                                        const void* hc, float neg_slope, float drop_p,
+                                        uint64_t seed, uint64_t offset, void* u, void* u_lo,
+                                        float* lse, float* uc, float* qc, msha_stream_t stream);
+MSHA_API int msha_edge_attention_bwd_fused_rs(
+    const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype, const float* el,
+    const float* ar, const void* hc, const float* lse, const void* u, const void* u_lo,
     const void* dU, float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
     const float* uc, const float* qc, float* d_el, float* d_er, void* d_hc, float* de, void* ws,
     size_t ws_bytes, msha_stream_t stream);

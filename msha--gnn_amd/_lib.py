@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 8  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 9  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -99,6 +99,11 @@ SIGNATURES = {
     "msha_edge_attention_fwd_ex": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P,
                                              P, P, P, P, P, P]),
     "msha_edge_attention_bwd_fused_ex": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,
+                                                   F32, U64, U64, P, P, P, P, P, P, P, SZ, P]),
+    "msha_edge_attention_row_scores_supported": (C.c_int, [GP, I32, I32, I32]),
+    "msha_edge_attention_fwd_rs": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P,
+                                             P, P, P, P, P]),
+    "msha_edge_attention_bwd_fused_rs": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,
                                                    F32, U64, U64, P, P, P, P, P, P, P, SZ, P]),
     "msha_edge_attention_bwd_rows": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, P, P,
                                                F32, F32, U64, U64, P, P, P, I32, P, P]),

@@ -448,6 +448,224 @@ edge_attn_fwd_bat_kernel(
   }
 }
 
+// ------------------------------------------------ forward, scores from the gathered row ---
+// In every caller of this path the gathered table scores its own rows: er_j = hc_j . a_r
+// per head (Ablation.py:266-267: a[:F] against h1_j, the row u aggregates).  Given a_r,
+// this forward computes er_j from the row its gather lanes already hold -- V fmas per lane
+// and the xor tree over the head's QH lanes (DPP) -- instead of gathering er_j per edge
+// (a 4H-byte piece of an (M, H) table that costs a whole cache line per edge once the
+// table outgrows L2: syn2m's 64 MB er table, 40M edges).
+// The softmax runs in the gather layout (lane = edge slot g_e x 16-byte piece q; every
+// (edge, head) score replicated over the head's QH lanes): chunk max / sum reduce the
+// NGI gather slots in registers and the EPI edge slots of a gather instruction by xor
+// over g_e, so no weight is shuffled to the gather lanes.  Dropout keep bits are drawn
+// in the score layout (one Philox call per (edge, head), as everywhere) and reach the
+// gather lanes by ballot.  Row terms (RT) as edge_attn_fwd_bat_kernel.
+// The fused backward's column pass recomputes er_j from hc_j in the same order (same
+// bits), so the scores of both passes agree exactly.
+template <int H, int F, typename T, int EPL, bool RT = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
+edge_attn_fwd_rs_kernel(
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
+    const float* __restrict__ el, const float* __restrict__ ar, const T* __restrict__ hc,
+    float slope, Dropout dp, T* __restrict__ u, T* __restrict__ u_lo, float* __restrict__ lse,
+    float* __restrict__ uc, float* __restrict__ qc) {
+  using G = Geo<H, F, T>;
+  static_assert(G::QPL == 1, "row-score forward: one 16-byte piece per lane");
+  constexpr int CEL = EPL * G::CE;    // edges per chunk
+  constexpr int NGI = CEL / G::EPI;   // gather instructions per chunk
+  const int lane = lane_id();
+  const int e_s = lane / H, h_s = lane % H;        // score layout (columns, dropout)
+  const int g_e = lane / G::NQ, q = lane % G::NQ;  // gather layout
+  const int hq = q / G::QH;                        // head of this lane's piece
+  const rsrc_t r_col = make_rsrc(col, (uint32_t)n_edges * 4u);
+  const rsrc_t r_hc = make_rsrc(hc, (uint32_t)n_cols * (uint32_t)(G::D * sizeof(T)));
+  const uint32_t q_off = 16u * q;
+  const int wave0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  const int nwaves = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
+  // this lane's piece of a_r ((H, F) fp32: piece q covers elements q*V .. q*V + V - 1)
+  Pk<T> arq;
+#pragma unroll
+  for (int v = 0; v < G::V; v += 4) {
+    const float4 a4 = *reinterpret_cast<const float4*>(ar + G::V * q + v);
+    arq.v[v] = a4.x; arq.v[v + 1] = a4.y; arq.v[v + 2] = a4.z; arq.v[v + 3] = a4.w;
+  }
+
+  int row = wave0;
+  if (row >= n_rows) return;
+  int32_t start = __builtin_amdgcn_readfirstlane(rowptr[row]);
+  int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
+  bool virt = rowflag != nullptr && rowflag[row] != 0;
+  float elq = el[(int64_t)row * H + hq];
+  int32_t j0[EPL], j1[EPL];
+#pragma unroll
+  for (int t = 0; t < EPL; ++t) {
+    const int32_t e0 = start + t * G::CE + e_s, e1 = e0 + CEL;
+    j0[t] = buf_i32(r_col, e0 < end ? (uint32_t)e0 * 4u : kOOB);
+    j1[t] = buf_i32(r_col, e1 < end ? (uint32_t)e1 * 4u : kOOB);
+  }
+  while (true) {
+    float m = -INFINITY, l = 0.f, lc = 0.f;
+    Pk<T> acc = pk_zero<T>(), accc = pk_zero<T>();
+    for (int32_t cs = start; cs < end; cs += CEL) {
+      const int nvalid = min(CEL, (int)(end - cs));
+      // (1) this chunk's gathers, all in flight together; columns two chunks ahead
+      u32x4_t raw[NGI];
+#pragma unroll
+      for (int gi = 0; gi < NGI; ++gi) {
+        const int g = gi * G::EPI;
+        const int t = g / G::CE;
+        const int ei = g % G::CE + g_e;
+        const int32_t jq = __shfl(j0[t], ei * H);
+        raw[gi] = buf_b128(r_hc, g + g_e < nvalid
+                                     ? (uint32_t)jq * (uint32_t)(G::D * sizeof(T)) + q_off
+                                     : kOOB);
+      }
+      int32_t j2[EPL];
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const int32_t e2 = cs + 2 * CEL + t * G::CE + e_s;
+        j2[t] = buf_i32(r_col, e2 < end ? (uint32_t)e2 * 4u : kOOB);
+      }
+      // (2) dropout keep bits of the chunk (score layout, one draw per (edge, head)),
+      // while the gathers fly
+      uint64_t keep[EPL];
+      if (dp.active) {
+#pragma unroll
+        for (int t = 0; t < EPL; ++t)
+          keep[t] = __ballot(dropout_factor(dp, (uint64_t)(cs + t * G::CE + e_s) * H + h_s) != 0.f);
+      }
+      // (3) scores from the gathered rows (gather layout)
+      float sc[NGI], pre[NGI];
+      float smax = -INFINITY;
+#pragma unroll
+      for (int gi = 0; gi < NGI; ++gi) {
+        const Pk<T> xr = pk_from_raw(raw[gi], (T*)nullptr);
+        const float erq = group_sum<G::QH>(pk_dot(xr, arq));
+        pre[gi] = elq + erq;
+        const bool valid = gi * G::EPI + g_e < nvalid;
+        sc[gi] = valid ? (virt ? 0.f : lrelu(pre[gi], slope)) : -INFINITY;
+        smax = fmaxf(smax, sc[gi]);
+      }
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) smax = fmaxf(smax, xor_shfl(smax, o));
+      const float mn = fmaxf(m, smax);
+      const float alpha = __expf(m - mn);
+      float w[NGI], psum = 0.f, pcsum = 0.f;
+#pragma unroll
+      for (int gi = 0; gi < NGI; ++gi) {
+        const float pe = __expf(sc[gi] - mn);  // masked slots: exp(-inf) = 0
+        psum += pe;
+        if (RT) pcsum = fmaf(pe, pre[gi] > 0.f ? 1.f : slope, pcsum);
+        w[gi] = pe;
+        if (dp.active) {
+          const int ec = gi * G::EPI;  // + g_e: edge slot of the chunk
+          const int bit = (ec % G::CE + g_e) * H + hq;
+          w[gi] = (keep[ec / G::CE] >> bit) & 1ull ? pe * dp.scale : 0.f;
+        }
+      }
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) psum += xor_shfl(psum, o);
+      l = fmaf(l, alpha, psum);
+      if (RT) {
+#pragma unroll
+        for (int o = G::NQ; o < 64; o <<= 1) pcsum += xor_shfl(pcsum, o);
+        lc = fmaf(lc, alpha, pcsum);
+      }
+      m = mn;
+      acc = pk_scale(acc, alpha);
+      if (RT) accc = pk_scale(accc, alpha);
+      // (4) accumulate in gather order (masked slots carry w = 0 and a zero row)
+#pragma unroll
+      for (int gi = 0; gi < NGI; ++gi) {
+        const Pk<T> xr = pk_from_raw(raw[gi], (T*)nullptr);
+        acc = pk_fma(w[gi], xr, acc);
+        if (RT) accc = pk_fma(w[gi] * (pre[gi] > 0.f ? 1.f : slope), xr, accc);
+      }
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        j0[t] = j1[t];
+        j1[t] = j2[t];
+      }
+    }
+    // the next row's bounds, flag, el and first columns before this row's epilogue
+    const int nrow_raw = row + nwaves;
+    const bool has_next = nrow_raw < n_rows;
+    const int nrow = has_next ? nrow_raw : row;
+    const int32_t nstart = __builtin_amdgcn_readfirstlane(rowptr[nrow]);
+    const int32_t nend = __builtin_amdgcn_readfirstlane(rowptr[nrow + 1]);
+    const bool nvirt = rowflag != nullptr && rowflag[nrow] != 0;
+    const float nelq = el[(int64_t)nrow * H + hq];
+    int32_t nj0[EPL], nj1[EPL];
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      const int32_t e0 = nstart + t * G::CE + e_s, e1 = e0 + CEL;
+      nj0[t] = buf_i32(r_col, e0 < nend ? (uint32_t)e0 * 4u : kOOB);
+      nj1[t] = buf_i32(r_col, e1 < nend ? (uint32_t)e1 * 4u : kOOB);
+    }
+    if (G::EPI > 1) {
+#pragma unroll
+      for (int o = G::NQ; o < 64; o <<= 1) acc = pk_xor_add(acc, o);
+      if (RT) {
+#pragma unroll
+        for (int o = G::NQ; o < 64; o <<= 1) accc = pk_xor_add(accc, o);
+      }
+    }
+    const float inv = l > 0.f ? 1.f / l : 0.f;  // l, m: this lane's head (replicated)
+    if (g_e == 0) {
+      const Pk<T> uk = pk_scale(acc, inv);
+      pk_store(u + (int64_t)row * G::D + G::V * q, uk);
+      if (sizeof(T) == 2 && u_lo != nullptr)
+        pk_store(u_lo + (int64_t)row * G::D + G::V * q, pk_residual(uk));
+      if (RT) {
+        const Pk<T> ck = pk_scale(accc, inv);
+        float* dst = uc + (int64_t)row * G::D + G::V * q;
+#pragma unroll
+        for (int v = 0; v < G::V; v += 4)
+          *reinterpret_cast<float4*>(dst + v) = make_float4(ck.v[v], ck.v[v + 1], ck.v[v + 2], ck.v[v + 3]);
+      }
+      if (q % G::QH == 0) {
+        lse[(int64_t)row * H + hq] = l > 0.f ? m + __logf(l) : -INFINITY;
+        if (RT) qc[(int64_t)row * H + hq] = l > 0.f ? lc / l : 0.f;
+      }
+    }
+    if (!has_next) break;
+    row = nrow;
+    start = nstart;
+    end = nend;
+    virt = nvirt;
+    elq = nelq;
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      j0[t] = nj0[t];
+      j1[t] = nj1[t];
+    }
+  }
+}
+
+// er_j = hc_j . a_r of one head from its QH 16-byte pieces, in the forward's order
+// (pk_dot per piece, then the xor tree of group_sum<QH>)
+template <int NV, typename T>
+__device__ __forceinline__ float head_score(const Pk<T> (&hv)[NV], const float* __restrict__ a) {
+  float d[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    Pk<T> ak;
+#pragma unroll
+    for (int v = 0; v < Pk<T>::V; v += 4) {
+      const float4 a4 = *reinterpret_cast<const float4*>(a + Pk<T>::V * k + v);
+      ak.v[v] = a4.x; ak.v[v + 1] = a4.y; ak.v[v + 2] = a4.z; ak.v[v + 3] = a4.w;
+    }
+    d[k] = pk_dot(hv[k], ak);
+  }
+#pragma unroll
+  for (int o = 1; o < NV; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < NV; k += 2 * o) d[k] = d[k] + d[k + o];
+  return d[0];
+}
+
 // --------------------------------------------------------------- backward rows ---
 // The gather-group loops unroll fully for fp32 and by BWR_UNR_BF16 for bf16 tables: the
 // kernel is latency-bound (R15 rows hold ~2.3 edges, so the first group is usually the
@@ -866,9 +1084,10 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
     const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid, int64_t n_rows,
     const uint8_t* __restrict__ rowflag, const float* __restrict__ rec,
-    const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
-    float slope, Dropout dp, bool slot_de, float* __restrict__ de, T* __restrict__ d_hc,
-    float* __restrict__ d_er, float* __restrict__ part, float* __restrict__ part_x) {
+    const float* __restrict__ er, const float* __restrict__ ar, const T* __restrict__ hc,
+    const T* __restrict__ dU, float slope, Dropout dp, bool slot_de, float* __restrict__ de,
+    T* __restrict__ d_hc, float* __restrict__ d_er, float* __restrict__ part,
+    float* __restrict__ part_x) {
   using G = Geo<H, F, T>;
   const int lane = lane_id();
   const int e_s = lane / H, h_s = lane % H;
@@ -892,12 +1111,21 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
     const int32_t ns0 = has_next ? chunk_start[nc] : 0;
     const int32_t ns1 = has_next ? chunk_end[nc] : 0;
     const bool whole = s0 == colptr[jc] && s1 == colptr[jc + 1];
-    const float erh = er[(int64_t)jc * H + h_s];
     Pk<T> hcq[G::QPL], acc[G::QPL];
 #pragma unroll
     for (int k = 0; k < G::QPL; ++k) {
       hcq[k] = pk_load(hc + (int64_t)jc * G::D + G::V * quad_of<G>(lane, k));
       acc[k] = pk_zero<T>();
+    }
+    float erh;
+    if (G::QPL == 1 && ar != nullptr) {  // er_j from hc_j in the row-score forward's order
+      const int q = lane % G::NQ;
+      Pk<T> aq;
+#pragma unroll
+      for (int v = 0; v < G::V; ++v) aq.v[v] = ar[G::V * q + v];
+      erh = __shfl(group_sum<G::QH>(pk_dot(hcq[0], aq)), h_s * G::QH);
+    } else {
+      erh = er[(int64_t)jc * H + h_s];
     }
     float xacc = 0.f;
     for (int32_t cs = s0; cs < s1; cs += G::CE) {
@@ -1052,9 +1280,10 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
     const int32_t* __restrict__ csc_row, const int32_t* __restrict__ csc_eid, int64_t n_edges,
     const uint8_t* __restrict__ rowflag, int64_t n_rows, const float* __restrict__ rec,
-    const float* __restrict__ er, const T* __restrict__ hc, const T* __restrict__ dU,
-    float slope, Dropout dp, bool slot_de, float* __restrict__ de, T* __restrict__ d_hc,
-    float* __restrict__ d_er, float* __restrict__ part, float* __restrict__ part_x) {
+    const float* __restrict__ er, const float* __restrict__ ar, const T* __restrict__ hc,
+    const T* __restrict__ dU, float slope, Dropout dp, bool slot_de, float* __restrict__ de,
+    T* __restrict__ d_hc, float* __restrict__ d_er, float* __restrict__ part,
+    float* __restrict__ part_x) {
   using G = Geo<H, F, T>;
   constexpr int NV = G::QH;  // 16-B pieces per head
   constexpr int NG = COLS_NG;
@@ -1086,13 +1315,15 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
     const int32_t ns0 = has_next ? chunk_start[nc] : 0;
     const int32_t ns1 = has_next ? chunk_end[nc] : 0;
     const bool whole = s0 == colptr[jc] && s1 == colptr[jc + 1];
-    const float erh = er[(int64_t)jc * H + h_s];
     Pk<T> hcv[NV], acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       hcv[k] = pk_load(hc + (int64_t)jc * G::D + h_s * F + G::V * k);
       acc[k] = pk_zero<T>();
     }
+    // er_j: from hc_j in the row-score forward's order when a_r is given
+    const float erh = ar != nullptr ? head_score<NV>(hcv, ar + h_s * F)
+                                    : er[(int64_t)jc * H + h_s];
     float xacc = 0.f;
     // one trip = COLS_NG slot groups: every group's loads leave before the first
     // group's compute and de store (the compiler may not hoist a buffer load above a
@@ -1526,7 +1757,7 @@ extern "C" size_t msha_edge_attention_bwd_fused_workspace_size(const msha_graph*
 
 template <typename T>
 static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const float* el,
-                             const float* er, const void* hc, const float* lse, const void* u,
+                             const float* er, const float* ar, const void* hc, const float* lse, const void* u,
                              const void* u_lo, const void* dU, float neg_slope, const Dropout& dp, float* d_el,
                              float* d_er, void* d_hc, float* de, float* rec, float* part,
                              float* part_x, const float* uc, const float* qc, hipStream_t s) {
@@ -1558,7 +1789,7 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
         hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
                            g->colptr, g->csc_row, g->csc_eid, g->n_edges, g->rowflag,          \
-                           g->n_rows, rec, er, (const T*)hc, (const T*)dU, neg_slope, dp,      \
+                           g->n_rows, rec, er, ar, (const T*)hc, (const T*)dU, neg_slope, dp,  \
                            slot_de, de,                                                        \
                            (T*)d_hc, d_er, part, part_x);                                      \
       else                                                                                     \
@@ -1567,7 +1798,7 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
         hipLaunchKernelGGL(kern, wave_grid(g->n_chunks), dim3(256), 0,                         \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
                            g->colptr, g->csc_row, g->csc_eid, g->n_rows, g->rowflag, rec, er,  \
-                           (const T*)hc, (const T*)dU, neg_slope, dp, slot_de,                 \
+                           ar, (const T*)hc, (const T*)dU, neg_slope, dp, slot_de,             \
                            de, (T*)d_hc, d_er,                                                 \
                            part, part_x);                                                      \
       }                                                                                        \
@@ -1625,10 +1856,101 @@ extern "C" int msha_edge_attention_bwd_fused_ex(
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
   if (dtype == MSHA_DTYPE_BF16)
-    launch_bwd_fused<bf16_t>(g, heads, feat, el, er, hc, lse, u, u_lo, dU, neg_slope, dp, d_el, d_er,
-                             d_hc, de, rec, part, part_x, uc, qc, s);
+    launch_bwd_fused<bf16_t>(g, heads, feat, el, er, nullptr, hc, lse, u, u_lo, dU, neg_slope, dp,
+                             d_el, d_er, d_hc, de, rec, part, part_x, uc, qc, s);
   else
-    launch_bwd_fused<float>(g, heads, feat, el, er, hc, lse, u, nullptr, dU, neg_slope, dp, d_el, d_er,
-                            d_hc, de, rec, part, part_x, uc, qc, s);
+    launch_bwd_fused<float>(g, heads, feat, el, er, nullptr, hc, lse, u, nullptr, dU, neg_slope, dp,
+                            d_el, d_er, d_hc, de, rec, part, part_x, uc, qc, s);
   return check_launch("edge_attention_bwd_fused");
+}
+
+// ---------------------------------------------------- scores from the gathered row ---
+extern "C" int msha_edge_attention_row_scores_supported(const msha_graph* g, int32_t heads,
+                                                        int32_t feat, int32_t dtype) {
+  if (g == nullptr || !shape_supported(heads, feat) || !dtype_ok(dtype, feat)) return 0;
+  if (env_int("MSHA_ROW_SCORES", 1) == 0) return 0;  // A/B: the er-gather forward
+  return fwd_bat_ok(g, heads, feat, dtype) ? 1 : 0;
+}
+
+extern "C" int msha_edge_attention_fwd_rs(const msha_graph* g, int32_t heads, int32_t feat,
+                                          int32_t dtype, const float* el, const float* ar,
+                                          const void* hc, float neg_slope, float drop_p,
+                                          uint64_t seed, uint64_t offset, void* u, void* u_lo,
+                                          float* lse, float* uc, float* qc,
+                                          msha_stream_t stream) {
+  if (int rc = check_graph(g, false)) return rc;
+  MSHA_ARG_CHECK(el && ar && hc && u && lse, "edge_attention_fwd_rs: null pointer");
+  MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_fwd_rs: p must be in [0,1]");
+  MSHA_ARG_CHECK((uc == nullptr) == (qc == nullptr), "edge_attention_fwd_rs: uc and qc go together");
+  MSHA_ARG_CHECK(((uintptr_t)ar & 15) == 0, "edge_attention_fwd_rs: a_r must be 16-byte aligned");
+  if (!msha_edge_attention_row_scores_supported(g, heads, feat, dtype))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd_rs: unsupported (heads, feat, dtype, sizes)");
+  hipStream_t s = (hipStream_t)stream;
+  const Dropout dp = make_dropout(drop_p, seed, offset, s);
+  int64_t cap = env_int("MSHA_FWD_WAVES", -1);
+  if (cap < 0)
+    cap = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows ? g->n_rows / FWD_SHORT_RPW : 0;
+  const dim3 grid = wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
+#define XR(h, f)                                                                               \
+  if (heads == h && feat == f) {                                                               \
+    if (dtype == MSHA_DTYPE_BF16) {                                                            \
+      if constexpr (f % 8 == 0 && h * f * 2 <= 1024) {                                         \
+        auto kern = uc != nullptr                                                              \
+            ? edge_attn_fwd_rs_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>(), true>             \
+            : edge_attn_fwd_rs_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>(), false>;           \
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,         \
+                           (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,    \
+                           ar, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u, (bf16_t*)u_lo,    \
+                           lse, uc, qc);                                                       \
+      }                                                                                        \
+    } else {                                                                                   \
+      if constexpr (h * f * 4 <= 1024) {                                                       \
+        auto kern = uc != nullptr                                                              \
+            ? edge_attn_fwd_rs_kernel<h, f, float, fwd_epl<h, f, float>(), true>               \
+            : edge_attn_fwd_rs_kernel<h, f, float, fwd_epl<h, f, float>(), false>;             \
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,         \
+                           (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,    \
+                           ar, (const float*)hc, neg_slope, dp, (float*)u, (float*)nullptr,    \
+                           lse, uc, qc);                                                       \
+      }                                                                                        \
+    }                                                                                          \
+  }
+  MSHA_FOR_EACH_SHAPE(XR)
+#undef XR
+  return check_launch("edge_attention_fwd_rs");
+}
+
+extern "C" int msha_edge_attention_bwd_fused_rs(
+    const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype, const float* el,
+    const float* ar, const void* hc, const float* lse, const void* u, const void* u_lo,
+    const void* dU, float neg_slope, float drop_p, uint64_t seed, uint64_t offset,
+    const float* uc, const float* qc, float* d_el, float* d_er, void* d_hc, float* de, void* ws,
+    size_t ws_bytes, msha_stream_t stream) {
+  if (int rc = check_graph(g, true)) return rc;
+  MSHA_ARG_CHECK(el && ar && hc && lse && u && dU && d_el && d_er && d_hc,
+                 "edge_attention_bwd_fused_rs: null pointer");
+  MSHA_ARG_CHECK((uc == nullptr) == (qc == nullptr), "edge_attention_bwd_fused_rs: uc and qc go together");
+  MSHA_ARG_CHECK(g->n_edges == 0 || ((de || uc) && g->csc_eid),
+                 "edge_attention_bwd_fused_rs: needs de scratch (or row terms) and csc_eid");
+  MSHA_ARG_CHECK(drop_p >= 0.f && drop_p <= 1.f, "edge_attention_bwd_fused_rs: p must be in [0,1]");
+  MSHA_ARG_CHECK(((uintptr_t)ar & 15) == 0, "edge_attention_bwd_fused_rs: a_r must be 16-byte aligned");
+  if (!msha_edge_attention_row_scores_supported(g, heads, feat, dtype))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_fused_rs: unsupported (heads, feat, dtype, sizes)");
+  MSHA_ARG_CHECK(ws != nullptr &&
+                     ws_bytes >= msha_edge_attention_bwd_fused_workspace_size(g, heads, feat),
+                 "edge_attention_bwd_fused_rs: workspace too small");
+  const int64_t D = (int64_t)heads * feat;
+  float* rec = (float*)ws;
+  const size_t rec_bytes = ((size_t)g->n_rows * rec_stride(heads) * sizeof(float) + 255) & ~(size_t)255;
+  float* part = (float*)((char*)ws + rec_bytes);
+  float* part_x = part + g->n_chunks * D;
+  hipStream_t s = (hipStream_t)stream;
+  const Dropout dp = make_dropout(drop_p, seed, offset, s);
+  if (dtype == MSHA_DTYPE_BF16)
+    launch_bwd_fused<bf16_t>(g, heads, feat, el, nullptr, ar, hc, lse, u, u_lo, dU, neg_slope, dp,
+                             d_el, d_er, d_hc, de, rec, part, part_x, uc, qc, s);
+  else
+    launch_bwd_fused<float>(g, heads, feat, el, nullptr, ar, hc, lse, u, nullptr, dU, neg_slope, dp,
+                            d_el, d_er, d_hc, de, rec, part, part_x, uc, qc, s);
+  return check_launch("edge_attention_bwd_fused_rs");
 }

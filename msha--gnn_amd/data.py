@@ -88,6 +88,33 @@ def synthetic_flows(n: int, m: int, deg_hist: np.ndarray, col_weight: np.ndarray
     return np.stack([np.concatenate(src), np.concatenate(dst)], 1).astype(np.int64)
 
 
+def synthetic_csr(n: int, m: int, deg_hist: np.ndarray, col_weight: np.ndarray, seed: int,
+                  block: int = 1 << 17):
+    """Repo-shape bipartite graph at any size (SURVEY.md §8d C4 'bipartite generator,
+    M = 32, 2015 degree law'), vectorised: per-source distinct degree drawn from
+    ``deg_hist`` (clipped to [1, m]), recipients drawn without replacement with
+    probability proportional to ``col_weight`` (Gumbel top-k: the same law as
+    ``synthetic_flows``' sequential draws, not the same stream).  Returns the CSR
+    (rowptr (n+1) int64, col int64, ascending within each row)."""
+    rng = np.random.default_rng(seed)
+    p_deg = np.asarray(deg_hist, np.float64) / np.sum(deg_hist)
+    degs = np.clip(rng.choice(len(p_deg), size=n, p=p_deg), 1, m).astype(np.int64)
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(degs, out=rowptr[1:])
+    col = np.empty(int(rowptr[-1]), np.int64)
+    logw = np.log(np.asarray(col_weight, np.float64) / np.sum(col_weight))
+    slots = np.arange(m)[None, :]
+    for b0 in range(0, n, block):
+        b1 = min(n, b0 + block)
+        d = degs[b0:b1, None]
+        keys = logw[None, :] - np.log(-np.log(rng.random((b1 - b0, m))))
+        order = np.argsort(-keys, axis=1)  # a weighted random permutation per row
+        pick = np.where(slots < d, order, m)
+        pick.sort(axis=1)  # the row's d columns ascending, then the m sentinels
+        col[rowptr[b0]:rowptr[b1]] = pick[slots < d]
+    return rowptr, col
+
+
 class HigherDataset(torch.utils.data.Dataset):
     """Drop-in for dataset.py:208-330 over ``anonymous_data/``."""
 

@@ -96,7 +96,7 @@ def _stream(t):
 
 class _EdgeAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, el, er, hc, hs, graph: Graph, p: float, seed: int, slope: float):
+    def forward(ctx, el, er, hc, hs, graph: Graph, p: float, seed: int, slope: float, ar=None):
         n, H = el.shape
         m, H2, F = hc.shape
         assert H2 == H and m == graph.n_cols and n == graph.n_rows
@@ -106,6 +106,12 @@ class _EdgeAttention(torch.autograd.Function):
         dev = el.device
         s = _stream(el)
         g = graph.desc
+        # scores from the gathered row (msha_edge_attention_fwd_rs): er_j = hc_j . a_r is
+        # recomputed from the row the kernel gathers anyway, in the forward and in the
+        # fused backward's column pass (the same bits in both); u-only path
+        rs = (ar is not None and hs is None and ROW_SCORES and FUSED_BWD
+              and _lib.load().msha_edge_attention_row_scores_supported(g, H, F, _code(dt)))
+        ar = ar.detach().to(torch.float32).contiguous().view(H, F) if rs else None
         u = torch.empty(n, H, F, device=dev, dtype=dt)
         # bf16 tables under autograd: keep the rounding residual of u for the backward's
         # D = dU . u (include/msha_gnn.h, u_lo)
@@ -122,9 +128,15 @@ class _EdgeAttention(torch.autograd.Function):
             uc = torch.empty(n, H, F, device=dev, dtype=torch.float32)
             qc = torch.empty(n, H, device=dev, dtype=torch.float32)
         ev = _timed("edge_attention_fwd")
-        _lib.call("msha_edge_attention_fwd_ex", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
-                  hc.data_ptr(), slope, p, seed, 0, u.data_ptr(), _lib.ptr(u_lo),
-                  lse.data_ptr(), _lib.ptr(attd), _lib.ptr(uc), _lib.ptr(qc), s)
+        if rs:
+            _lib.call("msha_edge_attention_fwd_rs", g, H, F, _code(dt), el.data_ptr(),
+                      ar.data_ptr(), hc.data_ptr(), slope, p, seed, 0, u.data_ptr(),
+                      _lib.ptr(u_lo), lse.data_ptr(), _lib.ptr(uc), _lib.ptr(qc), s)
+        else:
+            _lib.call("msha_edge_attention_fwd_ex", g, H, F, _code(dt), el.data_ptr(),
+                      er.data_ptr(), hc.data_ptr(), slope, p, seed, 0, u.data_ptr(),
+                      _lib.ptr(u_lo), lse.data_ptr(), _lib.ptr(attd), _lib.ptr(uc),
+                      _lib.ptr(qc), s)
         if ev is not None:
             ev[1].record()
         v = None
@@ -134,8 +146,10 @@ class _EdgeAttention(torch.autograd.Function):
         ctx.graph, ctx.p, ctx.seed, ctx.slope = graph, p, seed, slope
         ctx.has_hs = hs is not None
         ctx.rowterms = uc is not None
+        ctx.rs = bool(rs)
         ctx.save_for_backward(el, er, hc, hs if hs is not None else el.new_empty(0), lse, u,
                               u_lo if u_lo is not None else el.new_empty(0),
+                              ar if rs else el.new_empty(0),
                               *((uc, qc) if uc is not None else ()))
         if v is None:
             return u
@@ -143,8 +157,9 @@ class _EdgeAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dU, dV=None):
-        el, er, hc, hs, lse, u, u_lo, *rowterms = ctx.saved_tensors
+        el, er, hc, hs, lse, u, u_lo, ar, *rowterms = ctx.saved_tensors
         u_lo = u_lo if u_lo.numel() else None
+        ar = ar if ctx.rs else None
         graph = ctx.graph
         n, H = el.shape
         m, _, F = hc.shape
@@ -158,7 +173,7 @@ class _EdgeAttention(torch.autograd.Function):
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
         if not use_dv and FUSED_BWD:
-            return _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms)
+            return _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms, ar)
         # one (de, attd) record of 2H floats per edge: the column pass reads it as one
         # 64-B segment at C4 (the CSC visits edges in random order)
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)
@@ -181,7 +196,7 @@ class _EdgeAttention(torch.autograd.Function):
             ev[1].record()
         if ctx.has_hs and d_hs is None:
             d_hs = torch.zeros_like(hs)
-        return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None
+        return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None, None
 
 
 # u-only backward as one column pass (msha_edge_attention_bwd_fused) instead of
@@ -190,9 +205,12 @@ FUSED_BWD = True
 # row terms (uc, qc) from the forward where the library prefers them (large graphs);
 # module switch for A/B measurements
 ROWTERMS = True
+# scores from the gathered row when the caller passes a_r (msha_edge_attention_fwd_rs);
+# module switch for A/B measurements
+ROW_SCORES = True
 
 
-def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms=()):
+def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms=(), ar=None):
     graph = ctx.graph
     n, H = el.shape
     m, _, F = hc.shape
@@ -209,15 +227,16 @@ def _bwd_fused(ctx, el, er, hc, lse, u, u_lo, dU, d_el, hs, rowterms=()):
     d_hc = torch.empty(m, H, F, device=dev, dtype=hc.dtype)
     d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
     ev = _timed("edge_attention_bwd_fused")
-    _lib.call("msha_edge_attention_bwd_fused_ex", g, H, F, _code(hc.dtype), el.data_ptr(),
-              er.data_ptr(), hc.data_ptr(), lse.data_ptr(), u.data_ptr(), _lib.ptr(u_lo),
-              dU.data_ptr(), ctx.slope, ctx.p, ctx.seed, 0, _lib.ptr(uc), _lib.ptr(qc),
-              d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(), _lib.ptr(de), ws.data_ptr(),
-              wsb, s)
+    _lib.call("msha_edge_attention_bwd_fused_rs" if ar is not None else
+              "msha_edge_attention_bwd_fused_ex", g, H, F, _code(hc.dtype), el.data_ptr(),
+              ar.data_ptr() if ar is not None else er.data_ptr(), hc.data_ptr(), lse.data_ptr(),
+              u.data_ptr(), _lib.ptr(u_lo), dU.data_ptr(), ctx.slope, ctx.p, ctx.seed, 0,
+              _lib.ptr(uc), _lib.ptr(qc), d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
+              _lib.ptr(de), ws.data_ptr(), wsb, s)
     if ev is not None:
         ev[1].record()
     d_hs = torch.zeros_like(hs) if ctx.has_hs else None
-    return d_el, d_er, d_hc, d_hs, None, None, None, None
+    return d_el, d_er, d_hc, d_hs, None, None, None, None, None
 
 
 def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream, ld=0):
@@ -235,13 +254,19 @@ def _csc_aggregate(graph: Graph, H, F, w, x, table, out, out_x, stream, ld=0):
 
 
 def edge_attention(graph: Graph, el, er, hc, hs=None, p: float = 0.0, training: bool = False,
-                   slope: float = NEG_SLOPE, seed: int | None = None):
+                   slope: float = NEG_SLOPE, seed: int | None = None, ar=None):
     """Fused masked edge-softmax + aggregation.
 
     el (N,H), er (M,H), hc (M,H,F) [, hs (N,H,F)] ->  u (N,H,F)  [, v (M,H,F)]
     with att = softmax_row(lrelu(el_i + er_j)), u = drop(att) @ hc, v = drop(att).T @ hs.
     Tables (hc, hs, u, v and their gradients) are bf16 when hc or hs is bf16 (fp32
     arithmetic, config C3), else fp32; scores and statistics are always fp32.
+
+    ``ar`` (H, F), optional: the score vector er was computed with, er = hc . ar per
+    head (Ablation.py:266-267 scores the aggregated table itself).  Then the u-only
+    kernels recompute er_j from the gathered rows instead of gathering er per edge
+    (msha_edge_attention_fwd_rs / _bwd_fused_rs); the gradient w.r.t. er is returned
+    as before and reaches ar / hc through er's producer.
     """
     _lib.require_cuda(el, er, hc, hs)
     F = hc.shape[-1]
@@ -251,7 +276,9 @@ def edge_attention(graph: Graph, el, er, hc, hs=None, p: float = 0.0, training: 
     p = float(p) if training else 0.0
     if seed is None:
         seed = new_seed() if p > 0 else 0
-    return _EdgeAttention.apply(el, er, hc, hs, graph, p, seed, slope)
+    if ar is not None and tuple(ar.shape) not in ((H, F), (H * F,), (H * F, 1)):
+        raise ValueError(f"edge_attention: ar must hold heads x feat = {H} x {F} values")
+    return _EdgeAttention.apply(el, er, hc, hs, graph, p, seed, slope, ar)
 
 
 class _GAL(torch.autograd.Function):

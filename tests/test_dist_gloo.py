@@ -64,6 +64,25 @@ def _worker(rank, world, port, q):
         got = torch.cat([pt[: b_ - a_] for pt, (a_, b_) in zip(parts, sizes)]).numpy()
         ref = O.score_pairs(h, src, dst, "mlp", [(W, b), (None, None)])
         ok = np.allclose(got, ref, rtol=1e-6, atol=1e-6) and (plo, phi) == sizes[rank]
+        # double-buffered gather/score: a different table per batch (refresh), each batch
+        # scored against its own gather
+        tab2 = sharding.ShardedTable(n, F, world, rank, "cpu", buffers=2)
+        assert tab2.path() == "gloo"
+        scale = [1.0, -2.0, 0.5]
+
+        def refresh(k):
+            tab2.set_local(torch.as_tensor(h[lo:hi] * scale[k]))
+
+        bsz = [0, 1700, 3400, P]
+        batches = [(torch.as_tensor(src[a:b_]), torch.as_tensor(dst[a:b_]))
+                   for a, b_ in zip(bsz[:-1], bsz[1:])]
+        outs = sharding.PipelinedScorer(tab2, score, refresh).run(batches)
+        for k, (s_, d_) in enumerate(batches):
+            a_, b_ = sharding.pair_range(s_.numel(), world, rank)
+            want = O.score_pairs(h * scale[k], s_.numpy()[a_:b_], d_.numpy()[a_:b_], "mlp",
+                                 [(W, b), (None, None)])
+            ok = ok and outs[k][:2] == (a_, b_) and np.allclose(outs[k][2].numpy(), want,
+                                                                rtol=1e-6, atol=1e-6)
         # bench.py's timing reduction: the max over ranks
         t = torch.tensor([0.5 + rank])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

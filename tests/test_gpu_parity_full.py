@@ -145,6 +145,61 @@ def test_c4_forward_backward_every_row(cuda, c4, dt):
         tol_close(_np64(W.grad), dW_ref, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_c4_row_scores_every_row(cuda, c4, dt):
+    """The bench's default C4 path: scores from the gathered row (the forward and the
+    fused backward's column pass recompute er_j = h_j . a_r), every row against the fp64
+    C oracle fed er = h . a_r on the stored h; row terms on and off."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+
+    rowptr, col, colptr, csc_row, perm, graph = c4
+    n, fin, H, Fd = 100_000, 128, 8, 16
+    tol = F32_TOL if dt == torch.float32 else BF16_TOL
+    code = 1 if dt == torch.bfloat16 else 0
+    assert _lib.load().msha_edge_attention_row_scores_supported(graph.desc, H, Fd, code)
+    g = torch.Generator().manual_seed(8)
+    X = torch.rand(n, fin, generator=g).to(cuda, dt)
+    W = (torch.randn(fin, H * Fd, generator=g) * fin ** -0.5).to(cuda, dt)
+    al = torch.randn(H, Fd, generator=g).to(cuda)
+    ar = torch.randn(H, Fd, generator=g).to(cuda)
+    dU = torch.randn(n, H, Fd, generator=g).to(cuda, dt)
+    with torch.no_grad():
+        h, el, er = MF.project_scores(X, W, al, ar, heads=H)
+    hc64 = _np64(h).reshape(n, H, Fd)
+    el64, ar64, dU64 = _np64(el), _np64(ar), _np64(dU)
+    er64 = np.einsum("nhf,hf->nh", hc64, ar64)
+    u_ref, lse_ref = cpu_oracle.edge_attention_fwd(rowptr, col, el64, er64, hc64, fp64=True)
+    d_el_ref, d_er_ref, d_hc_ref = cpu_oracle.edge_attention_bwd(
+        rowptr, col, colptr, csc_row, perm, el64, er64, hc64, lse_ref, u_ref, dU64, fp64=True)
+    # lse of the row-score forward (raw ABI call)
+    u0 = torch.empty(n, H, Fd, device=cuda, dtype=dt)
+    lse = torch.empty(n, H, device=cuda)
+    _lib.call("msha_edge_attention_fwd_rs", graph.desc, H, Fd, code, el.data_ptr(),
+              ar.data_ptr(), h.data_ptr(), 0.2, 0.0, 0, 0, u0.data_ptr(), None, lse.data_ptr(),
+              None, None, _lib.stream_handle(cuda))
+    torch.cuda.synchronize()
+    tol_close(_np64(lse), lse_ref, F32_TOL, F32_TOL)
+    tol_close(_np64(u0), u_ref, tol, tol)
+    got = {}
+    for rt in ("0", "1"):
+        os.environ["MSHA_ROWTERMS"] = rt
+        try:
+            el_l = el.detach().clone().requires_grad_(True)
+            er_l = torch.zeros_like(er).requires_grad_(True)  # not read on this path
+            hc_l = h.detach().view(n, H, Fd).clone().requires_grad_(True)
+            u = MF.edge_attention(graph, el_l, er_l, hc_l, ar=ar)
+            u.backward(dU)
+        finally:
+            os.environ.pop("MSHA_ROWTERMS")
+        assert torch.equal(u.detach(), u0)  # the op is exactly that launch
+        got[rt] = (el_l.grad, er_l.grad, hc_l.grad)
+        tol_close(_np64(el_l.grad), d_el_ref, tol, tol)
+        tol_close(_np64(er_l.grad), d_er_ref, tol, tol)
+        tol_close(_np64(hc_l.grad), d_hc_ref, tol, tol)
+    assert torch.equal(got["0"][1], got["1"][1]) and torch.equal(got["0"][2], got["1"][2])
+
+
 # ------------------------------------------------------------- configs[1] / [2]
 def _year(msha, cuda, year):
     """Full graph of a year on the GPU: dense normalised adjacency (as train.py passes
