@@ -547,10 +547,13 @@ MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int3
  * fp32 or bf16 (dtype); rows, cols int64 (B).
  *   msha_nll_rows_fwd: loss[0] = -(1/B) sum_b logp[rows[b], cols[b]]  (fp32)
  *   msha_nll_rows_bwd: dlogp = 0 except dlogp[rows[b], cols[b]] += -gloss[0] / B for b in
- *                      order (repeated pairs accumulate); gloss is a device scalar. */
-MSHA_API int msha_nll_rows_fwd(int64_t B, const int64_t* rows, const int64_t* cols,
-                               int32_t dtype, const void* logp, int64_t ld, float* loss,
-                               msha_stream_t stream);
+ *                      order (repeated pairs accumulate); gloss is a device scalar.
+ * An entry outside [0, N) x [0, M) is never read or written (torch raises on it): the
+ * forward returns NaN for it (and for B = 0, torch's mean over nothing), the backward
+ * skips it.  (ABI 9: the forward takes N, M.) */
+MSHA_API int msha_nll_rows_fwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                               const int64_t* cols, int32_t dtype, const void* logp, int64_t ld,
+                               float* loss, msha_stream_t stream);
 MSHA_API int msha_nll_rows_bwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
                                const int64_t* cols, const float* gloss, int32_t dtype,
                                void* dlogp, int64_t ld, msha_stream_t stream);

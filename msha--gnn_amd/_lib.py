@@ -155,7 +155,7 @@ SIGNATURES = {
                                          P]),
     "msha_dropout_keep_mask4": (C.c_int, [U64, U64, I64, F32, P, P]),
     "msha_dropout_keep_mask_word": (C.c_int, [U64, U64, I64, F32, I32, P, P]),
-    "msha_nll_rows_fwd": (C.c_int, [I64, P, P, I32, P, I64, P, P]),
+    "msha_nll_rows_fwd": (C.c_int, [I64, I64, I64, P, P, I32, P, I64, P, P]),
     "msha_nll_rows_bwd": (C.c_int, [I64, I64, I64, P, P, P, I32, P, I64, P]),
     "msha_head_supported": (C.c_int, [I64, I32, I32]),
     "msha_head_workspace_size": (SZ, [GP, I32, I32]),

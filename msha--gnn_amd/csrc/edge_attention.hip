@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "edge_geo.h"
 
 #ifndef COLS_EH
 #define COLS_EH 1
@@ -42,35 +43,8 @@
 #ifndef COLS_NG
 #define COLS_NG 2  // slot groups whose loads are in flight together in the column pass
 #endif
-#ifndef FWD_EPL
-#define FWD_EPL 2
-#endif
-#ifndef FWD_EPL_BF16
-#define FWD_EPL_BF16 2
-#endif
 
 namespace msha {
-
-template <int H, int F, typename T>
-struct Geo {
-  static constexpr int V = Pk<T>::V;        // elements per 16-byte chunk (4 fp32 / 8 bf16)
-  static constexpr int D = H * F;
-  static constexpr int NQ = D / V;          // chunks per feature row
-  static constexpr int QPL = NQ > 64 ? NQ / 64 : 1;
-  static constexpr int EPI = NQ >= 64 ? 1 : 64 / NQ;
-  static constexpr int CE = 64 / H;
-  static constexpr int QH = F / V;          // chunks per head
-  static_assert(F % V == 0, "feat must be a multiple of the 16-byte chunk");
-  static_assert(H >= 1 && H <= 64 && (64 % H) == 0, "heads must divide 64");
-  static_assert(CE % EPI == 0, "score chunk must cover whole gather groups");
-  static_assert(QH <= 64 && (64 % QH) == 0, "chunks per head must divide 64");
-};
-
-// chunk index (within the feature row) owned by this lane for slot k
-template <class G>
-__device__ __forceinline__ int quad_of(int lane, int k) {
-  return G::QPL == 1 ? (lane % G::NQ) : (lane + 64 * k);
-}
 
 // ------------------------------------------------------------------ forward ---
 // EPL = edges per lane in the score layout: a chunk covers EPL * 64/H edges, so the
@@ -242,15 +216,6 @@ __global__ void __launch_bounds__(256) edge_attn_fwd_kernel(
 // rescale as u and l.  Then d_el_i = dU_i . uc_i - D_i qc_i per head (D_i = dU_i . u_i),
 // which is sum_j de_ij rearranged: the fused backward needs no per-edge de crossing
 // from CSC to CSR order (bwd_row_stats_kernel<RT> finishes d_el in its row pass).
-#ifndef FWD_WPE
-#define FWD_WPE 1
-#endif
-#ifndef FWD_SHORT_DEG
-#define FWD_SHORT_DEG 8
-#endif
-#ifndef FWD_SHORT_RPW
-#define FWD_SHORT_RPW 5  // rows per wave on short-row graphs (A/B: MSHA_FWD_WAVES)
-#endif
 template <int H, int F, typename T, int EPL, bool RT = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
 edge_attn_fwd_bat_kernel(
@@ -440,202 +405,6 @@ edge_attn_fwd_bat_kernel(
     end = nend;
     virt = nvirt;
     elh = nelh;
-#pragma unroll
-    for (int t = 0; t < EPL; ++t) {
-      j0[t] = nj0[t];
-      j1[t] = nj1[t];
-    }
-  }
-}
-
-// ------------------------------------------------ forward, scores from the gathered row ---
-// In every caller of this path the gathered table scores its own rows: er_j = hc_j . a_r
-// per head (Ablation.py:266-267: a[:F] against h1_j, the row u aggregates).  Given a_r,
-// this forward computes er_j from the row its gather lanes already hold -- V fmas per lane
-// and the xor tree over the head's QH lanes (DPP) -- instead of gathering er_j per edge
-// (a 4H-byte piece of an (M, H) table that costs a whole cache line per edge once the
-// table outgrows L2: syn2m's 64 MB er table, 40M edges).
-// The softmax runs in the gather layout (lane = edge slot g_e x 16-byte piece q; every
-// (edge, head) score replicated over the head's QH lanes): chunk max / sum reduce the
-// NGI gather slots in registers and the EPI edge slots of a gather instruction by xor
-// over g_e, so no weight is shuffled to the gather lanes.  Dropout keep bits are drawn
-// in the score layout (one Philox call per (edge, head), as everywhere) and reach the
-// gather lanes by ballot.  Row terms (RT) as edge_attn_fwd_bat_kernel.
-// The fused backward's column pass recomputes er_j from hc_j in the same order (same
-// bits), so the scores of both passes agree exactly.
-template <int H, int F, typename T, int EPL, bool RT = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
-edge_attn_fwd_rs_kernel(
-    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
-    const float* __restrict__ el, const float* __restrict__ ar, const T* __restrict__ hc,
-    float slope, Dropout dp, T* __restrict__ u, T* __restrict__ u_lo, float* __restrict__ lse,
-    float* __restrict__ uc, float* __restrict__ qc) {
-  using G = Geo<H, F, T>;
-  static_assert(G::QPL == 1, "row-score forward: one 16-byte piece per lane");
-  constexpr int CEL = EPL * G::CE;    // edges per chunk
-  constexpr int NGI = CEL / G::EPI;   // gather instructions per chunk
-  const int lane = lane_id();
-  const int e_s = lane / H, h_s = lane % H;        // score layout (columns, dropout)
-  const int g_e = lane / G::NQ, q = lane % G::NQ;  // gather layout
-  const int hq = q / G::QH;                        // head of this lane's piece
-  const rsrc_t r_col = make_rsrc(col, (uint32_t)n_edges * 4u);
-  const rsrc_t r_hc = make_rsrc(hc, (uint32_t)n_cols * (uint32_t)(G::D * sizeof(T)));
-  const uint32_t q_off = 16u * q;
-  const int wave0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-  const int nwaves = (int)(((int64_t)gridDim.x * blockDim.x) >> 6);
-  // this lane's piece of a_r ((H, F) fp32: piece q covers elements q*V .. q*V + V - 1)
-  Pk<T> arq;
-#pragma unroll
-  for (int v = 0; v < G::V; v += 4) {
-    const float4 a4 = *reinterpret_cast<const float4*>(ar + G::V * q + v);
-    arq.v[v] = a4.x; arq.v[v + 1] = a4.y; arq.v[v + 2] = a4.z; arq.v[v + 3] = a4.w;
-  }
-
-  int row = wave0;
-  if (row >= n_rows) return;
-  int32_t start = __builtin_amdgcn_readfirstlane(rowptr[row]);
-  int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
-  bool virt = rowflag != nullptr && rowflag[row] != 0;
-  float elq = el[(int64_t)row * H + hq];
-  int32_t j0[EPL], j1[EPL];
-#pragma unroll
-  for (int t = 0; t < EPL; ++t) {
-    const int32_t e0 = start + t * G::CE + e_s, e1 = e0 + CEL;
-    j0[t] = buf_i32(r_col, e0 < end ? (uint32_t)e0 * 4u : kOOB);
-    j1[t] = buf_i32(r_col, e1 < end ? (uint32_t)e1 * 4u : kOOB);
-  }
-  while (true) {
-    float m = -INFINITY, l = 0.f, lc = 0.f;
-    Pk<T> acc = pk_zero<T>(), accc = pk_zero<T>();
-    for (int32_t cs = start; cs < end; cs += CEL) {
-      const int nvalid = min(CEL, (int)(end - cs));
-      // (1) this chunk's gathers, all in flight together; columns two chunks ahead
-      u32x4_t raw[NGI];
-#pragma unroll
-      for (int gi = 0; gi < NGI; ++gi) {
-        const int g = gi * G::EPI;
-        const int t = g / G::CE;
-        const int ei = g % G::CE + g_e;
-        const int32_t jq = __shfl(j0[t], ei * H);
-        raw[gi] = buf_b128(r_hc, g + g_e < nvalid
-                                     ? (uint32_t)jq * (uint32_t)(G::D * sizeof(T)) + q_off
-                                     : kOOB);
-      }
-      int32_t j2[EPL];
-#pragma unroll
-      for (int t = 0; t < EPL; ++t) {
-        const int32_t e2 = cs + 2 * CEL + t * G::CE + e_s;
-        j2[t] = buf_i32(r_col, e2 < end ? (uint32_t)e2 * 4u : kOOB);
-      }
-      // (2) dropout keep bits of the chunk (score layout, one draw per (edge, head)),
-      // while the gathers fly
-      uint64_t keep[EPL];
-      if (dp.active) {
-#pragma unroll
-        for (int t = 0; t < EPL; ++t)
-          keep[t] = __ballot(dropout_factor(dp, (uint64_t)(cs + t * G::CE + e_s) * H + h_s) != 0.f);
-      }
-      // (3) scores from the gathered rows (gather layout)
-      float sc[NGI], pre[NGI];
-      float smax = -INFINITY;
-#pragma unroll
-      for (int gi = 0; gi < NGI; ++gi) {
-        const Pk<T> xr = pk_from_raw(raw[gi], (T*)nullptr);
-        const float erq = group_sum<G::QH>(pk_dot(xr, arq));
-        pre[gi] = elq + erq;
-        const bool valid = gi * G::EPI + g_e < nvalid;
-        sc[gi] = valid ? (virt ? 0.f : lrelu(pre[gi], slope)) : -INFINITY;
-        smax = fmaxf(smax, sc[gi]);
-      }
-#pragma unroll
-      for (int o = G::NQ; o < 64; o <<= 1) smax = fmaxf(smax, xor_shfl(smax, o));
-      const float mn = fmaxf(m, smax);
-      const float alpha = __expf(m - mn);
-      float w[NGI], psum = 0.f, pcsum = 0.f;
-#pragma unroll
-      for (int gi = 0; gi < NGI; ++gi) {
-        const float pe = __expf(sc[gi] - mn);  // masked slots: exp(-inf) = 0
-        psum += pe;
-        if (RT) pcsum = fmaf(pe, pre[gi] > 0.f ? 1.f : slope, pcsum);
-        w[gi] = pe;
-        if (dp.active) {
-          const int ec = gi * G::EPI;  // + g_e: edge slot of the chunk
-          const int bit = (ec % G::CE + g_e) * H + hq;
-          w[gi] = (keep[ec / G::CE] >> bit) & 1ull ? pe * dp.scale : 0.f;
-        }
-      }
-#pragma unroll
-      for (int o = G::NQ; o < 64; o <<= 1) psum += xor_shfl(psum, o);
-      l = fmaf(l, alpha, psum);
-      if (RT) {
-#pragma unroll
-        for (int o = G::NQ; o < 64; o <<= 1) pcsum += xor_shfl(pcsum, o);
-        lc = fmaf(lc, alpha, pcsum);
-      }
-      m = mn;
-      acc = pk_scale(acc, alpha);
-      if (RT) accc = pk_scale(accc, alpha);
-      // (4) accumulate in gather order (masked slots carry w = 0 and a zero row)
-#pragma unroll
-      for (int gi = 0; gi < NGI; ++gi) {
-        const Pk<T> xr = pk_from_raw(raw[gi], (T*)nullptr);
-        acc = pk_fma(w[gi], xr, acc);
-        if (RT) accc = pk_fma(w[gi] * (pre[gi] > 0.f ? 1.f : slope), xr, accc);
-      }
-#pragma unroll
-      for (int t = 0; t < EPL; ++t) {
-        j0[t] = j1[t];
-        j1[t] = j2[t];
-      }
-    }
-    // the next row's bounds, flag, el and first columns before this row's epilogue
-    const int nrow_raw = row + nwaves;
-    const bool has_next = nrow_raw < n_rows;
-    const int nrow = has_next ? nrow_raw : row;
-    const int32_t nstart = __builtin_amdgcn_readfirstlane(rowptr[nrow]);
-    const int32_t nend = __builtin_amdgcn_readfirstlane(rowptr[nrow + 1]);
-    const bool nvirt = rowflag != nullptr && rowflag[nrow] != 0;
-    const float nelq = el[(int64_t)nrow * H + hq];
-    int32_t nj0[EPL], nj1[EPL];
-#pragma unroll
-    for (int t = 0; t < EPL; ++t) {
-      const int32_t e0 = nstart + t * G::CE + e_s, e1 = e0 + CEL;
-      nj0[t] = buf_i32(r_col, e0 < nend ? (uint32_t)e0 * 4u : kOOB);
-      nj1[t] = buf_i32(r_col, e1 < nend ? (uint32_t)e1 * 4u : kOOB);
-    }
-    if (G::EPI > 1) {
-#pragma unroll
-      for (int o = G::NQ; o < 64; o <<= 1) acc = pk_xor_add(acc, o);
-      if (RT) {
-#pragma unroll
-        for (int o = G::NQ; o < 64; o <<= 1) accc = pk_xor_add(accc, o);
-      }
-    }
-    const float inv = l > 0.f ? 1.f / l : 0.f;  // l, m: this lane's head (replicated)
-    if (g_e == 0) {
-      const Pk<T> uk = pk_scale(acc, inv);
-      pk_store(u + (int64_t)row * G::D + G::V * q, uk);
-      if (sizeof(T) == 2 && u_lo != nullptr)
-        pk_store(u_lo + (int64_t)row * G::D + G::V * q, pk_residual(uk));
-      if (RT) {
-        const Pk<T> ck = pk_scale(accc, inv);
-        float* dst = uc + (int64_t)row * G::D + G::V * q;
-#pragma unroll
-        for (int v = 0; v < G::V; v += 4)
-          *reinterpret_cast<float4*>(dst + v) = make_float4(ck.v[v], ck.v[v + 1], ck.v[v + 2], ck.v[v + 3]);
-      }
-      if (q % G::QH == 0) {
-        lse[(int64_t)row * H + hq] = l > 0.f ? m + __logf(l) : -INFINITY;
-        if (RT) qc[(int64_t)row * H + hq] = l > 0.f ? lc / l : 0.f;
-      }
-    }
-    if (!has_next) break;
-    row = nrow;
-    start = nstart;
-    end = nend;
-    virt = nvirt;
-    elq = nelq;
 #pragma unroll
     for (int t = 0; t < EPL; ++t) {
       j0[t] = nj0[t];
@@ -1461,21 +1230,6 @@ __global__ void __launch_bounds__(256) bwd_row_sum_kernel(
 }
 
 // ------------------------------------------------------------------- dispatch ---
-// Compiled (heads, feat) set.  Extend here (and in msha_edge_attention_supported).
-#define MSHA_FOR_EACH_SHAPE(X) \
-  X(1, 8) X(1, 16) X(1, 32) X(1, 64) X(1, 128) \
-  X(2, 8) X(2, 16) X(2, 32) X(2, 64) X(2, 128) \
-  X(4, 8) X(4, 16) X(4, 32) X(4, 64) X(4, 128) \
-  X(8, 8) X(8, 16) X(8, 32) X(8, 64) X(8, 128)
-
-// edges per lane of the forward's score layout (2: amortise the per-chunk reductions
-// where a chunk is short and the gathers are single 16-byte pieces per lane)
-template <int H, int F, typename T>
-constexpr int fwd_epl() {
-  using G = Geo<H, F, T>;
-  return (G::QPL == 1 && G::CE <= 16) ? (sizeof(T) == 2 ? FWD_EPL_BF16 : FWD_EPL) : 1;
-}
-
 static bool shape_supported(int H, int F) {
 #define X(h, f) if (H == h && F == f) return true;
   MSHA_FOR_EACH_SHAPE(X)
@@ -1520,6 +1274,16 @@ static bool dtype_ok(int32_t dtype, int32_t feat) {
 
 // the batched-gather forward applies: one piece per lane, every table addressable by
 // 32-bit offsets
+// MSHA_FWD_WAVES caps the forward's grid (waves then walk rows with the next row
+// prefetched); default: short rows (mean degree <= FWD_SHORT_DEG) walk ~FWD_SHORT_RPW rows
+// per wave
+static dim3 fwd_grid(const msha_graph* g) {
+  int64_t cap = env_int("MSHA_FWD_WAVES", -1);
+  if (cap < 0)
+    cap = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows ? g->n_rows / FWD_SHORT_RPW : 0;
+  return wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
+}
+
 static bool fwd_bat_ok(const msha_graph* g, int heads, int feat, int32_t dtype) {
   const int64_t lim = (int64_t)1 << 31;
   const int64_t esz = dtype == MSHA_DTYPE_BF16 ? 2 : 4;
@@ -1570,12 +1334,14 @@ extern "C" int msha_edge_attention_fwd_ex(const msha_graph* g, int32_t heads, in
   if (uc != nullptr && !bat)
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd: row terms need the batched forward");
   if (bat) {
-    // MSHA_FWD_WAVES caps the grid (waves then walk rows with the next row prefetched);
-    // default: short rows (mean degree <= FWD_SHORT_DEG) walk ~FWD_SHORT_RPW rows per wave
-    int64_t cap = env_int("MSHA_FWD_WAVES", -1);
-    if (cap < 0)
-      cap = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows ? g->n_rows / FWD_SHORT_RPW : 0;
-    const dim3 grid = wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
+    const dim3 grid = fwd_grid(g);
+    // short rows (mean degree <= FWD_SHORT_DEG: R15, bip1m): the gather-layout forward
+    // with FWD_SHORT_CEL-edge chunks (MSHA_FWD_GL=0: the batched kernel, A/B)
+    const bool short_rows = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows;
+    if (short_rows && env_int("MSHA_FWD_GL", 1) != 0 &&
+        launch_fwd_gl(g, heads, feat, dtype, el, er, nullptr, hc, neg_slope, dp, u, u_lo, lse,
+                      attd, uc, qc, true, grid, s))
+      return check_launch("edge_attention_fwd");
 #define XB(h, f)                                                                               \
     if (heads == h && feat == f) {                                                             \
       if (dtype == MSHA_DTYPE_BF16) {                                                          \
@@ -1887,36 +1653,10 @@ extern "C" int msha_edge_attention_fwd_rs(const msha_graph* g, int32_t heads, in
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd_rs: unsupported (heads, feat, dtype, sizes)");
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
-  int64_t cap = env_int("MSHA_FWD_WAVES", -1);
-  if (cap < 0)
-    cap = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows ? g->n_rows / FWD_SHORT_RPW : 0;
-  const dim3 grid = wave_grid(cap > 0 && cap < g->n_rows ? cap : g->n_rows);
-#define XR(h, f)                                                                               \
-  if (heads == h && feat == f) {                                                               \
-    if (dtype == MSHA_DTYPE_BF16) {                                                            \
-      if constexpr (f % 8 == 0 && h * f * 2 <= 1024) {                                         \
-        auto kern = uc != nullptr                                                              \
-            ? edge_attn_fwd_rs_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>(), true>             \
-            : edge_attn_fwd_rs_kernel<h, f, bf16_t, fwd_epl<h, f, bf16_t>(), false>;           \
-        hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,         \
-                           (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,    \
-                           ar, (const bf16_t*)hc, neg_slope, dp, (bf16_t*)u, (bf16_t*)u_lo,    \
-                           lse, uc, qc);                                                       \
-      }                                                                                        \
-    } else {                                                                                   \
-      if constexpr (h * f * 4 <= 1024) {                                                       \
-        auto kern = uc != nullptr                                                              \
-            ? edge_attn_fwd_rs_kernel<h, f, float, fwd_epl<h, f, float>(), true>               \
-            : edge_attn_fwd_rs_kernel<h, f, float, fwd_epl<h, f, float>(), false>;             \
-        hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, g->rowptr, g->col, g->rowflag,         \
-                           (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges, el,    \
-                           ar, (const float*)hc, neg_slope, dp, (float*)u, (float*)nullptr,    \
-                           lse, uc, qc);                                                       \
-      }                                                                                        \
-    }                                                                                          \
-  }
-  MSHA_FOR_EACH_SHAPE(XR)
-#undef XR
+  const bool short_rows = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows;
+  if (!launch_fwd_gl(g, heads, feat, dtype, el, nullptr, ar, hc, neg_slope, dp, u, u_lo, lse,
+                     nullptr, uc, qc, short_rows, fwd_grid(g), s))
+    return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_fwd_rs: shape not compiled");
   return check_launch("edge_attention_fwd_rs");
 }
 

@@ -965,17 +965,29 @@ struct HeadLayout {
   size_t part_u, part_b, wflag, dz, rflag, red, total;
 };
 
+// rows per wave and waves of the backward row pass (msha_head_bwd launches exactly these)
+static int64_t head_bwd_rpw(int64_t N) {
+  int64_t rpw = (N + kHeadBwdWaves - 1) / kHeadBwdWaves;
+  return rpw < kHeadRowsPerWave ? kHeadRowsPerWave : rpw;
+}
+static int head_bwd_waves(int64_t N) {
+  const int64_t rpw = head_bwd_rpw(N);
+  return (int)((N + rpw - 1) / rpw);
+}
+
 static HeadLayout head_layout(int64_t N, int M, int H, int F) {
   const int HF = H * F, KX = H * M;
   HeadLayout L{};
   size_t off = 0;
   L.part_u = off;
   const size_t fwd = al256((size_t)bn_stats_blocks(N) * HF * sizeof(Wf));
-  // backward regions (the forward's partials are dead by then: they alias)
+  // backward regions (the forward's partials are dead by then: they alias); one partial
+  // slab per wave the row pass launches (<= kHeadBwdWaves)
+  const size_t nw = (size_t)head_bwd_waves(N);
   L.part_b = 0;
-  off = al256((size_t)kHeadBwdWaves * head_pt(HF, KX, M) * sizeof(float));
+  off = al256(nw * head_pt(HF, KX, M) * sizeof(float));
   L.wflag = off;
-  off += al256(kHeadBwdWaves * sizeof(int));
+  off += al256(nw * sizeof(int));
   L.dz = off;
   off += al256((size_t)N * HF * sizeof(float));
   L.rflag = off;
@@ -1141,9 +1153,8 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
   w.dz = (float*)(base + L.dz);
   w.rflag = (uint8_t*)(base + L.rflag);
   w.red = (float*)(base + L.red);
-  int64_t rpw = (a.N + kHeadBwdWaves - 1) / kHeadBwdWaves;
-  if (rpw < kHeadRowsPerWave) rpw = kHeadRowsPerWave;
-  const int nw = (int)((a.N + rpw - 1) / rpw);
+  const int64_t rpw = head_bwd_rpw(a.N);
+  const int nw = head_bwd_waves(a.N);
   const bool bf = dtype == MSHA_DTYPE_BF16;
   const size_t lds = bwd_lds(a.HF, a.KX, a.M);
   const int qm = (a.M + 63) / 64;

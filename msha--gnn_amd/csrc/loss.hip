@@ -7,6 +7,9 @@
 //   forward   loss = -(1/B) sum_b logp[rows[b], cols[b]]   (b ascending, fp32)
 //   backward  dlogp = 0 except dlogp[rows[b], cols[b]] += -g / B   (b ascending; repeated
 //             (row, col) pairs accumulate as index backward does)
+// An entry outside the (N, M) table (torch raises on such an index) is never read or
+// written: the forward returns NaN instead, as it does for an empty batch (torch's mean
+// over zero elements), and the backward skips it.
 // The backward zero-fills row ranges per block; each block then adds the batch entries
 // that fall in its own rows in batch order (one lane), so the result is deterministic
 // and no two blocks touch the same row.
@@ -19,20 +22,23 @@ constexpr int kLossRowsPerBlock = 64;
 
 template <typename T>
 __global__ void __launch_bounds__(kLossThreads) nll_rows_fwd_kernel(
-    int64_t B, const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
-    const T* __restrict__ logp, int64_t ld, float* __restrict__ loss) {
+    int64_t N, int64_t M, int64_t B, const int64_t* __restrict__ rows,
+    const int64_t* __restrict__ cols, const T* __restrict__ logp, int64_t ld,
+    float* __restrict__ loss) {
   __shared__ float part[kLossThreads];
   float s = 0.f;
   // thread t adds entries t, t + 256, ... in order; the partials then add in a fixed tree
-  for (int64_t b = threadIdx.x; b < B; b += kLossThreads)
-    s += to_f32(logp[rows[b] * ld + cols[b]]);
+  for (int64_t b = threadIdx.x; b < B; b += kLossThreads) {
+    const int64_t r = rows[b], c = cols[b];
+    s += (r >= 0 && r < N && c >= 0 && c < M) ? to_f32(logp[r * ld + c]) : __builtin_nanf("");
+  }
   part[threadIdx.x] = s;
   __syncthreads();
   for (int o = kLossThreads / 2; o >= 1; o >>= 1) {
     if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) loss[0] = B > 0 ? -part[0] / (float)B : 0.f;
+  if (threadIdx.x == 0) loss[0] = B > 0 ? -part[0] / (float)B : __builtin_nanf("");
 }
 
 template <typename T>
@@ -50,8 +56,8 @@ __global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
   if (threadIdx.x == 0 && B > 0) {
     const float v = -gloss[0] / (float)B;
     for (int64_t b = 0; b < B; ++b) {
-      const int64_t r = rows[b];
-      if (r < r0 || r >= r1) continue;
+      const int64_t r = rows[b], c = cols[b];
+      if (r < r0 || r >= r1 || c < 0 || c >= M) continue;
       T* p = dlogp + r * ld + cols[b];
       *p = from_f32<T>(to_f32(*p) + v);
     }
@@ -62,19 +68,20 @@ __global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
 
 using namespace msha;
 
-extern "C" int msha_nll_rows_fwd(int64_t B, const int64_t* rows, const int64_t* cols,
-                                 int32_t dtype, const void* logp, int64_t ld, float* loss,
-                                 msha_stream_t stream) {
+extern "C" int msha_nll_rows_fwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                                 const int64_t* cols, int32_t dtype, const void* logp, int64_t ld,
+                                 float* loss, msha_stream_t stream) {
   MSHA_ARG_CHECK(B >= 0 && loss != nullptr && (B == 0 || (rows && cols && logp)),
                  "nll_rows_fwd: null pointer");
+  MSHA_ARG_CHECK(N > 0 && M > 0 && ld >= M, "nll_rows_fwd: bad sizes");
   MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "nll_rows_fwd: bad dtype");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MSHA_DTYPE_BF16)
-    hipLaunchKernelGGL(nll_rows_fwd_kernel<bf16_t>, dim3(1), dim3(kLossThreads), 0, s, B, rows,
-                       cols, (const bf16_t*)logp, ld, loss);
+    hipLaunchKernelGGL(nll_rows_fwd_kernel<bf16_t>, dim3(1), dim3(kLossThreads), 0, s, N, M, B,
+                       rows, cols, (const bf16_t*)logp, ld, loss);
   else
-    hipLaunchKernelGGL(nll_rows_fwd_kernel<float>, dim3(1), dim3(kLossThreads), 0, s, B, rows,
-                       cols, (const float*)logp, ld, loss);
+    hipLaunchKernelGGL(nll_rows_fwd_kernel<float>, dim3(1), dim3(kLossThreads), 0, s, N, M, B,
+                       rows, cols, (const float*)logp, ld, loss);
   return check_launch("nll_rows_fwd");
 }
 

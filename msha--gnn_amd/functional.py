@@ -1123,11 +1123,22 @@ def model_head(graph: Graph, u, v, bns, out_W, out_a, p: float = 0.0, training: 
     _lib.require_cuda(u, v, out_W)
     N, H, F = u.shape
     bn0 = bns[0][0]
+    params = ([b[0].weight for b in bns] + [b[0].bias for b in bns] + [b[1].weight for b in bns]
+              + [b[1].bias for b in bns] + [out_a])
+    if not training:
+        # msha_head_bwd differentiates the training-mode BatchNorm (batch statistics);
+        # eval normalises with the running statistics, whose backward it does not have
+        if torch.is_grad_enabled() and any(t is not None and t.requires_grad
+                                           for t in (u, v, out_W, *params)):
+            raise NotImplementedError(
+                "model_head: gradients through eval-mode BatchNorm (running statistics) are "
+                "not implemented; call it under torch.no_grad() or use the unfused tail")
+        if any(bn.running_mean is None or bn.running_var is None for pair in bns for bn in pair):
+            raise ValueError("model_head: eval needs running statistics "
+                             "(BatchNorm1d(track_running_stats=True))")
     px = pa = float(p) if training else 0.0
     sx = new_seed() if px > 0 else 0
     sa = new_seed() if pa > 0 else 0
-    params = ([b[0].weight for b in bns] + [b[0].bias for b in bns] + [b[1].weight for b in bns]
-              + [b[1].bias for b in bns] + [out_a])
     return _ModelHead.apply(u, v, out_W, graph, bns, bool(training), float(bn0.eps),
                             float(bn0.momentum), float(slope), px, sx, pa, sa, *params)
 
@@ -1320,8 +1331,9 @@ class _NllRows(torch.autograd.Function):
         rows = rows.to(torch.int64).contiguous()
         cols = cols.to(torch.int64).contiguous()
         loss = torch.empty((), device=logp.device, dtype=torch.float32)
-        _lib.call("msha_nll_rows_fwd", rows.numel(), rows.data_ptr(), cols.data_ptr(), _code(dt),
-                  logp.data_ptr(), logp.stride(0), loss.data_ptr(), _stream(logp))
+        _lib.call("msha_nll_rows_fwd", logp.shape[0], logp.shape[1], rows.numel(),
+                  rows.data_ptr(), cols.data_ptr(), _code(dt), logp.data_ptr(), logp.stride(0),
+                  loss.data_ptr(), _stream(logp))
         ctx.save_for_backward(rows, cols)
         ctx.shape, ctx.dt = tuple(logp.shape), dt
         return loss

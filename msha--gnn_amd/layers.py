@@ -179,6 +179,10 @@ def _head_fusable(heads, graph: Graph, training) -> bool:
     if any(bn.momentum is None or bn.eps != bns[0].eps or bn.momentum != bns[0].momentum
            or bn.training != training or not bn.affine for bn in bns):
         return False
+    # eval without running statistics (track_running_stats=False): torch normalises with
+    # the batch statistics there, which the head's eval path does not do
+    if not training and any(bn.running_mean is None or bn.running_var is None for bn in bns):
+        return False
     return MF.head_supported(graph, len(heads), heads[0].out_features)
 
 

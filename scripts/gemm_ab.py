@@ -69,7 +69,7 @@ def cmp(a, b):
 
 
 def cmp1(a, b):
-    x, y = torch.load(a), torch.load(b)
+    x, y = torch.load(a, weights_only=True, map_location="cpu"), torch.load(b, weights_only=True, map_location="cpu")
     for k in x:
         xa = x[k][0] if isinstance(x[k], tuple) else x[k]
         ya = y[k][0] if isinstance(y[k], tuple) else y[k]

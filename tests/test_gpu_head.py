@@ -160,6 +160,35 @@ def test_head_eval_running_stats(cuda, msha):
     tol_close(out.detach().cpu().numpy(), ref.numpy(), 1e-5, 1e-5)
 
 
+def test_head_eval_with_autograd_refuses(cuda, msha):
+    """The head's backward is the training-mode BatchNorm's: the public model_head
+    refuses eval-mode gradients instead of returning wrong ones (the models route eval
+    with autograd to the unfused tail), and eval without running statistics."""
+    from msha_gnn_amd import functional as MF
+
+    g, _ = _graph(300, 32, 3, cuda)
+    bns = _bns(2, 64, cuda, 4)
+    for pair in bns:
+        for bn in pair:
+            bn.eval()
+    u = torch.randn(300, 2, 64, device=cuda, requires_grad=True)
+    v = torch.randn(32, 2, 64, device=cuda)
+    W = torch.randn(64, 32, device=cuda)
+    a = torch.zeros(64, 1, device=cuda)
+    with pytest.raises(NotImplementedError):
+        MF.model_head(g, u, v, bns, W, a, training=False)
+    with torch.no_grad():
+        out = MF.model_head(g, u, v, bns, W, a, training=False)
+    assert torch.isfinite(out).all()
+    nb = _bns(2, 64, cuda, 4)
+    for pair in nb:
+        for bn in pair:
+            bn.eval()
+            bn.running_mean = bn.running_var = None
+    with torch.no_grad(), pytest.raises(ValueError):
+        MF.model_head(g, u, v, nb, W, a, training=False)
+
+
 def test_head_bf16_vs_fp64(cuda, msha):
     """bf16 tables (u, v, out, du, dv): 1e-2 against fp64 on the same rounded inputs."""
     out, ref, gr, _, (u, v, W, _) = _run(cuda, 2000, 32, 2, 64, 0.0, True, torch.bfloat16,
@@ -339,3 +368,14 @@ def test_nll_loss_rows_matches_torch(cuda, msha, dtype):
     (3.0 * ref).backward()
     assert a.grad.dtype == dtype
     assert torch.equal(a.grad, b.grad)
+    # out-of-range entries are neither read nor written: NaN loss (torch raises), the
+    # backward leaves the table's gradient zero there; an empty batch is NaN (torch's mean)
+    bad_r, bad_c = rows.clone(), cols.clone()
+    bad_r[0], bad_c[1] = N + 7, M
+    c = logp.detach().clone().requires_grad_(True)
+    lb = MF.nll_loss_rows(c, bad_r, bad_c)
+    assert torch.isnan(lb).item()
+    lb.backward()
+    assert torch.isfinite(c.grad.float()).all()
+    e = torch.empty(0, dtype=torch.int64, device=cuda)
+    assert torch.isnan(MF.nll_loss_rows(logp, e, e)).item()

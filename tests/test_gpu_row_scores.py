@@ -69,7 +69,12 @@ def test_row_scores_vs_oracle(cuda, msha, case, p, dtype):
     ref = O.edge_aggregate_fwd(rowptr, col, el.astype(np.float64), er64, hc_s, keep=keep, p=p,
                                rowflag=empty)
     bw = O.edge_aggregate_bwd(rowptr, col, ref, hc_s, dU_s, keep=keep, p=p)
-    runs = {rt: _rs_grads(MF, graph, el, hc, ar, dU, p, seed, cuda, dtype, rt)
+    er32 = er64.astype(np.float32)
+    sup = _supported(MF, graph, H, F, dtype)
+    # where the row-score kernels apply, the er handed over is never read (a wrong one
+    # proves it); elsewhere (QPL > 1 shapes) the op falls back to reading er
+    hint = None if sup else er32
+    runs = {rt: _rs_grads(MF, graph, el, hc, ar, dU, p, seed, cuda, dtype, rt, er_hint=hint)
             for rt in (False, True)}
     for rt, got in runs.items():
         tol_close(got[0].float().cpu().numpy(), ref["u"], tol, tol)
@@ -80,10 +85,9 @@ def test_row_scores_vs_oracle(cuda, msha, case, p, dtype):
     for a, b, name in zip(runs[True], runs[False], ("u", "d_el", "d_er", "d_hc")):
         if name != "d_el":
             assert torch.equal(a, b), name
-    if _supported(MF, graph, H, F, dtype):
+    if sup:
         # the er-gather kernels fed the recomputed er agree to rounding (same scores up
         # to the dot's summation order)
-        er32 = np.einsum("mhf,hf->mh", hc_s, ar.astype(np.float64)).astype(np.float32)
         MF.ROW_SCORES = False
         try:
             base = _rs_grads(MF, graph, el, hc, ar, dU, p, seed, cuda, dtype, False, er_hint=er32)
