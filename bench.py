@@ -144,19 +144,22 @@ def pmc_lookup(patterns, glob_pat):
     return None, None
 
 
-def fwd_kernel_pattern(H, F, bf16, row_scores):
-    """rocprofv3 name of the forward edge kernel (demangled or mangled)."""
-    if row_scores:
-        return (rf"edge_attn_fwd_rs_kernelILi{H}ELi{F}EDF16b" if bf16 else
-                rf"edge_attn_fwd_rs_kernel<{H}, {F}, float")
+def fwd_kernel_pattern(H, F, bf16, variant="bat"):
+    """rocprofv3 name of the forward edge kernel (fp32 demangled, bf16 left mangled):
+    variant 'rs' (gather layout, scores from the row), 'gl' (gather layout, er table:
+    short rows) or 'bat' (score layout, er table)."""
+    if variant in ("rs", "gl"):
+        rs = "true" if variant == "rs" else "false"
+        return (rf"edge_attn_fwd_gl_kernelILi{H}ELi{F}EDF16bLi\d+ELb[01]ELb{int(variant == 'rs')}"
+                if bf16 else rf"edge_attn_fwd_gl_kernel<{H}, {F}, float, \d+, (true|false), {rs}")
     return (rf"edge_attn_fwd(?:_bat)?_kernelILi{H}ELi{F}EDF16b" if bf16 else
             rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?(, (true|false))?>")
 
 
-def pmc_traffic(H, F, bf16=False, workload="syn100k", row_scores=False):
+def pmc_traffic(H, F, bf16=False, workload="syn100k", variant="bat"):
     """HBM bytes per launch of the forward edge kernel from the newest committed PMC
     summary of this workload (None if absent)."""
-    return pmc_lookup([fwd_kernel_pattern(H, F, bf16, row_scores)], f"*{workload}_v*")
+    return pmc_lookup([fwd_kernel_pattern(H, F, bf16, variant)], f"*{workload}_v*")
 
 
 def bwd_rows_bytes(n, m, e, H, F, s=4):
@@ -247,8 +250,10 @@ class Layer:
                              and lib.msha_edge_attention_rowterms_preferred(self.graph.desc, H,
                                                                             F, code))
         self.row_scores = bool(not self.v_branch and MF.ROW_SCORES and MF.FUSED_BWD
-                               and lib.msha_edge_attention_row_scores_supported(self.graph.desc,
+                               and lib.msha_edge_attention_row_scores_preferred(self.graph.desc,
                                                                                 H, F, code))
+        short = self.graph.n_edges <= 8 * n and os.environ.get("MSHA_FWD_GL", "1") != "0"
+        self.fwd_variant = "rs" if self.row_scores else ("gl" if short else "bat")
 
     def step(self):
         for p in (self.W, self.al, self.ar):
@@ -358,7 +363,7 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
     # rocprofv3 leaves bf16 instantiations mangled (DF16b), fp32 ones demangled
     tmpl = (lambda k: rf"{k}ILi{H}ELi{F}EDF16b") if bf else (lambda k: rf"{k}<{H}, {F}, float")
     pats = {
-        "msha_edge_attention_fwd": [fwd_kernel_pattern(H, F, bf, rs)],
+        "msha_edge_attention_fwd": [fwd_kernel_pattern(H, F, bf, lay.fwd_variant)],
         "msha_edge_attention_bwd_fused": [tmpl("bwd_row_stats_kernel"),
                                           tmpl("bwd_cols(_eh)?_kernel")]
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
@@ -403,7 +408,7 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
     dt = dtg if dtg is not None else dte
     fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
     ach = fb / (k_ms * 1e-3) / 1e9
-    tr, src = (pmc_traffic(H, F, s == 2, workload, lay.row_scores) if workload
+    tr, src = (pmc_traffic(H, F, s == 2, workload, lay.fwd_variant) if workload
                else (None, None))
     res = {"workload": label, "value": world * e * steps / dt, "unit": "edges/s",
            "ms_per_step": dt / steps * 1e3, "ms_per_step_eager": dte / steps * 1e3,
@@ -411,6 +416,7 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
            "config": {"nodes": n, "cols": m, "edges": e, "in_features": fin, "heads": H,
                       "feat": F},
            "roofline": {"kernel": "msha_edge_attention_fwd" + ("_rs" if lay.row_scores else ""),
+                        "variant": lay.fwd_variant,
                         "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "traffic": tr,
                         "traffic_unit": "bytes per launch (rocprofv3 PMC)",

@@ -101,6 +101,7 @@ SIGNATURES = {
     "msha_edge_attention_bwd_fused_ex": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,
                                                    F32, U64, U64, P, P, P, P, P, P, P, SZ, P]),
     "msha_edge_attention_row_scores_supported": (C.c_int, [GP, I32, I32, I32]),
+    "msha_edge_attention_row_scores_preferred": (C.c_int, [GP, I32, I32, I32]),
     "msha_edge_attention_fwd_rs": (C.c_int, [GP, I32, I32, I32, P, P, P, F32, F32, U64, U64, P,
                                              P, P, P, P, P]),
     "msha_edge_attention_bwd_fused_rs": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,

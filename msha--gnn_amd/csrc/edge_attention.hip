@@ -1090,9 +1090,7 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
       hcv[k] = pk_load(hc + (int64_t)jc * G::D + h_s * F + G::V * k);
       acc[k] = pk_zero<T>();
     }
-    // er_j: from hc_j in the row-score forward's order when a_r is given
-    const float erh = ar != nullptr ? head_score<NV>(hcv, ar + h_s * F)
-                                    : er[(int64_t)jc * H + h_s];
+    const float er_tab = ar != nullptr ? 0.f : er[(int64_t)jc * H + h_s];
     float xacc = 0.f;
     // one trip = COLS_NG slot groups: every group's loads leave before the first
     // group's compute and de store (the compiler may not hoist a buffer load above a
@@ -1121,6 +1119,21 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
       for (int g = 0; g < NG; ++g) {
         const int32_t a = cs + (NG + g) * G::CE + e_s;
         ii[g] = buf_i32(r_row, a < s1 ? (uint32_t)a * 4u : kOOB);
+      }
+      // er_j: from hc_j in the row-score forward's order when a_r is given, recomputed
+      // per trip AFTER the trip's loads are in flight (computed before the loop, the wait
+      // for hc_j / a_r put one memory latency in front of every chunk's loads); the empty
+      // asm keeps it from being hoisted back out of the loop
+      float erh = er_tab;
+      if (ar != nullptr) {
+        Pk<T> hv[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          hv[k] = hcv[k];
+#pragma unroll
+          for (int v = 0; v < G::V; ++v) asm volatile("" : "+v"(hv[k].v[v]));
+        }
+        erh = head_score<NV>(hv, ar + h_s * F);
       }
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
@@ -1634,8 +1647,24 @@ extern "C" int msha_edge_attention_bwd_fused_ex(
 extern "C" int msha_edge_attention_row_scores_supported(const msha_graph* g, int32_t heads,
                                                         int32_t feat, int32_t dtype) {
   if (g == nullptr || !shape_supported(heads, feat) || !dtype_ok(dtype, feat)) return 0;
-  if (env_int("MSHA_ROW_SCORES", 1) == 0) return 0;  // A/B: the er-gather forward
   return fwd_bat_ok(g, heads, feat, dtype) ? 1 : 0;
+}
+
+// MSHA_ROW_SCORES: 1 = whenever supported, 0 = never (A/B).  Default: fp32 tables always
+// (C4 forward 174 -> 161 us, syn2m 3900 -> 3652 us); bf16 tables once the er table
+// outgrows an XCD's L2 (RS_BF16_MIN_BYTES): the bf16 forward is issue-bound and at C4
+// (3.2 MB er, L2-resident) the V extra fmas per gathered piece cost more (98 -> 111 us)
+// than the gather they replace.
+#ifndef RS_BF16_MIN_BYTES
+#define RS_BF16_MIN_BYTES (16ll << 20)
+#endif
+extern "C" int msha_edge_attention_row_scores_preferred(const msha_graph* g, int32_t heads,
+                                                        int32_t feat, int32_t dtype) {
+  if (!msha_edge_attention_row_scores_supported(g, heads, feat, dtype)) return 0;
+  const int knob = env_int("MSHA_ROW_SCORES", -1);
+  if (knob >= 0) return knob != 0;
+  if (dtype == MSHA_DTYPE_F32) return 1;
+  return g->n_cols * 4 * (int64_t)heads >= RS_BF16_MIN_BYTES ? 1 : 0;
 }
 
 extern "C" int msha_edge_attention_fwd_rs(const msha_graph* g, int32_t heads, int32_t feat,

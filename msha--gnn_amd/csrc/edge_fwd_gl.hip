@@ -60,12 +60,27 @@ edge_attn_fwd_gl_kernel(
       arq.v[v] = a4.x; arq.v[v + 1] = a4.y; arq.v[v + 2] = a4.z; arq.v[v + 3] = a4.w;
     }
   }
-  // columns of a chunk in the gather layout (slot gi * EPI + g_e; past the row: 0)
-  auto load_cols = [&](int32_t cs, int32_t end, int32_t (&j)[NGI]) {
+  // columns of a chunk.  Long chunks (whole score-layout chunks, CEL = SL * 64 / H): SL
+  // words per lane in the score layout (lane e_s * H + h_s holds edge t * CE + e_s), the
+  // gather lanes fetch theirs by ds_bpermute -- SL loads instead of NGI; short chunks:
+  // one word per gather instruction in the gather layout (slot gi * EPI + g_e).  Past
+  // the row: 0.
+  constexpr bool SLC = CEL % G::CE == 0;
+  constexpr int NJ = SLC ? CEL / G::CE : NGI;
+  const int e_s = lane / H;
+  auto load_cols = [&](int32_t cs, int32_t end, int32_t (&j)[NJ]) {
 #pragma unroll
-    for (int gi = 0; gi < NGI; ++gi) {
-      const int32_t e = cs + gi * G::EPI + g_e;
-      j[gi] = buf_i32(r_col, e < end ? (uint32_t)e * 4u : kOOB);
+    for (int k = 0; k < NJ; ++k) {
+      const int32_t e = SLC ? cs + k * G::CE + e_s : cs + k * G::EPI + g_e;
+      j[k] = buf_i32(r_col, e < end ? (uint32_t)e * 4u : kOOB);
+    }
+  };
+  auto col_of = [&](const int32_t (&j)[NJ], int gi) -> int32_t {
+    if constexpr (SLC) {
+      const int g = gi * G::EPI;
+      return __shfl(j[g / G::CE], (g % G::CE + g_e) * H);
+    } else {
+      return j[gi];
     }
   };
 
@@ -75,7 +90,7 @@ edge_attn_fwd_gl_kernel(
   int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
   bool virt = rowflag != nullptr && rowflag[row] != 0;
   float elq = el[(int64_t)row * H + hq];
-  int32_t jc[NGI], jn[NGI];
+  int32_t jc[NJ], jn[NJ];
   load_cols(start, end, jc);
   load_cols(start + CEL, end, jn);
   while (true) {
@@ -91,12 +106,13 @@ edge_attn_fwd_gl_kernel(
 #pragma unroll
       for (int gi = 0; gi < NGI; ++gi) {
         const bool valid = gi * G::EPI + g_e < nvalid;
-        raw[gi] = buf_b128(r_hc, valid ? (uint32_t)jc[gi] * (uint32_t)(G::D * sizeof(T)) + q_off
+        const int32_t j = col_of(jc, gi);
+        raw[gi] = buf_b128(r_hc, valid ? (uint32_t)j * (uint32_t)(G::D * sizeof(T)) + q_off
                                        : kOOB);
-        if (!RS) erq[gi] = buf_f32(r_er, valid ? (uint32_t)jc[gi] * (4u * H) + 4u * hq : kOOB);
+        if (!RS) erq[gi] = buf_f32(r_er, valid ? (uint32_t)j * (4u * H) + 4u * hq : kOOB);
       }
       // columns two chunks ahead
-      int32_t jnn[NGI];
+      int32_t jnn[NJ];
       load_cols(cs + 2 * CEL, end, jnn);
       // (2) dropout keep bits of the chunk, while the gathers fly: ballot b, lane l holds
       // edge (b * 64 + l) / H, head (b * 64 + l) % H of the chunk
@@ -167,9 +183,9 @@ edge_attn_fwd_gl_kernel(
         if (RT) accc = pk_fma(w[gi] * (pre[gi] > 0.f ? 1.f : slope), xr, accc);
       }
 #pragma unroll
-      for (int gi = 0; gi < NGI; ++gi) {
-        jc[gi] = jn[gi];
-        jn[gi] = jnn[gi];
+      for (int k = 0; k < NJ; ++k) {
+        jc[k] = jn[k];
+        jn[k] = jnn[k];
       }
     }
     // the next row's bounds, flag, el and first columns before this row's epilogue
@@ -180,7 +196,7 @@ edge_attn_fwd_gl_kernel(
     const int32_t nend = __builtin_amdgcn_readfirstlane(rowptr[nrow + 1]);
     const bool nvirt = rowflag != nullptr && rowflag[nrow] != 0;
     const float nelq = el[(int64_t)nrow * H + hq];
-    int32_t njc[NGI], njn[NGI];
+    int32_t njc[NJ], njn[NJ];
     load_cols(nstart, nend, njc);
     load_cols(nstart + CEL, nend, njn);
     if (G::EPI > 1) {
@@ -243,9 +259,9 @@ edge_attn_fwd_gl_kernel(
     virt = nvirt;
     elq = nelq;
 #pragma unroll
-    for (int gi = 0; gi < NGI; ++gi) {
-      jc[gi] = njc[gi];
-      jn[gi] = njn[gi];
+    for (int k = 0; k < NJ; ++k) {
+      jc[k] = njc[k];
+      jn[k] = njn[k];
     }
   }
 }

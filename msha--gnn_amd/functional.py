@@ -110,7 +110,7 @@ class _EdgeAttention(torch.autograd.Function):
         # recomputed from the row the kernel gathers anyway, in the forward and in the
         # fused backward's column pass (the same bits in both); u-only path
         rs = (ar is not None and hs is None and ROW_SCORES and FUSED_BWD
-              and _lib.load().msha_edge_attention_row_scores_supported(g, H, F, _code(dt)))
+              and _lib.load().msha_edge_attention_row_scores_preferred(g, H, F, _code(dt)))
         ar = ar.detach().to(torch.float32).contiguous().view(H, F) if rs else None
         u = torch.empty(n, H, F, device=dev, dtype=dt)
         # bf16 tables under autograd: keep the rounding residual of u for the backward's

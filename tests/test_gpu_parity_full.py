@@ -184,6 +184,7 @@ def test_c4_row_scores_every_row(cuda, c4, dt):
     got = {}
     for rt in ("0", "1"):
         os.environ["MSHA_ROWTERMS"] = rt
+        os.environ["MSHA_ROW_SCORES"] = "1"  # bf16 at C4 defaults to the er gather
         try:
             el_l = el.detach().clone().requires_grad_(True)
             er_l = torch.zeros_like(er).requires_grad_(True)  # not read on this path
@@ -192,6 +193,7 @@ def test_c4_row_scores_every_row(cuda, c4, dt):
             u.backward(dU)
         finally:
             os.environ.pop("MSHA_ROWTERMS")
+            os.environ.pop("MSHA_ROW_SCORES")
         assert torch.equal(u.detach(), u0)  # the op is exactly that launch
         got[rt] = (el_l.grad, er_l.grad, hc_l.grad)
         tol_close(_np64(el_l.grad), d_el_ref, tol, tol)
@@ -252,7 +254,7 @@ def test_bip1m_ourslayer3_core_every_row(cuda, bip1m, dt):
     rowptr, col, n, m, graph = bip1m
     H, Fd = 2, 64
     tol = F32_TOL if dt == torch.float32 else BF16_TOL
-    assert graph._plan["n_multi"] >= m and graph._plan["max_col"] > 70_000
+    assert graph._plan["n_multi"] >= m // 2 and graph._plan["max_col"] > 70_000
     g = torch.Generator().manual_seed(12)
     el = torch.randn(n, H, generator=g)
     er = torch.randn(m, H, generator=g)

@@ -25,6 +25,7 @@ EMB_RTOL = 1e-5
 
 def _rs_grads(MF, graph, el, hc, ar, dU, p, seed, dev, dtype, rowterms, er_hint=None):
     os.environ["MSHA_ROWTERMS"] = "1" if rowterms else "0"
+    os.environ["MSHA_ROW_SCORES"] = "1"  # wherever supported (the default skips small bf16)
     try:
         tel = t(el, dev).requires_grad_(True)
         H, F = ar.shape
@@ -38,6 +39,7 @@ def _rs_grads(MF, graph, el, hc, ar, dU, p, seed, dev, dtype, rowterms, er_hint=
         return u.detach(), tel.grad, ter.grad, thc.grad
     finally:
         os.environ.pop("MSHA_ROWTERMS", None)
+        os.environ.pop("MSHA_ROW_SCORES", None)
 
 
 def _supported(MF, graph, H, F, dtype):
