@@ -52,6 +52,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F32_MFMA_TFLOPS = 157.3  # exact-fp32 matrix peak (v_mfma_f32_*x*_f32), MI355X_MICROARCH.md
 BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 FUSED_ADAM = os.environ.get("MSHA_FUSED_ADAM", "1") != "0"
+# the train-step legs' optimizer: "msha" = msha_gnn_amd.optim.Adam (one launch, Sfeatures
+# updated inside its feature-dropout backward), "torch" = torch.optim.Adam (A/B)
+ADAM = os.environ.get("MSHA_ADAM", "msha")
 
 
 def synth_graph(n, e, seed=0):
@@ -634,16 +637,24 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
 
     e = graph_for(adj).n_edges
     res = dict(model=model_kind, year=year, dtype=str(dtype).replace("torch.", ""), nodes=n,
-               recipients=m, edges=e,
+               recipients=m, edges=e, optimizer=f"{ADAM} Adam",
                flows="shipped" if year == "2015" else "synthetic (2015 degree law)")
     for mode in ("eager", "hip_graph"):
         torch.manual_seed(0)
         model = cls(128, 64, m, 2, 0.5, gdp, n, m).to(dev, dtype)
         graphed = mode == "hip_graph"
-        # train.py's Adam (lr 1e-3, wd 5e-4); fused: one multi-tensor kernel per step
-        # instead of ~50 foreach / per-tensor launches (same update rule)
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4,
-                               capturable=graphed, fused=FUSED_ADAM)
+        # train.py's Adam (lr 1e-3, wd 5e-4): msha_adam_step, one launch for every
+        # parameter, with Sfeatures' update fused into its feature-dropout backward (its
+        # 5M-float gradient is never written); MSHA_ADAM=torch: torch's fused multi-tensor
+        # Adam (same update rule)
+        if ADAM == "msha":
+            from msha_gnn_amd.optim import Adam
+
+            opt = Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
+            opt.fuse_dropout_grad(model.Sfeatures)
+        else:
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4,
+                                   capturable=graphed, fused=FUSED_ADAM)
         model.train()
         si_s = torch.empty(64, dtype=torch.int64, device=dev)
         ri_s = torch.empty(64, dtype=torch.int64, device=dev)

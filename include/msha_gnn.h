@@ -331,6 +331,14 @@ MSHA_API int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const flo
  * Replaces Ablation.py:262-267's projection + the (N, M, 2F) score tensor: the
  * score of edge (i, j) is lrelu(el_i + er_j).  al/el and ar/er are optional pairs;
  * feat must be 4, 8, 16, 32, 64 or 128 when a score vector is given. */
+/* 1 when msha_project_scores(_bf16) at this shape (16-byte aligned X, W, h) computes its
+ * el / er from the STORED h in the order the row-score edge kernels recompute
+ * er_j = h_j . a_r from a gathered row (per 16-byte piece: last element first, fma
+ * downwards; then the xor tree over the head's pieces): er is then bit-identical to that
+ * recomputation and msha_edge_attention_bwd_fused_ex may read it in place of
+ * msha_edge_attention_bwd_fused_rs (ABI 9). */
+MSHA_API int msha_project_scores_row_order(int64_t M, int64_t K, int32_t heads, int32_t feat,
+                                           int32_t dtype);
 MSHA_API int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t feat,
                                  const float* X, const float* W, const float* al,
                                  const float* ar, float* h, float* el, float* er,
@@ -593,6 +601,37 @@ MSHA_API int msha_dropout_keep_mask4(uint64_t seed, uint64_t offset, int64_t n, 
 MSHA_API int msha_dropout_keep_mask_word(uint64_t seed, uint64_t offset, int64_t n, float p,
                                          int32_t word, uint8_t* keep, msha_stream_t stream);
 
+
+/* ---- Optimizer step (train.py:207,232: optim.Adam(lr, weight_decay) ... step()) ------ */
+/* torch.optim.Adam's update (L2 weight decay, no amsgrad / maximize) for up to
+ * MSHA_MAX_ADAM tensors in ONE launch, per element (fp32 arithmetic, bias corrections in
+ * double as torch computes them from its step count):
+ *   g  = grad (* keep * 1/(1-p) when drop_p > 0) + weight_decay * param
+ *   m  = m + (1 - beta1) (g - m);  v = beta2 v + (1 - beta2) g^2
+ *   t  = *step + 1;  param -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
+ * and *step += 1 once every block of the launch has read it (capturable: the step lives
+ * on the device).  param, grad, exp_avg, exp_avg_sq share `dtype` (bf16 state for bf16
+ * parameters, as torch keeps it), contiguous, n elements.  drop_p > 0 fuses a dropout
+ * backward into the gradient read: grad is then the dropout's OUTPUT gradient and keep is
+ * msha_segments' flat mask (element e: word e % 4 of the Philox4x32-10 block (drop_seed;
+ * counter {e / 4, drop_offset})), so the parameter's own gradient never exists (the
+ * feature dropout of Sfeatures, Ablation.py:296, Ours.py:161).  ws: 16 bytes of device
+ * memory, zero before the first call (the launch's completion counter; left zero). */
+#define MSHA_MAX_ADAM 64
+typedef struct msha_adam_tensor {
+  void* param;
+  const void* grad;
+  void* exp_avg;
+  void* exp_avg_sq;
+  float* step;
+  int64_t n;
+  int32_t dtype;
+  float drop_p;
+  uint64_t drop_seed, drop_offset;
+} msha_adam_tensor;
+MSHA_API int msha_adam_step(int32_t n, const msha_adam_tensor* tensors, double lr,
+                            double beta1, double beta2, double eps, double weight_decay,
+                            void* ws, msha_stream_t stream);
 
 /* ---- Projection of a small node table in one workgroup (the recipient side: R15 has 32
  * recipients; Ablation.py:262, :266-267): h = X @ W (M x N, N = heads*feat) with optional

@@ -69,6 +69,17 @@ class MshaHeadParams(C.Structure):
 HPP = C.POINTER(MshaHeadParams)
 
 MAX_SEGMENTS = 32
+MAX_ADAM = 64
+
+
+class MshaAdamTensor(C.Structure):
+    """Mirror of ``struct msha_adam_tensor`` (include/msha_gnn.h)."""
+
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p),
+                ("exp_avg_sq", C.c_void_p), ("step", C.c_void_p), ("n", C.c_int64),
+                ("dtype", C.c_int32), ("drop_p", C.c_float), ("drop_seed", C.c_uint64),
+                ("drop_offset", C.c_uint64)]
+
 
 
 class MshaSegment(C.Structure):
@@ -119,6 +130,7 @@ SIGNATURES = {
     "msha_gemm_f32": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, F32, I32, P, SZ,
                                 P]),
     "msha_project_scores": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
+    "msha_project_scores_row_order": (C.c_int, [I64, I64, I32, I32, I32]),
     "msha_gemm_f32_head_outer": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, F32,
                                            I32, P, SZ, I32, I32, I32, P, P, P, P, P]),
     "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
@@ -150,6 +162,8 @@ SIGNATURES = {
     "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, I32, F32, F32,
                                       U64, U64, P, P, P, P, P, P, P, SZ, P]),
     "msha_segments": (C.c_int, [I32, P, P]),
+    "msha_adam_step": (C.c_int, [I32, P, C.c_double, C.c_double, C.c_double, C.c_double,
+                                 C.c_double, P, P]),
     "msha_project_small_supported": (C.c_int, [I64, I64, I32, I32]),
     "msha_project_small": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P]),
     "msha_project_small_bwd": (C.c_int, [I64, I64, I32, I32, P, P, P, P, P, P, P, P, P, P, P, P,

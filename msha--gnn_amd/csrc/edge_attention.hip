@@ -847,7 +847,10 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
   }
 }
 
-template <int H, int F, typename T, bool BUF>
+// RSC (row scores, recomputed): er_j = hc_j . a_r in the gather-layout forward's order
+// instead of reading er (a separate instantiation: the extra registers stay out of the
+// er-reading kernel)
+template <int H, int F, typename T, bool BUF, bool RSC = false>
 __global__ void __launch_bounds__(256) bwd_cols_kernel(
     const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
@@ -887,7 +890,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
       acc[k] = pk_zero<T>();
     }
     float erh;
-    if (G::QPL == 1 && ar != nullptr) {  // er_j from hc_j in the row-score forward's order
+    if (RSC && G::QPL == 1) {  // er_j from hc_j in the row-score forward's order
       const int q = lane % G::NQ;
       Pk<T> aq;
 #pragma unroll
@@ -1043,7 +1046,7 @@ __global__ void __launch_bounds__(256) bwd_cols_kernel(
 // loop is branch-free and its waits exact; two slot groups per trip, each group's
 // CSC rows loaded two groups ahead into the register it just consumed.
 // Needs every table below 2 GiB (msha_edge_attention_bwd_fused checks).
-template <int H, int F, typename T>
+template <int H, int F, typename T, bool RSC = false>
 __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
     const int32_t* __restrict__ chunk_col, const int32_t* __restrict__ chunk_start,
     const int32_t* __restrict__ chunk_end, int64_t n_chunks, const int32_t* __restrict__ colptr,
@@ -1090,7 +1093,7 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
       hcv[k] = pk_load(hc + (int64_t)jc * G::D + h_s * F + G::V * k);
       acc[k] = pk_zero<T>();
     }
-    const float er_tab = ar != nullptr ? 0.f : er[(int64_t)jc * H + h_s];
+    const float er_tab = RSC ? 0.f : er[(int64_t)jc * H + h_s];
     float xacc = 0.f;
     // one trip = COLS_NG slot groups: every group's loads leave before the first
     // group's compute and de store (the compiler may not hoist a buffer load above a
@@ -1125,7 +1128,7 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
       // for hc_j / a_r put one memory latency in front of every chunk's loads); the empty
       // asm keeps it from being hoisted back out of the loop
       float erh = er_tab;
-      if (ar != nullptr) {
+      if (RSC) {
         Pk<T> hv[NV];
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
@@ -1450,6 +1453,13 @@ extern "C" int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, 
     return fail(MSHA_ERR_UNSUPPORTED, "edge_attention_bwd_rows: unsupported (heads, feat, dtype)");
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
+  // short rows (R15, bip1m): the gather-layout row pass (MSHA_BWD_GL=0: this file's, A/B)
+  const bool short_rows = g->n_edges <= (int64_t)FWD_SHORT_DEG * g->n_rows;
+  if (short_rows && env_int("MSHA_BWD_GL", 1) != 0 && fwd_bat_ok(g, heads, feat, dtype) &&
+      launch_bwd_rows_gl(g, heads, feat, dtype, el, er, hc, lse, u,
+                         dtype == MSHA_DTYPE_BF16 ? u_lo : nullptr, dU, hs, dV, row_coef,
+                         neg_slope, dp, d_el, de, attd, ld, d_hs, fwd_grid(g), s))
+    return check_launch("edge_attention_bwd_rows");
   if (dtype == MSHA_DTYPE_BF16)
     launch_bwd_rows<bf16_t>(g, heads, feat, el, er, hc, lse, u, u_lo, dU, hs, dV, row_coef,
                             neg_slope,
@@ -1565,7 +1575,9 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
                          (const T*)u, (const T*)u_lo, (const T*)dU, rec, uc, qc, g->rowflag,  \
                          d_el);                                                                \
       if (f * sizeof(T) <= 64 && COLS_EH && buf_ok)                                            \
-        hipLaunchKernelGGL((bwd_cols_eh_kernel<h, f, T>), wave_grid(g->n_chunks), dim3(256), 0, \
+        hipLaunchKernelGGL((ar != nullptr ? bwd_cols_eh_kernel<h, f, T, true>                 \
+                                           : bwd_cols_eh_kernel<h, f, T, false>),               \
+                           wave_grid(g->n_chunks), dim3(256), 0,                                \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
                            g->colptr, g->csc_row, g->csc_eid, g->n_edges, g->rowflag,          \
                            g->n_rows, rec, er, ar, (const T*)hc, (const T*)dU, neg_slope, dp,  \
@@ -1573,7 +1585,9 @@ static void launch_bwd_fused(const msha_graph* g, int heads, int feat, const flo
                            (T*)d_hc, d_er, part, part_x);                                      \
       else                                                                                     \
       {                                                                                        \
-        auto kern = buf_ok ? bwd_cols_kernel<h, f, T, true> : bwd_cols_kernel<h, f, T, false>; \
+        auto kern = ar != nullptr                                                              \
+            ? (buf_ok ? bwd_cols_kernel<h, f, T, true, true> : bwd_cols_kernel<h, f, T, false, true>) \
+            : (buf_ok ? bwd_cols_kernel<h, f, T, true> : bwd_cols_kernel<h, f, T, false>);     \
         hipLaunchKernelGGL(kern, wave_grid(g->n_chunks), dim3(256), 0,                         \
                            s, g->chunk_col, g->chunk_start, g->chunk_end, g->n_chunks,         \
                            g->colptr, g->csc_row, g->csc_eid, g->n_rows, g->rowflag, rec, er,  \

@@ -82,4 +82,12 @@ int launch_fwd_gl(const msha_graph* g, int heads, int feat, int32_t dtype, const
                   const Dropout& dp, void* u, void* u_lo, float* lse, float* attd, float* uc,
                   float* qc, bool short_rows, dim3 grid, hipStream_t s);
 
+// edge_bwd_gl.hip: the gather-layout row half of the backward for short rows (1 =
+// launched).
+int launch_bwd_rows_gl(const msha_graph* g, int heads, int feat, int32_t dtype, const float* el,
+                       const float* er, const void* hc, const float* lse, const void* u,
+                       const void* u_lo, const void* dU, const void* hs, const void* dV,
+                       const float* row_coef, float slope, const Dropout& dp, float* d_el,
+                       float* de, float* attd, int ld, void* d_hs, dim3 grid, hipStream_t s);
+
 }  // namespace msha

@@ -286,17 +286,26 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
           }
         }
         if constexpr (FE > 0) {
-          float sl = 0.f, sr = 0.f;
+          // the score dots of the STORED row (bf16 tables: the rounded values) in the
+          // order the gather-layout edge kernels recompute er_j = h_j . a_r from a gathered
+          // 16-byte piece (pk_dot: last element first, then fma downwards; then the xor
+          // tree over the head's pieces below): el / er are the same bits as that
+          // recomputation (msha_project_scores_row_order)
+          float av[G::EPL], rv[G::EPL], x[G::EPL];
 #pragma unroll
           for (int u = 0; u < G::EPL; u += 4) {
             const float4 a4 = *reinterpret_cast<const float4*>(als + col + u);
             const float4 r4 = *reinterpret_cast<const float4*>(ars + col + u);
-            const float av[4] = {a4.x, a4.y, a4.z, a4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
+            av[u] = a4.x; av[u + 1] = a4.y; av[u + 2] = a4.z; av[u + 3] = a4.w;
+            rv[u] = r4.x; rv[u + 1] = r4.y; rv[u + 2] = r4.z; rv[u + 3] = r4.w;
+          }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              sl = fmaf(e[u + j], av[j], sl);
-              sr = fmaf(e[u + j], rv[j], sr);
-            }
+          for (int j = 0; j < G::EPL; ++j) x[j] = G::F32 ? e[j] : (float)(bf16_t)e[j];
+          float sl = x[G::EPL - 1] * av[G::EPL - 1], sr = x[G::EPL - 1] * rv[G::EPL - 1];
+#pragma unroll
+          for (int j = G::EPL - 2; j >= 0; --j) {
+            sl = fmaf(x[j], av[j], sl);
+            sr = fmaf(x[j], rv[j], sr);
           }
 #pragma unroll
           for (int o = 1; o < FE / G::EPL; o <<= 1) {
@@ -925,6 +934,22 @@ static int proj_grid(int64_t M, int waves = sk::kProjWaves) {
   const int64_t blocks = (tiles + waves - 1) / waves;
   return (int)(blocks < 256 ? blocks : 256);  // one 8-wave block per CU
 }
+
+// whether skinny_project covers the shape (its score epilogue is then in the row-score
+// order; the caller also needs 16-byte aligned X, W, h)
+template <typename T>
+int skinny_project_covers(int64_t M, int64_t K, int heads, int feat, bool score) {
+  const int64_t N = (int64_t)heads * feat;
+  if (!skinny_enabled() || M < 1024 || M * K * (int64_t)sizeof(T) >= (1ll << 31)) return 0;
+  const int minfe = 16 / (int)sizeof(T);
+  if (score && (feat < minfe || N % feat != 0)) return 0;
+  const bool kn = (K == 128 || K == 64) && (N == 128 || N == 64);
+  if (!kn) return 0;
+  if (!score) return 1;
+  return feat == 16 || feat == 32 || feat == 64 || feat == N ? 1 : 0;
+}
+template int skinny_project_covers<float>(int64_t, int64_t, int, int, bool);
+template int skinny_project_covers<bf16_t>(int64_t, int64_t, int, int, bool);
 
 // Returns 1 when it launched, 0 when the shape is not covered (caller falls back).
 template <typename T>

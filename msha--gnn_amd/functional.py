@@ -111,6 +111,9 @@ class _EdgeAttention(torch.autograd.Function):
         # fused backward's column pass (the same bits in both); u-only path
         rs = (ar is not None and hs is None and ROW_SCORES and FUSED_BWD
               and _lib.load().msha_edge_attention_row_scores_preferred(g, H, F, _code(dt)))
+        # er from project_scores in the kernels' order is exactly what the forward
+        # recomputes: the backward then reads er per column (no recompute from a_r)
+        ctx.er_exact = bool(rs and getattr(er, "_msha_row_order", False))
         ar = ar.detach().to(torch.float32).contiguous().view(H, F) if rs else None
         u = torch.empty(n, H, F, device=dev, dtype=dt)
         # bf16 tables under autograd: keep the rounding residual of u for the backward's
@@ -159,7 +162,7 @@ class _EdgeAttention(torch.autograd.Function):
     def backward(ctx, dU, dV=None):
         el, er, hc, hs, lse, u, u_lo, ar, *rowterms = ctx.saved_tensors
         u_lo = u_lo if u_lo.numel() else None
-        ar = ar if ctx.rs else None
+        ar = ar if ctx.rs and not ctx.er_exact else None
         graph = ctx.graph
         n, H = el.shape
         m, _, F = hc.shape
@@ -576,7 +579,19 @@ def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = No
         al = al.reshape(heads, feat)
     if ar is not None:
         ar = ar.reshape(heads, feat)
-    return _ProjectScores.apply(X, W, al, ar, heads, feat)
+    out = _ProjectScores.apply(X, W, al, ar, heads, feat)
+    if ar is not None:
+        # er computed from the stored h in the order the row-score edge kernels recompute
+        # it (msha_project_scores_row_order): edge_attention(..., ar=) then reads this er
+        # where it needs er_j per column instead of recomputing it (the same bits)
+        dt = _table_dtype(X, W)
+        M, K = X.shape
+        small = dt == torch.float32 and bool(_lib.load().msha_project_small_supported(
+            M, K, heads, feat))
+        out[-1]._msha_row_order = bool(
+            not small and X.data_ptr() % 16 == 0 and W.data_ptr() % 16 == 0
+            and _lib.load().msha_project_scores_row_order(M, K, heads, feat, _code(dt)))
+    return out
 
 
 # ----------------------------------------------------------------- GCN SpMM ---
@@ -1176,10 +1191,13 @@ def _cast_many(pairs, stream):
 
 class _FeatureDropout(torch.autograd.Function):
     """dropout(Sfeatures), dropout(Rfeatures) (Ablation.py:296-297, Ours.py:161-162) in one
-    launch; the backward regenerates both Philox masks in one launch."""
+    launch; the backward regenerates both Philox masks in one launch.  A table registered
+    with ``optim.Adam.fuse_dropout_grad`` is updated by the backward itself (the Adam step
+    reads the dropout's output gradient and the mask): its gradient is never written."""
 
     @staticmethod
     def forward(ctx, S, R, p, s_seed, r_seed):
+        ctx.params = (S, R)  # the leaves themselves (a fused optimizer updates them)
         S, R = S.contiguous(), R.contiguous()
         So, Ro = torch.empty_like(S), torch.empty_like(R)
         _segments([(S.data_ptr(), So.data_ptr(), S.shape[0], S.shape[1], S.shape[1], S.shape[1],
@@ -1191,8 +1209,15 @@ class _FeatureDropout(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dSo, dRo):
+        from .optim import fused_optimizer_of
+
         segs, outs = [], []
-        for d, seed in ((dSo, ctx.seeds[0]), (dRo, ctx.seeds[1])):
+        for k, (d, seed) in enumerate(((dSo, ctx.seeds[0]), (dRo, ctx.seeds[1]))):
+            leaf = ctx.params[k]
+            opt = fused_optimizer_of(leaf) if d is not None else None
+            if opt is not None and ctx.needs_input_grad[k]:
+                opt.fused_update(leaf, d, ctx.p, seed)  # no gradient tensor for this leaf
+                d = None
             if d is None:
                 outs.append(None)
                 continue

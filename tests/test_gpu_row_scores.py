@@ -129,3 +129,44 @@ def test_row_scores_r15_multichunk(cuda, msha, dtype):
     tol_close(got[1].cpu().numpy(), bw["d_el"], max(tol, 1e-4), tol)
     tol_close(got[2].cpu().numpy(), bw["d_er"], max(tol, 1e-4), tol)
     tol_close(got[3].float().cpu().numpy(), bw["d_hc"], tol, tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("H,F", [(8, 16), (2, 64), (4, 32)])
+def test_projection_er_is_the_recomputed_er(cuda, msha, dtype, H, F):
+    """msha_project_scores' er (row-order epilogue) is bit-identical to the er_j = h_j . a_r
+    the row-score kernels recompute from the gathered row: the backward that reads this
+    er (the tagged tensor) and the one that recomputes it from a_r (an untagged copy)
+    give the same bits everywhere."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    n, K = 3000, 128
+    rng = np.random.default_rng(H * F)
+    deg = rng.integers(3, 20, n)
+    rowptr = np.concatenate([[0], np.cumsum(deg)])
+    col = np.concatenate([np.sort(rng.choice(n, d, replace=False)) for d in deg])
+    graph = Graph.from_csr(rowptr, col, n, cuda)
+    g = torch.Generator().manual_seed(H + F)
+    X = torch.rand(n, K, generator=g).to(cuda, dtype)
+    W = (torch.randn(K, H * F, generator=g) * K ** -0.5).to(cuda, dtype)
+    al = torch.randn(H, F, generator=g).to(cuda)
+    ar = torch.randn(H, F, generator=g).to(cuda)
+    dU = torch.randn(n, H, F, generator=g).to(cuda, dtype)
+    with torch.no_grad():
+        h, el, er = MF.project_scores(X, W, al, ar, heads=H)
+    assert getattr(er, "_msha_row_order", False)
+    os.environ["MSHA_ROW_SCORES"] = "1"
+    try:
+        runs = []
+        for er_in in (er, er.clone()):  # the clone carries no tag: recompute from a_r
+            leaves = [el.clone().requires_grad_(True), er_in.requires_grad_(True),
+                      h.view(n, H, F).clone().requires_grad_(True)]
+            u = MF.edge_attention(graph, *leaves, ar=ar)
+            u.backward(dU)
+            runs.append([u.detach()] + [x.grad for x in leaves])
+            er.requires_grad_(False)
+    finally:
+        os.environ.pop("MSHA_ROW_SCORES", None)
+    for a, b, name in zip(*runs, ("u", "d_el", "d_er", "d_hc")):
+        assert torch.equal(a, b), name
