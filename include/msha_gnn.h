@@ -331,12 +331,12 @@ MSHA_API int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const flo
  * Replaces Ablation.py:262-267's projection + the (N, M, 2F) score tensor: the
  * score of edge (i, j) is lrelu(el_i + er_j).  al/el and ar/er are optional pairs;
  * feat must be 4, 8, 16, 32, 64 or 128 when a score vector is given. */
-/* 1 when msha_project_scores(_bf16) at this shape (16-byte aligned X, W, h) computes its
- * el / er from the STORED h in the order the row-score edge kernels recompute
- * er_j = h_j . a_r from a gathered row (per 16-byte piece: last element first, fma
- * downwards; then the xor tree over the head's pieces): er is then bit-identical to that
- * recomputation and msha_edge_attention_bwd_fused_ex may read it in place of
- * msha_edge_attention_bwd_fused_rs (ABI 9). */
+/* 1 when msha_project_scores(_bf16) / msha_project_small at this shape compute el / er
+ * from the STORED h in the order the row-score edge kernels recompute er_j = h_j . a_r
+ * from a gathered row (per 16-byte piece: last element first, fma downwards; then the
+ * xor tree over the head's pieces): er is then bit-identical to that recomputation and
+ * msha_edge_attention_bwd_fused_ex may read it in place of msha_edge_attention_bwd_fused_rs
+ * (ABI 9: every projection path; feat a multiple of 4). */
 MSHA_API int msha_project_scores_row_order(int64_t M, int64_t K, int32_t heads, int32_t feat,
                                            int32_t dtype);
 MSHA_API int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t feat,

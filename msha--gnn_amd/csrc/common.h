@@ -325,8 +325,6 @@ template <typename T>
 int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, const void* W,
                    const float* al, const float* ar, void* h, float* el, float* er,
                    hipStream_t s);
-template <typename T>
-int skinny_project_covers(int64_t M, int64_t K, int heads, int feat, bool score);
 int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t ldg,
                        const int64_t* gi, const float* G2, int64_t ldg2, const int64_t* gj,
                        const float* W, const float* bias, int act, const Dropout& dp, float* out,

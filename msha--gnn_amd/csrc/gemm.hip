@@ -769,11 +769,13 @@ extern "C" int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const f
   return gemm_run(p, operand == 0 ? HO_A : HO_B, beta, splits, ws, ws_bytes, (hipStream_t)stream);
 }
 
+// every projection path computes its score dots in the row-score order (skinny.hip
+// proj_kernel, this file's EPI_SCORE f4_dot + xor tree, gemm_bf16.hip's EPI_SCORE on the
+// rounded row, small.hip): 1 for any valid shape
 extern "C" int msha_project_scores_row_order(int64_t M, int64_t K, int32_t heads, int32_t feat,
                                              int32_t dtype) {
   if (M <= 0 || K <= 0 || heads <= 0 || feat <= 0) return 0;
-  return dtype == MSHA_DTYPE_BF16 ? skinny_project_covers<bf16_t>(M, K, heads, feat, true)
-                                  : skinny_project_covers<float>(M, K, heads, feat, true);
+  return (dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16) && feat % 4 == 0 ? 1 : 0;
 }
 
 extern "C" int msha_project_scores(int64_t M, int64_t K, int32_t heads, int32_t feat,

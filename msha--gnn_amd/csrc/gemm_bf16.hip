@@ -313,11 +313,16 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(Args p) {
       }
       if (EPI == EPI_SCORE) {
         constexpr int FE = FEPI > 0 ? FEPI : 16;  // >= 8: a head covers FE / 8 lanes
-        float sl = 0.f, sr = 0.f;
+        // the stored (bf16-rounded) row in the row-score order of the edge kernels
+        // (msha_project_scores_row_order): last element first, fma downwards
+        float x8[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          sl = fmaf(e[u], al8[u], sl);
-          sr = fmaf(e[u], ar8[u], sr);
+        for (int u = 0; u < 8; ++u) x8[u] = (float)(bf16_t)e[u];
+        float sl = x8[7] * al8[7], sr = x8[7] * ar8[7];
+#pragma unroll
+        for (int u = 6; u >= 0; --u) {
+          sl = fmaf(x8[u], al8[u], sl);
+          sr = fmaf(x8[u], ar8[u], sr);
         }
 #pragma unroll
         for (int o = 1; o < FE / 8; o <<= 1) {

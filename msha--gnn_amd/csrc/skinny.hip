@@ -935,22 +935,6 @@ static int proj_grid(int64_t M, int waves = sk::kProjWaves) {
   return (int)(blocks < 256 ? blocks : 256);  // one 8-wave block per CU
 }
 
-// whether skinny_project covers the shape (its score epilogue is then in the row-score
-// order; the caller also needs 16-byte aligned X, W, h)
-template <typename T>
-int skinny_project_covers(int64_t M, int64_t K, int heads, int feat, bool score) {
-  const int64_t N = (int64_t)heads * feat;
-  if (!skinny_enabled() || M < 1024 || M * K * (int64_t)sizeof(T) >= (1ll << 31)) return 0;
-  const int minfe = 16 / (int)sizeof(T);
-  if (score && (feat < minfe || N % feat != 0)) return 0;
-  const bool kn = (K == 128 || K == 64) && (N == 128 || N == 64);
-  if (!kn) return 0;
-  if (!score) return 1;
-  return feat == 16 || feat == 32 || feat == 64 || feat == N ? 1 : 0;
-}
-template int skinny_project_covers<float>(int64_t, int64_t, int, int, bool);
-template int skinny_project_covers<bf16_t>(int64_t, int64_t, int, int, bool);
-
 // Returns 1 when it launched, 0 when the shape is not covered (caller falls back).
 template <typename T>
 int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, const void* W,

@@ -61,9 +61,18 @@ __global__ void __launch_bounds__(kSmallThreads) small_fwd_kernel(SmallArgs a) {
     const float* v = side == 0 ? a.al : a.ar;
     float* o = side == 0 ? a.el : a.er;
     if (v != nullptr) {
-      float sc = 0.f;
-      for (int f = 0; f < F; ++f) sc = fmaf(hr[hh * F + f], v[hh * F + f], sc);
-      o[(int64_t)i * a.H + hh] = sc;
+      // the row-score order of the edge kernels (msha_project_scores_row_order): per
+      // 4-element piece last element first, fma downwards; then the pieces' xor tree
+      float d[32];  // F / 4 <= 32 pieces
+      const int np = F / 4;
+      for (int k = 0; k < np; ++k) {
+        const float* x = hr + hh * F + 4 * k;
+        const float* vv = v + hh * F + 4 * k;
+        d[k] = fmaf(x[0], vv[0], fmaf(x[1], vv[1], fmaf(x[2], vv[2], x[3] * vv[3])));
+      }
+      for (int st = 1; st < np; st <<= 1)
+        for (int k = 0; k + st < np; k += 2 * st) d[k] = d[k] + d[k + st];
+      o[(int64_t)i * a.H + hh] = d[0];
     }
   }
 }

@@ -584,13 +584,9 @@ def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = No
         # er computed from the stored h in the order the row-score edge kernels recompute
         # it (msha_project_scores_row_order): edge_attention(..., ar=) then reads this er
         # where it needs er_j per column instead of recomputing it (the same bits)
-        dt = _table_dtype(X, W)
         M, K = X.shape
-        small = dt == torch.float32 and bool(_lib.load().msha_project_small_supported(
-            M, K, heads, feat))
-        out[-1]._msha_row_order = bool(
-            not small and X.data_ptr() % 16 == 0 and W.data_ptr() % 16 == 0
-            and _lib.load().msha_project_scores_row_order(M, K, heads, feat, _code(dt)))
+        out[-1]._msha_row_order = bool(_lib.load().msha_project_scores_row_order(
+            M, K, heads, feat, _code(_table_dtype(X, W))))
     return out
 
 

@@ -21,6 +21,9 @@ Fixtures
                   BN inputs and softmax outputs of both heads, in fp32 and fp64.
   gat_sub512.npz  GAT.py GAT (32 features, 2 heads) on the same subgraph.
   link.npz        LLP.LinkPredictor 'mlp' and 'inner': outputs and grads.
+  llp.npz         LLP.GAT (teacher, forward(input, adj)) on the 512-source subgraph and
+                  LLP.Teacher_LinkPredictor ('mlp' with 2 and 3 layers, 'inner', an
+                  unknown predictor): init, outputs, grads.
   edge_cases.npz  OursLayer3 / GAL on a hand-made adjacency: empty row, degree 1,
                   degree 65 and 80 (> one wavefront), one hot column; normalize
                   with a zero column (NaN spread) and on random counts.
@@ -30,7 +33,8 @@ Fixtures
                   512-source subgraph: init, train output, nll loss, grads.
   years.npz       per-year node counts, group ids and GDP (2015-2018).
 
-``python tests/golden/make_golden.py gcn`` regenerates only gcn_sub512.npz;
+``python tests/golden/make_golden.py gcn`` regenerates only gcn_sub512.npz; ``... llp``
+only llp.npz;
 ``... round2`` regenerates sub512.npz (adds the fp64 softmax outputs), link.npz (adds
 the num_layers=1 and unknown-predictor cases) and ours_record.npz.
 """
@@ -325,6 +329,62 @@ def make_link():
     np.savez_compressed(os.path.join(OUT, "link.npz"), **res)
 
 
+def make_llp():
+    """LLP.py's teacher GAT (forward(input, adj), LLP.py:148-168) and
+    Teacher_LinkPredictor (LLP.py:170-198), AST-extracted (LLP.py runs its training
+    script at import), on the 512-source subgraph of sub512.npz."""
+    ns = extract(os.path.join(REF, "LLP.py"),
+                 {"GraphAttentionLayer", "GAT", "Teacher_LinkPredictor"})
+    z = np.load(os.path.join(OUT, "sub512.npz"))
+    counts = torch.as_tensor(z["counts"])
+    n, m = counts.shape
+    flows = z["flows"].astype(np.int64)
+    adj = refmodel.normalize_adjacency_matrix(counts)
+    res = {}
+    torch.manual_seed(11)
+    gat = ns["GAT"](n_features=32, n_classes=m, n_heads=2, dropout=0.0, gdp=None, N=n)
+    for k, v in gat.state_dict().items():
+        res[f"gat.init.{k}"] = v.numpy()
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(n, 32, generator=g).requires_grad_(True)
+    bidx = torch.randperm(len(flows), generator=g)[:64]
+    si, ri = torch.as_tensor(flows[bidx, 0]), torch.as_tensor(flows[bidx, 1])
+    gat.train()
+    out = gat(x, adj)
+    loss = F.nll_loss(out[si], ri)
+    loss.backward()
+    res.update({"gat.input": x.detach().numpy(), "gat.source_index": si.numpy(),
+                "gat.recipient_index": ri.numpy(), "gat.out": np32(out), "gat.loss": np32(loss),
+                "gat.grad.input": np32(x.grad)})
+    for k, p_ in gat.named_parameters():
+        if p_.grad is not None:
+            res[f"gat.grad.{k}"] = np32(p_.grad)
+    TL = ns["Teacher_LinkPredictor"]
+    xi = torch.randn(200, 32, generator=g)
+    xj = torch.randn(200, 32, generator=g)
+    res["tlp.x_i"], res["tlp.x_j"] = xi.numpy(), xj.numpy()
+    for mode, pred, nl in (("mlp", "mlp", 2), ("mlp3", "mlp", 3), ("inner", "inner", 2),
+                           ("other", "cos", 2)):
+        torch.manual_seed(13)
+        lp = TL(pred, 32, 24, 1, nl, 0.0)
+        for k, v in lp.state_dict().items():
+            res[f"tlp.{mode}.init.{k}"] = v.numpy()
+        a = xi.clone().requires_grad_(True)
+        b = xj.clone().requires_grad_(True)
+        lp.train()
+        y = lp(a, b)
+        w = torch.randn(y.shape, generator=g)
+        (y * w).sum().backward()
+        res[f"tlp.{mode}.out"] = np32(y)
+        res[f"tlp.{mode}.dout"] = w.numpy()
+        res[f"tlp.{mode}.grad.x_i"] = np32(a.grad)
+        res[f"tlp.{mode}.grad.x_j"] = np32(b.grad)
+        for k, p_ in lp.named_parameters():
+            if p_.grad is not None:
+                res[f"tlp.{mode}.grad.{k}"] = np32(p_.grad)
+    np.savez_compressed(os.path.join(OUT, "llp.npz"), **res)
+
+
 def edge_adj():
     """40 x 80 count matrix: row 0 empty; row 1 degree 1; row 2 full (80 > 64);
     row 3 degree 65; rows 4..20 all in column 7 (hot column); the rest random."""
@@ -539,6 +599,9 @@ def main():
     if sys.argv[1:] == ["gcn"]:
         make_gcn()
         return
+    if sys.argv[1:] == ["llp"]:  # round 3: LLP.GAT / Teacher_LinkPredictor
+        make_llp()
+        return
     if sys.argv[1:] == ["round2"]:  # link quirks, sub512 fp64 softmax, Ours record dump
         g = load_2015()
         mask = (g["counts"] > 0).numpy()
@@ -551,6 +614,7 @@ def main():
     counts, gdp_sub, flows_sub = make_sub512(g, mask)
     make_gat(counts, gdp_sub, flows_sub)
     make_link()
+    make_llp()
     make_edge_cases()
     make_ours_small(g)
     make_ours_record(g)

@@ -174,6 +174,11 @@ def _u_only_grads(MF, graph, el, er, hc, dU, p, seed, dev, dtype, fused, rowterm
     MF.FUSED_BWD = fused
     if rowterms is not None:
         os.environ["MSHA_ROWTERMS"] = "1" if rowterms else "0"
+    if not fused:
+        # the split backward these tests hold the fused one to, bit for bit: the
+        # score-layout row pass (short-row graphs would take the gather-layout one, whose
+        # d_el sums in another order; tests/test_gpu_short_rows.py checks that one)
+        os.environ["MSHA_BWD_GL"] = "0"
     try:
         tel, ter = (t(x, dev).requires_grad_(True) for x in (el, er))
         thc = t(hc, dev, dtype).requires_grad_(True)
@@ -183,6 +188,7 @@ def _u_only_grads(MF, graph, el, er, hc, dU, p, seed, dev, dtype, fused, rowterm
     finally:
         MF.FUSED_BWD = True
         os.environ.pop("MSHA_ROWTERMS", None)
+        os.environ.pop("MSHA_BWD_GL", None)
 
 
 def _same_as_split(got, split, dtype=torch.float32):

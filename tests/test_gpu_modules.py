@@ -95,6 +95,64 @@ def test_gat_matches_reference(cuda, msha):
         tol_close(p.grad.cpu().numpy(), ref, 1e-4, 1e-5)
 
 
+def test_llp_teacher_gat_and_link_predictor(cuda, msha):
+    """LLP.py:148-168 (teacher GAT, forward(input, adj)) and LLP.py:170-198
+    (Teacher_LinkPredictor, the drop-in alias of LinkPredictor) against the reference's
+    own outputs and gradients (llp.npz): bit-identical init, 1e-5 outputs, 1e-4 grads."""
+    import os
+    import sys
+
+    from msha_gnn_amd import layers
+
+    z = golden("llp.npz")
+    s = golden("sub512.npz")
+    n, m = s["counts"].shape
+    torch.manual_seed(11)
+    gat = layers.LLPGAT(n_features=32, n_classes=m, n_heads=2, dropout=0.0, gdp=None, N=n)
+    for k, v in gat.state_dict().items():
+        assert np.array_equal(v.numpy(), z[f"gat.init.{k}"]), k
+    gat = gat.to(cuda).train()
+    adj = torch.as_tensor(s["adj_norm"], device=cuda)
+    x = torch.as_tensor(z["gat.input"], device=cuda).requires_grad_(True)
+    out = gat(x, adj)
+    tol_close(out.detach().cpu().numpy(), z["gat.out"], 1e-5, 1e-6)
+    si = torch.as_tensor(z["gat.source_index"], device=cuda)
+    loss = F.nll_loss(out[si], torch.as_tensor(z["gat.recipient_index"], device=cuda))
+    assert abs(float(loss) - float(z["gat.loss"])) <= 1e-5 * abs(float(z["gat.loss"]))
+    loss.backward()
+    tol_close(x.grad.cpu().numpy(), z["gat.grad.input"], 1e-4, 1e-5)
+    for k, p in gat.named_parameters():
+        ref = z[f"gat.grad.{k}"]
+        if k.endswith(".a"):  # the GAL score vector: exact 0 here, ~1e-7 in the reference
+            assert float(p.grad.abs().max()) == 0.0 and np.abs(ref).max() < 1e-5
+            continue
+        tol_close(p.grad.cpu().numpy(), ref, 1e-4, 1e-5)
+    sys.path.insert(0, os.path.join(os.path.dirname(layers.__file__), "dropin"))
+    import LLP as dropin_llp  # the drop-in module train scripts import
+
+    for mode, pred, nl in (("mlp", "mlp", 2), ("mlp3", "mlp", 3), ("inner", "inner", 2),
+                           ("other", "cos", 2)):
+        torch.manual_seed(13)
+        lp = dropin_llp.Teacher_LinkPredictor(pred, 32, 24, 1, nl, 0.0)
+        for k, v in lp.state_dict().items():
+            assert np.array_equal(v.numpy(), z[f"tlp.{mode}.init.{k}"]), (mode, k)
+        lp = lp.to(cuda).train()
+        a = torch.as_tensor(z["tlp.x_i"], device=cuda).requires_grad_(True)
+        b = torch.as_tensor(z["tlp.x_j"], device=cuda).requires_grad_(True)
+        y = lp(a, b)
+        assert tuple(y.shape) == z[f"tlp.{mode}.out"].shape
+        tol_close(y.detach().cpu().numpy(), z[f"tlp.{mode}.out"], 1e-5, 1e-6)
+        y.backward(torch.as_tensor(z[f"tlp.{mode}.dout"], device=cuda))
+        tol_close(a.grad.cpu().numpy(), z[f"tlp.{mode}.grad.x_i"], 1e-4, 1e-5)
+        tol_close(b.grad.cpu().numpy(), z[f"tlp.{mode}.grad.x_j"], 1e-4, 1e-5)
+        for k, p in lp.named_parameters():
+            key = f"tlp.{mode}.grad.{k}"
+            if key in z.files:
+                tol_close(p.grad.cpu().numpy(), z[key], 1e-4, 1e-5)
+            else:
+                assert p.grad is None, (mode, k)
+
+
 def test_ours_layer3_edge_cases(cuda, msha):
     """80 recipients: an empty row (uniform), degree 1, degree 80 and 65 (> one
     wavefront), a hot column; train-mode BN; gradients of every input."""

@@ -165,6 +165,26 @@ def test_link_predictor():
                                        atol=1e-6)
 
 
+def test_llp_teacher_fixtures():
+    """LLP.py's teacher GAT (forward(input, adj), LLP.py:148-168) and
+    Teacher_LinkPredictor (LLP.py:170-198) as the reference computed them (llp.npz):
+    the oracle's GAT / link-predictor restatements reproduce them."""
+    z = golden("llp.npz")
+    s = golden("sub512.npz")
+    rowptr, col = O.dense_to_csr(s["adj_norm"])
+    out = O.gat_fwd(z["gat.input"], [z["gat.init.attention_0.W"], z["gat.init.attention_1.W"]],
+                    z["gat.init.out_att.W"], rowptr, col)
+    np.testing.assert_allclose(out, z["gat.out"], rtol=1e-5, atol=1e-5)
+    xi, xj = z["tlp.x_i"], z["tlp.x_j"]
+    for mode, pred, nl in (("mlp", "mlp", 2), ("mlp3", "mlp", 3), ("inner", "inner", 2),
+                           ("other", "cos", 2)):
+        lins = [(z[f"tlp.{mode}.init.lins.{i}.weight"], z[f"tlp.{mode}.init.lins.{i}.bias"])
+                for i in range(nl)]
+        y = O.link_predict(xi, xj, pred, lins)
+        assert y.shape == z[f"tlp.{mode}.out"].shape
+        np.testing.assert_allclose(y, z[f"tlp.{mode}.out"], rtol=1e-6, atol=1e-6)
+
+
 def _dense_core_torch(rowptr, col, el, er, hc, hs, n_cols):
     """Dense torch restatement of the masked-softmax core for autograd (fp64)."""
     n = len(rowptr) - 1
