@@ -162,6 +162,7 @@ SIGNATURES = {
     "msha_ours_intra_bwd": (C.c_int, [GP, GRP, I64, P, I32, I32, I32, P, P, P, P, P, I32, F32, F32,
                                       U64, U64, P, P, P, P, P, P, P, SZ, P]),
     "msha_segments": (C.c_int, [I32, P, P]),
+    "msha_adam_workspace_size": (SZ, []),
     "msha_adam_step": (C.c_int, [I32, P, C.c_double, C.c_double, C.c_double, C.c_double,
                                  C.c_double, P, P]),
     "msha_project_small_supported": (C.c_int, [I64, I64, I32, I32]),

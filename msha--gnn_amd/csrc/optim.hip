@@ -6,7 +6,7 @@
 // gradient is never written or re-read.
 //
 // One thread owns 4 consecutive elements (16-B fp32 / 8-B bf16 pieces of every operand);
-// the grid's y dimension walks the tensors.  Arithmetic follows torch.optim.Adam's
+// each tensor gets its own range of blocks of a 1-D grid.  Arithmetic follows torch.optim.Adam's
 // single-tensor step (grad + wd * p, lerp of the first moment, addcmul of the second,
 // addcdiv with step_size = lr / bias_correction1), fp32 per element with the bias
 // corrections in double from the step count, as torch computes them on the host.
@@ -18,8 +18,8 @@ struct AdamBatch {
   msha_adam_tensor t[MSHA_MAX_ADAM];
   double lr, b1, b2, eps, wd;  // torch's Python-float hyperparameters
   int n;
-  int total_blocks;
-  int* done;            // completion counter (the last block advances the steps)
+  int first[MSHA_MAX_ADAM + 1];  // blocks [first[i], first[i+1]) update tensor i (1-D grid)
+  float2* scal;         // per tensor: (step_size, sqrt(bias_correction2)) of this step
   const uint64_t* ctr;  // device replay counter (dropout offsets)
 };
 
@@ -63,21 +63,52 @@ __device__ __forceinline__ void adam_elem(const AdamScalars& a, float g, float& 
   p = p - a.step_size * (m / denom);     // param.addcdiv_(exp_avg, denom, -step_size)
 }
 
+// The step counts advance in a one-block launch ahead of the update (as torch's
+// capturable Adam adds 1 to its device steps first): every block of the update then reads
+// finished scalars -- no completion counter, no per-block double-precision pow.
+__global__ void __launch_bounds__(64) adam_prep_kernel(AdamBatch b) {
+  const int i = threadIdx.x;
+  if (i >= b.n) return;
+  const float t = *b.t[i].step + 1.f;
+  *b.t[i].step = t;
+  // bias corrections from the step count in double (torch: 1 - beta ** step on the host);
+  // beta ** t by squaring (exact integer t: <= 2 log2 t double multiplies, a few ulps)
+  double p1 = 1.0, p2 = 1.0, s1 = b.b1, s2 = b.b2;
+  for (uint32_t e = (uint32_t)t; e != 0; e >>= 1) {
+    if (e & 1u) {
+      p1 *= s1;
+      p2 *= s2;
+    }
+    s1 *= s1;
+    s2 *= s2;
+  }
+  const double bc1 = 1.0 - p1;
+  const double bc2 = 1.0 - p2;
+  b.scal[i] = make_float2((float)(b.lr / bc1), (float)sqrt(bc2));
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
-  const msha_adam_tensor& T = b.t[blockIdx.y];
+  // the tensor of this block: first[ti] <= blockIdx.x < first[ti + 1] (binary search over
+  // the <= 64 boundaries; every block works -- a 2-D grid sized by the largest tensor left
+  // ~2k idle blocks per small tensor)
+  const int bid = blockIdx.x;
+  int lo = 0, hi = b.n;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (b.first[mid] <= bid) lo = mid; else hi = mid;
+  }
+  const int ti = lo;
+  const msha_adam_tensor& T = b.t[ti];
   const int dt = T.dtype;
-  // bias corrections from the step count, in double (torch: 1 - beta ** step on the host)
-  const double t = (double)*T.step + 1.0;
-  const double bc1 = 1.0 - pow(b.b1, t);
-  const double bc2 = 1.0 - pow(b.b2, t);
+  const float2 sc = b.scal[ti];
   AdamScalars a;  // the scalars torch hands its fp32 kernels
   a.b1c = (float)(1.0 - b.b1);
   a.b2c = (float)(1.0 - b.b2);
   a.b2 = (float)b.b2;
   a.wd = (float)b.wd;
   a.eps = (float)b.eps;
-  a.step_size = (float)(b.lr / bc1);
-  a.bc2_sqrt = (float)sqrt(bc2);
+  a.step_size = sc.x;
+  a.bc2_sqrt = sc.y;
   Dropout d{};
   d.active = T.drop_p > 0.f;
   uint64_t off = 0;
@@ -90,8 +121,8 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
     d.scale = T.drop_p < 1.f ? (float)(1.0 / (1.0 - (double)T.drop_p)) : 0.f;
     off = dropout_offset(d, d.offset);
   }
-  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthr = (int64_t)(b.first[ti + 1] - b.first[ti]) * blockDim.x;
+  const int64_t tid = (int64_t)(bid - b.first[ti]) * blockDim.x + threadIdx.x;
   const int64_t nq = T.n / 4;
   for (int64_t q = tid; q < nq; q += nthr) {
     float4 g = ad_ld4(T.grad, dt, q), p = ad_ld4(T.param, dt, q);
@@ -124,17 +155,6 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
     ad_st(T.exp_avg, dt, e, m);
     ad_st(T.exp_avg_sq, dt, e, v);
   }
-  // every block has read its tensor's step above; the last one to finish advances them all
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const int prev = atomicAdd(b.done, 1);
-    if (prev == b.total_blocks - 1) {
-      for (int i = 0; i < b.n; ++i) *b.t[i].step += 1.f;
-      *b.done = 0;
-      __threadfence();
-    }
-  }
 }
 
 }  // namespace msha
@@ -146,12 +166,12 @@ extern "C" int msha_adam_step(int32_t n, const msha_adam_tensor* tensors, double
                               void* ws, msha_stream_t stream) {
   MSHA_ARG_CHECK(n >= 0 && n <= MSHA_MAX_ADAM && (n == 0 || tensors != nullptr),
                  "adam_step: 0..MSHA_MAX_ADAM tensors");
-  MSHA_ARG_CHECK(ws != nullptr, "adam_step: needs the 16-byte workspace");
+  MSHA_ARG_CHECK(ws != nullptr, "adam_step: needs the msha_adam_workspace_size() workspace");
   MSHA_ARG_CHECK(beta1 >= 0.0 && beta1 < 1.0 && beta2 >= 0.0 && beta2 < 1.0 && eps >= 0.0,
                  "adam_step: bad hyperparameters");
   if (n == 0) return MSHA_OK;
   AdamBatch b{};
-  int64_t mx = 1;
+  int nblocks = 0;
   for (int i = 0; i < n; ++i) {
     const msha_adam_tensor& t = tensors[i];
     MSHA_ARG_CHECK(t.param && t.grad && t.exp_avg && t.exp_avg_sq && t.step && t.n >= 0,
@@ -164,8 +184,10 @@ extern "C" int msha_adam_step(int32_t n, const msha_adam_tensor* tensors, double
                      (uintptr_t)t.exp_avg_sq) & am) == 0,
                    "adam_step: operands must be aligned to 4 elements");
     b.t[i] = t;
-    if (t.n > mx) mx = t.n;
+    b.first[i] = nblocks;
+    nblocks += grid_for(t.n, 256 * 4, 2048);  // 4 elements per thread, grid-stride past 2048
   }
+  b.first[n] = nblocks;
   b.lr = lr;
   b.b1 = beta1;
   b.b2 = beta2;
@@ -174,9 +196,10 @@ extern "C" int msha_adam_step(int32_t n, const msha_adam_tensor* tensors, double
   b.n = n;
   hipStream_t s = (hipStream_t)stream;
   b.ctr = rng_counter(s);
-  b.done = (int*)ws;
-  const dim3 grid(grid_for(mx, 256 * 4, 2048), n);
-  b.total_blocks = (int)(grid.x * grid.y);
-  hipLaunchKernelGGL(adam_kernel, grid, dim3(256), 0, s, b);
+  b.scal = (float2*)ws;
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(64), 0, s, b);
+  hipLaunchKernelGGL(adam_kernel, dim3(nblocks), dim3(256), 0, s, b);
   return check_launch("adam_step");
 }
+
+extern "C" size_t msha_adam_workspace_size(void) { return sizeof(float2) * MSHA_MAX_ADAM; }

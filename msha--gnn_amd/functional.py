@@ -1188,8 +1188,8 @@ def _cast_many(pairs, stream):
 class _FeatureDropout(torch.autograd.Function):
     """dropout(Sfeatures), dropout(Rfeatures) (Ablation.py:296-297, Ours.py:161-162) in one
     launch; the backward regenerates both Philox masks in one launch.  A table registered
-    with ``optim.Adam.fuse_dropout_grad`` is updated by the backward itself (the Adam step
-    reads the dropout's output gradient and the mask): its gradient is never written."""
+    with ``optim.Adam.fuse_dropout_grad`` gets no gradient: the backward hands the
+    dropout's output gradient and mask seed to that optimizer, whose step reads them."""
 
     @staticmethod
     def forward(ctx, S, R, p, s_seed, r_seed):
@@ -1212,7 +1212,8 @@ class _FeatureDropout(torch.autograd.Function):
             leaf = ctx.params[k]
             opt = fused_optimizer_of(leaf) if d is not None else None
             if opt is not None and ctx.needs_input_grad[k]:
-                opt.fused_update(leaf, d, ctx.p, seed)  # no gradient tensor for this leaf
+                # no gradient tensor for this leaf: its optimizer step reads d + the mask
+                opt.stash_dropout_grad(leaf, d, ctx.p, seed)
                 d = None
             if d is None:
                 outs.append(None)

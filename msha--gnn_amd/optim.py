@@ -9,12 +9,13 @@ so a captured HIP graph (step.GraphedStep) replays the update with the right bia
 corrections.
 
 ``fuse_dropout_grad(param)``: the parameter's only consumer is the models' feature
-dropout (``Sfeatures``, Ablation.py:296 / Ours.py:161).  Its update then runs inside that
-dropout's backward, reading the dropout's output gradient and regenerating the Philox
-mask, instead of writing the 5M-float gradient for ``step()`` to read back; the
-parameter's ``.grad`` stays None and ``step()`` skips it.  (The update then happens during
-``loss.backward()``, as train.py's zero_grad / forward / backward / step loop allows; do
-not accumulate gradients over several backwards with a fused parameter.)
+dropout (``Sfeatures``, Ablation.py:296 / Ours.py:161).  Its backward then hands the
+dropout's OUTPUT gradient and mask seed to this optimizer instead of materialising the
+parameter's gradient, and ``step()`` folds the mask into its gradient read: the 5M-float
+gradient is never written or re-read, and every parameter still updates in ONE launch
+at ``step()``.  The parameter's ``.grad`` stays None.  (One backward per step for a fused
+parameter: a second backward before ``step()`` raises, as accumulation would need the
+gradient this path never forms.)
 """
 from __future__ import annotations
 
@@ -40,12 +41,13 @@ class Adam(torch.optim.Optimizer):
             raise ValueError("msha Adam: betas must be in [0, 1)")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps,
                                       weight_decay=weight_decay))
-        self._ws = {}  # device -> 16-byte completion counter of the launches
+        self._ws = {}  # device -> the launches' per-tensor scalars (stream-ordered reuse)
 
     def _workspace(self, dev):
         ws = self._ws.get(dev)
         if ws is None:
-            ws = self._ws[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
+            nb = int(_lib.load().msha_adam_workspace_size())
+            ws = self._ws[dev] = torch.zeros(nb, dtype=torch.uint8, device=dev)
         return ws
 
     def _state_of(self, p):
@@ -98,6 +100,13 @@ class Adam(torch.optim.Optimizer):
         for group in self.param_groups:
             by_dev = {}
             for p in group["params"]:
+                stash = getattr(p, "_msha_dropout_grad", None)
+                if stash is not None:  # fused: the dropout's output gradient + its mask
+                    dout, drop_p, seed = stash
+                    p._msha_dropout_grad = None
+                    self._check(p, dout)
+                    by_dev.setdefault(p.device, []).append(self._desc(p, dout, drop_p, seed))
+                    continue
                 if p.grad is None:
                     continue
                 g = p.grad
@@ -109,6 +118,13 @@ class Adam(torch.optim.Optimizer):
                 self._launch(group, descs, dev)
         return loss
 
+    def zero_grad(self, set_to_none: bool = True):
+        super().zero_grad(set_to_none)
+        for group in self.param_groups:
+            for p in group["params"]:
+                if getattr(p, "_msha_dropout_grad", None) is not None:
+                    p._msha_dropout_grad = None
+
     # ---------------------------------------------- fused dropout-backward updates
     def fuse_dropout_grad(self, param):
         """Update ``param`` inside its feature dropout's backward (functional.feature_dropout
@@ -117,14 +133,15 @@ class Adam(torch.optim.Optimizer):
         param._msha_fused_adam = weakref.ref(self)
         return param
 
-    @torch.no_grad()
-    def fused_update(self, param, dout, p: float, seed: int):
-        """One Adam step of ``param`` from the dropout's output gradient ``dout`` and its
-        mask (p, seed): called from the feature dropout's backward."""
+    def stash_dropout_grad(self, param, dout, p: float, seed: int):
+        """Called from the feature dropout's backward: keep the dropout's output gradient
+        ``dout`` and its mask (p, seed) for ``step()`` in place of ``param.grad``."""
+        if getattr(param, "_msha_dropout_grad", None) is not None:
+            raise RuntimeError("msha Adam: a fused parameter got a second backward before "
+                               "step(); gradient accumulation needs its .grad (do not fuse)")
         dout = dout.contiguous()
         self._check(param, dout)
-        group = self._group_of(param)
-        self._launch(group, [self._desc(param, dout, p, seed)], param.device)
+        param._msha_dropout_grad = (dout, float(p), int(seed))
 
 
 def fused_optimizer_of(param):

@@ -4,9 +4,10 @@ optimizer train.py builds (train.py:207: lr 1e-3, weight_decay 5e-4; stepped at 
 * the same gradients fed to both for 5 steps: parameters and moments within 1e-6
   relative (fp32; tails of n % 4 != 0 elements included), bf16 parameters within the
   bf16 bar;
-* the fused path: an ablation3 train loop where Sfeatures' update runs inside its
-  feature dropout's backward (fuse_dropout_grad) against the same loop with torch's
-  Adam -- every parameter after 5 steps within 1e-6, Sfeatures.grad never allocated;
+* the fused path: an ablation3 train loop where Sfeatures' update reads its feature
+  dropout's output gradient and mask (fuse_dropout_grad) against the same loop with
+  torch's Adam -- every parameter after 5 steps within 1e-6, Sfeatures.grad never
+  allocated;
 * the same loop replayed from a HIP graph (device step counts) gives the eager bits.
 """
 import numpy as np
@@ -103,7 +104,7 @@ def test_fused_feature_dropout_adam_matches_torch(cuda, msha):
     o_us.fuse_dropout_grad(m_us.Sfeatures)
     _train(m_ref, o_ref, adj, batches)
     _train(m_us, o_us, adj, batches)
-    assert m_us.Sfeatures.grad is None  # updated inside the dropout backward
+    assert m_us.Sfeatures.grad is None  # its step read the dropout's output gradient
     assert float(o_us.state[m_us.Sfeatures]["step"]) == len(batches)
     for (name, a), (_, b) in zip(m_ref.named_parameters(), m_us.named_parameters()):
         tol_close(b.detach().cpu().numpy(), a.detach().cpu().numpy(), 1e-6, 1e-6)
