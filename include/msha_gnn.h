@@ -103,6 +103,10 @@ typedef struct msha_groups {
 
 MSHA_API int msha_abi_version(void);
 MSHA_API const char* msha_last_error(void);
+/* Diagnostic (ABI 9): per-wave timeline of the skinny projection / weight-gradient kernels
+ * into a device buffer of `slots` x 64 uint64 words (NULL: off).  Only a library built with
+ * -DSK_TIMELINE records (build.py --variant timeline); otherwise MSHA_ERR_UNSUPPORTED. */
+MSHA_API int msha_debug_timeline(void* buf, int64_t slots);
 
 /* ---------------------------------------------------------------- dropout --- */
 /* Dropout under HIP-graph replay.  Every dropout draw of the library is Philox4x32-10

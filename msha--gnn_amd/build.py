@@ -21,6 +21,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIBDIR = os.path.join(PKG, "lib")
+# variants: "" (shipped) or "timeline" (-DSK_TIMELINE: the skinny kernels' per-wave
+# timeline, msha_debug_timeline; lib/libmsha_gnn_timeline.so, selected with MSHA_GNN_LIB)
+VARIANTS = {"": [], "timeline": ["-DSK_TIMELINE"]}
 OBJDIR = os.path.join(LIBDIR, "obj")
 LIB = os.path.join(LIBDIR, "libmsha_gnn.so")
 ARCH = os.environ.get("MSHA_OFFLOAD_ARCH", "gfx950")
@@ -42,11 +45,11 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src):
-    obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+def _compile(src, objdir=OBJDIR, defines=()):
+    obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
     if not _stale(obj, [src] + _headers()):
         return obj, None
-    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj + ".tmp"]
+    cmd = [HIPCC, *CFLAGS, *defines, "-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
@@ -54,27 +57,31 @@ def _compile(src):
     return obj, None
 
 
-def build(force: bool = False, jobs: int | None = None) -> str:
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force: bool = False, jobs: int | None = None, variant: str = "") -> str:
+    defines = VARIANTS[variant]
+    objdir = OBJDIR + (f"_{variant}" if variant else "")
+    lib = LIB.replace(".so", f"_{variant}.so") if variant else LIB
+    os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     if force:
-        for o in glob.glob(os.path.join(OBJDIR, "*.o")):
+        for o in glob.glob(os.path.join(objdir, "*.o")):
             os.remove(o)
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(_compile, srcs))
+        results = list(ex.map(lambda src: _compile(src, objdir, defines), srcs))
     errs = [e for _, e in results if e]
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
-    if force or _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+    if force or _stale(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-        os.replace(LIB + ".tmp", LIB)
-    return LIB
+        os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    v = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else ""
+    print(build(force="--force" in sys.argv, variant=v))

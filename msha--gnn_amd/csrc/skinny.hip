@@ -18,8 +18,9 @@
 //                 accumulator registers with v_mfma_f32_32x32x2_f32: per two rows a
 //                 lane loads one float4 of X and one of dh (+ de (x) a folded in), whose
 //                 4 elements feed 4 row (column) blocks, so the operands need no LDS at
-//                 all; the 4 waves of a block add their tiles in LDS in wave order and
-//                 the block writes one partial, reduced over blocks in block order.
+//                 all; the 4 row quarters of a block add their tiles pairwise through
+//                 LDS and the block writes one partial, reduced over blocks in block
+//                 order.
 //
 // Both are deterministic (fixed summation orders); numerics are the fp32 MFMA's exact
 // fma chain (fp32) or fp32 accumulation of bf16 products (bf16).
@@ -30,6 +31,50 @@
 
 namespace msha {
 namespace sk {
+
+// ---- per-wave timeline of the skinny kernels (diagnostic build, -DSK_TIMELINE) ---------
+// Lane 0 of every wave records into slot (global wave id) of a host-set buffer: word 0 =
+// XCC id << 32 | HW_ID (SIMD, CU, SE of the wave), word 1 = kernel tag, then (wall clock
+// at 100 MHz, shader clock) pairs at the kernel's marks.  scripts/skinny_timeline.py reads
+// them back.  In the shipped build every mark compiles to nothing.
+constexpr int kTlStride = 64;  // 64-bit words per wave slot
+#ifdef SK_TIMELINE
+__device__ uint64_t* g_tl_buf = nullptr;
+__device__ int64_t g_tl_slots = 0;
+struct Tl {
+  uint64_t* p;
+  int k;
+};
+__device__ __forceinline__ void tl_mark(Tl& r) {
+  if (r.p != nullptr && (threadIdx.x & 63) == 0 && r.k + 1 < kTlStride) {
+    r.p[r.k] = __builtin_amdgcn_s_memrealtime();
+    r.p[r.k + 1] = __builtin_amdgcn_s_memtime();
+  }
+  r.k += 2;
+}
+__device__ __forceinline__ Tl tl_open(int tag) {
+  const int64_t slot = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  Tl r{nullptr, 2};
+  if (g_tl_buf != nullptr && slot < g_tl_slots) r.p = g_tl_buf + slot * kTlStride;
+  if (r.p != nullptr && (threadIdx.x & 63) == 0) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    r.p[0] = ((uint64_t)xcc << 32) | hw;
+    r.p[1] = (uint64_t)tag;
+  }
+  tl_mark(r);
+  return r;
+}
+#define TL_OPEN(tag) ::msha::sk::Tl tl_ = ::msha::sk::tl_open(tag)
+#define TL_MARK() ::msha::sk::tl_mark(tl_)
+#else
+#define TL_OPEN(tag) \
+  do {               \
+  } while (0)
+#define TL_MARK() \
+  do {            \
+  } while (0)
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -63,20 +108,50 @@ struct ProjGeo {
 // consecutive k) and writes them to 4 image rows: a wave's 64 stores of one element
 // index fall in 8 banks (8-way).  One element per lane in M's order (k fastest) put every
 // lane of a wave on 2 banks (32-way), ~7 us of LDS time per block at K = N = 128.
-template <int K, int N>
-__device__ __forceinline__ void transpose_fill(float* Wl, const float* __restrict__ M, int tid,
-                                               int nthreads) {
-  using Gm = ProjGeo<float, K, N>;
-  for (int idx = tid; idx < K * N / 4; idx += nthreads) {
-    const int n = idx / (K / 4), k4 = idx % (K / 4);
-    const float4 v = *reinterpret_cast<const float4*>(M + n * K + 4 * k4);
-    const float e[4] = {v.x, v.y, v.z, v.w};
+// Every piece a thread copies is loaded before the first is written (one HBM round trip
+// for the whole fill instead of one per piece).
+template <int PIECES, int NT>
+struct Pieces {
+  static constexpr int IT = (PIECES + NT - 1) / NT;
+  static __device__ __forceinline__ bool ok(int idx) { return PIECES % NT == 0 || idx < PIECES; }
+  uint4 v[IT];
+  // buffer loads (a piece past the end reads 0): unlike plain loads of a __restrict__
+  // pointer, the compiler keeps them where they are written, ahead of later loads
+  __device__ __forceinline__ void load(const void* src, int tid) {
+    const rsrc_t r = make_rsrc(src, PIECES * 16u);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = 4 * k4 + j;
-      Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = e[j];
+    for (int i = 0; i < IT; ++i) {
+      const u32x4_t x = buf_b128(r, ok(tid + NT * i) ? 16u * (tid + NT * i) : kOOB);
+      v[i] = make_uint4(x[0], x[1], x[2], x[3]);
     }
   }
+};
+
+template <int K, int N, int NT>
+using WPieces = Pieces<K * N / 4, NT>;
+template <int K, int N, int NT>
+__device__ __forceinline__ void transpose_store(float* Wl, const WPieces<K, N, NT>& p, int tid) {
+  using Gm = ProjGeo<float, K, N>;
+#pragma unroll
+  for (int i = 0; i < p.IT; ++i) {
+    const int idx = tid + NT * i;
+    if (p.ok(idx)) {
+      const int n = idx / (K / 4), k4 = idx % (K / 4);
+      const uint4 v = p.v[i];
+      const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * k4 + j;
+        Wl[(4 * (k % Gm::KL) + k / Gm::KL) * Gm::PW + n] = __uint_as_float(e[j]);
+      }
+    }
+  }
+}
+template <int K, int N, int NT>
+__device__ __forceinline__ void transpose_fill(float* Wl, const float* __restrict__ M, int tid) {
+  WPieces<K, N, NT> p;
+  p.load(M, tid);
+  transpose_store<K, N, NT>(Wl, p, tid);
 }
 
 // proj_kernel's block: PROJ_WPS waves per SIMD when the resident W and one staging
@@ -125,6 +200,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int g = lane >> 4, r16 = lane & 15;
+  TL_OPEN(1);  // marks: entry, W resident, per item (start, MFMAs done), exit
 
   // Work items of a wave, in order: whole 16-row tiles gw, gw + nw, ... for the R rounds
   // every wave completes, then the tail: the L tiles left over are cut into PT column
@@ -153,41 +229,52 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
     return row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) + (uint32_t)(g * G::KL * sizeof(T))
                    : kOOB;
   };
-  // the first item's rows leave before the W copy, so their latency hides under it
+  // ---- W -> LDS once per block.  W's pieces load first, then the first item's rows:
+  // the W stores wait for W alone (vmcnt counts in order), so the block barrier is not
+  // held by the rows' HBM burst (every wave's first tile at once, ~16 MB at C4), whose
+  // latency hides under the W copy and the first steps instead.  (A load -> store loop
+  // paid one HBM round trip per W piece: ~4 us of a 40 us launch.)
+  Pieces<K * N * (int)sizeof(T) / 16, 64 * kWaves> wp;
+  wp.load(W, tid);
+  static_assert(N <= 64 * kWaves, "one score-vector element per thread");
+  const uint32_t aoff = tid < N ? 4u * tid : kOOB;
+  const float alv = FE > 0 ? buf_f32(make_rsrc(al, 4u * N), aoff) : 0.f;
+  const float arv = FE > 0 ? buf_f32(make_rsrc(ar, 4u * N), aoff) : 0.f;
+  asm volatile("" ::: "memory");  // keep the row loads behind W's
   u32x4_t buf[G::NLD];
   {
     const uint32_t off = n_items > 0 ? tile_off(item_tile(0)) : kOOB;
 #pragma unroll
     for (int i = 0; i < G::NLD; ++i) buf[i] = buf_b128(r_x, off + 16u * i);
   }
-
-  // ---- W -> LDS once per block
-  if (FE > 0) {
-    for (int n = tid; n < N; n += 64 * kWaves) {
-      als[n] = al != nullptr ? al[n] : 0.f;
-      ars[n] = ar != nullptr ? ar[n] : 0.f;
-    }
-  }
-  if (G::F32) {
-    for (int idx = tid; idx < K * N / 4; idx += 64 * kWaves) {
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < wp.IT; ++i) {
+    const int idx = tid + 64 * kWaves * i;
+    if (!wp.ok(idx)) continue;
+    if constexpr (G::F32) {
       const int k = idx / (N / 4), n4 = idx % (N / 4);
-      const float4 v = *reinterpret_cast<const float4*>(W + k * N + 4 * n4);
       const int kr = 4 * (k % G::KL) + k / G::KL;
-      *reinterpret_cast<float4*>(reinterpret_cast<float*>(Wl) + kr * G::PW + 4 * n4) = v;
-    }
-  } else {
-    for (int idx = tid; idx < K * N / 8; idx += 64 * kWaves) {
+      *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Wl) + kr * G::PW + 4 * n4) = wp.v[i];
+    } else {
       const int k = idx / (N / 8), n8 = idx % (N / 8);
-      const uint4 v = *reinterpret_cast<const uint4*>(W + k * N + 8 * n8);
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t e2[4] = {wp.v[i].x, wp.v[i].y, wp.v[i].z, wp.v[i].w};
       uint16_t* Wt = reinterpret_cast<uint16_t*>(Wl);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        Wt[(8 * n8 + e) * G::PW + k] = (uint16_t)(wv[e >> 1] >> (16 * (e & 1)));
+        Wt[(8 * n8 + e) * G::PW + k] = (uint16_t)(e2[e >> 1] >> (16 * (e & 1)));
     }
   }
+  if (FE > 0 && tid < N) {  // (a null al / ar reads 0: an empty descriptor)
+    als[tid] = alv;
+    ars[tid] = arv;
+  }
   __syncthreads();
-  if (n_items == 0) return;
+  TL_MARK();
+  if (n_items == 0) {
+    TL_MARK();
+    return;
+  }
 
   float* Tw = reinterpret_cast<float*>(smem + G::WBYTES) + w * 16 * S::TPS;
   // A register i of a tile feeds steps [i SPL, (i + 1) SPL): once they have issued, it is
@@ -197,8 +284,14 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   // step s + 1 read from LDS while step s's MFMAs issue), then the epilogue.  A column
   // block's accumulation and a head's score dot are the same operations in the same
   // order whichever item holds them, so a part's values are the whole tile's bits.
+  // (Running an item's epilogue inside the next item's MFMA steps instead -- two
+  // accumulator sets -- raised the MFMA share of the steady state from ~78 % to ~85 %
+  // but not the launch: 42.2 vs 40.6 us at C4, the last item's epilogue and the start
+  // dominate.  The two waves of a SIMD already overlap one's epilogue with the other's
+  // MFMAs.)
   auto tile = [&](auto nbp_c, int t, int cb0, u32x4_t* cur, uint32_t noff) {
     constexpr int NBP = decltype(nbp_c)::value;
+    TL_MARK();
     f32x4 acc[NBP];
 #pragma unroll
     for (int c = 0; c < NBP; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -248,6 +341,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
         for (int c = 0; c < NBP; ++c) bc[c] = bn[c];
       }
     }
+    TL_MARK();
     // ---- epilogue: stage the 16 x 16 NBP item (MFMA C layout: col = lane & 15, row =
     // 4 (lane >> 4) + reg), SWE columns at a time, then whole-row segments per wave
     // store + score dots
@@ -328,6 +422,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
     tile(std::integral_constant<int, G::NB>{}, item_tile(k), 0, buf, next_off(k));
   for (int k = R; k < n_items; ++k)
     tile(std::integral_constant<int, G::NB / PT>{}, item_tile(k), item_cb(k), buf, next_off(k));
+  TL_MARK();
 }
 
 // ------------------------------------------------------ pair linear (LLP 'mlp') ---
@@ -354,7 +449,7 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_kernel(
   const int g = lane >> 4, r16 = lane & 15;
 
   // ---- B[k][n] = Wlin[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL
-  transpose_fill<K, N>(Wl, Wlin, tid, 64 * kProjWaves);
+  transpose_fill<K, N, 64 * kProjWaves>(Wl, Wlin, tid);
   __syncthreads();
 
   float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
@@ -476,6 +571,7 @@ __global__ void __launch_bounds__(64 * kPairWaves) pair_bf16_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
 
+  // (a batched fill, as proj_kernel's, spills here at 3 waves per SIMD)
   for (int idx = tid; idx < N * K / 8; idx += 64 * kPairWaves) {
     const int n = idx / (K / 8), k8 = idx % (K / 8);
     *reinterpret_cast<uint4*>(Wl + n * Gm::PW + 8 * k8) =
@@ -612,14 +708,16 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
 
-  // B[k][n] = W[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL
-  transpose_fill<K, N>(Wl, Wt, tid, 64 * kProjWaves);
-  for (int k = tid; k < K; k += 64 * kProjWaves) {
-    a1s[k] = a1[k];
-    a2s[k] = a2 != nullptr ? a2[k] : 0.f;
-  }
-  __syncthreads();
-
+  // B[k][n] = W[n][k] -> the projection's W image [k'][n], k' = 4 (k % KL) + k / KL.
+  // W's pieces (and a1, a2) load before the first item's rows, so the block barrier
+  // waits for W alone (vmcnt counts in order) while the rows' burst is in flight.
+  WPieces<K, N, 64 * kProjWaves> wp;
+  wp.load(Wt, tid);
+  static_assert(K <= 64 * kProjWaves, "one score-vector element per thread");
+  const uint32_t aoff = tid < K ? 4u * tid : kOOB;
+  const float a1v = buf_f32(make_rsrc(a1, 4u * K), aoff);
+  const float a2v = buf_f32(make_rsrc(a2, 4u * K), aoff);  // (a null a2 reads 0)
+  asm volatile("" ::: "memory");  // keep the row loads behind W's
   float* Tw = reinterpret_cast<float*>(smem + Gm::WBYTES) + w * 16 * Gm::TPS;
   // items as proj_kernel: R whole-tile rounds, then the leftover tiles in PT column parts
   constexpr int PT = 4;
@@ -630,7 +728,6 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
   const int R = tiles / nw;
   const int units = PT * (tiles - R * nw);
   const int n_items = R + (gw < units ? (units - gw + nw - 1) / nw : 0);
-  if (n_items == 0) return;
   auto item_tile = [&](int k) -> int { return k < R ? gw + k * nw : R * nw + (gw + (k - R) * nw) / PT; };
   auto item_cb = [&](int k) -> int { return k < R ? 0 : ((gw + (k - R) * nw) % PT) * (Gm::NB / PT); };
 
@@ -713,7 +810,14 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
   };
   auto next_tile = [&](int k) -> int { return k < n_items ? item_tile(k) : tiles; };
   Tile ta, tb;
-  load_tile(item_tile(0), ta);
+  load_tile(next_tile(0), ta);  // (no items: rows past M, reads 0)
+  transpose_store<K, N, 64 * kProjWaves>(Wl, wp, tid);
+  if (tid < K) {
+    a1s[tid] = a1v;
+    a2s[tid] = a2v;
+  }
+  __syncthreads();
+  if (n_items == 0) return;
   for (int k = 0; k < n_items; k += 2) {
     load_tile(next_tile(k + 1), tb);
     __builtin_amdgcn_sched_barrier(0);
@@ -739,6 +843,7 @@ constexpr int kWgWaves = 8;
 #endif
 constexpr int kWgPD = WG_PD;  // two-row steps per load batch (two batches in flight)
 constexpr int kWgPitch = 132;
+constexpr int kWgImage = 128 * kWgPitch;  // floats of one 128 x 128 LDS tile image
 
 template <bool HO>
 __global__ void __launch_bounds__(64 * kWgWaves) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -746,7 +851,7 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
              int64_t ldd, const float* __restrict__ d1, const float* __restrict__ a1,
              const float* __restrict__ d2, const float* __restrict__ a2, int hH, int hF,
              float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float red[128 * kWgPitch];
+  __shared__ __attribute__((aligned(16))) float red[2 * kWgImage];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int nh = w & 1, rq = w >> 1;
@@ -757,6 +862,7 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
   const int r1 = __builtin_amdgcn_readfirstlane((int)(((int64_t)(gs + 1) * M) / nq));
   const int c0 = 64 * nh + 2 * i32;  // this lane's two dW columns
   const int hh = HO ? c0 / hF : 0;
+  TL_OPEN(2);  // marks: entry, row loop start, row loop done, block sum done, exit
   float2 av1 = make_float2(0.f, 0.f), av2 = av1;
   if (HO) {
     av1 = *reinterpret_cast<const float2*>(a1 + c0);
@@ -825,6 +931,7 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
   constexpr int R = 2 * kWgPD;
   Batch ba, bb;
   load(r0, ba);
+  TL_MARK();
   for (int rb = r0; rb < r1; rb += 2 * R) {
     // sched_barrier: the scheduler may not sink a batch's loads below the other
     // batch's MFMAs (it did, and the loop then waited on loads just issued)
@@ -837,67 +944,87 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
     compute(rb + R, bb);
     __builtin_amdgcn_sched_barrier(0);
   }
-  // ---- block sum (LDS): the 4 row quarters of each column half added in quarter order
+  TL_MARK();
+  // ---- block sum, pairwise: quarters 2, 3 park their tiles in LDS images 0, 1; quarters
+  // 0, 1 add them in; quarter 1 parks its sum in image 0; quarter 0 adds it and stores
+  // the block's partial straight from its accumulators.  Order (q0 + q2) + (q1 + q3).
+  // Every read of a tile is issued before its adds (16 in flight): the earlier in-place
+  // read-add-write per element serialised one LDS round trip per element (7 us a launch).
   // 32x32 C layout: reg v of lane l is row 8 (v / 4) + 4 (l >> 5) + (v % 4), col l & 31
-#pragma unroll 1
-  for (int qq = 0; qq < kWgWaves / 2; ++qq) {
-    if (rq == qq) {
+  auto row_of = [&](int t, int v) { return 4 * (8 * (v >> 2) + 4 * q + (v & 3)) + t; };
+  auto park = [&](int img) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int a = 4 * (8 * (v >> 2) + 4 * q + (v & 3)) + t;
-          float2* dst = reinterpret_cast<float2*>(red + a * kWgPitch + c0);
-          float2 s = make_float2(acc[t][0][v], acc[t][1][v]);
-          if (qq > 0) {
-            const float2 o = *dst;
-            s = make_float2(o.x + s.x, o.y + s.y);
-          }
-          *dst = s;
-        }
+      for (int v = 0; v < 16; ++v)
+        *reinterpret_cast<float2*>(red + img * kWgImage + row_of(t, v) * kWgPitch + c0) =
+            make_float2(acc[t][0][v], acc[t][1][v]);
+  };
+  auto absorb = [&](int img) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float2 o[16];
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        o[v] = *reinterpret_cast<const float2*>(red + img * kWgImage + row_of(t, v) * kWgPitch + c0);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        acc[t][0][v] += o[v].x;
+        acc[t][1][v] += o[v].y;
+      }
     }
-    __syncthreads();
-  }
-  float* out = slab + (int64_t)blockIdx.x * (128 * 128);
+  };
+  if (rq >= 2) park(rq - 2);
+  __syncthreads();
+  if (rq < 2) absorb(rq);
+  __syncthreads();
+  if (rq == 1) park(0);
+  __syncthreads();
+  TL_MARK();
+  if (rq == 0) {
+    absorb(0);
+    float* out = slab + (int64_t)blockIdx.x * (128 * 128);
 #pragma unroll
-  for (int k = 0; k < 4096 / (64 * kWgWaves); ++k) {
-    const int idx = tid + 64 * kWgWaves * k;  // float4 index: row idx / 32, col 4 (idx % 32)
-    const int a = idx >> 5, c4 = (idx & 31) * 4;
-    *reinterpret_cast<float4*>(out + a * 128 + c4) =
-        *reinterpret_cast<const float4*>(red + a * kWgPitch + c4);
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int v = 0; v < 16; ++v)  // a row's 32 lanes write 256 contiguous bytes
+        *reinterpret_cast<float2*>(out + row_of(t, v) * 128 + c0) =
+            make_float2(acc[t][0][v], acc[t][1][v]);
   }
+  TL_MARK();
 }
 
-// C[a, n] (= or +=) sum over blocks b of slab[b, a, n], b ascending within each of 16
-// interleaved groups, the groups added in a fixed LDS tree.  Block = 16 groups x 16
-// float4 columns; grid = 128 * 128 / 64 blocks.
+// C[a, n] (= or +=) sum over blocks b of slab[b, a, n], b ascending within each of 32
+// interleaved groups, the groups added in a fixed LDS tree.  Block = 32 groups x 8
+// float4 columns (128 contiguous bytes per group); grid = 128 * 128 / 32 blocks.  With
+// nb <= 256 every load of a thread is in flight at once (one HBM round trip; the
+// earlier 16-group layout took two and ran latency-bound at ~5 us).
+constexpr int kWrGroups = 32, kWrCols = 8, kWrRB = 8;
 template <typename TC>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nb,
                                                            TC* __restrict__ C, int64_t ldc,
                                                            float beta) {
   __shared__ float4 part[256];
-  const int zq = threadIdx.x >> 4, cq = threadIdx.x & 15;
-  const int f4 = blockIdx.x * 16 + cq;  // float4 index in the 128 x 128 tile
+  const int zq = threadIdx.x / kWrCols, cq = threadIdx.x % kWrCols;
+  const int f4 = blockIdx.x * kWrCols + cq;  // float4 index in the 128 x 128 tile
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  // 8 slabs' loads in flight before they are added (same order: b ascending)
-  constexpr int RB = 8;
-  for (int b0 = zq; b0 < nb; b0 += 16 * RB) {
-    float4 v[RB];
+  for (int b0 = zq; b0 < nb; b0 += kWrGroups * kWrRB) {
+    float4 v[kWrRB];
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int b = b0 + 16 * j;
+    for (int j = 0; j < kWrRB; ++j) {
+      const int b = b0 + kWrGroups * j;
       v[j] = b < nb ? reinterpret_cast<const float4*>(slab + (int64_t)b * (128 * 128))[f4]
                     : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int j = 0; j < RB; ++j)
-      if (b0 + 16 * j < nb) s = make_float4(s.x + v[j].x, s.y + v[j].y, s.z + v[j].z, s.w + v[j].w);
+    for (int j = 0; j < kWrRB; ++j)
+      if (b0 + kWrGroups * j < nb) s = make_float4(s.x + v[j].x, s.y + v[j].y, s.z + v[j].z, s.w + v[j].w);
   }
   part[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 8; o >= 1; o >>= 1) {
+  for (int o = kWrGroups / 2; o >= 1; o >>= 1) {
     if (zq < o) {
-      const float4 v = part[threadIdx.x + 16 * o];
+      const float4 v = part[threadIdx.x + kWrCols * o];
       float4& d = part[threadIdx.x];
       d = make_float4(d.x + v.x, d.y + v.y, d.z + v.z, d.w + v.w);
     }
@@ -1060,9 +1187,27 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
   else
     hipLaunchKernelGGL(sk::wgrad_kernel<false>, dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s, (int)K, A,
                        sAk, B, sBk, nullptr, nullptr, nullptr, nullptr, 1, 4, slab);
-  hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>, dim3(128 * 128 / 64), dim3(256), 0, s,
+  hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>, dim3(128 * 128 / (4 * sk::kWrCols)), dim3(256), 0, s,
                      (const float*)slab, (int)nb, C, ldc, beta);
   return 1;
 }
 
 }  // namespace msha
+
+// Diagnostic: install (buf != NULL) or remove the per-wave timeline buffer of the skinny
+// kernels (slots x 64 uint64 words, device memory); MSHA_ERR_UNSUPPORTED unless the library
+// was built with -DSK_TIMELINE (build.py --variant timeline).
+extern "C" int msha_debug_timeline(void* buf, int64_t slots) {
+#ifdef SK_TIMELINE
+  uint64_t* p = (uint64_t*)buf;
+  const int64_t n = buf != nullptr ? slots : 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::sk::g_tl_buf), &p, sizeof(p)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(msha::sk::g_tl_slots), &n, sizeof(n)) != hipSuccess)
+    return msha::fail(MSHA_ERR_HIP, "debug_timeline: hipMemcpyToSymbol failed");
+  return MSHA_OK;
+#else
+  (void)buf;
+  (void)slots;
+  return msha::fail(MSHA_ERR_UNSUPPORTED, "debug_timeline: library built without SK_TIMELINE");
+#endif
+}
