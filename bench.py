@@ -120,8 +120,8 @@ def _newest_first(path):  # round1_syn100k_v10 after _v9: compare the numbers
 
 def pmc_lookup(patterns, glob_pat):
     """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) summed over
-    the kernels matching ``patterns`` (regexes; each must match one kernel of the same
-    summary) in the newest committed profile matching ``glob_pat``
+    the kernels matching ``patterns`` (regexes; each must match a kernel of the same
+    summary, several matches of one pattern are averaged) in the newest committed profile matching ``glob_pat``
     (profiles/<glob>/pmc_summary.json, written by scripts/summarize_profile.py from
     separate rocprofv3 --pmc passes).  (None, None) if absent."""
     import glob
@@ -141,7 +141,8 @@ def pmc_lookup(patterns, glob_pat):
             if not hit:
                 ok = False
                 break
-            tot += float(hit[0]["hbm_bytes_per_launch_corrected"])
+            # (several instances of one pattern, e.g. the u and v aggregates: their mean)
+            tot += sum(float(h["hbm_bytes_per_launch_corrected"]) for h in hit) / len(hit)
         if ok:
             return tot, os.path.relpath(path, ROOT)
     return None, None
@@ -153,9 +154,11 @@ def fwd_kernel_pattern(H, F, bf16, variant="bat"):
     short rows) or 'bat' (score layout, er table)."""
     if variant in ("rs", "gl"):
         rs = "true" if variant == "rs" else "false"
-        return (rf"edge_attn_fwd_gl_kernelILi{H}ELi{F}EDF16bLi\d+ELb[01]ELb{int(variant == 'rs')}"
+        # (a demangled bf16 name reads "<H, F, bool _Accum, int, E, RT, RS, ATTD>")
+        return (rf"edge_attn_fwd_gl_kernel(ILi{H}ELi{F}EDF16bLi\d+ELb[01]ELb{int(variant == 'rs')}"
+                rf"|<{H}, {F}, bool _Accum, .*, (true|false), {rs}, (true|false)>)"
                 if bf16 else rf"edge_attn_fwd_gl_kernel<{H}, {F}, float, \d+, (true|false), {rs}")
-    return (rf"edge_attn_fwd(?:_bat)?_kernelILi{H}ELi{F}EDF16b" if bf16 else
+    return (rf"edge_attn_fwd(?:_bat)?_kernel(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)" if bf16 else
             rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?(, (true|false))?>")
 
 
@@ -363,13 +366,17 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
     nch = lay.graph._plan["n_chunks"]
     rt, rs = lay.rowterms, lay.row_scores
     bf = s == 2
-    # rocprofv3 leaves bf16 instantiations mangled (DF16b), fp32 ones demangled
-    tmpl = (lambda k: rf"{k}ILi{H}ELi{F}EDF16b") if bf else (lambda k: rf"{k}<{H}, {F}, float")
+    # rocprofv3 leaves most bf16 instantiations mangled (DF16b) and demangles some with
+    # the bf16 type as "bool _Accum"; fp32 ones are demangled
+    tmpl = ((lambda k: rf"{k}(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)") if bf else
+            (lambda k: rf"{k}<{H}, {F}, float"))
     pats = {
         "msha_edge_attention_fwd": [fwd_kernel_pattern(H, F, bf, lay.fwd_variant)],
         "msha_edge_attention_bwd_fused": [tmpl("bwd_row_stats_kernel"),
                                           tmpl("bwd_cols(_eh)?_kernel")]
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
+        "msha_edge_attention_bwd_rows": [tmpl("edge_attn_bwd_rows(_gl)?_kernel")],
+        "msha_csc_aggregate": [tmpl("csc_aggregate_kernel")],
     }
     out = []
     v = lay.v_branch
@@ -579,9 +586,9 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, group_ok, steps=16, wa
 
 def _pair_pattern(mode, bf16):
     """rocprofv3 names of the pair kernels (skinny.hip pair_kernel, scorer.hip inner)."""
-    if mode == "mlp":
-        return r"pair_kernel.*bf16|pair_kernel.*DF16b" if bf16 else r"pair_kernel(?!.*(bf16|DF16b))"
-    return r"pair_inner.*(bf16|DF16b)" if bf16 else r"pair_inner(?!.*(bf16|DF16b))"
+    if mode == "mlp":  # skinny.hip pair_bf16_kernel (left mangled) / pair_kernel<K, N>
+        return r"pair_bf16_kernel" if bf16 else r"sk::pair_kernel<"
+    return r"pair_inner_kernelIDF16b" if bf16 else r"pair_inner_kernel<float>"
 
 
 def _year_graph(year):
@@ -993,8 +1000,9 @@ def main():
         rowptr, col = synth_graph(n, w["e"], seed=0)
     e = len(col)
     K, Wu = args.steps, args.warmup
+    # (bip1m: the OursLayer3 core with its u and v aggregates, as the default run's leg)
     head, graph = layer_leg(clock, dev, f"gat_layer_{wl}", rowptr, col, n, m, fin, H, F, K, Wu,
-                            world, args.eager, workload=wl)
+                            world, args.eager, workload=wl, v_branch=wl == "bip1m")
     drop_leg = None
     if not args.no_dropout_leg:
         # the reference's training forward drops attention at p = 0.5 (Ablation.py:271):
@@ -1009,7 +1017,7 @@ def main():
         bf16_leg, _ = layer_leg(clock, dev, f"gat_layer_{wl} (config C3: bf16 tables, bf16 "
                                 "MFMA projection, fp32 scores/softmax)", rowptr, col, n, m, fin,
                                 H, F, K, Wu, world, args.eager, dtype=torch.bfloat16,
-                                graph=graph, workload=wl)
+                                graph=graph, workload=wl, v_branch=wl == "bip1m")
     link = None
     if not args.no_link_score and wl not in ("r15", "bip1m"):
         done = None if dist else _world1_group(dev)
