@@ -190,44 +190,6 @@ def test_ours_attention_bf16_vs_fp32(cuda, msha):
 
 
 # ------------------------------------------------------------------ modules
-def test_ablation3_bf16_model(cuda, msha):
-    """ablation3.to(bfloat16) train step vs the same model in fp32 with the
-    bf16-rounded parameters (sub512 fixture graph)."""
-    import torch.nn.functional as Fn
-    from msha_gnn_amd import layers
-
-    z = golden("sub512.npz")
-    gdp = {i: float(x) for i, x in enumerate(z["gdp"])}
-    torch.manual_seed(0)
-    m32 = layers.ablation3(128, 64, 32, 2, 0.0, gdp, 512, 32).to(cuda)
-    with torch.no_grad():
-        for prm in m32.parameters():
-            prm.copy_(prm.to(BF).float())
-    m16 = layers.ablation3(128, 64, 32, 2, 0.0, gdp, 512, 32).to(cuda)
-    m16.load_state_dict(m32.state_dict())
-    m16 = m16.to(BF)
-    adj = torch.as_tensor(z["adj_norm"], device=cuda)
-    si = torch.as_tensor(z["source_index"], device=cuda)
-    ri = torch.as_tensor(z["recipient_index"], device=cuda)
-    outs = {}
-    for name, model in (("f32", m32), ("bf16", m16)):
-        model.train()
-        out = model(adj, None, None, si)
-        loss = Fn.nll_loss(out[si].float(), ri)
-        loss.backward()
-        outs[name] = (out.float().detach().cpu().numpy(), loss.item(),
-                      {k: p.grad.float().cpu().numpy() for k, p in model.named_parameters()
-                       if p.grad is not None})
-    tol_close(outs["bf16"][0], outs["f32"][0], 3e-2, 3e-2)
-    assert abs(outs["bf16"][1] - outs["f32"][1]) < 3e-2 * abs(outs["f32"][1])
-    assert outs["bf16"][2].keys() == outs["f32"][2].keys()
-    for k in ("attention_0.W1", "attention_0.W2", "attention_1.W1", "Sfeatures"):
-        g16, g32 = outs["bf16"][2][k], outs["f32"][2][k]
-        assert np.isfinite(g16).all(), k
-        cos = float((g16 * g32).sum() / (np.linalg.norm(g16) * np.linalg.norm(g32) + 1e-30))
-        assert cos > 0.99, (k, cos)
-
-
 @pytest.mark.parametrize("mode", ["inner", "mlp"])
 def test_score_pairs_bf16(cuda, mode):
     """Fused gather + LinkPredictor (LLP.py:104-115, :233) on a bf16 table (config C5)

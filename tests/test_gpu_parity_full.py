@@ -139,10 +139,10 @@ def test_c4_forward_backward_every_row(cuda, c4, dt):
         dh_q = (g_def[2].float() + g_def[0][:, :, None] * al.detach()[None]
                 + g_def[1][:, :, None] * ar.detach()[None]).to(torch.bfloat16)
         tol_close(_np64(W.grad), X64.T @ _np64(dh_q).reshape(n, H * Fd), tol, tol)
-        # ... and end to end, where the 100k-row reduction of bf16-rounded dh (2^-9
-        # relative per element) lands within 2e-2 of the fp64 value (a weight gradient:
-        # the north_star bf16 bar names attention weights and embeddings)
-        tol_close(_np64(W.grad), dW_ref, 2e-2, 2e-2)
+        # ... and end to end against fp64 at the bf16 bar: measured 1.9e-3 of max|dW|
+        # (scripts/bf16_dw_probe.py: the bf16 storage of W.grad itself, 2^-9, dominates;
+        # the bf16 operand dh adds 1.3e-3, the edge kernels' d_hc error 1e-5)
+        tol_close(_np64(W.grad), dW_ref, BF16_TOL, BF16_TOL)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
@@ -522,6 +522,50 @@ def test_model_train_step_full_2015(cuda, msha, kind):
                 assert params[name].grad is None
                 continue
             tol_close(params[name].grad.cpu().numpy(), p64[k].grad.numpy(), F32_TOL, F32_TOL)
+
+
+def test_ablation3_bf16_model_vs_fp64(cuda, msha):
+    """configs[2] for the whole model train.py builds (ablation3, train.py:206) after
+    ``model.to(bfloat16)``: log-probabilities and the nll loss against the dense fp64
+    restatement on the same bf16-rounded parameters (the north_star bf16 bar, 1e-2),
+    on the full 2015 graph; the embedding gradient (Sfeatures) within 1e-2 on >= 99 %
+    of its elements, every other gradient finite and printed against fp64."""
+    from msha_gnn_amd import layers
+
+    yg = _year(msha, cuda, "2015")
+    n, m = yg["n"], yg["m"]
+    gdp = {i: 0.01 * (i % 97) for i in range(n)}
+    torch.manual_seed(0)
+    model = layers.ablation3(128, 64, m, 2, 0.0, gdp, n, m).to(cuda).to(torch.bfloat16)
+    model.train()
+    src_t = torch.as_tensor(_batch(yg), device=cuda)
+    tgt = torch.as_tensor(yg["flows"][np.random.default_rng(1).choice(len(yg["flows"]), 64), 1],
+                          device=cuda)
+    with _Branches() as rec:
+        out = model(yg["adj"], None, None, src_t)
+    assert out.dtype == torch.bfloat16
+    loss = F.nll_loss(out[src_t].float(), tgt)
+    loss.backward()
+    out64, loss64, Sf, Rf, oW, heads = _model_grads_vs_dense(model, yg, src_t, tgt, False,
+                                                             rec.heads(2))
+    tol_close(out.detach().float().cpu().numpy(), out64.detach().numpy(), BF16_TOL, BF16_TOL)
+    assert abs(float(loss.detach()) - float(loss64.detach())) <= BF16_TOL * abs(float(loss64.detach()))
+    pairs = [("Sfeatures", model.Sfeatures.grad, Sf.grad), ("Rfeatures", model.Rfeatures.grad,
+                                                             Rf.grad),
+             ("out_att.W", model.out_att.W.grad, oW.grad)]
+    for i, (att, p64) in enumerate(zip(model.attentions, heads)):
+        params = dict(att.named_parameters())
+        pairs += [(f"attention_{i}.{name}", params[name].grad, p64[k].grad)
+                  for k, name in D.GRAD_KEYS.items() if k not in ("a3", "a4")]
+    for name, got, r64 in pairs:
+        got, r64 = got.float().cpu().numpy(), r64.numpy()
+        assert np.isfinite(got).all(), name
+        scale = np.abs(r64).max()
+        bad = np.abs(got - r64) > BF16_TOL * np.abs(r64) + BF16_TOL * scale
+        print(f"{name}: max err {np.abs(got - r64).max() / scale:.3g} of max; "
+              f"{bad.mean():.3%} of elements > 1e-2")
+        if name == "Sfeatures":
+            assert bad.mean() <= 0.01, f"{name}: {bad.mean():.3%} of elements off by > 1e-2"
 
 
 @pytest.mark.parametrize("year", ["2015", "2018"])
