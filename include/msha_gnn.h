@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 9
+#define MSHA_ABI_VERSION 10
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -329,6 +329,22 @@ MSHA_API int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const flo
                                       int32_t heads, int32_t feat, const float* de,
                                       const float* a, const float* de2, const float* a2,
                                       msha_stream_t stream);
+
+/* The projection's whole parameter backward in one pass over the rows (replaces
+ * msha_gemm_f32_head_outer with operand 1 + msha_head_colsum, Ablation.py:262-267
+ * backward): C = A (B + de (x) a [+ de2 (x) a2]) (dW = X^T dh'), and
+ * cs1[n] = sum_k de[k, n / feat] T[k, n], cs2 likewise with de2 (d_al, d_ar with T the
+ * forward's h), T laid out as B (row pitch sBk, unit column stride).  beta = 0.  Only
+ * the resident-accumulator weight-gradient shape (M = N = 128, K >= 4096, splits >= 16);
+ * MSHA_ERR_UNSUPPORTED (nothing launched) otherwise.  cs_ws: at least
+ * msha_head_outer_colsum_workspace_size(N) bytes; ws as msha_gemm_f32. */
+MSHA_API size_t msha_head_outer_colsum_workspace_size(int64_t N);
+MSHA_API int msha_gemm_f32_head_outer_colsum(
+    int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk, const float* B,
+    int64_t sBk, int64_t sBn, float* C, int64_t ldc, int32_t splits, void* ws, size_t ws_bytes,
+    int32_t heads, int32_t feat, const float* de, const float* a, const float* de2,
+    const float* a2, const float* T, float* cs1, float* cs2, void* cs_ws, size_t cs_ws_bytes,
+    msha_stream_t stream);
 
 /* Projection with the attention-score halves fused into its epilogue:
  *   h = X @ W  (M x heads*feat),  el[m,h] = h[m,h,:] . al[h,:],  er[m,h] = h[m,h,:] . ar[h,:]

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 9  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 10  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -134,6 +134,10 @@ SIGNATURES = {
     "msha_project_scores_row_order": (C.c_int, [I64, I64, I32, I32, I32]),
     "msha_gemm_f32_head_outer": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, F32,
                                            I32, P, SZ, I32, I32, I32, P, P, P, P, P]),
+    "msha_head_outer_colsum_workspace_size": (SZ, [I64]),
+    "msha_gemm_f32_head_outer_colsum": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P,
+                                                  I64, I32, P, SZ, I32, I32, P, P, P, P, P, P,
+                                                  P, P, SZ, P]),
     "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
     "msha_head_colsum_workspace_size": (SZ, [I64, I32, I32]),
     "msha_head_colsum": (C.c_int, [I64, I32, I32, I32, P, P, P, P, P, P, SZ, P]),

@@ -11,6 +11,12 @@
 #ifndef FWD_EPL_BF16
 #define FWD_EPL_BF16 2
 #endif
+#ifndef GL_EPL_BF16
+#define GL_EPL_BF16 FWD_EPL_BF16  // the gather-layout forward's long chunks, bf16 tables
+#endif
+#ifndef GL_EPL_F32
+#define GL_EPL_F32 FWD_EPL
+#endif
 #ifndef FWD_WPE
 #define FWD_WPE 1
 #endif
@@ -67,7 +73,8 @@ constexpr int fwd_epl() {
 template <int H, int F, typename T>
 constexpr int gl_ngi_long() {
   using G = Geo<H, F, T>;
-  return fwd_epl<H, F, T>() * G::CE / G::EPI;
+  constexpr int epl = (G::QPL == 1 && G::CE <= 16) ? (sizeof(T) == 2 ? GL_EPL_BF16 : GL_EPL_F32) : 1;
+  return epl * G::CE / G::EPI;
 }
 template <int H, int F, typename T>
 constexpr int gl_ngi_short() {

@@ -769,6 +769,44 @@ extern "C" int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const f
   return gemm_run(p, operand == 0 ? HO_A : HO_B, beta, splits, ws, ws_bytes, (hipStream_t)stream);
 }
 
+extern "C" size_t msha_head_outer_colsum_workspace_size(int64_t N) {
+  return N > 0 ? (size_t)2 * (size_t)N * 256 * sizeof(float) : 0;
+}
+
+// The projection's weight gradient and score-vector gradients in one pass over the rows
+// (Ablation.py:262-267 backward): C = A (B + de (x) a [+ de2 (x) a2]) as
+// msha_gemm_f32_head_outer with operand 1, plus cs1[n] = sum_k de[k, n / feat] T[k, n]
+// (cs2 with de2) -- msha_head_colsum's outputs -- accumulated by the same launch from a
+// table T with B's layout.  Only the resident-accumulator weight-gradient shape (skinny.hip:
+// M = N = 128, K >= 4096 rows, fp32); MSHA_ERR_UNSUPPORTED (nothing launched) otherwise,
+// and the caller runs the two ops.
+extern "C" int msha_gemm_f32_head_outer_colsum(
+    int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk, const float* B,
+    int64_t sBk, int64_t sBn, float* C, int64_t ldc, int32_t splits, void* ws, size_t ws_bytes,
+    int32_t heads, int32_t feat, const float* de, const float* a, const float* de2,
+    const float* a2, const float* T, float* cs1, float* cs2, void* cs_ws, size_t cs_ws_bytes,
+    msha_stream_t stream) {
+  MSHA_ARG_CHECK(M > 0 && N > 0 && K > 0, "gemm_f32_head_outer_colsum: bad sizes");
+  MSHA_ARG_CHECK(A && B && C && de && a && T && cs1 && ((de2 == nullptr) == (a2 == nullptr)) &&
+                     ((de2 == nullptr) == (cs2 == nullptr)),
+                 "gemm_f32_head_outer_colsum: null pointer");
+  MSHA_ARG_CHECK(heads > 0 && feat > 0 && feat % 4 == 0 && N == (int64_t)heads * feat,
+                 "gemm_f32_head_outer_colsum: N must be heads*feat, feat a multiple of 4");
+  MSHA_ARG_CHECK(splits >= 1 && splits <= 65535, "gemm_f32_head_outer_colsum: splits out of range");
+  MSHA_ARG_CHECK(cs_ws && cs_ws_bytes >= msha_head_outer_colsum_workspace_size(N),
+                 "gemm_f32_head_outer_colsum: colsum workspace too small");
+  if (!aligned16(a) || (a2 != nullptr && !aligned16(a2)))
+    return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum: 16-byte aligned a, a2");
+  hipStream_t s = (hipStream_t)stream;
+  int nb = 0;
+  if (!skinny_wgrad(M, N, K, A, sAm, sAk, B, sBk, sBn, C, ldc, 0.f, splits, ws, ws_bytes, heads,
+                    feat, de, a, de2, a2, s, T, (float*)cs_ws, &nb))
+    return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum: shape outside the fused kernel");
+  hipLaunchKernelGGL(head_colsum_reduce_kernel, dim3((unsigned)((2 * N + 3) / 4)), dim3(256), 0, s,
+                     nb, (int)N, (const float*)cs_ws, cs1, cs2);
+  return check_launch("gemm_f32_head_outer_colsum");
+}
+
 // every projection path computes its score dots in the row-score order (skinny.hip
 // proj_kernel, this file's EPI_SCORE f4_dot + xor tree, gemm_bf16.hip's EPI_SCORE on the
 // rounded row, small.hip): 1 for any valid shape

@@ -837,6 +837,11 @@ __global__ void __launch_bounds__(64 * kProjWaves) dx_kernel(
 // -> A of row blocks t = 0..3 (dW row 4i + t), D'[r+q, 64 nh + 2i .. +1] -> B of
 // column blocks u = 0..1 (dW column 64 nh + 2i + u).  v_mfma_f32_32x32x2_f32, k = q.
 // Block = 8 waves: column half nh = w & 1, row quarter w >> 1 of the block's rows.
+// CS (the projection's score-vector gradients, Ablation.py:266-267 backward): the same
+// rows also give dal[n] = sum_r d1[r, n / hF] hs[r, n] (and dar with d2) -- one 8-byte
+// load of the forward's h per lane and row next to D's, 4 fmas -- written as per-block
+// partials part[which][n][block] for head_colsum_reduce_kernel (gemm.hip), instead of a
+// second pass over h (msha_head_colsum).
 constexpr int kWgWaves = 8;
 #ifndef WG_PD
 #define WG_PD 2
@@ -845,13 +850,15 @@ constexpr int kWgPD = WG_PD;  // two-row steps per load batch (two batches in fl
 constexpr int kWgPitch = 132;
 constexpr int kWgImage = 128 * kWgPitch;  // floats of one 128 x 128 LDS tile image
 
-template <bool HO>
+template <bool HO, bool CS>
 __global__ void __launch_bounds__(64 * kWgWaves) __attribute__((amdgpu_waves_per_eu(2, 2)))
 wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __restrict__ D,
              int64_t ldd, const float* __restrict__ d1, const float* __restrict__ a1,
              const float* __restrict__ d2, const float* __restrict__ a2, int hH, int hF,
-             float* __restrict__ slab) {
+             float* __restrict__ slab, const float* __restrict__ hs, float* __restrict__ cpart) {
+  static_assert(!CS || HO, "the score-vector gradients need the head terms");
   __shared__ __attribute__((aligned(16))) float red[2 * kWgImage];
+  __shared__ float csred[CS ? 4 * 2 * 128 : 1];  // [row quarter][which][column]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int nh = w & 1, rq = w >> 1;
@@ -882,12 +889,15 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
   const rsrc_t r_d = make_rsrc(D, (uint32_t)((int64_t)M * ldd * 4));
   const rsrc_t r_e1 = make_rsrc(HO ? d1 : nullptr, HO ? (uint32_t)((int64_t)M * hH * 4) : 0u);
   const rsrc_t r_e2 = make_rsrc(HO ? d2 : nullptr, HO && d2 ? (uint32_t)((int64_t)M * hH * 4) : 0u);
+  const rsrc_t r_h = make_rsrc(CS ? hs : nullptr, CS ? (uint32_t)((int64_t)M * ldd * 4) : 0u);
+  float2 cs1 = make_float2(0.f, 0.f), cs2 = cs1;  // CS: this lane's rows' dal, dar terms
   const uint32_t sx = (uint32_t)ldx * 4u, sd = (uint32_t)ldd * 4u, se = (uint32_t)hH * 4u;
   const uint32_t ox = 16u * i32, od = 4u * c0, oe = 4u * hh;
   struct Batch {
     u32x4_t x[kWgPD];
     float d0[kWgPD], d1v[kWgPD];
     float e1[kWgPD], e2[kWgPD];
+    float h0[CS ? kWgPD : 1], h1[CS ? kWgPD : 1];
   };
   auto load = [&](int rb, Batch& b) {
 #pragma unroll
@@ -905,6 +915,11 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
         b.e1[p] = buf_f32(r_e1, (ur * se + oe) | m);
         b.e2[p] = buf_f32(r_e2, (ur * se + oe) | m);
       }
+      if (CS) {  // (h has D's row pitch: the host checks)
+        const auto hv = __builtin_amdgcn_raw_buffer_load_b64(r_h, (ur * sd + od) | m, 0, 0);
+        b.h0[p] = __uint_as_float(hv[0]);
+        b.h1[p] = __uint_as_float(hv[1]);
+      }
     }
   };
   auto compute = [&](int rb, const Batch& cb) {
@@ -914,6 +929,12 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
       if (HO) {
         d[0] = fmaf(cb.e2[p], av2.x, fmaf(cb.e1[p], av1.x, d[0]));
         d[1] = fmaf(cb.e2[p], av2.y, fmaf(cb.e1[p], av1.y, d[1]));
+      }
+      if (CS) {
+        cs1.x = fmaf(cb.e1[p], cb.h0[p], cs1.x);
+        cs1.y = fmaf(cb.e1[p], cb.h1[p], cs1.y);
+        cs2.x = fmaf(cb.e2[p], cb.h0[p], cs2.x);
+        cs2.y = fmaf(cb.e2[p], cb.h1[p], cs2.y);
       }
       const float xa[4] = {__uint_as_float(cb.x[p].x), __uint_as_float(cb.x[p].y),
                            __uint_as_float(cb.x[p].z), __uint_as_float(cb.x[p].w)};
@@ -974,6 +995,16 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
       }
     }
   };
+  if (CS) {  // the two row parities of the lane pair, then the quarters via LDS
+    cs1.x += __shfl_xor(cs1.x, 32);
+    cs1.y += __shfl_xor(cs1.y, 32);
+    cs2.x += __shfl_xor(cs2.x, 32);
+    cs2.y += __shfl_xor(cs2.y, 32);
+    if (q == 0) {
+      *reinterpret_cast<float2*>(csred + (rq * 2 + 0) * 128 + c0) = cs1;
+      *reinterpret_cast<float2*>(csred + (rq * 2 + 1) * 128 + c0) = cs2;
+    }
+  }
   if (rq >= 2) park(rq - 2);
   __syncthreads();
   if (rq < 2) absorb(rq);
@@ -981,6 +1012,18 @@ wgrad_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __res
   if (rq == 1) park(0);
   __syncthreads();
   TL_MARK();
+  if (CS && rq == 0 && q == 0) {  // quarters in order; part[which][n][block]
+    const int nb = gridDim.x;
+#pragma unroll
+    for (int which = 0; which < 2; ++which)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += csred[(k * 2 + which) * 128 + c0 + u];
+        cpart[((int64_t)which * 128 + c0 + u) * nb + blockIdx.x] = v;
+      }
+  }
   if (rq == 0) {
     absorb(0);
     float* out = slab + (int64_t)blockIdx.x * (128 * 128);
@@ -1170,7 +1213,8 @@ int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, 
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
-                 const float* a, const float* de2, const float* a2, hipStream_t s) {
+                 const float* a, const float* de2, const float* a2, hipStream_t s,
+                 const float* cs_tab, float* cs_part, int* cs_nb) {
   if (!skinny_enabled() || M != 128 || N != 128 || sAm != 1 || sBn != 1) return 0;
   if (K < 4096 || K >= (1ll << 31) || splits < 16) return 0;
   if (sAk % 4 || sBk % 4 || ((uintptr_t)A | (uintptr_t)B) & 15) return 0;
@@ -1180,13 +1224,20 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
   if (nb > splits) nb = splits;
   if (nb > 256) nb = 256;
   if (nb < 16 || ws == nullptr) return 0;
+  if (cs_tab != nullptr && (de == nullptr || cs_part == nullptr || ((uintptr_t)cs_tab & 7)))
+    return 0;
   float* slab = (float*)ws;
-  if (de != nullptr)
-    hipLaunchKernelGGL(sk::wgrad_kernel<true>, dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s, (int)K, A, sAk,
-                       B, sBk, de, a, de2, a2, hH, hF, slab);
+  if (cs_tab != nullptr)
+    hipLaunchKernelGGL((sk::wgrad_kernel<true, true>), dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s,
+                       (int)K, A, sAk, B, sBk, de, a, de2, a2, hH, hF, slab, cs_tab, cs_part);
+  else if (de != nullptr)
+    hipLaunchKernelGGL((sk::wgrad_kernel<true, false>), dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s,
+                       (int)K, A, sAk, B, sBk, de, a, de2, a2, hH, hF, slab, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(sk::wgrad_kernel<false>, dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s, (int)K, A,
-                       sAk, B, sBk, nullptr, nullptr, nullptr, nullptr, 1, 4, slab);
+    hipLaunchKernelGGL((sk::wgrad_kernel<false, false>), dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s,
+                       (int)K, A, sAk, B, sBk, nullptr, nullptr, nullptr, nullptr, 1, 4, slab, nullptr,
+                       nullptr);
+  if (cs_nb != nullptr) *cs_nb = (int)nb;
   hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>, dim3(128 * 128 / (4 * sk::kWrCols)), dim3(256), 0, s,
                      (const float*)slab, (int)nb, C, ldc, beta);
   return 1;

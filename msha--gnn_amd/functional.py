@@ -541,6 +541,13 @@ class _ProjectScores(torch.autograd.Function):
                 dX = gemm_head_outer(dh, W.t(), 0, outer, **kw)
             if ctx.needs_input_grad[1]:
                 kw["out_dtype"] = wdt if dt == BF16 else None
+                if dt == torch.float32 and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
+                    # dW, dal, dar in one pass over the rows where the shape allows
+                    fused = _wgrad_colsum(X, dh, outer, h)
+                    if fused is not None:
+                        dW, o1, o2 = fused
+                        dal, dar = _score_grads(d_el, d_er, o1, o2, al, ar, aldt, ardt)
+                        return dX, dW, dal, dar, None, None
                 dW = gemm_head_outer(X.t(), dh, 1, outer, **kw)
         else:
             if ctx.needs_input_grad[0]:
@@ -559,14 +566,52 @@ class _ProjectScores(torch.autograd.Function):
             _lib.call("msha_head_colsum", M, H, Fd, _code(dt), d1.data_ptr(),
                       _lib.ptr(d2), h.data_ptr(), o1.data_ptr(), _lib.ptr(o2),
                       ws.data_ptr(), ws.numel(), s)
-            outs = [o1] + ([o2] if o2 is not None else [])
-            k = 0
-            if d_el is not None:
-                dal = outs[k].reshape(al.shape).to(aldt)
-                k += 1
-            if d_er is not None:
-                dar = outs[k].reshape(ar.shape).to(ardt)
+            dal, dar = _score_grads(d_el, d_er, o1, o2, al, ar, aldt, ardt)
         return dX, dW, dal, dar, None, None
+
+
+def _score_grads(d_el, d_er, o1, o2, al, ar, aldt, ardt):
+    """(dal, dar) from the column sums of the present score terms, in order."""
+    outs = [o1] + ([o2] if o2 is not None else [])
+    dal = dar = None
+    k = 0
+    if d_el is not None:
+        dal = outs[k].reshape(al.shape).to(aldt)
+        k += 1
+    if d_er is not None:
+        dar = outs[k].reshape(ar.shape).to(ardt)
+    return dal, dar
+
+
+def _wgrad_colsum(X, dh, outer, h):
+    """dW = X^T (dh + d1 (x) a1 [+ d2 (x) a2]) and the column sums of d1 (x) h, d2 (x) h
+    (msha_gemm_f32_head_outer_colsum: one pass over the rows), or None where the fused
+    kernel does not cover the shape (the caller runs the two ops)."""
+    H, Fd, d1, a1, d2, a2 = outer
+    M, K = X.shape
+    N = dh.shape[1]
+    if M < 4096 or not (dh.is_contiguous() and h.is_contiguous() and h.shape == dh.shape):
+        return None
+    splits = _splits_for(M, K, N)
+    dev = X.device
+    dW = torch.empty(K, N, device=dev, dtype=torch.float32)
+    ws = torch.empty(int(_lib.load().msha_gemm_workspace_size(K, N, splits)), dtype=torch.uint8,
+                     device=dev)
+    cws = torch.empty(int(_lib.load().msha_head_outer_colsum_workspace_size(N)),
+                      dtype=torch.uint8, device=dev)
+    o1 = torch.empty(H, Fd, device=dev, dtype=torch.float32)
+    o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
+    A = X.t()
+    rc = _lib.load().msha_gemm_f32_head_outer_colsum(
+        K, N, M, A.data_ptr(), A.stride(0), A.stride(1), dh.data_ptr(), dh.stride(0),
+        dh.stride(1), dW.data_ptr(), dW.stride(0), splits, ws.data_ptr(), ws.numel(), H, Fd,
+        d1.data_ptr(), a1.data_ptr(), _lib.ptr(d2), _lib.ptr(a2), h.data_ptr(), o1.data_ptr(),
+        _lib.ptr(o2), cws.data_ptr(), cws.numel(), _stream(X))
+    if rc == _lib.MSHA_ERR_UNSUPPORTED:
+        return None
+    if rc != 0:
+        _lib.raise_for(rc, "msha_gemm_f32_head_outer_colsum")
+    return dW, o1, o2
 
 
 def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = None):

@@ -774,3 +774,44 @@ def test_pair_linear_resident_w(cuda, msha, K, N):
     z = np.maximum((h[src].astype(np.float64) * h[dst]) @ W.T.astype(np.float64) + b, 0)
     ref = 1 / (1 + np.exp(-(z * keep / (1 - p))))
     tol_close(out.cpu().numpy(), ref, 1e-5, 1e-6)
+
+
+@pytest.mark.parametrize("M,H,F,two", [(100000, 8, 16, True), (50015, 2, 64, True),
+                                       (4096, 8, 16, False), (8191, 1, 128, True)])
+def test_gemm_head_outer_colsum(cuda, M, H, F, two):
+    """msha_gemm_f32_head_outer_colsum: dW = X^T (dh + de (x) a [+ de2 (x) a2]) and the
+    score-vector gradients sum_r de[r,h] T[r,h*F+f] from one pass over the rows, vs
+    torch fp64 (1e-5), deterministic across calls; a shape outside the fused kernel
+    (K != 128) is refused with nothing written."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M + H)
+    D, K = H * F, 128
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    dh = rng.standard_normal((M, D)).astype(np.float32)
+    T = rng.standard_normal((M, D)).astype(np.float32)
+    de = rng.standard_normal((M, H)).astype(np.float32)
+    a = rng.standard_normal((H, F)).astype(np.float32)
+    de2 = rng.standard_normal((M, H)).astype(np.float32) if two else None
+    a2 = rng.standard_normal((H, F)).astype(np.float32) if two else None
+    outer = (H, F, t(de, cuda), t(a, cuda), t(de2, cuda) if two else None,
+             t(a2, cuda) if two else None)
+    runs = [MF._wgrad_colsum(t(X, cuda), t(dh, cuda), outer, t(T, cuda)) for _ in range(2)]
+    assert runs[0] is not None
+    for x, y in zip(runs[0], runs[1]):
+        assert (x is None and y is None) or torch.equal(x, y)
+    tot = dh.astype(np.float64) + np.repeat(de, F, 1) * a.reshape(-1)
+    if two:
+        tot += np.repeat(de2, F, 1) * a2.reshape(-1)
+    dW, o1, o2 = runs[0]
+    tol_close(dW.cpu().numpy(), X.T.astype(np.float64) @ tot, 1e-5, 1e-5)
+    T3 = T.astype(np.float64).reshape(M, H, F)
+    tol_close(o1.cpu().numpy(), np.einsum("mh,mhf->hf", de.astype(np.float64), T3), 1e-5, 1e-5)
+    if two:
+        tol_close(o2.cpu().numpy(), np.einsum("mh,mhf->hf", de2.astype(np.float64), T3), 1e-5,
+                  1e-5)
+    else:
+        assert o2 is None
+    # K = 64 columns of X: not the fused kernel's shape
+    assert MF._wgrad_colsum(t(X[:, :64], cuda), t(dh, cuda), outer, t(T, cuda)) is None

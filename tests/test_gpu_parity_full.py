@@ -511,7 +511,7 @@ def test_model_train_step_full_2015(cuda, msha, kind):
     out64, loss64, Sf, Rf, oW, heads = _model_grads_vs_dense(model, yg, src_t, tgt,
                                                              kind == "Ours", rec.heads(2))
     tol_close(out.detach().cpu().numpy(), out64.detach().numpy(), F32_TOL, F32_TOL)
-    assert abs(float(loss.detach()) - float(loss64.detach())) <= F32_TOL * abs(float(loss64))
+    assert abs(float(loss.detach()) - float(loss64.detach())) <= F32_TOL * abs(float(loss64.detach()))
     tol_close(model.Sfeatures.grad.cpu().numpy(), Sf.grad.numpy(), F32_TOL, F32_TOL)
     tol_close(model.Rfeatures.grad.cpu().numpy(), Rf.grad.numpy(), F32_TOL, F32_TOL)
     tol_close(model.out_att.W.grad.cpu().numpy(), oW.grad.numpy(), F32_TOL, F32_TOL)
