@@ -336,13 +336,14 @@ int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int6
 int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, float* C,
               int hH, int hF, const float* d1, const float* a1, const float* d2, const float* a2,
               hipStream_t s);
-// cs_tab (optional): also the per-block partials of sum_r de[r, n / hF] cs_tab[r, n] (and
-// de2) into cs_part ([2][N][blocks], blocks reported in *cs_nb); cs_tab has B's row pitch
+// cs_tab (optional): also cs_out1[n] = sum_r de[r, n / hF] cs_tab[r, n] (cs_out2 with de2)
+// through the per-block partials in cs_part (2 x N x 256 floats); cs_tab has B's row pitch
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
                  const float* a, const float* de2, const float* a2, hipStream_t s,
-                 const float* cs_tab = nullptr, float* cs_part = nullptr, int* cs_nb = nullptr);
+                 const float* cs_tab = nullptr, float* cs_part = nullptr,
+                 float* cs_out1 = nullptr, float* cs_out2 = nullptr);
 
 // Welford triple (count, mean, M2) and Chan's combination (bn.hip, head.hip)
 struct Wf {

@@ -798,12 +798,9 @@ extern "C" int msha_gemm_f32_head_outer_colsum(
   if (!aligned16(a) || (a2 != nullptr && !aligned16(a2)))
     return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum: 16-byte aligned a, a2");
   hipStream_t s = (hipStream_t)stream;
-  int nb = 0;
   if (!skinny_wgrad(M, N, K, A, sAm, sAk, B, sBk, sBn, C, ldc, 0.f, splits, ws, ws_bytes, heads,
-                    feat, de, a, de2, a2, s, T, (float*)cs_ws, &nb))
+                    feat, de, a, de2, a2, s, T, (float*)cs_ws, cs1, cs2))
     return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum: shape outside the fused kernel");
-  hipLaunchKernelGGL(head_colsum_reduce_kernel, dim3((unsigned)((2 * N + 3) / 4)), dim3(256), 0, s,
-                     nb, (int)N, (const float*)cs_ws, cs1, cs2);
   return check_launch("gemm_f32_head_outer_colsum");
 }
 

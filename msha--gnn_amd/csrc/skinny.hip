@@ -1046,8 +1046,32 @@ constexpr int kWrGroups = 32, kWrCols = 8, kWrRB = 8;
 template <typename TC>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int nb,
                                                            TC* __restrict__ C, int64_t ldc,
-                                                           float beta) {
+                                                           float beta, const float* __restrict__ cpart,
+                                                           float* __restrict__ cs1,
+                                                           float* __restrict__ cs2) {
   __shared__ float4 part[256];
+  if (blockIdx.x >= 128 * 128 / (4 * kWrCols)) {
+    // the CS partials of wgrad_kernel (part[which][n][block]): one wave per output, lane
+    // l adds blocks l, l + 64, ... in order, then a fixed xor tree (head_colsum_reduce's
+    // order)
+    const int t = (int)((blockIdx.x - 128 * 128 / (4 * kWrCols)) * 4 + (threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63, which = t / 128, d = t % 128;
+    float* out = which == 0 ? cs1 : cs2;
+    if (t >= 256 || out == nullptr) return;
+    const float* src = cpart + ((int64_t)which * 128 + d) * nb;
+    float s0 = 0.f, s1 = 0.f;
+    int b = lane;
+    for (; b + 64 < nb; b += 128) {
+      s0 += src[b];
+      s1 += src[b + 64];
+    }
+    if (b < nb) s0 += src[b];
+    float v = s0 + s1;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) out[d] = v;
+    return;
+  }
   const int zq = threadIdx.x / kWrCols, cq = threadIdx.x % kWrCols;
   const int f4 = blockIdx.x * kWrCols + cq;  // float4 index in the 128 x 128 tile
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1214,7 +1238,7 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
                  const float* a, const float* de2, const float* a2, hipStream_t s,
-                 const float* cs_tab, float* cs_part, int* cs_nb) {
+                 const float* cs_tab, float* cs_part, float* cs_out1, float* cs_out2) {
   if (!skinny_enabled() || M != 128 || N != 128 || sAm != 1 || sBn != 1) return 0;
   if (K < 4096 || K >= (1ll << 31) || splits < 16) return 0;
   if (sAk % 4 || sBk % 4 || ((uintptr_t)A | (uintptr_t)B) & 15) return 0;
@@ -1224,7 +1248,8 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
   if (nb > splits) nb = splits;
   if (nb > 256) nb = 256;
   if (nb < 16 || ws == nullptr) return 0;
-  if (cs_tab != nullptr && (de == nullptr || cs_part == nullptr || ((uintptr_t)cs_tab & 7)))
+  if (cs_tab != nullptr && (de == nullptr || cs_part == nullptr || cs_out1 == nullptr ||
+                          (de2 != nullptr) != (cs_out2 != nullptr) || ((uintptr_t)cs_tab & 7)))
     return 0;
   float* slab = (float*)ws;
   if (cs_tab != nullptr)
@@ -1237,9 +1262,11 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
     hipLaunchKernelGGL((sk::wgrad_kernel<false, false>), dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s,
                        (int)K, A, sAk, B, sBk, nullptr, nullptr, nullptr, nullptr, 1, 4, slab, nullptr,
                        nullptr);
-  if (cs_nb != nullptr) *cs_nb = (int)nb;
-  hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>, dim3(128 * 128 / (4 * sk::kWrCols)), dim3(256), 0, s,
-                     (const float*)slab, (int)nb, C, ldc, beta);
+  // (+ 64 blocks of one wave per output for the CS partials)
+  hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>,
+                     dim3(128 * 128 / (4 * sk::kWrCols) + (cs_tab != nullptr ? 2 * 128 / 4 : 0)),
+                     dim3(256), 0, s, (const float*)slab, (int)nb, C, ldc, beta,
+                     (const float*)cs_part, cs_out1, cs_out2);
   return 1;
 }
 
