@@ -639,7 +639,9 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
     cls = layers.Ours if model_kind == "Ours" else layers.ablation3
     g = torch.Generator().manual_seed(0)
     picks = [torch.randint(0, len(flows), (64,), generator=g).to(dev) for _ in range(8)]
-    batches = [(src_t[b], dst_t[b]) for b in picks]
+    # one (2, 64) tensor per batch: a step's feed is one device copy (source and
+    # recipient rows of the static input together)
+    batches = [torch.stack([src_t[b], dst_t[b]]) for b in picks]
     from msha_gnn_amd.graph import graph_for
 
     e = graph_for(adj).n_edges
@@ -663,8 +665,8 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
             opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4,
                                    capturable=graphed, fused=FUSED_ADAM)
         model.train()
-        si_s = torch.empty(64, dtype=torch.int64, device=dev)
-        ri_s = torch.empty(64, dtype=torch.int64, device=dev)
+        sr_s = torch.empty(2, 64, dtype=torch.int64, device=dev)
+        si_s, ri_s = sr_s[0], sr_s[1]
 
         def body():
             opt.zero_grad(set_to_none=True)
@@ -677,8 +679,7 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
             return loss
 
         def feed(k):
-            si_s.copy_(batches[k % len(batches)][0])
-            ri_s.copy_(batches[k % len(batches)][1])
+            sr_s.copy_(batches[k % len(batches)])
 
         if graphed:
             from msha_gnn_amd.step import GraphedStep

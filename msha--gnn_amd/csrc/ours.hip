@@ -402,6 +402,7 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, 
 //   and the sums over b run a wave per output with lanes across f / b and a fixed xor
 //   tree; the batch sources sit in LDS for the repeated-source scans.
 constexpr int kFinishLds = 2048;
+constexpr int kFinishKB = 8;  // items per wave whose loads are issued together
 
 template <typename T>
 __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
@@ -410,27 +411,30 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     float* __restrict__ da4s, T* __restrict__ d_hs) {
   __shared__ int64_t s_src[kFinishLds];
   __shared__ int32_t s_next[kFinishLds];  // next batch entry with the same source, -1 = none
-  __shared__ uint8_t s_first[kFinishLds];  // first batch entry of its source
+  __shared__ int32_t s_first[kFinishLds];  // first batch entry of its source
   const int H = a.H, F = a.F, D = H * F;
   const int64_t B = a.B;
   const bool in_lds = B <= kFinishLds;
   if (in_lds)
-    for (int64_t t = threadIdx.x; t < B; t += blockDim.x) s_src[t] = a.src[t];
+    for (int64_t t = threadIdx.x; t < B; t += blockDim.x) {
+      s_src[t] = a.src[t];
+      s_first[t] = 1;
+      s_next[t] = INT32_MAX;
+    }
   __syncthreads();
-  auto SRC = [&](int64_t b) { return in_lds ? s_src[b] : a.src[b]; };
   if (in_lds) {
-    for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
-      const int64_t i = s_src[b];
-      bool first = true;
-      for (int64_t q = 0; q < b && first; ++q) first = s_src[q] != i;
-      int32_t nx = -1;
-      for (int64_t q = b + 1; q < B; ++q)
-        if (s_src[q] == i) { nx = (int32_t)q; break; }
-      s_first[b] = first ? 1 : 0;
-      s_next[b] = nx;
+    // every (b, q) pair of the batch at once (one LDS min per match), instead of a
+    // serial scan per entry: next = the smallest later entry with b's source
+    for (int64_t t = threadIdx.x; t < B * B; t += blockDim.x) {
+      const int64_t b = t / B, q = t % B;
+      if (q != b && s_src[q] == s_src[b]) {
+        if (q < b) s_first[b] = 0;
+        else atomicMin(&s_next[b], (int32_t)q);
+      }
     }
     __syncthreads();
   }
+  auto SRC = [&](int64_t b) { return in_lds ? s_src[b] : a.src[b]; };
   // batch entries of b's source in batch order (b first): the per-row sums below
   auto is_first = [&](int64_t b) {
     if (in_lds) return s_first[b] != 0;
@@ -440,7 +444,7 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     return true;
   };
   auto next_same = [&](int64_t q) -> int64_t {
-    if (in_lds) return s_next[q];
+    if (in_lds) return s_next[q] == INT32_MAX ? -1 : s_next[q];
     const int64_t i = a.src[q];
     for (int64_t r = q + 1; r < B; ++r)
       if (a.src[r] == i) return r;
@@ -448,27 +452,47 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
   };
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (mode == 0) {
-    // dots dw3 = G3 . h2_b, dw4 = G4 . h2_b: a wave per (b, h), lanes across f; parked
-    // in bgrad[.., 0..1], then the scalar chain runs a thread per (b, h) in parallel
-    for (int64_t t = wv; t < B * H; t += nw) {
-      const int64_t b = t / H;
-      const int h = (int)(t % H);
-      const int64_t i = SRC(b);
-      float dw3 = 0.f, dw4 = 0.f;
-      for (int f = lane; f < F; f += 64) {
-        const float x = ldt<T>(a.h2, i * D + h * F + f);
-        dw3 = fmaf(G[(b * 2 + 0) * D + h * F + f], x, dw3);
-        dw4 = fmaf(G[(b * 2 + 1) * D + h * F + f], x, dw4);
+    // dots dw3 = G3 . h2_b, dw4 = G4 . h2_b: a wave per (b, h), lanes across f, kFinishKB
+    // items' loads in flight together; parked in bgrad[.., 0..1]
+    const int64_t nt = B * H;
+    for (int64_t t0 = wv; t0 < nt; t0 += (int64_t)nw * kFinishKB) {
+      float d3[kFinishKB], d4[kFinishKB];
+#pragma unroll
+      for (int k = 0; k < kFinishKB; ++k) d3[k] = d4[k] = 0.f;
+      for (int f0 = 0; f0 < F; f0 += 64) {
+        const int f = f0 + lane;
+        float x[kFinishKB], g3[kFinishKB], g4[kFinishKB];
+#pragma unroll
+        for (int k = 0; k < kFinishKB; ++k) {
+          const int64_t t = t0 + (int64_t)k * nw;
+          const bool ok = t < nt && f < F;
+          const int64_t b = ok ? t / H : 0;
+          const int h = ok ? (int)(t % H) : 0;
+          x[k] = ok ? ldt<T>(a.h2, SRC(b) * D + h * F + f) : 0.f;
+          g3[k] = ok ? G[(b * 2 + 0) * D + h * F + f] : 0.f;
+          g4[k] = ok ? G[(b * 2 + 1) * D + h * F + f] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < kFinishKB; ++k) {
+          d3[k] = fmaf(g3[k], x[k], d3[k]);
+          d4[k] = fmaf(g4[k], x[k], d4[k]);
+        }
       }
-      dw3 = wave_xor_sum<1>(dw3);
-      dw4 = wave_xor_sum<1>(dw4);
-      if (lane == 0) {
-        bgrad[t * 4 + 0] = dw3;
-        bgrad[t * 4 + 1] = dw4;
+#pragma unroll
+      for (int k = 0; k < kFinishKB; ++k) {
+        const float dw3 = wave_xor_sum<1>(d3[k]);
+        const float dw4 = wave_xor_sum<1>(d4[k]);
+        const int64_t t = t0 + (int64_t)k * nw;
+        if (lane == 0 && t < nt) {
+          bgrad[t * 4 + 0] = dw3;
+          bgrad[t * 4 + 1] = dw4;
+        }
       }
     }
     __syncthreads();
-    for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
+    // the scalar chain, a thread per (b, h) (its dependent group-size loads overlap
+    // across threads; on one lane per wave they ran one item after another)
+    for (int64_t t = threadIdx.x; t < nt; t += blockDim.x) {
       const int64_t b = t / H;
       const int h = (int)(t % H);
       const int64_t i = SRC(b);
@@ -495,19 +519,39 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       for (int64_t q = b; q >= 0; q = next_same(q)) s += bgrad[(q * H + h) * 4 + 2];
       row_coef[SRC(b) * H + h] = s;
     }
-    for (int64_t t = wv; t < (int64_t)H * F; t += nw) {
-      const int h = (int)(t / F);
-      float s3 = 0.f, s4 = 0.f;
+    // da3s[t] = sum_b dpre3_b h2_b[t] (da4s): a wave per output, lanes across b,
+    // kFinishKB outputs' loads in flight together
+    for (int64_t t0 = wv; t0 < (int64_t)D; t0 += (int64_t)nw * kFinishKB) {
+      float s3[kFinishKB], s4[kFinishKB];
+#pragma unroll
+      for (int k = 0; k < kFinishKB; ++k) s3[k] = s4[k] = 0.f;
       for (int64_t b = lane; b < B; b += 64) {
-        const float x = ldt<T>(a.h2, SRC(b) * D + t);
-        s3 = fmaf(bgrad[(b * H + h) * 4 + 0], x, s3);
-        s4 = fmaf(bgrad[(b * H + h) * 4 + 1], x, s4);
+        const int64_t ib = SRC(b);
+        float x[kFinishKB], w3[kFinishKB], w4[kFinishKB];
+#pragma unroll
+        for (int k = 0; k < kFinishKB; ++k) {
+          const int64_t t = t0 + (int64_t)k * nw;
+          const bool ok = t < D;
+          const int h = ok ? (int)(t / F) : 0;
+          x[k] = ok ? ldt<T>(a.h2, ib * D + t) : 0.f;
+          w3[k] = ok ? bgrad[(b * H + h) * 4 + 0] : 0.f;
+          w4[k] = ok ? bgrad[(b * H + h) * 4 + 1] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < kFinishKB; ++k) {
+          s3[k] = fmaf(w3[k], x[k], s3[k]);
+          s4[k] = fmaf(w4[k], x[k], s4[k]);
+        }
       }
-      s3 = wave_xor_sum<1>(s3);
-      s4 = wave_xor_sum<1>(s4);
-      if (lane == 0) {
-        da3s[t] = s3;
-        da4s[t] = s4;
+#pragma unroll
+      for (int k = 0; k < kFinishKB; ++k) {
+        const float r3 = wave_xor_sum<1>(s3[k]);
+        const float r4 = wave_xor_sum<1>(s4[k]);
+        const int64_t t = t0 + (int64_t)k * nw;
+        if (lane == 0 && t < D) {
+          da3s[t] = r3;
+          da4s[t] = r4;
+        }
       }
     }
   } else {

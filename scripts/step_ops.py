@@ -24,7 +24,11 @@ padj = GroupAdjacency(torch.as_tensor(prov, device=dev))
 gdp = {i: float(x) for i, x in enumerate(gdp_arr)}
 torch.manual_seed(0)
 model = layers.Ours(128, 64, m, 2, 0.5, gdp, n, m).to(dev)
-opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4, fused=True)
+from msha_gnn_amd import functional as MF  # noqa: E402
+from msha_gnn_amd.optim import Adam  # noqa: E402
+
+opt = Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)  # bench.train_step_leg's step
+opt.fuse_dropout_grad(model.Sfeatures)
 si = torch.randint(0, len(flows), (64,), device=dev)
 s_i, r_i = src_t[si], dst_t[si]
 
@@ -32,7 +36,7 @@ s_i, r_i = src_t[si], dst_t[si]
 def body():
     opt.zero_grad(set_to_none=True)
     out = model(adj, cadj, padj, s_i)
-    loss = torch.nn.functional.nll_loss(out[s_i], r_i)
+    loss = MF.nll_loss_rows(out, s_i, r_i)
     loss.backward()
     opt.step()
 
