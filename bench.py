@@ -148,24 +148,28 @@ def pmc_lookup(patterns, glob_pat):
     return None, None
 
 
-def fwd_kernel_pattern(H, F, bf16, variant="bat"):
-    """rocprofv3 name of the forward edge kernel (fp32 demangled, bf16 left mangled):
-    variant 'rs' (gather layout, scores from the row), 'gl' (gather layout, er table:
-    short rows) or 'bat' (score layout, er table)."""
+def fwd_kernel_pattern(H, F, bf16, variant="bat", rowterms=None):
+    """rocprofv3 name of the forward edge kernel (fp32 demangled, bf16 mangled or
+    demangled with the type as "bool _Accum"): variant 'rs' (gather layout, scores from
+    the row), 'gl' (gather layout, er table: short rows) or 'bat' (score layout, er
+    table); rowterms (None = either) pins the instantiation's row-term flag."""
+    rt = "(true|false)" if rowterms is None else ("true" if rowterms else "false")
+    rtb = "[01]" if rowterms is None else str(int(bool(rowterms)))
     if variant in ("rs", "gl"):
         rs = "true" if variant == "rs" else "false"
-        # (a demangled bf16 name reads "<H, F, bool _Accum, int, E, RT, RS, ATTD>")
-        return (rf"edge_attn_fwd_gl_kernel(ILi{H}ELi{F}EDF16bLi\d+ELb[01]ELb{int(variant == 'rs')}"
-                rf"|<{H}, {F}, bool _Accum, .*, (true|false), {rs}, (true|false)>)"
-                if bf16 else rf"edge_attn_fwd_gl_kernel<{H}, {F}, float, \d+, (true|false), {rs}")
-    return (rf"edge_attn_fwd(?:_bat)?_kernel(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)" if bf16 else
-            rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}(, float)?(, \d+)?(, (true|false))?>")
+        # <H, F, T, NGI, RT, RS, ATTD>
+        return (rf"edge_attn_fwd_gl_kernel(ILi{H}ELi{F}EDF16bLi\d+ELb{rtb}ELb{int(variant == 'rs')}"
+                rf"|<{H}, {F}, bool _Accum, .*, {rt}, {rs}, (true|false)>)"
+                if bf16 else rf"edge_attn_fwd_gl_kernel<{H}, {F}, float, \d+, {rt}, {rs}")
+    # <H, F, T, EPL, RT>
+    return (rf"edge_attn_fwd(?:_bat)?_kernel(ILi{H}ELi{F}EDF16bLi\d+ELb{rtb}|<{H}, {F}, bool _Accum)"
+            if bf16 else rf"edge_attn_fwd(?:_bat)?_kernel<{H}, {F}, float, \d+, {rt}>")
 
 
-def pmc_traffic(H, F, bf16=False, workload="syn100k", variant="bat"):
+def pmc_traffic(H, F, bf16=False, workload="syn100k", variant="bat", rowterms=None):
     """HBM bytes per launch of the forward edge kernel from the newest committed PMC
     summary of this workload (None if absent)."""
-    return pmc_lookup([fwd_kernel_pattern(H, F, bf16, variant)], f"*{workload}_v*")
+    return pmc_lookup([fwd_kernel_pattern(H, F, bf16, variant, rowterms)], f"*{workload}_v*")
 
 
 def bwd_rows_bytes(n, m, e, H, F, s=4):
@@ -371,8 +375,12 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
     tmpl = ((lambda k: rf"{k}(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)") if bf else
             (lambda k: rf"{k}<{H}, {F}, float"))
     pats = {
-        "msha_edge_attention_fwd": [fwd_kernel_pattern(H, F, bf, lay.fwd_variant)],
-        "msha_edge_attention_bwd_fused": [tmpl("bwd_row_stats_kernel"),
+        "msha_edge_attention_fwd": [fwd_kernel_pattern(H, F, bf, lay.fwd_variant, rt)],
+        # (bwd_row_stats_kernel<H, F, T, RT>: the flag pins the instantiation where the
+        # name keeps it)
+        "msha_edge_attention_bwd_fused": [tmpl("bwd_row_stats_kernel")
+                                          + (rf"(Lb{int(rt)}E|, {str(rt).lower()}>|, bool, E>)"
+                                             if bf else rf", {str(rt).lower()}>"),
                                           tmpl("bwd_cols(_eh)?_kernel")]
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
         "msha_edge_attention_bwd_rows": [tmpl("edge_attn_bwd_rows(_gl)?_kernel")],
@@ -418,7 +426,7 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
     dt = dtg if dtg is not None else dte
     fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
     ach = fb / (k_ms * 1e-3) / 1e9
-    tr, src = (pmc_traffic(H, F, s == 2, workload, lay.fwd_variant) if workload
+    tr, src = (pmc_traffic(H, F, s == 2, workload, lay.fwd_variant, lay.rowterms) if workload
                else (None, None))
     res = {"workload": label, "value": world * e * steps / dt, "unit": "edges/s",
            "ms_per_step": dt / steps * 1e3, "ms_per_step_eager": dte / steps * 1e3,

@@ -12,7 +12,7 @@
 #define FWD_EPL_BF16 2
 #endif
 #ifndef GL_EPL_BF16
-#define GL_EPL_BF16 FWD_EPL_BF16  // the gather-layout forward's long chunks, bf16 tables
+#define GL_EPL_BF16 1  // the gather-layout forward's long chunks, bf16 tables (CEL 8)
 #endif
 #ifndef GL_EPL_F32
 #define GL_EPL_F32 FWD_EPL
