@@ -218,6 +218,25 @@ def fwd_bytes(n, m, e, H, F, s=4, rowterms=False, row_scores=False, attd=False):
             + 4 * n * H + rt + (4 * e * H if attd else 0))
 
 
+def bip_fwd_bytes(n, m, e, H, F, s=4, hs=False, attd=False):
+    """Compulsory HBM bytes of msha_bip_attention_fwd (edge_bip.hip): per row rowptr, el,
+    the u write and lse (+ the hs read with the v branch); per edge its column (+ the
+    attention export); the column side (hc, er; v out) once.  hc_j is read from LDS, not
+    gathered per edge, so no per-edge table bytes."""
+    D = H * F
+    return (4 * (n + 1) + 4 * e + 4 * n * H + s * n * D + 4 * n * H + (s * n * D if hs else 0)
+            + (4 * e * H if attd else 0) + m * (s * D + 4 * H) + (s * m * D if hs else 0))
+
+
+def bip_bwd_bytes(n, m, e, H, F, s=4, hs=False):
+    """Compulsory HBM bytes of msha_bip_attention_bwd: per row rowptr, el, lse, dU in,
+    d_el out (+ hs in and d_hs out with the v branch); per edge its column; the column
+    side (hc, er, dV in; d_hc, d_er out) once."""
+    D = H * F
+    return (4 * (n + 1) + 4 * e + 8 * n * H + s * n * D + 4 * n * H
+            + (2 * s * n * D if hs else 0) + m * (s * D + 4 * H) * 2 + (s * m * D if hs else 0))
+
+
 class Layer:
     """The benchmarked GAT layer (one replica).  Square graphs (C4, syn2m): h = X W is
     both the gathered table and the score source (u-only).  Bipartite graphs (R15,
@@ -264,6 +283,12 @@ class Layer:
                                                                                 H, F, code))
         short = self.graph.n_edges <= 8 * n and os.environ.get("MSHA_FWD_GL", "1") != "0"
         self.fwd_variant = "rs" if self.row_scores else ("gl" if short else "bat")
+        # the repo's adjacency shape (M <= 32 recipients): msha_bip_attention_fwd/_bwd
+        self.bip = bool(self.v_branch and MF.BIP
+                        and lib.msha_bip_supported(self.graph.desc, H, F, code))
+        if self.bip:
+            self.rowterms = self.row_scores = False
+            self.fwd_variant = "bip"
 
     def step(self):
         for p in (self.W, self.al, self.ar):
@@ -356,8 +381,9 @@ class Clock:
         lay.MF.KERNEL_EVENTS = None
         ms = {name: float(np.mean([a.elapsed_time(b) for a, b in lst]))
               for name, lst in evs.items() if lst}
-        events = evs.get("edge_attention_fwd", [])
-        k = ms.get("edge_attention_fwd", float("nan"))
+        fk = "bip_attention_fwd" if getattr(lay, "bip", False) else "edge_attention_fwd"
+        events = evs.get(fk, [])
+        k = ms.get(fk, float("nan"))
         dt_ = self.max_over_ranks(dt_)
         lay.kernel_ms = ms
         return dt_, k, len(events)
@@ -385,6 +411,11 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
         "msha_edge_attention_bwd_rows": [tmpl("edge_attn_bwd_rows(_gl)?_kernel")],
         "msha_csc_aggregate": [tmpl("csc_aggregate_kernel")],
+        "msha_bip_attention_fwd": [tmpl("bip_fwd_kernel") + (rf"(ELb{int(lay.v_branch)}E|, "
+                                                             rf"{str(lay.v_branch).lower()}>)"
+                                                             if bf else
+                                                             rf", {str(lay.v_branch).lower()}>")],
+        "msha_bip_attention_bwd": [tmpl("bip_bwd_kernel")],
     }
     out = []
     v = lay.v_branch
@@ -393,7 +424,9 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
                          ("msha_edge_attention_bwd_rows", bwd_rows_bytes(n, m, e, H, F, s)),
                          ("msha_csc_aggregate", csc_bytes(m, e, H, F, nch, s)),
                          ("msha_edge_attention_bwd_fused",
-                          bwd_fused_bytes(n, m, e, H, F, nch, s, rt))):
+                          bwd_fused_bytes(n, m, e, H, F, nch, s, rt)),
+                         ("msha_bip_attention_fwd", bip_fwd_bytes(n, m, e, H, F, s, hs=v)),
+                         ("msha_bip_attention_bwd", bip_bwd_bytes(n, m, e, H, F, s, hs=v))):
         key = name[len("msha_"):]
         if key not in lay.kernel_ms:
             continue
@@ -424,16 +457,24 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
     dte, k_ms, nl = clock.timed(lay, steps, warmup)
     dtg = None if eager else clock.timed_graph(lay, steps)
     dt = dtg if dtg is not None else dte
-    fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
+    if lay.bip:
+        fb = bip_fwd_bytes(n, m, e, H, F, s, hs=lay.v_branch)
+        bpat = ((rf"bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(lay.v_branch)}E|<{H}, {F}, bool _Accum, "
+                 rf"{str(lay.v_branch).lower()}>)") if s == 2 else
+                rf"bip_fwd_kernel<{H}, {F}, float, {str(lay.v_branch).lower()}>")
+        tr, src = pmc_lookup([bpat], f"*{workload}_v*") if workload else (None, None)
+    else:
+        fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
+        tr, src = (pmc_traffic(H, F, s == 2, workload, lay.fwd_variant, lay.rowterms)
+                   if workload else (None, None))
     ach = fb / (k_ms * 1e-3) / 1e9
-    tr, src = (pmc_traffic(H, F, s == 2, workload, lay.fwd_variant, lay.rowterms) if workload
-               else (None, None))
     res = {"workload": label, "value": world * e * steps / dt, "unit": "edges/s",
            "ms_per_step": dt / steps * 1e3, "ms_per_step_eager": dte / steps * 1e3,
            "dtype": "bf16" if s == 2 else "f32",
            "config": {"nodes": n, "cols": m, "edges": e, "in_features": fin, "heads": H,
                       "feat": F},
-           "roofline": {"kernel": "msha_edge_attention_fwd" + ("_rs" if lay.row_scores else ""),
+           "roofline": {"kernel": ("msha_bip_attention_fwd" if lay.bip else
+                                   "msha_edge_attention_fwd" + ("_rs" if lay.row_scores else "")),
                         "variant": lay.fwd_variant,
                         "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "traffic": tr,

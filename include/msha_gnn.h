@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 10
+#define MSHA_ABI_VERSION 11
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -216,6 +216,37 @@ MSHA_API int msha_edge_attention_bwd_rows(const msha_graph* g, int32_t heads, in
                                           uint64_t seed, uint64_t offset, float* d_el, float* de,
                                           float* attd, int32_t edge_ld, void* d_hs,
                                           msha_stream_t stream);
+
+/* Bipartite small-M attention (ABI 11): the repo's own adjacency shape, N sources x
+ * M recipients with M * heads * feat <= 4096 (M = 32 at 2 heads x 64: every shipped
+ * year).  The column side (hc, er, dV) stays in LDS and the column reductions run in
+ * per-wave LDS slabs beside the row work, so one launch (+ a block-partial reduce)
+ * replaces msha_edge_attention_fwd + msha_csc_aggregate (v) and one replaces
+ * msha_edge_attention_bwd_rows + msha_csc_aggregate (d_hc, d_er).  Deterministic (wave
+ * and block order), no atomics; the rows of g must have distinct columns (every CSR the
+ * library builds does).  Reference: Ablation.py:266-274, Ours.py:84-86.
+ *   fwd: u, lse, attd (nullable), v = attd^T hs (hs, v: both or neither).  u_lo as in
+ *        msha_edge_attention_fwd.  Same dropout stream (element e * heads + h).
+ *   bwd: d_el, d_er, d_hc, and with dV: d_hs = attd dV (hs, dV, d_hs together);
+ *        row_coef (nullable) as in msha_edge_attention_bwd_rows.  No u / u_lo needed:
+ *        D_i = sum_e attd_e g_e.
+ * ws: msha_bip_workspace_size bytes (block partials; fwd needs it only with hs). */
+MSHA_API int msha_bip_supported(const msha_graph* g, int32_t heads, int32_t feat, int32_t dtype);
+MSHA_API size_t msha_bip_workspace_size(const msha_graph* g, int32_t heads, int32_t feat);
+MSHA_API int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
+                                    int32_t dtype, const float* el, const float* er,
+                                    const void* hc, const void* hs, float neg_slope,
+                                    float drop_p, uint64_t seed, uint64_t offset, void* u,
+                                    void* u_lo, float* lse, float* attd, void* v, void* ws,
+                                    size_t ws_bytes, msha_stream_t stream);
+MSHA_API int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_t feat,
+                                    int32_t dtype, const float* el, const float* er,
+                                    const void* hc, const float* lse, const void* dU,
+                                    const void* hs, const void* dV, const float* row_coef,
+                                    float neg_slope, float drop_p, uint64_t seed,
+                                    uint64_t offset, float* d_el, float* d_er, void* d_hc,
+                                    void* d_hs, void* ws, size_t ws_bytes,
+                                    msha_stream_t stream);
 
 /* Column-side (transposed) aggregate over the CSC view:
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 10  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 11  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -123,6 +123,12 @@ SIGNATURES = {
     "msha_edge_attention_bwd_fused_workspace_size": (SZ, [GP, I32, I32]),
     "msha_edge_attention_bwd_fused": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, F32,
                                                 F32, U64, U64, P, P, P, P, P, SZ, P]),
+    "msha_bip_supported": (C.c_int, [GP, I32, I32, I32]),
+    "msha_bip_workspace_size": (SZ, [GP, I32, I32]),
+    "msha_bip_attention_fwd": (C.c_int, [GP, I32, I32, I32, P, P, P, P, F32, F32, U64, U64, P,
+                                         P, P, P, P, P, SZ, P]),
+    "msha_bip_attention_bwd": (C.c_int, [GP, I32, I32, I32, P, P, P, P, P, P, P, P, F32, F32,
+                                         U64, U64, P, P, P, P, P, SZ, P]),
     "msha_csc_aggregate_workspace_size": (SZ, [GP, I32, I32]),
     "msha_csc_aggregate": (C.c_int, [GP, I32, I32, I32, P, P, I32, P, P, P, P, SZ, P]),
     "msha_gal_fwd": (C.c_int, [GP, P, F32, U64, U64, P, P]),

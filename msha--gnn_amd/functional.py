@@ -106,6 +106,26 @@ class _EdgeAttention(torch.autograd.Function):
         dev = el.device
         s = _stream(el)
         g = graph.desc
+        # (u-only with a_r keeps the row-score contract: er is then never read)
+        if (BIP and (hs is not None or ar is None)
+                and _lib.load().msha_bip_supported(g, H, F, _code(dt))):
+            # the repo's adjacency shape (M <= 32 recipients): msha_bip_attention_fwd,
+            # u and v in one pass over the rows (the column side stays in LDS)
+            u = torch.empty(n, H, F, device=dev, dtype=dt)
+            lse = torch.empty(n, H, device=dev, dtype=torch.float32)
+            v = torch.empty(m, H, F, device=dev, dtype=dt) if hs is not None else None
+            ws = _bip_ws(g, H, F, dev)
+            ev = _timed("bip_attention_fwd")
+            _lib.call("msha_bip_attention_fwd", g, H, F, _code(dt), el.data_ptr(),
+                      er.data_ptr(), hc.data_ptr(), _lib.ptr(hs), slope, p, seed, 0,
+                      u.data_ptr(), None, lse.data_ptr(), None, _lib.ptr(v), ws.data_ptr(),
+                      ws.numel(), s)
+            if ev is not None:
+                ev[1].record()
+            ctx.graph, ctx.p, ctx.seed, ctx.slope = graph, p, seed, slope
+            ctx.has_hs, ctx.bip = hs is not None, True
+            ctx.save_for_backward(el, er, hc, hs if hs is not None else el.new_empty(0), lse)
+            return u if v is None else (u, v)
         # scores from the gathered row (msha_edge_attention_fwd_rs): er_j = hc_j . a_r is
         # recomputed from the row the kernel gathers anyway, in the forward and in the
         # fused backward's column pass (the same bits in both); u-only path
@@ -147,7 +167,7 @@ class _EdgeAttention(torch.autograd.Function):
             v = torch.empty(m, H, F, device=dev, dtype=dt)
             _csc_aggregate(graph, H, F, attd, None, hs, v, None, s)
         ctx.graph, ctx.p, ctx.seed, ctx.slope = graph, p, seed, slope
-        ctx.has_hs = hs is not None
+        ctx.has_hs, ctx.bip = hs is not None, False
         ctx.rowterms = uc is not None
         ctx.rs = bool(rs)
         ctx.save_for_backward(el, er, hc, hs if hs is not None else el.new_empty(0), lse, u,
@@ -160,6 +180,8 @@ class _EdgeAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dU, dV=None):
+        if ctx.bip:
+            return _bip_bwd(ctx, dU, dV)
         el, er, hc, hs, lse, u, u_lo, ar, *rowterms = ctx.saved_tensors
         u_lo = u_lo if u_lo.numel() else None
         ar = ar if ctx.rs and not ctx.er_exact else None
@@ -200,6 +222,46 @@ class _EdgeAttention(torch.autograd.Function):
         if ctx.has_hs and d_hs is None:
             d_hs = torch.zeros_like(hs)
         return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None, None
+
+
+# bipartite small-M kernels (msha_bip_attention_fwd/_bwd) wherever the library covers
+# the graph (M * heads * feat <= 4096: every shipped year, bip1m).  Module switch for A/B.
+BIP = True
+
+
+def _bip_ws(g, H, F, dev):
+    return torch.empty(int(_lib.load().msha_bip_workspace_size(g, H, F)), dtype=torch.uint8,
+                       device=dev)
+
+
+def _bip_bwd(ctx, dU, dV):
+    """Backward of the bipartite forward: one row pass (msha_bip_attention_bwd) gives
+    d_el, d_hs and the column gradients d_hc, d_er through per-wave LDS slabs."""
+    el, er, hc, hs, lse = ctx.saved_tensors
+    n, H = el.shape
+    m, _, F = hc.shape
+    dt = hc.dtype
+    dev = el.device
+    s = _stream(el)
+    g = ctx.graph.desc
+    dU = torch.zeros(n, H, F, device=dev, dtype=dt) if dU is None else _tc(dU, dt)
+    use_dv = ctx.has_hs and dV is not None
+    dV = _tc(dV, dt) if use_dv else None
+    d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
+    d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
+    d_hc = torch.empty(m, H, F, device=dev, dtype=dt)
+    d_hs = torch.empty(n, H, F, device=dev, dtype=dt) if use_dv else None
+    ws = _bip_ws(g, H, F, dev)
+    ev = _timed("bip_attention_bwd")
+    _lib.call("msha_bip_attention_bwd", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
+              hc.data_ptr(), lse.data_ptr(), dU.data_ptr(), hs.data_ptr() if use_dv else None,
+              _lib.ptr(dV), None, ctx.slope, ctx.p, ctx.seed, 0, d_el.data_ptr(),
+              d_er.data_ptr(), d_hc.data_ptr(), _lib.ptr(d_hs), ws.data_ptr(), ws.numel(), s)
+    if ev is not None:
+        ev[1].record()
+    if ctx.has_hs and d_hs is None:
+        d_hs = torch.zeros_like(hs)
+    return d_el, d_er, d_hc, (d_hs if ctx.has_hs else None), None, None, None, None, None
 
 
 # u-only backward as one column pass (msha_edge_attention_bwd_fused) instead of
@@ -933,14 +995,25 @@ class _OursAttention(torch.autograd.Function):
         s = _stream(el)
         g = graph.desc
         u_inter = torch.empty(n, H, Fd, device=dev, dtype=dt)
-        u_lo = torch.empty_like(u_inter) if dt == BF16 and any(ctx.needs_input_grad[:4]) else None
+        bip = BIP and bool(_lib.load().msha_bip_supported(g, H, Fd, _code(dt)))
+        u_lo = (torch.empty_like(u_inter) if dt == BF16 and not bip
+                and any(ctx.needs_input_grad[:4]) else None)
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)
         attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
-        _lib.call("msha_edge_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
-                  h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(), _lib.ptr(u_lo),
-                  lse.data_ptr(), attd.data_ptr(), s)
         v = torch.empty(m, H, Fd, device=dev, dtype=dt)
-        _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
+        if bip:
+            # u, v and the attention export in one pass (msha_bip_attention_fwd)
+            ws = _bip_ws(g, H, Fd, dev)
+            _lib.call("msha_bip_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
+                      er.data_ptr(), h1.data_ptr(), h2.data_ptr(), slope, p, seed, 0,
+                      u_inter.data_ptr(), None, lse.data_ptr(), attd.data_ptr(), v.data_ptr(),
+                      ws.data_ptr(), ws.numel(), s)
+        else:
+            _lib.call("msha_edge_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
+                      er.data_ptr(), h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(),
+                      _lib.ptr(u_lo), lse.data_ptr(), attd.data_ptr(), s)
+            _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
+        ctx.bip = bip
         bstat = torch.empty(max(B, 1), H, 8, device=dev, dtype=torch.float32)
         u = torch.empty_like(u_inter)
         _lib.call("msha_ours_intra_fwd", g, groups.desc, B, src.data_ptr(), H, Fd, _code(dt),
@@ -984,17 +1057,29 @@ class _OursAttention(torch.autograd.Function):
                   ws.data_ptr(), ws.numel(), s)
         E = max(graph.n_edges, 1)
         d_el = torch.empty(n, H, device=dev, dtype=torch.float32)
+        d_hs = torch.empty(n, H, Fd, device=dev, dtype=dt)
+        d_hc = torch.empty(m, H, Fd, device=dev, dtype=dt)
+        d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
+        if ctx.bip:
+            # row and column gradients of the inter attention in one pass
+            ws = _bip_ws(g, H, Fd, dev)
+            _lib.call("msha_bip_attention_bwd", g, H, Fd, _code(dt), el.data_ptr(),
+                      er.data_ptr(), h1.data_ptr(), lse.data_ptr(), dU.data_ptr(),
+                      h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p,
+                      ctx.seed, 0, d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
+                      d_hs.data_ptr(), ws.data_ptr(), ws.numel(), s)
+            _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0,
+                      G.data_ptr(), bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), None,
+                      0, s)
+            return d_el, d_er, d_hc, d_hs, da3s, da4s, None, None, None, None, None, None
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)  # (de, attd) per edge
         de, attd = rec[:, 0], rec[:, 1]
-        d_hs = torch.empty(n, H, Fd, device=dev, dtype=dt)
         _lib.call("msha_edge_attention_bwd_rows", g, H, Fd, _code(dt), el.data_ptr(), er.data_ptr(),
                   h1.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), _lib.ptr(u_lo), dU.data_ptr(),
                   h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p, ctx.seed,
                   0, d_el.data_ptr(), de.data_ptr(), attd.data_ptr(), 2 * H, d_hs.data_ptr(), s)
         _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
                   bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), None, 0, s)
-        d_hc = torch.empty(m, H, Fd, device=dev, dtype=dt)
-        d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
         _csc_aggregate(graph, H, Fd, attd, de, dU, d_hc, d_er, s, ld=2 * H)
         return d_el, d_er, d_hc, d_hs, da3s, da4s, None, None, None, None, None, None
 

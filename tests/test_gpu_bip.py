@@ -1,0 +1,139 @@
+"""Bipartite small-M kernels (msha_bip_attention_fwd/_bwd, csrc/edge_bip.hip): the
+repo's adjacency shape, N sources x M <= 32 recipients (every shipped year; bip1m).
+u, v, lse, the attention export and every gradient against the fp64 oracle on the
+stored values (fp32 1e-5, bf16 1e-2) and against the general kernels they replace
+(functional.BIP = False), with virtual rows, a hot column, full rows, dropout (the
+kernels' Philox masks injected) and groups that straddle keep-bit pages."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import random_counts, t, tol_close, virtual_csr
+from oracle import gnn_oracle as O
+from test_gpu_kernels import _keep_mask
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (n, m, H, F, max_deg, extra); M * H <= 64 (one row's slots fit one group)
+    (3000, 32, 2, 64, 6, dict(empty_rows=(3, 7, 2999), hot_col=4)),   # R15 shape
+    (700, 32, 2, 64, 32, dict(full_rows=(1, 2, 3, 40))),             # 64-slot rows
+    (900, 8, 8, 16, 5, dict(empty_rows=(0,))),                        # C4 head shape
+    (400, 17, 1, 64, 4, dict(hot_col=16)),                            # V = 1, odd M
+    (300, 16, 2, 128, 7, dict(empty_rows=(5,))),                      # V = 4
+    (257, 16, 4, 32, 3, dict()),
+    (5000, 32, 2, 64, 2, dict()),                                     # groups capped by rows
+]
+
+
+def _run(MF, graph, el, er, hc, hs, dU, dV, p, seed, dev, dtype, bip):
+    old = MF.BIP
+    MF.BIP = bip
+    try:
+        leaves = [t(el, dev).requires_grad_(True), t(er, dev).requires_grad_(True),
+                  t(hc, dev, dtype).requires_grad_(True), t(hs, dev, dtype).requires_grad_(True)]
+        u, v = MF.edge_attention(graph, *leaves[:3], hs=leaves[3], p=p, training=p > 0,
+                                 seed=seed)
+        torch.autograd.backward([u, v], [t(dU, dev, dtype), t(dV, dev, dtype)])
+        torch.cuda.synchronize()
+        return [u.detach(), v.detach()] + [x.grad for x in leaves]
+    finally:
+        MF.BIP = old
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}m{c[1]}H{c[2]}F{c[3]}d{c[4]}")
+@pytest.mark.parametrize("p", [0.0, 0.5])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype):
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    n, m, H, F, max_deg, kw = case
+    rng = np.random.default_rng(n + 7 * H + F)
+    c = random_counts(rng, n, m, max_deg, **kw)
+    rowptr, col, empty = virtual_csr(c)
+    el = rng.standard_normal((n, H)).astype(np.float32)
+    er = rng.standard_normal((m, H)).astype(np.float32)
+    hc = rng.standard_normal((m, H, F)).astype(np.float32)
+    hs = rng.standard_normal((n, H, F)).astype(np.float32)
+    dU = rng.standard_normal((n, H, F)).astype(np.float32)
+    dV = rng.standard_normal((m, H, F)).astype(np.float32)
+    graph = Graph.from_dense(t(c, cuda))
+    code = 1 if dtype == torch.bfloat16 else 0
+    assert _lib.load().msha_bip_supported(graph.desc, H, F, code) == 1
+    seed = 31
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    got = _run(MF, graph, el, er, hc, hs, dU, dV, p, seed, cuda, dtype, True)
+    gen = _run(MF, graph, el, er, hc, hs, dU, dV, p, seed, cuda, dtype, False)
+    st = lambda x: t(x, cuda, dtype).double().cpu().numpy()  # noqa: E731  stored values
+    keep = _keep_mask(graph.n_edges, H, p, seed, cuda)
+    ref = O.edge_aggregate_fwd(rowptr, col, el.astype(np.float64), er.astype(np.float64), st(hc),
+                               hs=st(hs), keep=keep, p=p, rowflag=empty)
+    bw = O.edge_aggregate_bwd(rowptr, col, ref, st(hc), st(dU), hs=st(hs), dV=st(dV), keep=keep,
+                              p=p)
+    names = ("u", "v", "d_el", "d_er", "d_hc", "d_hs")
+    refs = (ref["u"], ref["v"], bw["d_el"], bw["d_er"], bw["d_hc"], bw["d_hs"])
+    for name, a, b, r in zip(names, got, gen, refs):
+        rt = max(tol, 1e-4) if name in ("d_el", "d_er") else tol
+        tol_close(a.float().cpu().numpy(), r, rt, tol)
+        tol_close(a.float().cpu().numpy(), b.float().cpu().numpy(), rt, tol)
+
+
+def test_bip_raw_abi_lse_attd_deterministic(cuda, msha):
+    """The C ABI directly: lse and the attention export against the oracle, u-only
+    (no hs) forward, and bitwise-identical repeats (wave- and block-ordered sums)."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd.graph import Graph
+
+    n, m, H, F = 5000, 32, 2, 64
+    rng = np.random.default_rng(5)
+    c = random_counts(rng, n, m, 5, empty_rows=(11,), hot_col=0)
+    rowptr, col, empty = virtual_csr(c)
+    el = rng.standard_normal((n, H)).astype(np.float32)
+    er = rng.standard_normal((m, H)).astype(np.float32)
+    hc = rng.standard_normal((m, H, F)).astype(np.float32)
+    hs = rng.standard_normal((n, H, F)).astype(np.float32)
+    graph = Graph.from_dense(t(c, cuda))
+    g = graph.desc
+    L = _lib.load()
+    E = graph.n_edges
+    ws = torch.empty(int(L.msha_bip_workspace_size(g, H, F)), dtype=torch.uint8, device=cuda)
+    s = _lib.stream_handle(cuda)
+    el_d, er_d, hc_d, hs_d = t(el, cuda), t(er, cuda), t(hc, cuda), t(hs, cuda)
+    outs = []
+    for rep in range(2):
+        u = torch.empty(n, H, F, device=cuda)
+        v = torch.empty(m, H, F, device=cuda)
+        lse = torch.empty(n, H, device=cuda)
+        attd = torch.empty(E, H, device=cuda)
+        _lib.call("msha_bip_attention_fwd", g, H, F, 0, el_d.data_ptr(), er_d.data_ptr(),
+                  hc_d.data_ptr(), hs_d.data_ptr(), 0.2, 0.0, 0, 0, u.data_ptr(), None,
+                  lse.data_ptr(), attd.data_ptr(), v.data_ptr(), ws.data_ptr(), ws.numel(), s)
+        outs.append((u, v, lse, attd))
+    u1 = torch.empty(n, H, F, device=cuda)
+    lse1 = torch.empty(n, H, device=cuda)
+    _lib.call("msha_bip_attention_fwd", g, H, F, 0, el_d.data_ptr(), er_d.data_ptr(),
+              hc_d.data_ptr(), None, 0.2, 0.0, 0, 0, u1.data_ptr(), None, lse1.data_ptr(), None,
+              None, None, 0, s)
+    torch.cuda.synchronize()
+    ref = O.edge_aggregate_fwd(rowptr, col, el.astype(np.float64), er.astype(np.float64),
+                               hc.astype(np.float64), hs=hs.astype(np.float64), rowflag=empty)
+    u, v, lse, attd = (x.cpu().numpy() for x in outs[0])
+    tol_close(u, ref["u"], 1e-5, 1e-5)
+    tol_close(v, ref["v"], 1e-5, 1e-5)
+    np.testing.assert_allclose(attd, ref["att"], atol=1e-5)
+    sc = np.where(ref["pre"] > 0, ref["pre"], 0.2 * ref["pre"])
+    seg = np.repeat(np.arange(n), np.diff(rowptr))
+    sc[empty[seg]] = 0.0  # virtual rows: constant score
+    lse_ref = np.zeros((n, H))
+    for h in range(H):
+        mx = np.full(n, -np.inf)
+        np.maximum.at(mx, seg, sc[:, h])
+        acc = np.zeros(n)
+        np.add.at(acc, seg, np.exp(sc[:, h] - mx[seg]))
+        lse_ref[:, h] = mx + np.log(acc)
+    np.testing.assert_allclose(lse, lse_ref, rtol=1e-5, atol=1e-5)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert torch.equal(u1, outs[0][0]) and torch.equal(lse1, outs[0][2])

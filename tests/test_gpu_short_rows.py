@@ -30,6 +30,8 @@ SHORT_CASES = [
 
 def _run(MF, graph, el, er, hc, hs, dU, dV, p, seed, dev, dtype, gl):
     os.environ["MSHA_FWD_GL"] = os.environ["MSHA_BWD_GL"] = "1" if gl else "0"
+    bip = MF.BIP
+    MF.BIP = False  # these cases test the general short-row kernels (test_gpu_bip.py: M <= 32)
     try:
         leaves = [t(el, dev).requires_grad_(True), t(er, dev).requires_grad_(True),
                   t(hc, dev, dtype).requires_grad_(True), t(hs, dev, dtype).requires_grad_(True)]
@@ -38,6 +40,7 @@ def _run(MF, graph, el, er, hc, hs, dU, dV, p, seed, dev, dtype, gl):
         torch.autograd.backward([u, v], [t(dU, dev, dtype), t(dV, dev, dtype)])
         return [u.detach(), v.detach()] + [x.grad for x in leaves]
     finally:
+        MF.BIP = bip
         os.environ.pop("MSHA_FWD_GL", None)
         os.environ.pop("MSHA_BWD_GL", None)
 
