@@ -579,9 +579,13 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
         const int h = lane % H;
         const int rsl = sl.t * H + h;
         const bool virt = (vmask >> sl.t) & 1ull;
-        const float pre = __shfl(cur.s0, rsl) + ert[sl.j * H + h];
+        // (the row scalars live on lanes t * H + h, which may be idle slot lanes: every
+        // shuffle runs with all lanes active -- ds_bpermute reads 0 from an inactive lane)
+        const float elq = __shfl(cur.s0, rsl), lsq = __shfl(cur.s1, rsl);
+        const float cfq = COEF ? __shfl(cur.s2, rsl) : 0.f;
+        const float pre = elq + ert[sl.j * H + h];
         const float sc = virt ? 0.f : lrelu(pre, slope);
-        const float att = sl.valid ? __expf(sc - __shfl(cur.s1, rsl)) : 0.f;
+        const float att = sl.valid ? __expf(sc - lsq) : 0.f;
         const float kf = slot_keep(dp, doff, Es, H, lane);
         const float ad = att * kf;
         sad[lane] = ad;
@@ -643,7 +647,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
         // (3) slot lanes: D_i, de_e, d_el_i, the d_er slab
         {
           float g = sg[lane];
-          if (COEF && sl.valid) g = fmaf(__shfl(cur.s2, rsl), expf(ad), g);
+          if (COEF && sl.valid) g = fmaf(cfq, expf(ad), g);
           const float Dq = seg_sum<H>(sl.valid ? ad * g : 0.f, lane, sl.sk, sl.ek);
           const float ds = att * (g * kf - Dq);
           const float dev = sl.valid && !virt ? ds * (pre > 0.f ? 1.f : slope) : 0.f;
