@@ -13,7 +13,7 @@ for W in "$@"; do
     RX="pair_|score_|gather"
   else
     B="$R/bench.py --workload $W --steps 6 --warmup 2 --no-cpu-baseline --no-link-score --no-r15 --no-syn2m --no-bip1m --no-dropout-leg"
-    RX="edge_attn|bwd_row|bwd_cols|csc_|proj_kernel|wgrad|head_colsum|segments|ours_|head_"
+    RX="edge_attn|bwd_row|bwd_cols|csc_|bip_|proj_kernel|wgrad|head_colsum|segments|ours_|head_|adam"
   fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 $B > "$OUT/bench_trace.log" 2>&1 \
     || { echo "trace $W failed"; tail -20 "$OUT/bench_trace.log"; exit 2; }
