@@ -411,10 +411,9 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
         "msha_edge_attention_bwd_rows": [tmpl("edge_attn_bwd_rows(_gl)?_kernel")],
         "msha_csc_aggregate": [tmpl("csc_aggregate_kernel")],
-        "msha_bip_attention_fwd": [tmpl("bip_fwd_kernel") + (rf"(ELb{int(lay.v_branch)}E|, "
-                                                             rf"{str(lay.v_branch).lower()}>)"
+        "msha_bip_attention_fwd": [tmpl("bip_fwd_kernel") + (rf"(ELb{int(lay.v_branch)}E|, bool, E, false>)"
                                                              if bf else
-                                                             rf", {str(lay.v_branch).lower()}>")],
+                                                             rf", {str(lay.v_branch).lower()}, false>")],
         "msha_bip_attention_bwd": [tmpl("bip_bwd_kernel")],
     }
     out = []
@@ -459,9 +458,10 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
     dt = dtg if dtg is not None else dte
     if lay.bip:
         fb = bip_fwd_bytes(n, m, e, H, F, s, hs=lay.v_branch)
+        # (<H, F, T, HS, ATTD>; rocprofv3 demangles some bf16 instances as "bool _Accum")
         bpat = ((rf"bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(lay.v_branch)}E|<{H}, {F}, bool _Accum, "
-                 rf"{str(lay.v_branch).lower()}>)") if s == 2 else
-                rf"bip_fwd_kernel<{H}, {F}, float, {str(lay.v_branch).lower()}>")
+                 rf"bool, E, false>)") if s == 2 else
+                rf"bip_fwd_kernel<{H}, {F}, float, {str(lay.v_branch).lower()}, false>")
         tr, src = pmc_lookup([bpat], f"*{workload}_v*") if workload else (None, None)
     else:
         fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)

@@ -280,6 +280,20 @@ __device__ __forceinline__ float seg_sum(float v, int lane, int sk, int ek) {
   return __shfl(v, sk);
 }
 
+// two dot products per head at once (QH = 32: a head is two 16-lane rows): the rows swap
+// so lanes with bit 4 clear collect p0 and the others p1, then one rotation tree per row.
+// Lanes (l & 16) == 0 of each head end up with sum(p0), the others with sum(p1).
+__device__ __forceinline__ float pair_sum32(float p0, float p1, int lane) {
+  const bool hi = (lane & 16) != 0;
+  float v = hi ? p1 : p0;
+  v += swap16(hi ? p0 : p1, lane);
+  v += ror16<8>(v);
+  v += ror16<4>(v);
+  v += ror16<2>(v);
+  v += ror16<1>(v);
+  return v;
+}
+
 // per-row all-reduce over a sub-group's slot lanes (rows t0 <= r < t1, independent, so
 // their chains interleave): rowv[r] = the value of (row r, this lane's head); returns the
 // value of this slot's own row
@@ -623,10 +637,16 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
                   wacc[t][v] = fmaf(a1, y1[v], fmaf(a0, y0[v], wacc[t][v]));
                 }
               }
-              const float g0 = lanes_sum<QH>(p0, lane), g1 = lanes_sum<QH>(p1, lane);
-              if (lead) {
-                sg[q0 * H + hl] = g0;
-                if (two) sg[(q0 + 1) * H + hl] = g1;
+              if constexpr (QH == 32) {
+                const float gp = pair_sum32(p0, p1, lane);
+                if (lane % 16 == 0 && (two || (lane & 16) == 0))
+                  sg[(q0 + ((lane >> 4) & 1)) * H + hl] = gp;
+              } else {
+                const float g0 = lanes_sum<QH>(p0, lane), g1 = lanes_sum<QH>(p1, lane);
+                if (lead) {
+                  sg[q0 * H + hl] = g0;
+                  if (two) sg[(q0 + 1) * H + hl] = g1;
+                }
               }
               float z[V];
               float* sp0 = slab + j0 * D + lane * V;
