@@ -284,8 +284,7 @@ class Layer:
         short = self.graph.n_edges <= 8 * n and os.environ.get("MSHA_FWD_GL", "1") != "0"
         self.fwd_variant = "rs" if self.row_scores else ("gl" if short else "bat")
         # the repo's adjacency shape (M <= 32 recipients): msha_bip_attention_fwd/_bwd
-        self.bip = bool(self.v_branch and MF.BIP
-                        and lib.msha_bip_supported(self.graph.desc, H, F, code))
+        self.bip = bool(self.v_branch and MF.bip_ok(self.graph, H, F, dtype))
         if self.bip:
             self.rowterms = self.row_scores = False
             self.fwd_variant = "bip"

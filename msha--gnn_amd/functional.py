@@ -107,8 +107,7 @@ class _EdgeAttention(torch.autograd.Function):
         s = _stream(el)
         g = graph.desc
         # (u-only with a_r keeps the row-score contract: er is then never read)
-        if (BIP and (hs is not None or ar is None)
-                and _lib.load().msha_bip_supported(g, H, F, _code(dt))):
+        if (hs is not None or ar is None) and bip_ok(graph, H, F, dt):
             # the repo's adjacency shape (M <= 32 recipients): msha_bip_attention_fwd,
             # u and v in one pass over the rows (the column side stays in LDS)
             u = torch.empty(n, H, F, device=dev, dtype=dt)
@@ -227,6 +226,14 @@ class _EdgeAttention(torch.autograd.Function):
 # bipartite small-M kernels (msha_bip_attention_fwd/_bwd) wherever the library covers
 # the graph (M * heads * feat <= 4096: every shipped year, bip1m).  Module switch for A/B.
 BIP = True
+
+
+def bip_ok(graph, H, F, dtype) -> bool:
+    """The bipartite kernels cover the graph: the library's shape rule (M <= 32,
+    M * H <= 64, M * H * F <= 4096) and rows with distinct columns, at most 64 / H each
+    (every graph from_dense builds; checked on the host for from_csr)."""
+    return bool(BIP and graph.distinct_cols and graph.max_deg * H <= 64
+                and _lib.load().msha_bip_supported(graph.desc, H, F, _code(dtype)))
 
 
 def _bip_ws(g, H, F, dev):
@@ -995,7 +1002,7 @@ class _OursAttention(torch.autograd.Function):
         s = _stream(el)
         g = graph.desc
         u_inter = torch.empty(n, H, Fd, device=dev, dtype=dt)
-        bip = BIP and bool(_lib.load().msha_bip_supported(g, H, Fd, _code(dt)))
+        bip = bip_ok(graph, H, Fd, dt)
         u_lo = (torch.empty_like(u_inter) if dt == BF16 and not bip
                 and any(ctx.needs_input_grad[:4]) else None)
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)

@@ -44,6 +44,9 @@ class Graph:
         self._plan = None
         self._chunk = chunk if chunk is not None else csc_chunk_for(self.n_edges)
         self._desc = None
+        # rows with distinct columns and at most max_deg edges (from_dense: by construction,
+        # max_deg <= n_cols): what the bipartite kernels require (functional.bip_ok)
+        self.distinct_cols, self.max_deg = True, self.n_cols
         if colptr is not None:
             self._build_plan(colptr.cpu().numpy().astype(np.int64))
 
@@ -162,13 +165,20 @@ class Graph:
                              "virtual full rows)")
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a, np.int32), device=device)  # noqa
         n = len(rowptr) - 1
+        rows_of = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr))
+        distinct = len(np.unique(rows_of * max(int(n_cols), 1) + col)) == len(col)
+        max_deg = int(np.diff(rowptr).max()) if n else 0
         if not with_csc:
-            return cls(n, n_cols, t(rowptr), t(col))
+            g = cls(n, n_cols, t(rowptr), t(col))
+            g.distinct_cols, g.max_deg = distinct, max_deg
+            return g
         perm = np.argsort(col, kind="stable")
         rows = np.repeat(np.arange(n), np.diff(rowptr))
         colptr = np.zeros(n_cols + 1, np.int64)
         np.cumsum(np.bincount(col, minlength=n_cols), out=colptr[1:])
-        return cls(n, n_cols, t(rowptr), t(col), None, t(colptr), t(rows[perm]), t(perm))
+        g = cls(n, n_cols, t(rowptr), t(col), None, t(colptr), t(rows[perm]), t(perm))
+        g.distinct_cols, g.max_deg = distinct, max_deg
+        return g
 
 
 _CACHE: dict = {}

@@ -11,6 +11,6 @@ rc=$?; tail -4 "$OUT/pytest.log"; grep -E "FAILED|Error" "$OUT/pytest.log" | hea
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; tail -20 "$OUT/smoke.log"; exit 3; }
 tail -1 "$OUT/smoke.log"
-timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-brc=$?; python3 scripts/bench_brief.py "$OUT/bench.json" 2>/dev/null | head -40; echo "pytest rc=$rc bench rc=$brc"
+T0=$SECONDS; timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+brc=$?; echo "bench wall $((SECONDS - T0)) s"; python3 scripts/bench_brief.py "$OUT/bench.json" 2>/dev/null | head -40; echo "pytest rc=$rc bench rc=$brc"
 exit $brc

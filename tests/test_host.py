@@ -152,3 +152,17 @@ def test_gcn_init_bit_identical(msha):
     assert sorted(sd) == sorted(k[len("init."):] for k in z.files if k.startswith("init."))
     for k, v in sd.items():
         assert np.array_equal(v.numpy(), z["init." + k]), k
+
+
+def test_from_csr_records_what_the_bipartite_kernels_need(msha):
+    """Graph.from_csr notes duplicate columns in a row and the largest row degree on the
+    host; functional.bip_ok keeps such graphs off the bipartite kernels (rows with
+    distinct columns, at most 64 / heads each)."""
+    import numpy as np
+
+    from msha_gnn_amd.graph import Graph
+
+    g = Graph.from_csr(np.array([0, 2, 3]), np.array([1, 1, 0]), 4, "cpu")
+    assert (g.distinct_cols, g.max_deg) == (False, 2)
+    g = Graph.from_csr(np.array([0, 2, 5]), np.array([1, 3, 0, 2, 3]), 4, "cpu")
+    assert (g.distinct_cols, g.max_deg) == (True, 3)
