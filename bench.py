@@ -738,6 +738,11 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
             def one(k):
                 feed(k)
                 return gs.replay()
+
+            # untimed replays: a graph's first launches carry one-time setup (an occasional
+            # ~25 ms first-replay stall put one year's step at 1.9 ms instead of 0.5)
+            for k in range(warmup):
+                one(k)
         else:
             def one(k):
                 feed(k)
