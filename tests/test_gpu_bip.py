@@ -166,3 +166,33 @@ def test_bip_many_groups_per_wave_vs_general(cuda, msha, p):
     for name, a, b in zip(("u", "v", "d_el", "d_er", "d_hc", "d_hs"), got, gen):
         rt = 1e-4 if name in ("d_el", "d_er") else 1e-5
         tol_close(a.cpu().numpy(), b.cpu().numpy(), rt, 1e-5)
+
+
+def test_shipped_graph_models_run_on_the_bipartite_kernels(cuda, msha):
+    """ablation3 on the full shipped 2015 graph (39,179 x 32) takes the bipartite kernels
+    both ways -- not the general edge kernels -- and its train-step forward stays a
+    normalised distribution per row."""
+    from conftest import golden
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd import layers
+
+    g = golden("r15_graph.npz")
+    n = int(g["n"])
+    c = np.zeros((n, 32), np.float32)
+    c[O.edge_rows(g["rowptr"]), g["col"].astype(np.int64)] = g["cnt"]
+    gdp = {i: float(x) for i, x in enumerate(g["gdp"])}
+    torch.manual_seed(0)
+    model = layers.ablation3(128, 64, 32, 2, 0.5, gdp, n, 32).to(cuda)
+    adj = msha.normalize_adjacency_matrix(torch.as_tensor(c, device=cuda))
+    model.train()
+    MF.KERNEL_EVENTS = {}
+    try:
+        out = model(adj, None, None, None)
+        out[:64].sum().backward()
+        torch.cuda.synchronize()
+        names = set(MF.KERNEL_EVENTS)
+    finally:
+        MF.KERNEL_EVENTS = None
+    assert {"bip_attention_fwd", "bip_attention_bwd"} <= names, names
+    assert not names & {"edge_attention_fwd", "edge_attention_bwd_rows", "csc_aggregate"}, names
+    assert torch.allclose(out.detach().exp().sum(1), torch.ones(n, device=cuda), atol=1e-4)
