@@ -11,14 +11,16 @@
 // Slabs are summed in wave order per block and the block partials in block order by
 // bip_reduce_kernel: deterministic, no atomics.
 //
-// Layout: one row per wave at a time, lane l owning elements [l V, l V + V) of the
-// H * F row (V = H F / 64); the lane's head is hl = l V / F, so a head's dot products
-// reduce over its QH = F / V consecutive lanes.  Per-edge scalars (column, score,
-// attention, keep bit) are wave-uniform per head: a row's edges are walked as a uniform
-// loop, columns come from a per-group register page by v_readlane, er from LDS.
-// Rows go in groups of PD (one vector load each for rowptr, el, lse, coef and the
-// group's columns; one Philox call per lane covers 64 (edge, head) keep bits), and the
-// next group's loads are in flight while this group runs.
+// Layout: a wave walks a contiguous row range in groups of kPD = 8 rows.  Per group one
+// buffer load each brings rowptr, the group's <= 256 columns, el / lse / coef and the
+// rows' slices of the streamed tables; every global load and store of the loop is an
+// unconditional buffer op (masked lanes at kOOB), so the next group's loads are in
+// flight while this group runs and the compiler's vmcnt waits stay exact.  A group is cut
+// into sub-groups whose (edge, head) pairs fill <= 64 slot lanes: slot lanes compute the
+// scores, the row softmax (lane-segmented scans), the keep bits and the attention once;
+// element lanes (lane l owns elements [l V, l V + V) of the H * F row, V = H F / 64, so
+// a head's dot products reduce over its QH = F / V lanes) then walk each row's edges with
+// the attention and hc_j read from LDS.
 //
 // Reference: Ablation.py:266-274 (OursLayer3 scores, masked softmax, dropout,
 // u = att @ h1, v = att.T @ h2), Ours.py:84-86 (the backward's row coefficients).
@@ -715,29 +717,32 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
 }
 
 // out[i] = sum_b part[b][i] in block order (i < n_t -> out_t as T, else out_f fp32).
-// One 64-entry column slice per block; its 16 waves sum contiguous block ranges, then
-// the range sums add in wave order.
+// A block owns 16 consecutive entries; its 64 streams (lane / 16 of each wave, wave-major)
+// sum contiguous block ranges (every load of a stream in flight at once), then the
+// stream sums add in stream order.  256 blocks at M x H x F = 4096: the whole chip reads
+// the partials (64 blocks of one 64-entry slice each ran latency-bound, 6.6 us).
 template <typename T>
 __global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restrict__ part,
                                                           int32_t nb, int32_t stride,
                                                           int32_t n_t, T* __restrict__ out_t,
                                                           float* __restrict__ out_f) {
-  __shared__ float red[16][64];
+  __shared__ float red[64][17];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;
-  const int per = (nb + 15) / 16;
-  const int b0 = wv * per, b1 = min(nb, b0 + per);
+  const int c = lane & 15, st = wv * 4 + (lane >> 4);  // entry in the slice, stream
+  const int i = blockIdx.x * 16 + c;
+  const int per = (nb + 63) / 64;
+  const int b0 = st * per, b1 = min(nb, b0 + per);
   float a = 0.f;
   if (i < stride)
     for (int b = b0; b < b1; ++b) a += part[(int64_t)b * stride + i];
-  red[wv][lane] = a;
+  red[st][c] = a;
   __syncthreads();
-  if (wv == 0 && i < stride) {
-    float s = red[0][lane];
-#pragma unroll
-    for (int q = 1; q < 16; ++q) s += red[q][lane];
-    if (i < n_t) out_t[i] = from_f32<T>(s);
-    else out_f[i - n_t] = s;
+  if (threadIdx.x < 16 && i < stride) {
+    float sum = red[0][c];
+#pragma unroll 8
+    for (int q = 1; q < 64; ++q) sum += red[q][c];
+    if (i < n_t) out_t[i] = from_f32<T>(sum);
+    else out_f[i - n_t] = sum;
   }
 }
 
@@ -805,7 +810,7 @@ static void bip_launch_fwd(const msha_graph* g, const float* el, const float* er
     if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, true, true>);
     else go(bip::bip_fwd_kernel<H, F, T, true, false>);
     const int32_t MD = (int32_t)(g->n_cols * H * F);
-    hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + 63) / 64), dim3(1024), 0, s, part,
+    hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + 15) / 16), dim3(1024), 0, s, part,
                        nb, MD, MD, (T*)v, (float*)nullptr);
   } else {
     if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, false, true>);
@@ -832,7 +837,7 @@ static void bip_launch_bwd(const msha_graph* g, const float* el, const float* er
   else if (cf) go(bip::bip_bwd_kernel<H, F, T, false, true>);
   else go(bip::bip_bwd_kernel<H, F, T, false, false>);
   const int32_t MD = (int32_t)(g->n_cols * H * F), MH = (int32_t)(g->n_cols * H);
-  hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + MH + 63) / 64), dim3(1024), 0, s, part,
+  hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + MH + 15) / 16), dim3(1024), 0, s, part,
                      nb, MD + MH, MD, (T*)d_hc, d_er);
 }
 
