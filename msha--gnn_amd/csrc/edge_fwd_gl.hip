@@ -28,7 +28,7 @@ namespace msha {
 // it): from the scores still in registers for one-chunk rows, else a second pass over
 // the row's columns and er (not with RS).
 // RT: the row terms uc, qc of the fused backward (see edge_attn_fwd_bat_kernel).
-template <int H, int F, typename T, int NGI, bool RT, bool RS, bool ATTD>
+template <int H, int F, typename T, int NGI, bool RT, bool RS, bool ATTD, bool PF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FWD_WPE)))
 edge_attn_fwd_gl_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
@@ -90,6 +90,19 @@ edge_attn_fwd_gl_kernel(
   int32_t end = __builtin_amdgcn_readfirstlane(rowptr[row + 1]);
   bool virt = rowflag != nullptr && rowflag[row] != 0;
   float elq = el[(int64_t)row * H + hq];
+  // one chunk's gathers (and er), all in flight together; slots past the row read 0
+  auto gather = [&](int32_t cs, int32_t end, const int32_t (&j)[NJ], u32x4_t (&raw)[NGI],
+                    float (&erq)[NGI]) {
+    const int nvalid = min(CEL, (int)(end - cs));
+#pragma unroll
+    for (int gi = 0; gi < NGI; ++gi) {
+      const bool valid = gi * G::EPI + g_e < nvalid;
+      const int32_t jj = col_of(j, gi);
+      raw[gi] = buf_b128(r_hc, valid ? (uint32_t)jj * (uint32_t)(G::D * sizeof(T)) + q_off
+                                     : kOOB);
+      if (!RS) erq[gi] = buf_f32(r_er, valid ? (uint32_t)jj * (4u * H) + 4u * hq : kOOB);
+    }
+  };
   int32_t jc[NJ], jn[NJ];
   load_cols(start, end, jc);
   load_cols(start + CEL, end, jn);
@@ -98,19 +111,18 @@ edge_attn_fwd_gl_kernel(
     Pk<T> acc = pk_zero<T>(), accc = pk_zero<T>();
     float sc_keep[NGI];   // ATTD: the scores of a one-chunk row
     uint64_t kb_keep[NB];
+    // PF (long rows): chunk c + 1's gathers leave before chunk c's scores are reduced
+    // (two chunks in flight per wave); otherwise each chunk's gathers leave at its start
+    u32x4_t raw[NGI];
+    float erq[NGI];
+    if (PF) gather(start, end, jc, raw, erq);
     for (int32_t cs = start; cs < end; cs += CEL) {
       const int nvalid = min(CEL, (int)(end - cs));
-      // (1) this chunk's gathers (and er), all in flight together
-      u32x4_t raw[NGI];
-      float erq[NGI];
-#pragma unroll
-      for (int gi = 0; gi < NGI; ++gi) {
-        const bool valid = gi * G::EPI + g_e < nvalid;
-        const int32_t j = col_of(jc, gi);
-        raw[gi] = buf_b128(r_hc, valid ? (uint32_t)j * (uint32_t)(G::D * sizeof(T)) + q_off
-                                       : kOOB);
-        if (!RS) erq[gi] = buf_f32(r_er, valid ? (uint32_t)j * (4u * H) + 4u * hq : kOOB);
-      }
+      // (1) the gathers: this chunk's, or (prefetch) the next chunk's
+      u32x4_t rawn[NGI];
+      float erqn[NGI];
+      if (PF) gather(cs + CEL, end, jn, rawn, erqn);
+      else gather(cs, end, jc, raw, erq);
       // columns two chunks ahead
       int32_t jnn[NJ];
       load_cols(cs + 2 * CEL, end, jnn);
@@ -186,6 +198,13 @@ edge_attn_fwd_gl_kernel(
       for (int k = 0; k < NJ; ++k) {
         jc[k] = jn[k];
         jn[k] = jnn[k];
+      }
+      if (PF) {
+#pragma unroll
+        for (int gi = 0; gi < NGI; ++gi) {
+          raw[gi] = rawn[gi];
+          if (!RS) erq[gi] = erqn[gi];
+        }
       }
     }
     // the next row's bounds, flag, el and first columns before this row's epilogue
@@ -266,7 +285,7 @@ edge_attn_fwd_gl_kernel(
   }
 }
 
-template <int H, int F, typename T, int NGI>
+template <int H, int F, typename T, int NGI, bool PF>
 static void launch_gl_shape(const msha_graph* g, const float* el, const float* er,
                             const float* ar, const void* hc, float slope, const Dropout& dp,
                             void* u, void* u_lo, float* lse, float* attd, float* uc, float* qc,
@@ -278,14 +297,14 @@ static void launch_gl_shape(const msha_graph* g, const float* el, const float* e
                        (const T*)hc, slope, dp, (T*)u, (T*)u_lo, lse, attd, uc, qc);
   };
   if (rs) {
-    if (rt) go(edge_attn_fwd_gl_kernel<H, F, T, NGI, true, true, false>);
-    else go(edge_attn_fwd_gl_kernel<H, F, T, NGI, false, true, false>);
+    if (rt) go(edge_attn_fwd_gl_kernel<H, F, T, NGI, true, true, false, PF>);
+    else go(edge_attn_fwd_gl_kernel<H, F, T, NGI, false, true, false, PF>);
   } else if (at) {
-    go(edge_attn_fwd_gl_kernel<H, F, T, NGI, false, false, true>);
+    go(edge_attn_fwd_gl_kernel<H, F, T, NGI, false, false, true, PF>);
   } else if (rt) {
-    go(edge_attn_fwd_gl_kernel<H, F, T, NGI, true, false, false>);
+    go(edge_attn_fwd_gl_kernel<H, F, T, NGI, true, false, false, PF>);
   } else {
-    go(edge_attn_fwd_gl_kernel<H, F, T, NGI, false, false, false>);
+    go(edge_attn_fwd_gl_kernel<H, F, T, NGI, false, false, false, PF>);
   }
 }
 
@@ -304,20 +323,20 @@ int launch_fwd_gl(const msha_graph* g, int heads, int feat, int32_t dtype, const
     if (dtype == MSHA_DTYPE_BF16) {                                                           \
       if constexpr (f % 8 == 0 && h * f * 2 <= 1024) {                                        \
         if (short_rows)                                                                       \
-          launch_gl_shape<h, f, bf16_t, gl_ngi_short<h, f, bf16_t>()>(                        \
+          launch_gl_shape<h, f, bf16_t, gl_ngi_short<h, f, bf16_t>(), false>(                        \
               g, el, er, ar, hc, slope, dp, u, u_lo, lse, attd, uc, qc, grid, s);             \
         else                                                                                  \
-          launch_gl_shape<h, f, bf16_t, gl_ngi_long<h, f, bf16_t>()>(                         \
+          launch_gl_shape<h, f, bf16_t, gl_ngi_long<h, f, bf16_t>(), GL_PREFETCH_BF16>(                         \
               g, el, er, ar, hc, slope, dp, u, u_lo, lse, attd, uc, qc, grid, s);             \
         done = 1;                                                                             \
       }                                                                                       \
     } else {                                                                                  \
       if constexpr (h * f * 4 <= 1024) {                                                      \
         if (short_rows)                                                                       \
-          launch_gl_shape<h, f, float, gl_ngi_short<h, f, float>()>(                          \
+          launch_gl_shape<h, f, float, gl_ngi_short<h, f, float>(), false>(                          \
               g, el, er, ar, hc, slope, dp, u, nullptr, lse, attd, uc, qc, grid, s);          \
         else                                                                                  \
-          launch_gl_shape<h, f, float, gl_ngi_long<h, f, float>()>(                           \
+          launch_gl_shape<h, f, float, gl_ngi_long<h, f, float>(), GL_PREFETCH_F32>(                           \
               g, el, er, ar, hc, slope, dp, u, nullptr, lse, attd, uc, qc, grid, s);          \
         done = 1;                                                                             \
       }                                                                                       \

@@ -15,7 +15,16 @@
 #define GL_EPL_BF16 1  // the gather-layout forward's long chunks, bf16 tables (CEL 8)
 #endif
 #ifndef GL_EPL_F32
-#define GL_EPL_F32 FWD_EPL
+#define GL_EPL_F32 1  // fp32 tables: CEL 8 with the prefetch (CEL 16 without it)
+#endif
+// the gather-layout forward's long rows issue the next chunk's gathers before this
+// chunk's softmax (syn2m forward: bf16 2460 -> 2262 us, fp32 at CEL 8 3728 -> 3649 us; fp32
+// at CEL 16 lost a wave per SIMD to the second buffer and ran slower, 3961 us)
+#ifndef GL_PREFETCH_BF16
+#define GL_PREFETCH_BF16 1
+#endif
+#ifndef GL_PREFETCH_F32
+#define GL_PREFETCH_F32 1
 #endif
 #ifndef FWD_WPE
 #define FWD_WPE 1
