@@ -3,7 +3,7 @@
 # C4 / syn2m legs only; each variant's forward parity tests first.
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/r3_pfab${1:-}"; mkdir -p "$OUT"; cd "$R"
-for V in "" f32pf bf16e2; do
+for V in "" wpe6; do
   L="$R/msha--gnn_amd/lib/libmsha_gnn${V:+_$V}.so"
   MSHA_GNN_LIB="$L" timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
     tests/test_gpu_parity_full.py tests/test_gpu_row_scores.py > "$OUT/tests_$V.log" 2>&1
