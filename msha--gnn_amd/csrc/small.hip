@@ -60,9 +60,10 @@ __global__ void __launch_bounds__(kSmallThreads) small_fwd_kernel(SmallArgs a) {
     const int side = t / a.H, hh = t - side * a.H;
     const float* v = side == 0 ? a.al : a.ar;
     float* o = side == 0 ? a.el : a.er;
-    if (v != nullptr) {
-      // the row-score order of the edge kernels (msha_project_scores_row_order): per
-      // 4-element piece last element first, fma downwards; then the pieces' xor tree
+    if (v != nullptr && F % 4 == 0) {
+      // the row-score order of the edge kernels (msha_project_scores_row_order, which
+      // covers feat % 4 == 0): per 4-element piece last element first, fma downwards;
+      // then the pieces' xor tree
       float d[32];  // F / 4 <= 32 pieces
       const int np = F / 4;
       for (int k = 0; k < np; ++k) {
@@ -73,6 +74,11 @@ __global__ void __launch_bounds__(kSmallThreads) small_fwd_kernel(SmallArgs a) {
       for (int st = 1; st < np; st <<= 1)
         for (int k = 0; k + st < np; k += 2 * st) d[k] = d[k] + d[k + st];
       o[(int64_t)i * a.H + hh] = d[0];
+    } else if (v != nullptr) {
+      // any other feat: an fma chain in element order over the whole head
+      float d = 0.f;
+      for (int f = 0; f < F; ++f) d = fmaf(hr[hh * F + f], v[hh * F + f], d);
+      o[(int64_t)i * a.H + hh] = d;
     }
   }
 }

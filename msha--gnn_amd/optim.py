@@ -39,8 +39,14 @@ class Adam(torch.optim.Optimizer):
             raise ValueError("msha Adam: lr, eps and weight_decay must be >= 0")
         if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError("msha Adam: betas must be in [0, 1)")
+        # capturable / fused in the defaults: torch's load_state_dict then moves every
+        # loaded 'step' to the parameter's device as fp32 (a CPU step from a
+        # map_location='cpu' checkpoint or a torch.optim.Adam state_dict would otherwise
+        # stay on the host, and the kernel reads it through a device pointer)
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps,
-                                      weight_decay=weight_decay))
+                                      weight_decay=weight_decay, amsgrad=False,
+                                      maximize=False, foreach=None, capturable=True,
+                                      differentiable=False, fused=False))
         self._ws = {}  # device -> the launches' per-tensor scalars (stream-ordered reuse)
 
     def _workspace(self, dev):
@@ -56,6 +62,18 @@ class Adam(torch.optim.Optimizer):
             st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+            return st
+        # state loaded from elsewhere: the kernel reads 'step' (fp32) and the moments (the
+        # parameter's dtype, contiguous) through device pointers
+        stp = st["step"]
+        if not (torch.is_tensor(stp) and stp.device == p.device and stp.dtype == torch.float32
+                and stp.numel() == 1):
+            st["step"] = torch.as_tensor(float(stp), dtype=torch.float32,
+                                         device=p.device).reshape(())
+        for k in ("exp_avg", "exp_avg_sq"):
+            m = st[k]
+            if m.device != p.device or m.dtype != p.dtype or not m.is_contiguous():
+                st[k] = m.to(device=p.device, dtype=p.dtype).contiguous()
         return st
 
     def _group_of(self, p):
@@ -102,6 +120,12 @@ class Adam(torch.optim.Optimizer):
             for p in group["params"]:
                 stash = getattr(p, "_msha_dropout_grad", None)
                 if stash is not None:  # fused: the dropout's output gradient + its mask
+                    if p.grad is not None:
+                        # a second consumer of the fused parameter put a gradient in .grad:
+                        # the fused update would silently drop it
+                        raise RuntimeError(
+                            "msha Adam: a fuse_dropout_grad parameter also has a .grad (it has "
+                            "another consumer besides its feature dropout): do not fuse it")
                     dout, drop_p, seed = stash
                     p._msha_dropout_grad = None
                     self._check(p, dout)

@@ -36,8 +36,13 @@ def pair_range(n_pairs: int, world: int, rank: int):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def _group_ready(group) -> bool:
-    return dist.is_available() and dist.is_initialized()
+def _group_ready(group, world: int) -> bool:
+    """Run the collective: a process group is initialised and either one was passed or
+    the default group spans exactly this table's world.  (A rank-local world-1 table in
+    a multi-process job copies its rows instead of failing the world-size check.)"""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return group is not None or dist.get_world_size() == world
 
 
 class ShardedTable:
@@ -53,7 +58,7 @@ class ShardedTable:
         self.fulls = [torch.empty(self.R * world, feat, device=device, dtype=dtype)
                       for _ in range(max(1, buffers))]
         self.cur = 0
-        if _group_ready(group):
+        if _group_ready(group, world):
             gw = dist.get_world_size(group)
             if gw != world:
                 raise ValueError(f"ShardedTable: world {world} but the process group has {gw}")
@@ -71,7 +76,7 @@ class ShardedTable:
     def path(self) -> str:
         """Which exchange ``gather`` runs: 'rccl' (all_gather_into_tensor on a CUDA
         group), 'gloo' (list all_gather, CPU tests) or 'copy' (no process group)."""
-        if not _group_ready(self.group):
+        if not _group_ready(self.group, self.world):
             if self.world != 1:
                 raise RuntimeError("ShardedTable: world > 1 needs an initialised process group")
             return "copy"

@@ -83,6 +83,11 @@ def _worker(rank, world, port, q):
                                  [(W, b), (None, None)])
             ok = ok and outs[k][:2] == (a_, b_) and np.allclose(outs[k][2].numpy(), want,
                                                                 rtol=1e-6, atol=1e-6)
+        # a rank-local world-1 table inside this multi-process job: no
+        # world-size error, its rows are copied
+        solo = sharding.ShardedTable(n, F, 1, 0, "cpu")
+        solo.set_local(torch.as_tensor(h))
+        ok = ok and solo.path() == "copy" and torch.equal(solo.gather(), torch.as_tensor(h))
         # bench.py's timing reduction: the max over ranks
         t = torch.tensor([0.5 + rank])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -454,7 +454,11 @@ def test_gemm_f32(cuda, M, N, K, trans_a, trans_b, splits):
 @pytest.mark.parametrize("M,K,H,F", [(3000, 128, 8, 16), (517, 128, 2, 64), (80, 16, 1, 8),
                                      (300, 64, 4, 32), (200, 32, 1, 128),
                                      # resident-W kernel (skinny.hip): ragged last tile
-                                     (5001, 64, 2, 64), (2050, 128, 4, 32)])
+                                     (5001, 64, 2, 64), (2050, 128, 4, 32),
+                                     # the small-table kernel (M <= 256, small.hip) at feat
+                                     # % 4 != 0 (its 4-piece score order)
+                                     (32, 128, 1, 3), (32, 64, 2, 6), (32, 128, 4, 10),
+                                     (32, 128, 2, 50)])
 def test_project_scores_fwd_bwd(cuda, M, K, H, F):
     from msha_gnn_amd import functional as MF
 

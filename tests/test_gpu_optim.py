@@ -154,3 +154,54 @@ def test_graphed_fused_adam_matches_eager(cuda, msha):
         params[graphed] = [p.detach().clone() for p in model.parameters()]
     for a, b in zip(params[False], params[True]):
         assert torch.equal(a, b)
+
+
+def test_adam_loads_torch_state_dict_from_cpu(cuda, msha):
+    """a torch.optim.Adam state_dict saved and loaded with map_location='cpu'
+    (its 'step' a CPU tensor) continues bit-for-bit like torch on the device: the loaded
+    step moves to the parameter's device (capturable in the defaults / _state_of)."""
+    import io
+
+    from msha_gnn_amd.optim import Adam
+
+    g = torch.Generator().manual_seed(2)
+    shapes = [(300, 64), (17,)]
+    ref = [torch.randn(s, generator=g).to(cuda).requires_grad_(True) for s in shapes]
+    o_ref = torch.optim.Adam(ref, lr=1e-3, weight_decay=5e-4)
+    grads = [[torch.randn(s, generator=g).to(cuda) for s in shapes] for _ in range(5)]
+    for k in range(3):
+        for p, gr in zip(ref, grads[k]):
+            p.grad = gr.clone()
+        o_ref.step()
+    buf = io.BytesIO()
+    torch.save(o_ref.state_dict(), buf)
+    buf.seek(0)
+    sd = torch.load(buf, map_location="cpu", weights_only=True)
+    assert sd["state"][0]["step"].device.type == "cpu"
+    ours = [p.detach().clone().requires_grad_(True) for p in ref]
+    o_us = Adam(ours, lr=1e-3, weight_decay=5e-4)
+    o_us.load_state_dict(sd)
+    for k in range(3, 5):
+        for a, b, gr in zip(ref, ours, grads[k]):
+            a.grad, b.grad = gr.clone(), gr.clone()
+        o_ref.step()
+        o_us.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, ours):
+        assert o_us.state[b]["step"].device == b.device
+        assert float(o_us.state[b]["step"]) == 5.0
+        tol_close(b.detach().cpu().numpy(), a.detach().cpu().numpy(), 1e-6, 1e-6)
+
+
+def test_adam_fused_param_with_grad_raises(cuda, msha):
+    """a fuse_dropout_grad parameter that also received a .grad (a second
+    consumer) makes step() raise instead of dropping that gradient."""
+    from msha_gnn_amd.optim import Adam
+
+    p = torch.randn(64, 8, device=cuda, requires_grad=True)
+    opt = Adam([p], lr=1e-3)
+    opt.fuse_dropout_grad(p)
+    opt.stash_dropout_grad(p, torch.randn(64, 8, device=cuda), 0.5, 7)
+    p.grad = torch.randn(64, 8, device=cuda)
+    with pytest.raises(RuntimeError, match="another consumer"):
+        opt.step()
