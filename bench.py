@@ -118,21 +118,47 @@ def _newest_first(path):  # round1_syn100k_v10 after _v9: compare the numbers
     return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", tag)]
 
 
-def pmc_lookup(patterns, glob_pat):
+def kernel_source_id() -> str:
+    """Identity of the HIP sources the library is built from: sha256 over
+    msha--gnn_amd/csrc/*.hip|*.h and include/*.h (sorted).  scripts/profile.sh records it
+    with each profile; pmc_lookup attaches PMC traffic only from a profile of the same
+    sources (no traffic figure from a different build)."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "msha--gnn_amd", "csrc", "*.hip"))
+                   + glob.glob(os.path.join(ROOT, "msha--gnn_amd", "csrc", "*.h"))
+                   + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def pmc_lookup(patterns, glob_pat, profiles_dir=None):
     """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) summed over
     the kernels matching ``patterns`` (regexes; each must match a kernel of the same
     summary, several matches of one pattern are averaged) in the newest committed profile matching ``glob_pat``
     (profiles/<glob>/pmc_summary.json, written by scripts/summarize_profile.py from
-    separate rocprofv3 --pmc passes).  (None, None) if absent."""
+    separate rocprofv3 --pmc passes) whose recorded source id is this build's
+    (kernel_source_id).  (None, None) if absent; (None, note) if only profiles of other
+    sources exist."""
     import glob
     import re
 
     pats = [re.compile(p) for p in patterns]
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", glob_pat, "pmc_summary.json")),
+    sid = kernel_source_id()
+    stale = None
+    pdir = profiles_dir or os.path.join(ROOT, "profiles")
+    for path in sorted(glob.glob(os.path.join(pdir, glob_pat, "pmc_summary.json")),
                        key=_newest_first, reverse=True):
         try:
             summ = json.load(open(path))
         except (OSError, ValueError):
+            continue
+        if summ.get("_meta", {}).get("source_id") != sid:
+            stale = stale or os.path.relpath(path, ROOT)
             continue
         tot, ok = 0.0, True
         for p in pats:
@@ -145,6 +171,8 @@ def pmc_lookup(patterns, glob_pat):
             tot += sum(float(h["hbm_bytes_per_launch_corrected"]) for h in hit) / len(hit)
         if ok:
             return tot, os.path.relpath(path, ROOT)
+    if stale is not None:  # the newest profile is of other sources: no traffic figure
+        return None, f"none of this build (newest: {stale}, other sources)"
     return None, None
 
 
@@ -496,6 +524,18 @@ def pair_bytes(F, s, mode, hidden):
     return 16 + 2 * s * F + out
 
 
+IC_GATHER_PEAK_GBS = 8600.0  # random 1,152-B rows from a 38 MB table (MI355X_MICROARCH.md)
+
+
+def pair_compulsory_bytes(n, F, s, mode, hidden, P):
+    """Compulsory HBM bytes of one pair-scoring launch: every table row read once (the
+    table, n x F), the two int64 indices per pair, the scores written (fp32 inner; mlp:
+    hidden scores in the table's dtype) and, for mlp, W and the bias."""
+    out = 4 if mode == "inner" else s * hidden
+    w = (hidden * F * s + 4 * hidden) if mode == "mlp" else 0
+    return n * F * s + P * (16 + out) + w
+
+
 def link_score_bench(dev, rowptr, col, n, F, world, rank, group_ok, steps=16, warmup=3,
                      hidden=128, n_pairs=4_000_000, dtype=torch.float32, amortise=8):
     """score P = 4M pairs (2M graph edges + 2M uniform negatives,
@@ -599,24 +639,46 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, group_ok, steps=16, wa
         torch.cuda.synchronize(dev)
         us = float(np.mean([a.elapsed_time(z) for a, z in evs])) * 1e3
         P = phi - plo
-        nbytes = P * pair_bytes(F, s, mode, hidden)
+        gathered = P * pair_bytes(F, s, mode, hidden)
+        comp = pair_compulsory_bytes(n, F, s, mode, hidden, P)
         flops = P * (2 * F * hidden + F) if mode == "mlp" else P * 2 * F
         kname = ("pair_kernel" if mode == "mlp" else "pair_inner")
         tr, src_ = pmc_lookup([_pair_pattern(mode, s == 2)], "*link*")
+        t_s = us * 1e-6
+        # memory side: the compulsory HBM bytes (every table row once, the indices, the
+        # scores) against the 8 TB/s HBM peak, and -- the table (25-51 MB) being gathered
+        # ~80x per batch from the Infinity Cache -- the measured PMC bytes against the
+        # guide's random-row Infinity-Cache rate (MI355X_MICROARCH.md "Indexed rows")
+        mem = {"compulsory_bytes_per_launch": comp,
+               "compulsory_GBs": comp / t_s / 1e9,
+               "frac_compulsory_hbm": comp / t_s / 1e9 / HBM_PEAK_GBS,
+               "gathered_bytes_per_launch": gathered,
+               "gathered_note": "per-pair model: both rows counted for every pair (each row is "
+                                f"gathered ~{2 * n_pairs // max(n, 1)}x per batch); not a "
+                                "roofline numerator",
+               "traffic": tr, "traffic_source": src_,
+               "traffic_note": "rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch: L2->fabric "
+                               "bytes incl. Infinity-Cache hits"}
+        if tr is not None:
+            mem.update(traffic_GBs=tr / t_s / 1e9, ic_peak_GBs=IC_GATHER_PEAK_GBS,
+                       frac_traffic_ic=tr / t_s / 1e9 / IC_GATHER_PEAK_GBS)
         if mode == "mlp" and s == 4:
-            ach = flops / (us * 1e-6) / 1e12
+            ach = flops / t_s / 1e12
             roof = {"kernel": kname, "bound": "mfma", "achieved": ach, "peak": F32_MFMA_TFLOPS,
                     "unit": "TFLOP/s", "frac": ach / F32_MFMA_TFLOPS}
+        elif tr is not None:
+            roof = {"kernel": kname, "bound": "ic", "achieved": tr / t_s / 1e9,
+                    "peak": IC_GATHER_PEAK_GBS, "unit": "GB/s",
+                    "frac": tr / t_s / 1e9 / IC_GATHER_PEAK_GBS,
+                    "ceiling": "random-row Infinity-Cache gather rate (8.6 TB/s, "
+                               "MI355X_MICROARCH.md) on the PMC bytes"}
         else:
-            ach = nbytes / (us * 1e-6) / 1e9
-            roof = {"kernel": kname, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": ach / HBM_PEAK_GBS}
-        roof.update(avg_launch_us=us, pairs_per_launch=P, algorithmic_bytes_per_launch=nbytes,
-                    flops_per_launch=flops, kernel_pairs_per_sec=P / (us * 1e-6),
-                    traffic=tr, traffic_source=src_,
-                    traffic_note="rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch: L2->fabric "
-                                 "bytes incl. Infinity-Cache hits (each table row is gathered "
-                                 f"~{2 * n_pairs // max(n, 1)}x per batch)")
+            roof = {"kernel": kname, "bound": "hbm", "achieved": comp / t_s / 1e9,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": comp / t_s / 1e9 / HBM_PEAK_GBS,
+                    "ceiling": "compulsory HBM bytes at 8 TB/s (no PMC profile of this build)"}
+        roof.update(avg_launch_us=us, pairs_per_launch=P, flops_per_launch=flops,
+                    kernel_pairs_per_sec=P / t_s, memory=mem)
         res[f"roofline_{mode}"] = roof
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -773,6 +835,66 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
     return res
 
 
+def train_py_literal_leg(dev, model_kind="ablation3", steps=20, warmup=5):
+    """train.py as written (train.py:180-232, msha_gnn_amd.trainpy): the zero-argument
+    HigherDataset over the shipped 2015 data in anonymous_data format, its DataLoader
+    (batch 64, shuffle), torch.optim.Adam(lr 1e-3, weight_decay 5e-4) as train.py:207
+    builds it, and per step the loop body statement for statement -- next batch from the
+    loader, .to(device), zero_grad, the model, F.nll_loss(output[source_index], ...),
+    loss.item(), backward, step -- eagerly, no HIP graph.  ms per step = median of three
+    windows of ``steps`` iterations (the loader's own time included; reported apart)."""
+    import tempfile
+
+    import msha_loader
+
+    msha_loader.load()
+    from msha_gnn_amd import trainpy
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    yz = np.load(os.path.join(ROOT, "tests", "golden", "years.npz"))
+    rows = np.repeat(np.arange(int(z["n"])), np.diff(z["rowptr"]))
+    flows = np.stack([np.repeat(rows, z["cnt"].astype(np.int64)),
+                      np.repeat(z["col"].astype(np.int64), z["cnt"].astype(np.int64))], 1)
+    res = dict(model=model_kind, year="2015", dtype="float32", optimizer="torch.optim.Adam",
+               loss="F.nll_loss(output[source_index], recipient_index)", hip_graph=False)
+    with tempfile.TemporaryDirectory(prefix="msha_trainpy_") as d:
+        trainpy.write_year(d, "2015", yz["2015.city"], yz["2015.prov"], yz["2015.gdp"], flows,
+                           int(z["m"]))
+        with trainpy.namespace(d, dev) as ns:
+            tp = trainpy.TrainPy(ns, dev, dropout=0.5, model_kind=model_kind)
+            state = {"it": iter(tp.train_loader)}
+
+            def next_batch():
+                try:
+                    return next(state["it"])
+                except StopIteration:  # a new epoch of the loader, as train.py's next call
+                    state["it"] = iter(tp.train_loader)
+                    return next(state["it"])
+
+            for _ in range(warmup):
+                tp.iteration(next_batch())
+            windows, loader = [], []
+            for _ in range(3):
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    loss = tp.iteration(next_batch())
+                torch.cuda.synchronize(dev)
+                windows.append((time.perf_counter() - t0) / steps * 1e3)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                next_batch()
+            loader = (time.perf_counter() - t0) / steps * 1e3
+            res.update(nodes=int(z["n"]), recipients=int(z["m"]),
+                       edges=int(len(z["col"])), flows=int(len(flows)))
+    res["ms_per_step_windows"] = [round(x, 4) for x in windows]
+    res["ms_per_step"] = sorted(windows)[1]
+    res["loader_ms_per_batch"] = loader
+    res["loss"] = float(loss)
+    res["edges_per_sec"] = res["edges"] / (res["ms_per_step"] * 1e-3)
+    return res
+
+
 def cpu_share():
     """CPUs this process may use: its affinity, capped by the cgroup's CPU quota (the GPU
     box grants each GPU a share of a large host; os.cpu_count() reports the host)."""
@@ -841,6 +963,55 @@ def cpu_baseline(rowptr, col, n, fin, H, F, budget_s=10.0):
                 sample=f"whole graph ({n} rows, {len(col)} edges), {reps} fwd+bwd steps in "
                        f"{el_t:.1f}s: numpy X@W + oracle/edge_attention_cpu.c (OpenMP, "
                        f"{cpu_oracle.threads()} threads = OMP_NUM_THREADS)")
+
+
+def cpu_baseline_bip1m(rowptr, col, n, m, fin=128, H=2, F=64, budget_s=10.0):
+    """bip1m CPU baseline: the same OursLayer3-core step as the bip1m leg (h1 = R W,
+    h2 = S W, scores, u = att @ h1 AND v = att.T @ h2, the backward incl. the hs . dV
+    term, d_hs, and dW) on this host's cores: numpy BLAS for the projections and
+    oracle/edge_attention_cpu.c (OpenMP) for the edge softmax / aggregates, whole graph,
+    repeated for ~budget_s."""
+    from oracle import cpu_oracle
+    from oracle import gnn_oracle as O
+
+    rng = np.random.default_rng(0)
+    X = rng.random((n, fin), dtype=np.float32)
+    Xr = rng.random((m, fin), dtype=np.float32)
+    W = (rng.standard_normal((fin, H * F)) * fin ** -0.5).astype(np.float32)
+    al = rng.standard_normal((H, F)).astype(np.float32)
+    ar = rng.standard_normal((H, F)).astype(np.float32)
+    dU = rng.standard_normal((n, H, F)).astype(np.float32)
+    dV = rng.standard_normal((m, H, F)).astype(np.float32)
+    colptr, perm = O.csr_to_csc(rowptr, col, m)
+    csc_row = O.edge_rows(rowptr)[perm]
+
+    def one():
+        h2 = (X @ W).reshape(n, H, F)
+        h1 = (Xr @ W).reshape(m, H, F)
+        el = np.einsum("nhf,hf->nh", h2, al)
+        er = np.einsum("mhf,hf->mh", h1, ar)
+        u, lse, v = cpu_oracle.edge_attention_fwd(rowptr, col, el, er, h1, hs=h2, colptr=colptr,
+                                                  csc_row=csc_row, csc_eid=perm)
+        d_el, d_er, d_hc, d_hs = cpu_oracle.edge_attention_bwd(
+            rowptr, col, colptr, csc_row, perm, el, er, h1, lse, u, dU, hs=h2, dV=dV)
+        dh2 = (d_hs + d_el[:, :, None] * al[None]).reshape(n, H * F)
+        dh1 = (d_hc + d_er[:, :, None] * ar[None]).reshape(m, H * F)
+        _ = X.T @ dh2 + Xr.T @ dh1  # dW
+
+    one()  # warm-up (page-in, thread pool)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        one()
+        reps += 1
+        el_t = time.perf_counter() - t0
+        if el_t >= budget_s or reps >= 50:
+            break
+    return dict(value=len(col) * reps / el_t, unit="edges/s", cores=cpu_oracle.threads(),
+                kind="port",
+                sample=f"whole bip1m graph ({n} x {m}, {len(col)} edges), {reps} OursLayer3-core "
+                       f"fwd+bwd steps (u and v, d_hs, dW) in {el_t:.1f}s: numpy projections + "
+                       f"oracle/edge_attention_cpu.c (OpenMP, {cpu_oracle.threads()} threads)")
 
 
 def host_cpu():
@@ -940,6 +1111,36 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd + list(argv))
 
 
+def rank_census(dist_on, dev):
+    """Who took part, recorded in the JSON line so a multi-GPU run proves its own shape:
+    the process group's world size and backend (nccl = RCCL on ROCm), and per rank its
+    RANK / LOCAL_RANK, device and the device's PCI bus id (all_gather_object over the
+    group; one entry without a group)."""
+    import socket
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    me = {"rank": int(os.environ.get("RANK", "0")), "local_rank": local,
+          "host": socket.gethostname(), "device": str(dev)}
+    if dev is not None and torch.device(dev).type == "cuda":
+        props = torch.cuda.get_device_properties(dev)
+        me["device_name"] = props.name
+        try:
+            me["pci_bus_id"] = (f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:"
+                                f"{props.pci_device_id:02x}")
+        except AttributeError:
+            pass
+    if not dist_on:
+        return {"world_size": 1, "backend": None, "ranks": [me]}
+    import torch.distributed as tdist
+
+    ranks = [None] * tdist.get_world_size()
+    tdist.all_gather_object(ranks, me)
+    backend = str(tdist.get_backend())
+    return {"world_size": tdist.get_world_size(),
+            "backend": backend + (" (RCCL)" if backend == "nccl" else ""),
+            "ranks": ranks}
+
+
 def dry_run(world, rank):
     """CPU rehearsal of the multi-rank path (gloo): rank launch, the sharded table's
     all-gather (serial and double-buffered), the contiguous pair split and the
@@ -971,11 +1172,12 @@ def dry_run(world, rank):
     if world > 1:
         tdist.all_reduce(cnt)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+    census = rank_census(world > 1, torch.device("cpu"))
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_reporting": int(cnt[2]),
                           "pairs_covered": int(cnt[0]), "pairs": P,
                           "table_ok_ranks": int(cnt[1]), "max_rank_s": float(tt),
-                          "exchange": tab.path()}), flush=True)
+                          "exchange": tab.path(), **census}), flush=True)
     if world > 1:
         tdist.destroy_process_group()
 
@@ -1047,6 +1249,11 @@ def main():
         tdist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     clock = Clock(dev, dist)
+    census = rank_census(dist, dev)
+    if census["world_size"] != world:
+        print(f"bench.py: the process group has {census['world_size']} ranks, WORLD_SIZE={world}",
+              file=sys.stderr)
+        sys.exit(2)
 
     wl = args.workload
     if wl == "r15":
@@ -1092,7 +1299,7 @@ def main():
             done()
     del graph
     torch.cuda.empty_cache()
-    syn2m = bip1m = None
+    syn2m = bip1m = cpu_bip1m = None
     if wl == "syn100k" and not args.no_syn2m:
         # the cache-busting variant: a 1 GB fp32 table outside the 256 MB Infinity Cache
         w2 = WORKLOADS["syn2m"]
@@ -1120,6 +1327,8 @@ def main():
                                        dtype=dt_, graph=gb, v_branch=True, workload="bip1m")
         del gb
         torch.cuda.empty_cache()
+        if world == 1 and rank == 0 and not args.no_cpu_baseline:
+            cpu_bip1m = cpu_baseline_bip1m(rpb, cb, nb, mb, budget_s=args.cpu_budget)
     if rank != 0:
         if dist:
             tdist.destroy_process_group()
@@ -1137,6 +1346,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"gat_layer_{wl}", "nodes": n, "cols": m, "edges": e,
                    "in_features": fin, "heads": H, "feat": F, "parallelism": f"replicas{world}"},
+        "ranks": census,
         "roofline": head["roofline"],
         "edge_kernels": head["edge_kernels"],
     }
@@ -1159,6 +1369,11 @@ def main():
                                         "container (BASELINE.md)",
             "runs": [train_step_leg(dev, y, "Ours") for y in ("2015", "2016", "2017", "2018")]
             + [train_step_leg(dev, "2015", "ablation3")]}
+        out["train_py_literal"] = {
+            "workload": "train.py:221-232 as written through the drop-in modules (DataLoader, "
+                        "torch.optim.Adam, F.nll_loss(output[source_index], ...), loss.item() "
+                        "per step, eager, no HIP graph), shipped 2015 graph, fp32",
+            "runs": [train_py_literal_leg(dev, k) for k in ("ablation3", "Ours")]}
         if not args.no_bf16:
             out["train_step_configs2"] = {
                 "workload": "configs[2]: the same Ours model in bf16 (model.to(bfloat16): bf16 "
@@ -1173,6 +1388,8 @@ def main():
             cb["configs1_ablation3"] = cpu_baseline_r15(args.cpu_budget)
         if link is not None:
             cb["link_score"] = cpu_baseline_pairs(n, H * F)
+        if cpu_bip1m is not None:
+            cb["bip1m"] = cpu_bip1m
         out["cpu_baseline"] = cb
     print(json.dumps(out), flush=True)
     if dist:

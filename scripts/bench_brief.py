@@ -13,7 +13,12 @@ def leg(tag, x):
               f"  traffic {k.get('traffic')}")
 
 
-def main(path):
+def main(*paths):
+    for path in paths:
+        brief(path)
+
+
+def brief(path):
     lines = [ln for ln in open(path) if ln.startswith("{")]
     d = json.loads(lines[-1])
     leg("head", d)
@@ -32,12 +37,19 @@ def main(path):
                         if k.startswith("pairs_per_sec")}, "allgather_ms", round(x["allgather_ms"], 4))
             for m in ("mlp", "inner"):
                 r = x[f"roofline_{m}"]
+                mem = r.get("memory", {})
                 print(f"   {m:6s} {r['bound']} {r['achieved']:9.1f} {r['unit']} frac {r['frac']:.3f}"
-                      f"  {r['avg_launch_us']:8.1f} us  traffic {r.get('traffic')}")
-    for key in ("train_step_configs1", "train_step_configs2"):
+                      f"  {r['avg_launch_us']:8.1f} us  compulsory-HBM frac "
+                      f"{mem.get('frac_compulsory_hbm', float('nan')):.3f}  IC frac "
+                      f"{mem.get('frac_traffic_ic', float('nan')):.3f}  traffic "
+                      f"{mem.get('traffic', r.get('traffic'))}")
+    for key in ("train_step_configs1", "train_step_configs2", "train_py_literal"):
         for r in d.get(key, {}).get("runs", []):
             print(f"{key} {r['model']} {r['year']} {r['dtype']}: {r['ms_per_step']:.3f} ms")
+    for k, v in d.get("cpu_baseline", {}).items():
+        if isinstance(v, dict) and "value" in v:
+            print(f"cpu_baseline {k}: {v['value']:.4g} {v['unit']} ({v.get('cores')} cores)")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:])

@@ -39,3 +39,95 @@ def tol_close(a, b, rtol, atol_rel):
     b = np.asarray(b, np.float64)
     scale = max(np.abs(b).max(), 1e-30)
     np.testing.assert_allclose(a, b, rtol=rtol, atol=atol_rel * scale)
+
+
+U32 = 2.0 ** -24  # fp32 unit roundoff
+
+
+def bounded_close(got, ref, absterms, nterms, rtol, frac=None, name=""):
+    """fp32 sums against an fp64 reference, elementwise:
+
+    * every element within the forward-error bound of an n-term fp32 sum,
+      |got - ref| <= rtol |ref| + n 2^-24 A, where A = the sum of the absolute values of
+      the terms (incl. the magnitudes inside each term, e.g. |g| + |D| of a score
+      gradient) and n = the number of terms plus the ops inside a term and the block
+      reduce levels (``nterms``, scalar or per element);
+    * with ``frac``: at least that fraction of the elements within rtol |ref| alone
+      (elementwise relative, no max-based floor).
+    Returns (max err / bound, fraction within rtol) for reporting."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    A = np.broadcast_to(np.asarray(absterms, np.float64), ref.shape)
+    n = np.asarray(nterms, np.float64)
+    if n.ndim == 1 and ref.ndim > 1:  # per leading index (row / column)
+        n = n.reshape((-1,) + (1,) * (ref.ndim - 1))
+    n = np.broadcast_to(n, ref.shape)
+    err = np.abs(got - ref)
+    bound = rtol * np.abs(ref) + n * U32 * A + 1e-300
+    worst = float((err / bound).max()) if err.size else 0.0
+    assert np.all(err <= bound), (
+        f"{name}: {int((err > bound).sum())} of {err.size} elements beyond rtol|ref| + n u A "
+        f"(worst {worst:.3g}x the bound)")
+    inside = float(np.mean(err <= rtol * np.abs(ref))) if err.size else 1.0
+    if frac is not None:
+        assert inside >= frac, f"{name}: {inside:.4%} of elements within rtol {rtol} (< {frac})"
+    return worst, inside
+
+
+def _seg_sum(x, ptr):
+    """Sums of x over the contiguous segments [ptr[k], ptr[k+1]) of axis 0 (empty ones 0),
+    via a running sum (the terms here are non-negative)."""
+    cs = np.concatenate([np.zeros((1,) + x.shape[1:]), np.cumsum(x, axis=0)])
+    return cs[ptr[1:]] - cs[ptr[:-1]]
+
+
+def edge_abs_terms(rowptr, col, fwd, hc, dU, hs=None, dV=None, keep=None, p=0.0, slope=0.2):
+    """Absolute-term sums A for ``bounded_close`` of the OursLayer3 core (fp64, from the
+    oracle's forward dict: att, attd, pre): per row u (att |hc_j|), d_hs (att |dV_j|),
+    d_el; per column v (att |hs_i|), d_hc (att |dU_i|), d_er.  The score gradient
+    de = att (keep g - D) lrelu' has A_e = att (keep |g|_abs + |D|_abs) |lrelu'| with
+    |g|_abs = sum_f |dU_if hc_jf| + |hs_if dV_jf|, |D|_abs = sum_row attd |g|_abs.
+    Also n_row / n_col, the term counts for the bound."""
+    rowptr = np.asarray(rowptr, np.int64)
+    n = len(rowptr) - 1
+    m, H, F = hc.shape
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    c64 = np.asarray(col, np.int64)
+    perm = np.argsort(c64, kind="stable")
+    nnz = np.bincount(c64, minlength=m)
+    colptr = np.concatenate([[0], np.cumsum(nnz)])
+    att, attd = fwd["att"].astype(np.float64), fwd["attd"].astype(np.float64)
+    kf = np.ones_like(att) if keep is None else keep.astype(np.float64) / (1.0 - p)
+    dl = np.where(fwd["pre"] > 0, 1.0, slope)
+    out = {k: np.zeros(s) for k, s in (("u", (n, H, F)), ("d_hs", (n, H, F)),
+                                         ("v", (m, H, F)), ("d_hc", (m, H, F)),
+                                         ("d_el", (n, H)), ("d_er", (m, H)))}
+    for h in range(H):
+        ah, adu = np.abs(hc[:, h].astype(np.float64)), np.abs(dU[:, h].astype(np.float64))
+        w = attd[:, h:h + 1]
+        hcj, dui = ah[c64], adu[rows]
+        gabs = np.einsum("ef,ef->e", dui, hcj)
+        out["u"][:, h] = _seg_sum(w * hcj, rowptr)
+        out["d_hc"][:, h] = _seg_sum((w * dui)[perm], colptr)
+        del hcj
+        if hs is not None:
+            ahs = np.abs(hs[:, h].astype(np.float64))
+            hsi = ahs[rows]
+            out["v"][:, h] = _seg_sum((w * hsi)[perm], colptr)
+            if dV is not None:
+                dvj = np.abs(dV[:, h].astype(np.float64))[c64]
+                gabs += np.einsum("ef,ef->e", hsi, dvj)
+                out["d_hs"][:, h] = _seg_sum(w * dvj, rowptr)
+                del dvj
+            del hsi
+        del dui
+        dabs = _seg_sum(attd[:, h] * gabs, rowptr)
+        T = att[:, h] * (kf[:, h] * gabs + dabs[rows]) * dl[:, h]
+        out["d_el"][:, h] = _seg_sum(T, rowptr)
+        out["d_er"][:, h] = _seg_sum(T[perm], colptr)
+    # terms per output: the outer sum, the 2F-term dots inside g, 16 elementwise ops, and
+    # up to 80 levels of the wave / block partial reduce
+    k_in = 2 * F + 96
+    out["n_row"] = np.diff(rowptr).astype(np.float64) + k_in
+    out["n_col"] = nnz.astype(np.float64) + k_in
+    return out

@@ -57,14 +57,28 @@ def test_algorithmic_bytes_match_design():
         n * (4 * D + 4 * H)
 
 
-def test_pmc_traffic_reads_newest_profile():
-    """bench.pmc_traffic finds the forward kernel in the newest committed PMC summary
-    (FETCH_SIZE x 2 + WRITE_SIZE per launch), close to the algorithmic bytes."""
-    t32, src32 = bench.pmc_traffic(8, 16, False, "syn100k")
-    t16, src16 = bench.pmc_traffic(8, 16, True, "syn100k")
-    assert src32 is not None and src16 is not None
-    assert 1.0e9 < t32 < 1.4e9
-    assert 0.5e9 < t16 < 0.8e9
+def test_pmc_traffic_only_from_this_build(tmp_path):
+    """bench.pmc_lookup attaches PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE per launch) only
+    from a profile whose recorded source id is this build's (scripts/profile.sh writes it,
+    summarize_profile.py keeps it): the newest such profile wins, a newer profile of
+    other sources is skipped and named."""
+    import json
+
+    name = "void msha::bip::bip_fwd_kernel<2, 64, float, true, false>"
+    pat = r"bip_fwd_kernel<2, 64, float, true, false>"
+    entry = {name: {"hbm_bytes_per_launch_corrected": 1.5e9}}
+    for tag, sid, val in (("round4_bip1m_v1", bench.kernel_source_id(), 1.5e9),
+                          ("round4_bip1m_v2", "0123456789abcdef", 9.9e9)):
+        d = tmp_path / tag
+        d.mkdir()
+        entry[name]["hbm_bytes_per_launch_corrected"] = val
+        json.dump(dict(entry, _meta={"source_id": sid}), open(d / "pmc_summary.json", "w"))
+    tr, src = bench.pmc_lookup([pat], "*bip1m_v*", profiles_dir=str(tmp_path))
+    assert tr == 1.5e9 and src.endswith("round4_bip1m_v1/pmc_summary.json")
+    (tmp_path / "round4_bip1m_v1" / "pmc_summary.json").unlink()
+    tr, src = bench.pmc_lookup([pat], "*bip1m_v*", profiles_dir=str(tmp_path))
+    assert tr is None and "other sources" in src
+    assert len(bench.kernel_source_id()) == 16
 
 
 def test_gpus_flag_launches_ranks():
@@ -84,6 +98,28 @@ def test_gpus_flag_launches_ranks():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["ranks_reporting"] == 2 and d["table_ok_ranks"] == 2
     assert d["pairs_covered"] == d["pairs"]
+
+
+def test_dry_run_world4_records_the_ranks():
+    """``--gpus 4 --dry-run`` (gloo, CPU): the line records the process group's world
+    size and backend and one census entry per rank (RANK / LOCAL_RANK / device), the
+    fields a driver's 8-GPU run uses to prove how many ranks RCCL formed."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["world_size"] == 4 and d["backend"] == "gloo"
+    assert sorted(x["rank"] for x in d["ranks"]) == [0, 1, 2, 3]
+    assert sorted(x["local_rank"] for x in d["ranks"]) == [0, 1, 2, 3]
+    assert d["ranks_reporting"] == 4 and d["table_ok_ranks"] == 4
+    assert d["pairs_covered"] == d["pairs"] and d["exchange"] == "gloo"
 
 
 def test_gpus_flag_mismatch_fails():

@@ -8,31 +8,20 @@ iterations of the ``train()`` loop body.  The data directory is written from the
 fixtures in the reference's ``anonymous_data`` file formats (Adjacent / GDP json,
 Flow csv with one row per flow).
 """
-import contextlib
-import json
-import os
-import sys
-
 import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, golden
+from conftest import golden
 
-DROPIN = os.path.join(ROOT, "msha--gnn_amd", "dropin")
-REF_MODULES = ("Ablation", "model", "HGANE", "dataset", "_boot", "GAT", "Ours", "LLP")
+import msha_loader
+
+msha_loader.load()
+from msha_gnn_amd import trainpy  # noqa: E402
 
 
 def _write_year(path, year, city, prov, gdp, flows, m):
-    n = len(city)
-    adj = {"source_index": {str(i): [int(city[i]), int(prov[i])] for i in range(n)},
-           "recipient_index": {f"r{j}": j for j in range(m)}}
-    (path / f"Adjacent{year}.json").write_text(json.dumps(adj))
-    (path / f"GDP{year}.json").write_text(
-        json.dumps({"GDP_embedding": {str(i): float(g) for i, g in enumerate(gdp)}}))
-    lines = ["source,recipient,city,province"] + [
-        f"{s},{r},{city[s]},{prov[s]}" for s, r in flows]
-    (path / f"Flow{year}.csv").write_text("\n".join(lines) + "\n", encoding="gb18030")
+    trainpy.write_year(str(path), year, city, prov, gdp, flows, m)
 
 
 @pytest.fixture()
@@ -57,38 +46,7 @@ def sub512_dir(tmp_path):
     return str(tmp_path)
 
 
-@contextlib.contextmanager
-def train_namespace(data_dir, device):
-    """train.py:6-15's imports, through the dropin directory, into a fresh namespace."""
-    saved = {k: sys.modules.pop(k) for k in REF_MODULES if k in sys.modules}
-    env = {k: os.environ.get(k) for k in ("MSHA_DATA_DIR", "MSHA_YEAR", "MSHA_DEVICE")}
-    os.environ.update(MSHA_DATA_DIR=data_dir, MSHA_YEAR="2015", MSHA_DEVICE=str(device))
-    sys.path.insert(0, DROPIN)
-    ns = {}
-    try:
-        exec(compile("from __future__ import division\n"
-                     "from __future__ import print_function\n"
-                     "import time\n"
-                     "import argparse\n"
-                     "from Ablation import *\n"
-                     "import torch.optim as optim\n"
-                     "import gc\n"
-                     "from model import *\n"
-                     "from HGANE import *\n"
-                     "from torch.utils.data import Dataset, DataLoader, random_split\n"
-                     "import dataset\n"
-                     "from dataset import *\n", "train.py:1-15", "exec"), ns)
-        yield ns
-    finally:
-        sys.path.remove(DROPIN)
-        for k in REF_MODULES:
-            sys.modules.pop(k, None)
-        sys.modules.update(saved)
-        for k, v in env.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+train_namespace = trainpy.namespace
 
 
 def test_train_imports_resolve(sub512_dir):
@@ -112,42 +70,10 @@ def test_train_imports_resolve(sub512_dir):
 
 def _train_py(ns, device, dropout, batches=None, iters=3, seed=0):
     """train.py:181-232 on the namespace: returns (model, inter_adj, losses)."""
-    torch.manual_seed(seed)
-    Dataset = ns["dataset"].HigherDataset()
-    train_size = int(0.9 * len(Dataset))
-    test_size = len(Dataset) - train_size
-    train_dataset, _ = ns["random_split"](Dataset, [train_size, test_size])
-    train_loader = ns["DataLoader"](train_dataset, batch_size=64, shuffle=True)
-    Scount, Rcount = Dataset.get_count()
-    inter_adj, city_adj, province_adj = Dataset.get_adjacent()
-    nrm = ns["normalize_adjacency_matrix"]
-    inter_adj = nrm(inter_adj)
-    city_adj = nrm(city_adj)
-    province_adj = nrm(province_adj)
-    GDP = Dataset.get_gdp()
-    torch.manual_seed(seed)
-    model = ns["ablation3"](in_features=128, out_features=64, n_classes=Rcount, n_heads=2,
-                            dropout=dropout, gdp=GDP, Scount=Scount, Rcount=Rcount)
-    optimizer = ns["optim"].Adam(model.parameters(), lr=0.001, weight_decay=5e-4)
-    model = model.to(device)
-    inter_adj = inter_adj.to(device)
-    city_adj = city_adj.to(device)
-    province_adj = province_adj.to(device)
-    F = ns["F"]
-    model.train()
-    losses = []
-    it = iter(batches) if batches is not None else iter(train_loader)
-    for _ in range(iters):
-        source_index, recipient_index = next(it)
-        source_index = source_index.to(device)
-        recipient_index = recipient_index.to(device)
-        optimizer.zero_grad()
-        output = model(inter_adj, city_adj, province_adj, source_index)
-        loss_train = F.nll_loss(output[source_index], recipient_index)
-        losses.append(loss_train.item())
-        loss_train.backward()
-        optimizer.step()
-    return model, inter_adj, losses
+    tp = trainpy.TrainPy(ns, device, dropout=dropout, seed=seed)
+    it = iter(batches) if batches is not None else iter(tp.train_loader)
+    losses = [tp.iteration(next(it)) for _ in range(iters)]
+    return tp.model, tp.inter_adj, losses
 
 
 @pytest.mark.gpu

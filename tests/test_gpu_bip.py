@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_helpers import random_counts, t, tol_close, virtual_csr
+from gpu_helpers import bounded_close, edge_abs_terms, random_counts, t, tol_close, virtual_csr
 from oracle import gnn_oracle as O
 from test_gpu_kernels import _keep_mask
 
@@ -74,10 +74,18 @@ def test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype):
                               p=p)
     names = ("u", "v", "d_el", "d_er", "d_hc", "d_hs")
     refs = (ref["u"], ref["v"], bw["d_el"], bw["d_er"], bw["d_hc"], bw["d_hs"])
+    # every output within the fp32 forward-error bound of its sum (gpu_helpers.
+    # bounded_close: |got - ref| <= rtol |ref| + n 2^-24 A with A the absolute terms) and,
+    # for the fp32 tables, at least 99 % of the elements within 1e-5 |ref| alone; the
+    # score gradients d_el / d_er carry the softmax backward's cancellation
+    # (sum_j att (g - D) = 0 before lrelu'), so for them only the bound applies.
+    A = edge_abs_terms(rowptr, col, ref, st(hc), st(dU), hs=st(hs), dV=st(dV), keep=keep, p=p)
+    per = {"u": "n_row", "d_hs": "n_row", "d_el": "n_row", "v": "n_col", "d_hc": "n_col",
+           "d_er": "n_col"}
     for name, a, b, r in zip(names, got, gen, refs):
-        rt = max(tol, 1e-4) if name in ("d_el", "d_er") else tol
-        tol_close(a.float().cpu().numpy(), r, rt, tol)
-        tol_close(a.float().cpu().numpy(), b.float().cpu().numpy(), rt, tol)
+        frac = 0.99 if dtype == torch.float32 and name not in ("d_el", "d_er") else None
+        bounded_close(a.float().cpu().numpy(), r, A[name], A[per[name]], tol, frac, name)
+        bounded_close(b.float().cpu().numpy(), r, A[name], A[per[name]], tol, None, name + " (general)")
 
 
 def test_bip_raw_abi_lse_attd_deterministic(cuda, msha):
@@ -163,9 +171,19 @@ def test_bip_many_groups_per_wave_vs_general(cuda, msha, p):
     dV = rng.standard_normal((m, H, F)).astype(np.float32)
     got = _run(MF, graph, el, er, hc, hs, dU, dV, p, 13, cuda, torch.float32, True)
     gen = _run(MF, graph, el, er, hc, hs, dU, dV, p, 13, cuda, torch.float32, False)
+    keep = _keep_mask(graph.n_edges, H, p, 13, cuda)
+    d64 = lambda x: x.astype(np.float64)  # noqa: E731
+    ref = O.edge_aggregate_fwd(rowptr, col, d64(el), d64(er), d64(hc), hs=d64(hs), keep=keep, p=p)
+    bw = O.edge_aggregate_bwd(rowptr, col, ref, d64(hc), d64(dU), hs=d64(hs), dV=d64(dV),
+                              keep=keep, p=p)
+    A = edge_abs_terms(rowptr, col, ref, hc, dU, hs=hs, dV=dV, keep=keep, p=p)
+    refs = dict(u=ref["u"], v=ref["v"], d_el=bw["d_el"], d_er=bw["d_er"], d_hc=bw["d_hc"],
+                d_hs=bw["d_hs"])
     for name, a, b in zip(("u", "v", "d_el", "d_er", "d_hc", "d_hs"), got, gen):
-        rt = 1e-4 if name in ("d_el", "d_er") else 1e-5
-        tol_close(a.cpu().numpy(), b.cpu().numpy(), rt, 1e-5)
+        nt = A["n_row"] if name in ("u", "d_hs", "d_el") else A["n_col"]
+        frac = None if name in ("d_el", "d_er") else 0.99
+        bounded_close(a.cpu().numpy(), refs[name], A[name], nt, 1e-5, frac, name)
+        bounded_close(b.cpu().numpy(), refs[name], A[name], nt, 1e-5, None, name + " (general)")
 
 
 def test_shipped_graph_models_run_on_the_bipartite_kernels(cuda, msha):

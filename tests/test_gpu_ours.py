@@ -86,8 +86,10 @@ def _dense_ours_core(el, er, h1, h2, a3s, a4s, mask, city, prov, src, keep_e=Non
     return u, v
 
 
-@pytest.mark.parametrize("p", [0.0, 0.4])
-def test_ours_attention_kernels_vs_dense(cuda, msha, p):
+def check_ours_attention_vs_dense(cuda, p, dtype=torch.float32, tol_out=1e-5, tol_grad=1e-4):
+    """ours_attention (u, v and every input gradient) against the dense fp64 restatement
+    with the kernels' dropout masks; ``dtype`` = storage of the node tables h1 / h2 (bf16:
+    the reference is fed the same bf16-rounded tables and upstream gradients)."""
     from msha_gnn_amd import functional as MF
     from msha_gnn_amd.graph import Graph, Groups
 
@@ -110,13 +112,19 @@ def test_ours_attention_kernels_vs_dense(cuda, msha, p):
     a4s = rng.standard_normal((H, Fd)) * 0.2
     dU = rng.standard_normal((n, H, Fd))
     dV = rng.standard_normal((m, H, Fd))
+    if dtype != torch.float32:  # the values the bf16 kernels read
+        rnd = lambda x: torch.as_tensor(x).to(dtype).double().numpy()  # noqa: E731
+        h1, h2, dU, dV = rnd(h1), rnd(h2), rnd(dU), rnd(dV)
     graph = Graph.from_dense(t(counts, cuda))
     groups = Groups(city, prov, cuda)
     seed = 5
     tg = [t(x, cuda).requires_grad_(True) for x in (el, er, h1, h2, a3s, a4s)]
+    tg[2] = t(h1, cuda, dtype).requires_grad_(True)
+    tg[3] = t(h2, cuda, dtype).requires_grad_(True)
     u, v = MF.ours_attention(graph, groups, torch.as_tensor(src, device=cuda), *tg, p=p,
                              training=p > 0, seed=seed)
-    (u * t(dU, cuda)).sum().add_((v * t(dV, cuda)).sum()).backward()
+    assert u.dtype == dtype and v.dtype == dtype
+    (u.float() * t(dU, cuda)).sum().add_((v.float() * t(dV, cuda)).sum()).backward()
     # dense fp64 reference, head by head, with the kernels' masks (edge ids follow the
     # CSR with virtual full rows; the reference's scores use the real mask: an empty
     # row is the softmax of all -9e15 = uniform)
@@ -145,13 +153,19 @@ def test_ours_attention_kernels_vs_dense(cuda, msha, p):
                                  .cpu().numpy().reshape(B, n), dtype=torch.float64)
         ru, rv = _dense_ours_core(*rs, ra3, ra4, torch.as_tensor(counts > 0), torch.as_tensor(city),
                                   torch.as_tensor(prov), torch.as_tensor(src), ke, k3, k4, p)
-        tol_close(u[:, h].detach().cpu().numpy(), ru.detach().numpy(), 1e-5, 1e-5)
-        tol_close(v[:, h].detach().cpu().numpy(), rv.detach().numpy(), 1e-5, 1e-5)
+        tol_close(u[:, h].detach().float().cpu().numpy(), ru.detach().numpy(), tol_out, tol_out)
+        tol_close(v[:, h].detach().float().cpu().numpy(), rv.detach().numpy(), tol_out, tol_out)
         ((ru * torch.tensor(dU[:, h])).sum() + (rv * torch.tensor(dV[:, h])).sum()).backward()
         for got, ref in ((tg[0].grad[:, h], rs[0].grad), (tg[1].grad[:, h], rs[1].grad),
                          (tg[2].grad[:, h], rs[2].grad), (tg[3].grad[:, h], rs[3].grad),
                          (tg[4].grad[h], ra3.grad), (tg[5].grad[h], ra4.grad)):
-            tol_close(got.cpu().numpy(), ref.numpy(), 1e-4, 1e-5)
+            tol_close(got.float().cpu().numpy(), ref.numpy(), tol_grad, 1e-5 if tol_grad < 1e-3
+                      else tol_grad)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.4])
+def test_ours_attention_kernels_vs_dense(cuda, msha, p):
+    check_ours_attention_vs_dense(cuda, p)
 
 
 def test_ours_model_record_and_train_step(cuda, msha):

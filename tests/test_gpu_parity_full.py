@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 
 import dense_ref as D
-from gpu_helpers import tol_close
+from gpu_helpers import bounded_close, edge_abs_terms, tol_close
 from oracle import cpu_oracle
 from oracle import gnn_oracle as O
 
@@ -218,7 +218,7 @@ def _dense_ours3_core(rowptr, col, n, m, el, er, hc, hs, dU, dV, slope=0.2):
     g = dU h1^T + h2 dV^T, ds = att (g - rowsum(att g)), de = ds lrelu'(pre)."""
     rows = np.repeat(np.arange(n), np.diff(rowptr))
     H = el.shape[1]
-    out = {k: [] for k in ("u", "v", "lse", "d_el", "d_er", "d_hc", "d_hs")}
+    out = {k: [] for k in ("u", "v", "lse", "d_el", "d_er", "d_hc", "d_hs", "att_e", "pre_e")}
     for h in range(H):
         pre = np.full((n, m), -np.inf)
         pre[rows, col] = el[rows, h] + er[col, h]
@@ -229,6 +229,8 @@ def _dense_ours3_core(rowptr, col, n, m, el, er, hc, hs, dU, dV, slope=0.2):
         den = ex.sum(1, keepdims=True)
         att = ex / den
         out["lse"].append((mx + np.log(den))[:, 0])
+        out["att_e"].append(att[rows, col])
+        out["pre_e"].append(pre[rows, col])
         out["u"].append(att @ hc[:, h])
         out["v"].append(att.T @ hs[:, h])
         g = dU[:, h] @ hc[:, h].T + hs[:, h] @ dV[:, h].T
@@ -268,11 +270,20 @@ def test_bip1m_ourslayer3_core_every_row(cuda, bip1m, dt):
     n64 = lambda x: x.double().numpy()  # noqa: E731
     ref = _dense_ours3_core(rowptr, col, n, m, n64(el), n64(er), n64(hc), n64(hs), n64(dU),
                             n64(dV))
-    tol_close(_np64(u), ref["u"], tol, tol)
-    tol_close(_np64(v), ref["v"], tol, tol)
-    for leaf, key in zip(leaves, ("d_el", "d_er", "d_hc", "d_hs")):
-        tol_close(_np64(leaf.grad), ref[key], max(tol, 1e-4) if key in ("d_el", "d_er") else tol,
-                  tol)
+    # every element within the fp32 forward-error bound of its sum (|got - ref| <= tol |ref|
+    # + n 2^-24 A, A the absolute terms: gpu_helpers.bounded_close) and, fp32, >= 99 % of
+    # the elements within 1e-5 |ref| alone (elementwise relative; v and d_er are column
+    # sums over ~40k-140k edges); d_el carries the softmax backward's cancellation, so
+    # the bound alone
+    A = edge_abs_terms(rowptr, col, dict(att=ref["att_e"], attd=ref["att_e"], pre=ref["pre_e"]),
+                       n64(hc), n64(dU), hs=n64(hs), dV=n64(dV))
+    got = dict(u=u, v=v, d_el=leaves[0].grad, d_er=leaves[1].grad, d_hc=leaves[2].grad,
+               d_hs=leaves[3].grad)
+    for key in ("u", "v", "d_el", "d_er", "d_hc", "d_hs"):
+        nt = A["n_row"] if key in ("u", "d_el", "d_hs") else A["n_col"]
+        frac = 0.99 if dt == torch.float32 and key != "d_el" else None
+        worst, inside = bounded_close(_np64(got[key]), ref[key], A[key], nt, tol, frac, key)
+        print(f"bip1m {key}: worst {worst:.3g} of the bound, {inside:.4%} within {tol} |ref|")
     # the dense restatement agrees with the pinned C oracle on the u path
     u_c, lse_c = cpu_oracle.edge_attention_fwd(rowptr, col, n64(el), n64(er), n64(hc), fp64=True)
     tol_close(ref["u"], u_c, 1e-10, 1e-12)
@@ -528,8 +539,10 @@ def test_ablation3_bf16_model_vs_fp64(cuda, msha):
     """configs[2] for the whole model train.py builds (ablation3, train.py:206) after
     ``model.to(bfloat16)``: log-probabilities and the nll loss against the dense fp64
     restatement on the same bf16-rounded parameters (the north_star bf16 bar, 1e-2),
-    on the full 2015 graph; the embedding gradient (Sfeatures) within 1e-2 on >= 99 %
-    of its elements, every other gradient finite and printed against fp64."""
+    on the full 2015 graph; every parameter gradient (Sfeatures, Rfeatures, each
+    head's W / a / BatchNorm weights, out_att.W) finite and within 1e-2 (|got - ref| <=
+    1e-2 |ref| + 1e-2 max|ref|) on >= 99 % of its elements.  (The parameters are stored
+    bf16, so each gradient is rounded to bf16 once: 2^-9 relative.)"""
     from msha_gnn_amd import layers
 
     yg = _year(msha, cuda, "2015")
@@ -564,8 +577,7 @@ def test_ablation3_bf16_model_vs_fp64(cuda, msha):
         bad = np.abs(got - r64) > BF16_TOL * np.abs(r64) + BF16_TOL * scale
         print(f"{name}: max err {np.abs(got - r64).max() / scale:.3g} of max; "
               f"{bad.mean():.3%} of elements > 1e-2")
-        if name == "Sfeatures":
-            assert bad.mean() <= 0.01, f"{name}: {bad.mean():.3%} of elements off by > 1e-2"
+        assert bad.mean() <= 0.01, f"{name}: {bad.mean():.3%} of elements off by > 1e-2"
 
 
 @pytest.mark.parametrize("year", ["2015", "2018"])
