@@ -16,12 +16,17 @@
 // rows' slices of the streamed tables; every global load and store of the loop is an
 // unconditional buffer op (masked lanes at kOOB), so the next group's loads are in
 // flight while this group runs and the compiler's vmcnt waits stay exact.  A group is cut
-// into sub-groups whose (edge, head) pairs fill <= 64 slot lanes: slot lanes compute the
-// scores, the row softmax (lane-segmented scans), the keep bits and the attention once;
-// element lanes (lane l owns elements [l V, l V + V) of the H * F row, V = H F / 64, so
-// a head's dot products reduce over its QH = F / V lanes) then walk each row's edges with
-// the attention and hc_j read from LDS.
-//
+// into sub-groups of whole rows whose edges fill <= W = 64 / H slots per head.
+//   slot lanes (head-major: lane h W + k = edge k, head h) compute the scores and the row
+//     softmax with VALU-only segmented scans (DPP row_shr / row_bcast) and write one
+//     record {attd, byte offset of hc_j} per slot to LDS;
+//   element lanes (lane l owns elements [l V, l V + V) of the H * F row, V = H F / 64)
+//     walk each row's edges: one record read, hc_j from LDS, u_i += attd hc_j in
+//     registers, and the column sums v_j += attd hs_i (forward) / d_hc_j += attd dU_i
+//     (backward) into the wave's slab, two edges of a row a step (distinct columns: both
+//     read before either is written).  Sums land in program order: deterministic.
+//     (LDS float atomics for the slab measured 5x slower: 1590 vs ~330 us at bip1m.)
+//     d_er_j is one LDS float add per slot.
 // Reference: Ablation.py:266-274 (OursLayer3 scores, masked softmax, dropout,
 // u = att @ h1, v = att.T @ h2), Ours.py:84-86 (the backward's row coefficients).
 #include "edge_geo.h"
@@ -30,8 +35,8 @@ namespace msha {
 namespace bip {
 
 constexpr int kMaxMD = 4096;  // floats of one (M, H*F) LDS table: M = 32 at H*F = 128
-constexpr int kWaves = 7;     // fwd: 16 KB table + 7 x (16 KB v slab + scratch) = 156 KB;
-                              // bwd: two 16 KB tables + 7 x (d_hc, d_er slabs + scratch)
+constexpr int kWavesF = 8;    // fwd: 16 KB table + 8 x (16 KB v slab + 1.1 KB) = 153 KB
+constexpr int kWavesB = 7;    // bwd: two 16 KB tables + 7 x (d_hc slab + 1.6 KB) = 153 KB
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) {
   return __builtin_amdgcn_readlane(v, l);
@@ -140,8 +145,13 @@ __device__ __forceinline__ void bst_row(rsrc_t r, uint32_t off, const float (&x)
   }
 }
 
+// floats per block partial (16-byte aligned rows: the blocks store float4 pieces)
+__host__ __device__ constexpr int32_t part_stride(int32_t n) { return (n + 3) & ~3; }
+
 constexpr int kPD = 8;        // rows per group
 constexpr int kColPages = 4;  // a group's columns: <= kPD * 32 = 256 edges
+constexpr int kNCol = 64 * kColPages;
+constexpr int kRec = 72;      // slot records per wave: 64 slots + the pair loop's overrun
 
 // A group: rows [r0, r0 + kPD) of the wave's range.  rp lane t = rowptr[min(r0 + t, re)];
 // colv[p] lane q = column of edge E0 + 64 p + q; s0/s1/s2 lane t * H + h = el/lse/coef of
@@ -191,32 +201,6 @@ __device__ __forceinline__ void load_grp(Grp<V, NT>& g, const Srcs& S, int32_t r
   }
 }
 
-// A sub-group: rows [t0, t1) of a group whose edges fill <= 64 (edge, head) slots (M * H
-// <= 64, so one row always fits).  Slot lane k = (edge Es + k / H, head k % H): its row t,
-// the row's slot segment [sk, ek) (stride H) and column j.
-struct Slot {
-  int t, sk, ek;
-  int32_t j;
-  bool valid;
-};
-
-template <int H>
-__device__ __forceinline__ Slot slot_of(int32_t rp, int t0, int t1, int32_t Es, int nEs,
-                                        int32_t E0, const int32_t* cols, int lane, int M) {
-  Slot sl;
-  const int q = lane / H, h = lane % H;
-  sl.valid = lane < nEs * H;
-  int t = t0;
-#pragma unroll
-  for (int u = 1; u < kPD; ++u)
-    if (u > t0 && u < t1) t += rdlane(rp, u) <= Es + q ? 1 : 0;
-  sl.t = t;
-  sl.sk = (__shfl(rp, t) - Es) * H + h;
-  sl.ek = (__shfl(rp, t + 1) - Es) * H;
-  sl.j = min(max(cols[(Es - E0 + q) & (64 * kColPages - 1)], 0), M - 1);
-  return sl;
-}
-
 // all-reduce over the lanes of one head (lane % H): rotations inside 16-lane rows by
 // 8, 4, .. H (DPP row_ror keeps lane % H when H divides the shift), then across rows by
 // v_permlane16/32_swap -- VALU only, no LDS round trip
@@ -229,21 +213,6 @@ __device__ __forceinline__ float swap16(float v, int lane) {
   const unsigned x = __builtin_bit_cast(unsigned, v);
   const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
   return __builtin_bit_cast(float, (lane & 16) ? r[0] : r[1]);
-}
-__device__ __forceinline__ float swap32(float v, int lane) {
-  const unsigned x = __builtin_bit_cast(unsigned, v);
-  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  return __builtin_bit_cast(float, lane < 32 ? r[1] : r[0]);
-}
-template <int H, bool MAX>
-__device__ __forceinline__ float head_allreduce(float v, int lane) {
-  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
-  if (H <= 8) v = op(v, ror16<8>(v));
-  if (H <= 4) v = op(v, ror16<4>(v));
-  if (H <= 2) v = op(v, ror16<2>(v));
-  if (H <= 1) v = op(v, ror16<1>(v));
-  v = op(v, swap16(v, lane));
-  return op(v, swap32(v, lane));
 }
 // sum over an aligned group of G lanes: 32 = two 16-lane rows (rotations, then the row
 // swap), else the xor tree
@@ -261,27 +230,6 @@ __device__ __forceinline__ float lanes_sum(float v, int lane) {
   }
 }
 
-// segmented reductions over a row's slots (lanes sk, sk + H, ... < ek): every lane ends
-// up with its segment's total (doubling toward the segment end, then the head's value)
-template <int H>
-__device__ __forceinline__ float seg_max(float v, int lane, int sk, int ek) {
-#pragma unroll
-  for (int o = H; o < 64; o <<= 1) {
-    const float w = __shfl_down(v, o);
-    if (lane + o < ek) v = fmaxf(v, w);
-  }
-  return __shfl(v, sk);
-}
-template <int H>
-__device__ __forceinline__ float seg_sum(float v, int lane, int sk, int ek) {
-#pragma unroll
-  for (int o = H; o < 64; o <<= 1) {
-    const float w = __shfl_down(v, o);
-    if (lane + o < ek) v += w;
-  }
-  return __shfl(v, sk);
-}
-
 // two dot products per head at once (QH = 32: a head is two 16-lane rows): the rows swap
 // so lanes with bit 4 clear collect p0 and the others p1, then one rotation tree per row.
 // Lanes (l & 16) == 0 of each head end up with sum(p0), the others with sum(p1).
@@ -296,82 +244,141 @@ __device__ __forceinline__ float pair_sum32(float p0, float p1, int lane) {
   return v;
 }
 
-// per-row all-reduce over a sub-group's slot lanes (rows t0 <= r < t1, independent, so
-// their chains interleave): rowv[r] = the value of (row r, this lane's head); returns the
-// value of this slot's own row
-template <int H, bool MAX>
-__device__ __forceinline__ float rows_reduce(float x, int slot_t, bool valid, int t0, int t1,
-                                             int lane, float (&rowv)[kPD]) {
-  const float idn = MAX ? -INFINITY : 0.f;
-  float out = idn;
-#pragma unroll
-  for (int r = 0; r < kPD; ++r) {
-    if (r >= t0 && r < t1) {
-      const float y = head_allreduce<H, MAX>(valid && slot_t == r ? x : idn, lane);
-      rowv[r] = y;
-      out = slot_t == r ? y : out;
-    }
+// Slot layout: head-major, W = 64 / H lanes per head; lane h * W + k holds (edge Es + k,
+// head h) of a sub-group (<= W edges, whole rows).  A row's slots are a contiguous lane
+// segment of its head block, [lane - d, end].
+//
+// Segmented inclusive scan over that segment, VALU only: DPP row_shr 1/2/4/8 inside
+// 16-lane rows, then row_bcast15 (rows 1, 3 take lane 15 / 47) and row_bcast31 (rows 2,
+// 3 take lane 31) for the head blocks that span rows -- a source lane contributes only
+// when it lies in the lane's own segment (d reaches back to it).
+// v of the DPP source lane (CTRL), `old` where the row is masked off (RM) or the source
+// lies outside the 16-lane row
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp_src(float x, float old) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                               __builtin_bit_cast(int, x), CTRL,
+                                                               RM, 0xF, false));
+}
+
+template <int W, bool MAX>
+__device__ __forceinline__ float seg_scan(float v, int lane, int d) {
+  const int lr = lane & 15;
+  constexpr float idn = MAX ? -INFINITY : 0.f;
+  // (max as a select: fmaxf's NaN rules would add two canonicalising moves per step)
+  auto op = [](float a, float b) { return MAX ? (a > b ? a : b) : a + b; };
+  {
+    const float y = dpp_src<0x111, 0xF>(v, idn);
+    v = (d >= 1 && lr >= 1) ? op(v, y) : v;
   }
-  return out;
+  if constexpr (W > 2) {
+    const float y = dpp_src<0x112, 0xF>(v, idn);
+    v = (d >= 2 && lr >= 2) ? op(v, y) : v;
+  }
+  if constexpr (W > 4) {
+    const float y = dpp_src<0x114, 0xF>(v, idn);
+    v = (d >= 4 && lr >= 4) ? op(v, y) : v;
+  }
+  if constexpr (W > 8) {
+    const float y = dpp_src<0x118, 0xF>(v, idn);
+    v = (d >= 8 && lr >= 8) ? op(v, y) : v;
+  }
+  if constexpr (W >= 32) {
+    const float y = dpp_src<0x142, 0xA>(v, idn);
+    v = ((lane & 16) && d > lr) ? op(v, y) : v;
+  }
+  if constexpr (W == 64) {
+    const float y = dpp_src<0x143, 0xC>(v, idn);
+    v = (lane >= 32 && d > lane - 32) ? op(v, y) : v;
+  }
+  return v;
 }
 
-// keep factor of element e * H + h = Es * H + k of the edge-dropout stream (the other
-// edge kernels' element order)
-__device__ __forceinline__ float slot_keep(const Dropout& dp, uint64_t doff, int32_t Es, int H,
-                                           int lane) {
+// keep factor of element e * H + h of the edge-dropout stream (the other edge kernels'
+// element order)
+__device__ __forceinline__ float slot_keep(const Dropout& dp, uint64_t doff, int64_t elem) {
   if (!dp.active) return 1.f;
-  return philox_x(dp.seed, doff, (uint64_t)Es * H + (uint64_t)lane) >= dp.threshold ? dp.scale
-                                                                                    : 0.f;
+  return philox_x(dp.seed, doff, (uint64_t)elem) >= dp.threshold ? dp.scale : 0.f;
 }
 
-// the sub-group after t0: rows while their edges fit 64 slots
-template <int H>
+// the sub-group after t0: rows while their edges fit W slots
+template <int W>
 __device__ __forceinline__ int sub_end(int32_t rp, int t0, int lane) {
   const int32_t Es = rdlane(rp, t0);
-  const uint64_t fit = __ballot(lane > t0 && lane <= kPD && rp - Es <= 64 / H);
+  const uint64_t fit = __ballot(lane > t0 && lane <= kPD && rp - Es <= W);
   return t0 + max(1, (int)__popcll(fit));
+}
+
+// Per-slot geometry of a sub-group: its row t (in the group), d = slots back to the
+// row's first, the lane holding the row's last slot, the column j.
+struct Slot {
+  int t, d, endl, j;
+  bool valid;
+};
+
+template <int H>
+__device__ __forceinline__ Slot slot_geo(const int32_t (&srp)[kPD + 1], int32_t rp, int32_t Es,
+                                         int nEs, int32_t E0, const uint8_t* colb, int lane,
+                                         int M) {
+  constexpr int W = 64 / H;
+  Slot s;
+  const int h = lane / W, k = lane % W;
+  const int32_t x = Es + k;
+  int t = 0;
+#pragma unroll
+  for (int u = 1; u < kPD; ++u) t += srp[u] <= x ? 1 : 0;
+  s.t = t;
+  s.valid = k < nEs;
+  const int32_t rs = __shfl(rp, t), re = __shfl(rp, t + 1);
+  s.d = x - rs;
+  s.endl = h * W + (re - Es) - 1;
+  s.j = min((int)colb[(x - E0) & (kNCol - 1)], M - 1);
+  return s;
 }
 
 // ------------------------------------------------------------------------ forward ---
 // u_i = sum_e attd_e hc_j, lse_i, (ATTD: attd_e), and with HS the block partials of
 // v_j = sum_e attd_e hs_i.  attd_e = softmax_row(lrelu(el_i + er_j))_e * keep_e.
-// Per sub-group: scores, the row softmax (segmented max / sum across slot lanes) and keep
-// bits once per slot; then per row and edge pair independent LDS reads (attention, hc_j)
-// and the v slab update.  The next group's loads are in flight meanwhile.
+// Per sub-group: slot lanes compute scores, the row softmax (segmented max / sum scans)
+// and keep bits once, and leave one record {attd, byte offset of hc_j} per slot in LDS.
+// Element lanes then walk each row's edges: one record read, the hc_j read, u += attd hc_j,
+// and v_j += attd hs_i as LDS float adds into the wave's slab (one wave's adds land in
+// program order: deterministic).  The next group's loads are in flight meanwhile.
 template <int H, int F, typename T, bool HS, bool ATTD>
-__global__ void __launch_bounds__(kWaves * 64) bip_fwd_kernel(
+__global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
     const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
     const T* __restrict__ hs, float slope, Dropout dp, T* __restrict__ u,
     T* __restrict__ u_lo, float* __restrict__ lse, float* __restrict__ attd,
     float* __restrict__ part) {
-  constexpr int D = H * F, V = D / 64, QH = F / V, PD = kPD, WB = kWaves;
+  constexpr int D = H * F, V = D / 64, PD = kPD, WB = kWavesF, W = 64 / H;
   constexpr int NT = HS ? 1 : 0;
-  constexpr int SLAB = HS ? kMaxMD : 0;
-  constexpr int NCOL = 64 * kColPages;
-  constexpr int NATT = ATTD ? kPD * 64 : 0;  // a group's slots (<= kPD * M * H)
-  constexpr int PER_WAVE = SLAB + NCOL + 64 + 64 + NATT;
-  __shared__ __attribute__((aligned(16))) float smem[kMaxMD + 64 + WB * PER_WAVE];
+  __shared__ __attribute__((aligned(16))) float tab[kMaxMD];
+  __shared__ float ert[64];
+  __shared__ __attribute__((aligned(16))) float slab[HS ? WB : 1][HS ? kMaxMD : 4];
+  __shared__ __attribute__((aligned(16))) float2 rec[WB][kRec];
+  __shared__ uint8_t colb[WB][kNCol];
+  __shared__ float lses[WB][64];
   const int M = n_cols, MD = M * D;
-  float* tab = smem;
-  float* ert = smem + kMaxMD;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  float* slab = smem + kMaxMD + 64 + wv * PER_WAVE;
-  int32_t* cols = reinterpret_cast<int32_t*>(slab + SLAB);
-  float* scr = reinterpret_cast<float*>(cols + NCOL);
-  float* lses = scr + 64;
-  float* atts = lses + 64;
-  for (int i = tid; i < MD; i += WB * 64) tab[i] = to_f32(hc[i]);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid * 4; i < MD; i += WB * 256) {
+    float x[4];
+    ld_row<4>(hc + i, x);
+    st_row<4>(tab + i, x);
+  }
   for (int i = tid; i < M * H; i += WB * 64) ert[i] = er[i];
   if (HS)
-    for (int i = lane; i < MD; i += 64) slab[i] = 0.f;
+    for (int i = lane * 4; i < MD; i += 256)
+      *reinterpret_cast<float4*>(&slab[wv][i]) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane < kRec - 64) rec[wv][64 + lane] = make_float2(0.f, 0.f);
   __syncthreads();
 
-  const int hl = lane * V / F;
+  const int hl = lane * V / F;  // head of this element lane
   const uint64_t doff = dp.active ? dropout_offset(dp, dp.offset) : 0;
-  const int64_t W = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
-  const int32_t rb = (int32_t)(w * n_rows / W), re = (int32_t)((w + 1) * n_rows / W);
+  const int64_t Wt = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
+  const int32_t rb = (int32_t)(w * n_rows / Wt), re = (int32_t)((w + 1) * n_rows / Wt);
   const uint32_t TB = (uint32_t)n_rows * D * (uint32_t)sizeof(T);
   Srcs S;
   S.rp = make_rsrc(rowptr, (uint32_t)(n_rows + 1) * 4u);
@@ -386,6 +393,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip_fwd_kernel(
   const rsrc_t r_ulo = make_rsrc(sizeof(T) == 2 ? u_lo : nullptr, TB);
   const rsrc_t r_lse = make_rsrc(lse, (uint32_t)n_rows * H * 4u);
   const rsrc_t r_att = make_rsrc(ATTD ? attd : nullptr, (uint32_t)n_edges * H * 4u);
+  const char* tabc = reinterpret_cast<const char*>(tab) + lane * V * 4;
+  char* slabc = reinterpret_cast<char*>(&slab[wv][0]) + lane * V * 4;
+  const float2* recl = &rec[wv][hl * W];
   if (rb < re) {
     using Gp = Grp<V, NT>;
     const int ng = (re - rb + PD - 1) / PD;
@@ -398,107 +408,99 @@ __global__ void __launch_bounds__(kWaves * 64) bip_fwd_kernel(
       load_grp<H, V, NT, T>(nxt, S, r0 + PD, rp_n, lane);
       rp_n = load_rp(S, r0 + 2 * PD, lane);
 
-      const int32_t E0 = rdlane(cur.rp, 0);
+      int32_t srp[PD + 1];
 #pragma unroll
-      for (int p = 0; p < kColPages; ++p) cols[64 * p + lane] = cur.colv[p];
+      for (int u = 0; u <= PD; ++u) srp[u] = rdlane(cur.rp, u);
+      const int32_t E0 = srp[0];
+#pragma unroll
+      for (int p = 0; p < kColPages; ++p) colb[wv][64 * p + lane] = (uint8_t)cur.colv[p];
       const uint64_t vmask = __ballot(lane < PD && cur.flag != 0);
-      lses[lane] = -INFINITY;  // rows without edges (and no virtual row)
-      float acc[PD][V];
-#pragma unroll
-      for (int t = 0; t < PD; ++t)
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[t][v] = 0.f;
+      lses[wv][lane] = -INFINITY;  // rows without edges (and no virtual row)
       for (int t0 = 0; t0 < PD;) {
-        const int t1 = sub_end<H>(cur.rp, t0, lane);
+        const int t1 = sub_end<W>(cur.rp, t0, lane);
         const int32_t Es = rdlane(cur.rp, t0);
-        const int nEs = min(64 / H, rdlane(cur.rp, t1) - Es);
-        // (1) slot lanes: score, row softmax, keep, attention
-        const Slot sl = slot_of<H>(cur.rp, t0, t1, Es, nEs, E0, cols, lane, M);
+        const int nEs = min(W, rdlane(cur.rp, t1) - Es);
+        // (1) slot lanes: score, row softmax, keep, attention -> records
         {
-          const int h = lane % H;
+          const Slot sl = slot_geo<H>(srp, cur.rp, Es, nEs, E0, colb[wv], lane, M);
+          const int h = lane / W, k = lane % W;
           const float elv = __shfl(cur.s0, sl.t * H + h);
           const bool virt = (vmask >> sl.t) & 1ull;
-          const float sc = sl.valid ? (virt ? 0.f : lrelu(elv + ert[sl.j * H + h], slope)) : -INFINITY;
-          const float mx = seg_max<H>(sc, lane, sl.sk, sl.ek);
+          const float sc = sl.valid ? (virt ? 0.f : lrelu(elv + ert[sl.j * H + h], slope))
+                                    : -INFINITY;
+          const float mx = __shfl(seg_scan<W, true>(sc, lane, sl.d), sl.endl);
           const float pe = sl.valid ? __expf(sc - mx) : 0.f;
-          const float sm = seg_sum<H>(pe, lane, sl.sk, sl.ek);
-          const float ad = sl.valid ? pe / sm * slot_keep(dp, doff, Es, H, lane) : 0.f;
-          if (sl.valid && lane == sl.sk) lses[sl.t * H + h] = mx + __logf(sm);
-          scr[lane] = ad;
-          if (ATTD && sl.valid) atts[((Es - E0) * H + lane) & (NATT > 0 ? NATT - 1 : 0)] = ad;
+          const float sm = __shfl(seg_scan<W, false>(pe, lane, sl.d), sl.endl);
+          const int64_t elem = (int64_t)(Es + k) * H + h;
+          const float ad = sl.valid ? pe / sm * slot_keep(dp, doff, elem) : 0.f;
+          rec[wv][lane] = make_float2(ad, __int_as_float(sl.j * D * 4));
+          if (sl.valid && lane == sl.endl) lses[wv][sl.t * H + h] = mx + __logf(sm);
+          if (ATTD) buf_store_f32(r_att, sl.valid ? (uint32_t)elem * 4u : kOOB, ad);
         }
-        // (2) element lanes: u_i and the v slab of the sub-group's rows, two edges a step
+        // (2) element lanes: per row, its edges' records; u in registers, v by LDS adds
 #pragma unroll
         for (int t = 0; t < PD; ++t) {
           if (t >= t0 && t < t1) {
-            const int32_t s = rdlane(cur.rp, t), e1 = rdlane(cur.rp, t + 1);
-            for (int32_t e = s; e < e1; e += 2) {
-              const bool two = e + 1 < e1;
-              const int32_t q0 = e - Es;
-              const int32_t j0 = rdlane(sl.j, q0 * H);
-              const int32_t j1 = rdlane(sl.j, (two ? q0 + 1 : q0) * H);
-              const float a0 = scr[q0 * H + hl];
-              const float a1 = two ? scr[(q0 + 1) * H + hl] : 0.f;
+            const int32_t q0 = srp[t] - Es, q1 = srp[t + 1] - Es;
+            float acc[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[v] = 0.f;
+            // two edges a step: a row's columns are distinct, so both slab entries are
+            // read before either is written (the next step's reads follow these writes)
+            for (int32_t q = q0; q < q1; q += 2) {
+              const bool two = q + 1 < q1;
+              const float2 ra = recl[q], rb2 = recl[q + 1];
+              const float a0 = ra.x, a1 = two ? rb2.x : 0.f;
+              const int j0 = __float_as_int(ra.y), j1 = __float_as_int(rb2.y);
               float x0[V], x1[V];
-              ld_row<V>(tab + j0 * D + lane * V, x0);
-              ld_row<V>(tab + j1 * D + lane * V, x1);
+              ld_row<V>(reinterpret_cast<const float*>(tabc + j0), x0);
+              ld_row<V>(reinterpret_cast<const float*>(tabc + j1), x1);
 #pragma unroll
-              for (int v = 0; v < V; ++v) acc[t][v] = fmaf(a1, x1[v], fmaf(a0, x0[v], acc[t][v]));
+              for (int v = 0; v < V; ++v) acc[v] = fmaf(a1, x1[v], fmaf(a0, x0[v], acc[v]));
               if (HS) {
-                float* sp0 = slab + j0 * D + lane * V;
-                float y[V];
-                ld_row<V>(sp0, y);
+                float* sp0 = reinterpret_cast<float*>(slabc + j0);
+                float* sp1 = reinterpret_cast<float*>(slabc + j1);
+                float y0[V], y1[V];
+                ld_row<V>(sp0, y0);
+                ld_row<V>(sp1, y1);
 #pragma unroll
-                for (int v = 0; v < V; ++v) y[v] = fmaf(a0, cur.rows[0][t][v], y[v]);
-                st_row<V>(sp0, y);
-                if (two) {
-                  float* sp1 = slab + j1 * D + lane * V;
-                  ld_row<V>(sp1, y);
-#pragma unroll
-                  for (int v = 0; v < V; ++v) y[v] = fmaf(a1, cur.rows[0][t][v], y[v]);
-                  st_row<V>(sp1, y);
+                for (int v = 0; v < V; ++v) {
+                  y0[v] = fmaf(a0, cur.rows[0][t][v], y0[v]);
+                  y1[v] = fmaf(a1, cur.rows[0][t][v], y1[v]);
                 }
+                st_row<V>(sp0, y0);
+                if (two) st_row<V>(sp1, y1);
               }
+            }
+            const uint32_t ro = r0 + t < re
+                                    ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
+                                    : kOOB;
+            bst_row<T, V>(r_u, ro, acc);
+            if (sizeof(T) == 2) {
+              float res[V];
+#pragma unroll
+              for (int v = 0; v < V; ++v) res[v] = acc[v] - (float)(bf16_t)acc[v];
+              bst_row<T, V>(r_ulo, ro, res);
             }
           }
         }
         t0 = t1;
       }
-      // (3) the group's stores, a fixed set (masked lanes dropped)
-#pragma unroll
-      for (int t = 0; t < PD; ++t) {
-        const uint32_t ro = r0 + t < re ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
-                                        : kOOB;
-        bst_row<T, V>(r_u, ro, acc[t]);
-        if (sizeof(T) == 2) {
-          float res[V];
-#pragma unroll
-          for (int v = 0; v < V; ++v) res[v] = acc[t][v] - (float)(bf16_t)acc[t][v];
-          bst_row<T, V>(r_ulo, ro, res);
-        }
-      }
       const bool lr = lane < PD * H && r0 + lane / H < re;
-      buf_store_f32(r_lse, lr ? (uint32_t)(r0 * H + lane) * 4u : kOOB, lses[lane]);
-      if (ATTD) {
-        const int32_t nE = rdlane(cur.rp, PD) - E0;
-#pragma unroll
-        for (int p = 0; p < (NATT > 0 ? NATT / 64 : 1); ++p) {
-          const int32_t sidx = 64 * p + lane;
-          buf_store_f32(r_att, sidx < nE * H ? (uint32_t)(E0 * H + sidx) * 4u : kOOB,
-                        atts[sidx & (NATT > 0 ? NATT - 1 : 0)]);
-        }
-      }
+      buf_store_f32(r_lse, lr ? (uint32_t)(r0 * H + lane) * 4u : kOOB, lses[wv][lane]);
     }
   }
   if (HS) {
     __syncthreads();
     float* dst = part + (int64_t)blockIdx.x * MD;
-    const float* slabs = smem + kMaxMD + 64;
-    for (int i = tid; i < MD; i += WB * 64) {
-      float a = slabs[i];
+    for (int i = tid * 4; i < MD; i += WB * 256) {
+      float4 a = *reinterpret_cast<const float4*>(&slab[0][i]);
 #pragma unroll
-      for (int q = 1; q < WB; ++q) a += slabs[q * PER_WAVE + i];
-      dst[i] = a;
+      for (int q = 1; q < WB; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(&slab[q][i]);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      *reinterpret_cast<float4*>(dst + i) = a;
     }
   }
 }
@@ -509,47 +511,50 @@ __global__ void __launch_bounds__(kWaves * 64) bip_fwd_kernel(
 //   D_i  = sum_e attd_e g_e
 //   ds_e = att_e (keep_e g_e - D_i),  de_e = ds_e lrelu'(pre_e),  d_el_i = sum_e de_e
 //   d_hs_i = sum_e attd_e dV_j;  block partials of d_hc_j = sum attd_e dU_i, d_er_j = sum de_e
-// Per sub-group: slot lanes give att, keep; element lanes give g_e (dots over the head's
-// lanes), d_hs and the d_hc slab; slot lanes finish D, de, d_el (segmented sums) and add
-// de into the d_er slab one row at a time (a row's columns are distinct).
+// Per sub-group: slot lanes give att, keep and the records; element lanes walk each
+// row's edges two at a time (g_e dots reduced together, d_hs in registers, d_hc as LDS
+// adds into the wave's slab, g_e back into the record); slot lanes finish D, de, d_el
+// (segmented scans) and add de into the wave's d_er slab (LDS adds).
 template <int H, int F, typename T, bool HS, bool COEF>
-__global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
+__global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
     const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
     const float* __restrict__ lse, const T* __restrict__ dU, const T* __restrict__ hs,
     const T* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
     float* __restrict__ d_el, T* __restrict__ d_hs, float* __restrict__ part) {
-  constexpr int D = H * F, V = D / 64, QH = F / V, PD = kPD, WB = kWaves;
+  constexpr int D = H * F, V = D / 64, QH = F / V, PD = kPD, WB = kWavesB, W = 64 / H;
   constexpr int NT = HS ? 2 : 1;
-  constexpr int NCOL = 64 * kColPages;
-  constexpr int PER_WAVE = kMaxMD + 64 + NCOL + 3 * 64;  // d_hc, d_er slabs; cols; scratch
-  __shared__ __attribute__((aligned(16))) float smem[2 * kMaxMD + 64 + WB * PER_WAVE];
+  __shared__ __attribute__((aligned(16))) float tab[HS ? 2 : 1][kMaxMD];  // hc, dV
+  __shared__ float ert[64];
+  __shared__ __attribute__((aligned(16))) float slab[WB][kMaxMD];  // d_hc
+  __shared__ float sder[WB][64];                                  // d_er, lane j * H + h
+  __shared__ __attribute__((aligned(16))) float2 rec[WB][kRec];
+  __shared__ uint8_t colb[WB][kNCol];
+  __shared__ float dels[WB][64];
   const int M = n_cols, MD = M * D, MH = M * H;
-  float* tab = smem;
-  float* tdv = smem + kMaxMD;
-  float* ert = smem + 2 * kMaxMD;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  float* slab = smem + 2 * kMaxMD + 64 + wv * PER_WAVE;
-  float* sder = slab + kMaxMD;
-  int32_t* cols = reinterpret_cast<int32_t*>(sder + 64);
-  float* sad = reinterpret_cast<float*>(cols + NCOL);
-  float* sg = sad + 64;
-  float* dels = sg + 64;
-  for (int i = tid; i < MD; i += WB * 64) {
-    tab[i] = to_f32(hc[i]);
-    if (HS) tdv[i] = to_f32(dV[i]);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid * 4; i < MD; i += WB * 256) {
+    float x[4];
+    ld_row<4>(hc + i, x);
+    st_row<4>(&tab[0][i], x);
+    if (HS) {
+      ld_row<4>(dV + i, x);
+      st_row<4>(&tab[HS ? 1 : 0][i], x);
+    }
   }
   for (int i = tid; i < MH; i += WB * 64) ert[i] = er[i];
-  for (int i = lane; i < MD; i += 64) slab[i] = 0.f;
-  sder[lane] = 0.f;
+  for (int i = lane * 4; i < MD; i += 256)
+    *reinterpret_cast<float4*>(&slab[wv][i]) = make_float4(0.f, 0.f, 0.f, 0.f);
+  sder[wv][lane] = 0.f;
+  if (lane < kRec - 64) rec[wv][64 + lane] = make_float2(0.f, 0.f);
   __syncthreads();
 
   const int hl = lane * V / F;
-  const bool lead = lane % QH == 0;
   const uint64_t doff = dp.active ? dropout_offset(dp, dp.offset) : 0;
-  const int64_t W = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
-  const int32_t rb = (int32_t)(w * n_rows / W), re = (int32_t)((w + 1) * n_rows / W);
+  const int64_t Wt = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
+  const int32_t rb = (int32_t)(w * n_rows / Wt), re = (int32_t)((w + 1) * n_rows / Wt);
   const uint32_t TB = (uint32_t)n_rows * D * (uint32_t)sizeof(T);
   Srcs S;
   S.rp = make_rsrc(rowptr, (uint32_t)(n_rows + 1) * 4u);
@@ -563,7 +568,10 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
   S.re = re;
   const rsrc_t r_dhs = make_rsrc(HS ? d_hs : nullptr, TB);
   const rsrc_t r_del = make_rsrc(d_el, (uint32_t)n_rows * H * 4u);
-  float der = 0.f;  // d_er of (column lane / H, head lane % H) over the wave's edges
+  const char* tabc = reinterpret_cast<const char*>(&tab[0][0]) + lane * V * 4;
+  const char* tdvc = reinterpret_cast<const char*>(&tab[HS ? 1 : 0][0]) + lane * V * 4;
+  char* slabc = reinterpret_cast<char*>(&slab[wv][0]) + lane * V * 4;
+  float2* recl = &rec[wv][hl * W];
   if (rb < re) {
     using Gp = Grp<V, NT>;
     const int ng = (re - rb + PD - 1) / PD;
@@ -576,52 +584,51 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
       load_grp<H, V, NT, T>(nxt, S, r0 + PD, rp_n, lane);
       rp_n = load_rp(S, r0 + 2 * PD, lane);
 
-      const int32_t E0 = rdlane(cur.rp, 0);
+      int32_t srp[PD + 1];
 #pragma unroll
-      for (int p = 0; p < kColPages; ++p) cols[64 * p + lane] = cur.colv[p];
+      for (int u = 0; u <= PD; ++u) srp[u] = rdlane(cur.rp, u);
+      const int32_t E0 = srp[0];
+#pragma unroll
+      for (int p = 0; p < kColPages; ++p) colb[wv][64 * p + lane] = (uint8_t)cur.colv[p];
       const uint64_t vmask = __ballot(lane < PD && cur.flag != 0);
-      dels[lane] = 0.f;  // rows without edges (and no virtual row)
-      float wacc[PD][V];
-#pragma unroll
-      for (int t = 0; t < PD; ++t)
-#pragma unroll
-        for (int v = 0; v < V; ++v) wacc[t][v] = 0.f;
+      dels[wv][lane] = 0.f;  // rows without edges (and no virtual row)
       for (int t0 = 0; t0 < PD;) {
-        const int t1 = sub_end<H>(cur.rp, t0, lane);
+        const int t1 = sub_end<W>(cur.rp, t0, lane);
         const int32_t Es = rdlane(cur.rp, t0);
-        const int nEs = min(64 / H, rdlane(cur.rp, t1) - Es);
-        // (1) slot lanes: score, attention, keep
-        const Slot sl = slot_of<H>(cur.rp, t0, t1, Es, nEs, E0, cols, lane, M);
-        const int h = lane % H;
+        const int nEs = min(W, rdlane(cur.rp, t1) - Es);
+        // (1) slot lanes: score, attention, keep -> records
+        const Slot sl = slot_geo<H>(srp, cur.rp, Es, nEs, E0, colb[wv], lane, M);
+        const int h = lane / W, k = lane % W;
         const int rsl = sl.t * H + h;
         const bool virt = (vmask >> sl.t) & 1ull;
-        // (the row scalars live on lanes t * H + h, which may be idle slot lanes: every
-        // shuffle runs with all lanes active -- ds_bpermute reads 0 from an inactive lane)
+        // (the row scalars live on lanes t * H + h: every shuffle runs with all lanes
+        // active -- ds_bpermute reads 0 from an inactive lane)
         const float elq = __shfl(cur.s0, rsl), lsq = __shfl(cur.s1, rsl);
         const float cfq = COEF ? __shfl(cur.s2, rsl) : 0.f;
         const float pre = elq + ert[sl.j * H + h];
         const float sc = virt ? 0.f : lrelu(pre, slope);
         const float att = sl.valid ? __expf(sc - lsq) : 0.f;
-        const float kf = slot_keep(dp, doff, Es, H, lane);
+        const float kf = slot_keep(dp, doff, (int64_t)(Es + k) * H + h);
         const float ad = att * kf;
-        sad[lane] = ad;
-        // (2) element lanes: g_e, d_hs, the d_hc slab
+        rec[wv][lane] = make_float2(ad, __int_as_float(sl.j * D * 4));
+        // (2) element lanes: g_e (into the record), d_hs, the d_hc slab
 #pragma unroll
         for (int t = 0; t < PD; ++t) {
           if (t >= t0 && t < t1) {
-            const int32_t s = rdlane(cur.rp, t), e1 = rdlane(cur.rp, t + 1);
+            const int32_t q0 = srp[t] - Es, q1 = srp[t + 1] - Es;
             const float(&dUr)[V] = cur.rows[0][t];
             const float(&hsr)[V] = cur.rows[NT - 1][t];
-            for (int32_t e = s; e < e1; e += 2) {
-              const bool two = e + 1 < e1;
-              const int32_t q0 = e - Es;
-              const int32_t j0 = rdlane(sl.j, q0 * H);
-              const int32_t j1 = rdlane(sl.j, (two ? q0 + 1 : q0) * H);
-              const float a0 = sad[q0 * H + hl];
-              const float a1 = two ? sad[(q0 + 1) * H + hl] : 0.f;
+            float wacc[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) wacc[v] = 0.f;
+            for (int32_t q = q0; q < q1; q += 2) {
+              const bool two = q + 1 < q1;
+              const float2 ra = recl[q], rb2 = recl[q + 1];
+              const float a0 = ra.x, a1 = two ? rb2.x : 0.f;
+              const int j0 = __float_as_int(ra.y), j1 = __float_as_int(rb2.y);
               float x0[V], x1[V];
-              ld_row<V>(tab + j0 * D + lane * V, x0);
-              ld_row<V>(tab + j1 * D + lane * V, x1);
+              ld_row<V>(reinterpret_cast<const float*>(tabc + j0), x0);
+              ld_row<V>(reinterpret_cast<const float*>(tabc + j1), x1);
               float p0 = 0.f, p1 = 0.f;
 #pragma unroll
               for (int v = 0; v < V; ++v) {
@@ -630,89 +637,84 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
               }
               if (HS) {
                 float y0[V], y1[V];
-                ld_row<V>(tdv + j0 * D + lane * V, y0);
-                ld_row<V>(tdv + j1 * D + lane * V, y1);
+                ld_row<V>(reinterpret_cast<const float*>(tdvc + j0), y0);
+                ld_row<V>(reinterpret_cast<const float*>(tdvc + j1), y1);
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                   p0 = fmaf(hsr[v], y0[v], p0);
                   p1 = fmaf(hsr[v], y1[v], p1);
-                  wacc[t][v] = fmaf(a1, y1[v], fmaf(a0, y0[v], wacc[t][v]));
+                  wacc[v] = fmaf(a1, y1[v], fmaf(a0, y0[v], wacc[v]));
                 }
               }
               if constexpr (QH == 32) {
                 const float gp = pair_sum32(p0, p1, lane);
                 if (lane % 16 == 0 && (two || (lane & 16) == 0))
-                  sg[(q0 + ((lane >> 4) & 1)) * H + hl] = gp;
+                  recl[q + ((lane >> 4) & 1)].x = gp;
               } else {
                 const float g0 = lanes_sum<QH>(p0, lane), g1 = lanes_sum<QH>(p1, lane);
-                if (lead) {
-                  sg[q0 * H + hl] = g0;
-                  if (two) sg[(q0 + 1) * H + hl] = g1;
+                if (lane % QH == 0) {
+                  recl[q].x = g0;
+                  if (two) recl[q + 1].x = g1;
                 }
               }
-              float z[V];
-              float* sp0 = slab + j0 * D + lane * V;
-              ld_row<V>(sp0, z);
+              {
+                float* sp0 = reinterpret_cast<float*>(slabc + j0);
+                float* sp1 = reinterpret_cast<float*>(slabc + j1);
+                float z0[V], z1[V];
+                ld_row<V>(sp0, z0);
+                ld_row<V>(sp1, z1);
 #pragma unroll
-              for (int v = 0; v < V; ++v) z[v] = fmaf(a0, dUr[v], z[v]);
-              st_row<V>(sp0, z);
-              if (two) {
-                float* sp1 = slab + j1 * D + lane * V;
-                ld_row<V>(sp1, z);
-#pragma unroll
-                for (int v = 0; v < V; ++v) z[v] = fmaf(a1, dUr[v], z[v]);
-                st_row<V>(sp1, z);
+                for (int v = 0; v < V; ++v) {
+                  z0[v] = fmaf(a0, dUr[v], z0[v]);
+                  z1[v] = fmaf(a1, dUr[v], z1[v]);
+                }
+                st_row<V>(sp0, z0);
+                if (two) st_row<V>(sp1, z1);
               }
+            }
+            if (HS) {
+              const uint32_t ro = r0 + t < re
+                                      ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
+                                      : kOOB;
+              bst_row<T, V>(r_dhs, ro, wacc);
             }
           }
         }
         // (3) slot lanes: D_i, de_e, d_el_i, the d_er slab
         {
-          float g = sg[lane];
+          float g = rec[wv][lane].x;
           if (COEF && sl.valid) g = fmaf(cfq, expf(ad), g);
-          const float Dq = seg_sum<H>(sl.valid ? ad * g : 0.f, lane, sl.sk, sl.ek);
+          const float Dq = __shfl(seg_scan<W, false>(sl.valid ? ad * g : 0.f, lane, sl.d), sl.endl);
           const float ds = att * (g * kf - Dq);
           const float dev = sl.valid && !virt ? ds * (pre > 0.f ? 1.f : slope) : 0.f;
-          const float del = seg_sum<H>(dev, lane, sl.sk, sl.ek);
-          if (sl.valid && lane == sl.sk) dels[rsl] = del;
-          // d_er in registers, lane j * H + h (M * H <= 64), edges in order
-          for (int q = 0; q < nEs; ++q) {
-            const int32_t jq = rdlane(sl.j, q * H);
-            float dq = 0.f;
-#pragma unroll
-            for (int hh = 0; hh < H; ++hh) {
-              const float v = __builtin_bit_cast(float, rdlane(__builtin_bit_cast(int32_t, dev), q * H + hh));
-              dq = lane % H == hh ? v : dq;
-            }
-            der += lane / H == jq ? dq : 0.f;
-          }
+          const float del = seg_scan<W, false>(dev, lane, sl.d);
+          if (sl.valid && lane == sl.endl) dels[wv][rsl] = del;
+          if (sl.valid)
+            __hip_atomic_fetch_add(&sder[wv][sl.j * H + h], dev, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
         t0 = t1;
       }
-      // (4) the group's stores, a fixed set (masked lanes dropped)
-      if (HS) {
-#pragma unroll
-        for (int t = 0; t < PD; ++t) {
-          const uint32_t ro = r0 + t < re
-                                  ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
-                                  : kOOB;
-          bst_row<T, V>(r_dhs, ro, wacc[t]);
-        }
-      }
       const bool lr = lane < PD * H && r0 + lane / H < re;
-      buf_store_f32(r_del, lr ? (uint32_t)(r0 * H + lane) * 4u : kOOB, dels[lane]);
+      buf_store_f32(r_del, lr ? (uint32_t)(r0 * H + lane) * 4u : kOOB, dels[wv][lane]);
     }
   }
-  sder[lane] = der;
   __syncthreads();
-  float* dst = part + (int64_t)blockIdx.x * (MD + MH);
-  const float* base = smem + 2 * kMaxMD + 64;
-  for (int i = tid; i < MD + MH; i += WB * 64) {
-    const int o = i < MD ? i : kMaxMD + (i - MD);
-    float a = base[o];
+  float* dst = part + (int64_t)blockIdx.x * part_stride(MD + MH);
+  for (int i = tid * 4; i < MD; i += WB * 256) {
+    float4 a = *reinterpret_cast<const float4*>(&slab[0][i]);
 #pragma unroll
-    for (int q = 1; q < WB; ++q) a += base[q * PER_WAVE + o];
-    dst[i] = a;
+    for (int q = 1; q < WB; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(&slab[q][i]);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    *reinterpret_cast<float4*>(dst + i) = a;
+  }
+  for (int i = tid; i < MH; i += WB * 64) {
+    float a = sder[0][i];
+#pragma unroll
+    for (int q = 1; q < WB; ++q) a += sder[q][i];
+    dst[MD + i] = a;
   }
 }
 
@@ -723,7 +725,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip_bwd_kernel(
 // the partials (64 blocks of one 64-entry slice each ran latency-bound, 6.6 us).
 template <typename T>
 __global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restrict__ part,
-                                                          int32_t nb, int32_t stride,
+                                                          int32_t nb, int32_t stride, int32_t n,
                                                           int32_t n_t, T* __restrict__ out_t,
                                                           float* __restrict__ out_f) {
   __shared__ float red[64][17];
@@ -733,11 +735,11 @@ __global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restric
   const int per = (nb + 63) / 64;
   const int b0 = st * per, b1 = min(nb, b0 + per);
   float a = 0.f;
-  if (i < stride)
+  if (i < n)
     for (int b = b0; b < b1; ++b) a += part[(int64_t)b * stride + i];
   red[st][c] = a;
   __syncthreads();
-  if (threadIdx.x < 16 && i < stride) {
+  if (threadIdx.x < 16 && i < n) {
     float sum = red[0][c];
 #pragma unroll 8
     for (int q = 1; q < 64; ++q) sum += red[q][c];
@@ -792,7 +794,7 @@ extern "C" int msha_bip_supported(const msha_graph* g, int32_t heads, int32_t fe
 
 extern "C" size_t msha_bip_workspace_size(const msha_graph* g, int32_t heads, int32_t feat) {
   if (g == nullptr || heads <= 0 || feat <= 0) return 0;
-  const size_t rec = (size_t)g->n_cols * ((size_t)heads * feat + heads);
+  const size_t rec = (size_t)bip::part_stride((int32_t)(g->n_cols * ((int64_t)heads * feat + heads)));
   return (size_t)bip::cu_count() * rec * sizeof(float) + 256;
 }
 
@@ -801,7 +803,7 @@ static void bip_launch_fwd(const msha_graph* g, const float* el, const float* er
                            const void* hs, float slope, const Dropout& dp, void* u, void* u_lo,
                            float* lse, float* attd, void* v, float* part, int nb, hipStream_t s) {
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(bip::kWaves * 64), 0, s, g->rowptr, g->col,
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(bip::kWavesF * 64), 0, s, g->rowptr, g->col,
                        g->rowflag, (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges,
                        el, er, (const T*)hc, (const T*)hs, slope, dp, (T*)u, (T*)u_lo, lse, attd,
                        part);
@@ -811,7 +813,7 @@ static void bip_launch_fwd(const msha_graph* g, const float* el, const float* er
     else go(bip::bip_fwd_kernel<H, F, T, true, false>);
     const int32_t MD = (int32_t)(g->n_cols * H * F);
     hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + 15) / 16), dim3(1024), 0, s, part,
-                       nb, MD, MD, (T*)v, (float*)nullptr);
+                       nb, MD, MD, MD, (T*)v, (float*)nullptr);
   } else {
     if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, false, true>);
     else go(bip::bip_fwd_kernel<H, F, T, false, false>);
@@ -825,7 +827,7 @@ static void bip_launch_bwd(const msha_graph* g, const float* el, const float* er
                            float* d_er, void* d_hc, void* d_hs, float* part, int nb,
                            hipStream_t s) {
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(bip::kWaves * 64), 0, s, g->rowptr, g->col,
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(bip::kWavesB * 64), 0, s, g->rowptr, g->col,
                        g->rowflag, (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges,
                        el, er, (const T*)hc,
                        lse, (const T*)dU, (const T*)hs, (const T*)dV, row_coef, slope, dp, d_el,
@@ -838,7 +840,7 @@ static void bip_launch_bwd(const msha_graph* g, const float* el, const float* er
   else go(bip::bip_bwd_kernel<H, F, T, false, false>);
   const int32_t MD = (int32_t)(g->n_cols * H * F), MH = (int32_t)(g->n_cols * H);
   hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + MH + 15) / 16), dim3(1024), 0, s, part,
-                     nb, MD + MH, MD, (T*)d_hc, d_er);
+                     nb, bip::part_stride(MD + MH), MD + MH, MD, (T*)d_hc, d_er);
 }
 
 extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,

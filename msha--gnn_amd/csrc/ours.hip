@@ -274,6 +274,102 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
   }
 }
 
+// Batch of <= 64 sources with D <= 256 (train.py's 64 flows): the batch's h2 rows (fp32,
+// B x D) and intra weights w3 / w4 (B x H) are staged in LDS once per block, so a node's
+// matches read LDS instead of a dependent global round trip each (the global-gather form
+// above took 43 us at the 2015 graph: ~5 nodes per wave, one L2 latency chain per node).
+// A persistent grid walks the nodes; the next node's group ids and u_in are loaded before
+// this node's matches run.  Same sums in the same order as ours_fwd_kernel.
+template <typename T, int KD>
+__global__ void __launch_bounds__(256) ours_fwd_lds_kernel(OursArgs a,
+                                                           const float* __restrict__ bstat,
+                                                           const T* __restrict__ u_in,
+                                                           T* __restrict__ u_out) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // [B][D], then w3 [B][H], w4
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const int D = a.H * a.F, H = a.H;
+  const int B = (int)a.B;
+  float* w3s = sx + B * D;
+  float* w4s = w3s + B * H;
+  for (int b = wv; b < B; b += 4) {
+    const int64_t ib = a.src[b];
+    for (int d = lane; d < D; d += 64) sx[b * D + d] = ldt<T>(a.h2, ib * D + d);
+  }
+  for (int i = threadIdx.x; i < B * H; i += 256) {
+    w3s[i] = bstat[(int64_t)i * BS_N + BS_W3];
+    w4s[i] = bstat[(int64_t)i * BS_N + BS_W4];
+  }
+  const bool bvalid = lane < B;
+  const int64_t ib = bvalid ? a.src[lane] : 0;
+  const int32_t bg3 = bvalid ? a.gid3[ib] : 0, bg4 = bvalid ? a.gid4[ib] : 0;
+  __syncthreads();
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (n >= a.N) return;
+  int hk[KD];
+#pragma unroll
+  for (int k = 0; k < KD; ++k) hk[k] = min(lane + 64 * k, D - 1) / a.F;
+  int32_t g3 = a.gid3[n], g4 = a.gid4[n];
+  float uin[KD];
+#pragma unroll
+  for (int k = 0; k < KD; ++k) {
+    const int d = lane + 64 * k;
+    uin[k] = d < D ? to_f32(u_in[n * D + d]) : 0.f;
+  }
+  while (true) {
+    const int64_t nn = n + nwaves;
+    const bool has_next = nn < a.N;
+    const int32_t ng3 = has_next ? a.gid3[nn] : 0, ng4 = has_next ? a.gid4[nn] : 0;
+    float nuin[KD];
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = lane + 64 * k;
+      nuin[k] = has_next && d < D ? to_f32(u_in[nn * D + d]) : 0.f;
+    }
+    float acc3[KD], acc4[KD];
+#pragma unroll
+    for (int k = 0; k < KD; ++k) acc3[k] = acc4[k] = 0.f;
+    const uint64_t bal3 = __ballot(bvalid && bg3 == g3);
+    const uint64_t bal4 = __ballot(bvalid && bg4 == g4);
+    uint32_t kb3 = 0xffffffffu, kb4 = 0xffffffffu;
+    if (a.dp.active && (bal3 | bal4)) intra_keep_bits(a.dp, a.H, (uint64_t)lane * a.N + n, kb3, kb4);
+    for (int kind = 0; kind < 2; ++kind) {
+      uint64_t bal = kind == 0 ? bal3 : bal4;
+      const uint32_t kbk = kind == 0 ? kb3 : kb4;
+      const float* ws = kind == 0 ? w3s : w4s;
+      while (bal) {
+        const int bit = __ffsll((long long)bal) - 1;
+        bal &= bal - 1;
+        const uint32_t kbits = __shfl(kbk, bit);
+#pragma unroll
+        for (int k = 0; k < KD; ++k) {
+          const int d = min(lane + 64 * k, D - 1);
+          const int h = hk[k];
+          float drop = 1.f;
+          if (a.dp.active)
+            drop = h < 32 ? (((kbits >> h) & 1u) ? a.dp.scale : 0.f)
+                          : intra_drop(a.dp, kind, h, (uint64_t)bit * a.N + n);
+          const float w = ws[bit * H + h] * drop;
+          const float x = sx[bit * D + d];
+          if (kind == 0) acc3[k] = fmaf(w, x, acc3[k]);
+          else acc4[k] = fmaf(w, x, acc4[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KD; ++k) {
+      const int d = lane + 64 * k;
+      if (d < D) u_out[n * D + d] = from_f32<T>(uin[k] + (acc3[k] + acc4[k]));
+    }
+    if (!has_next) break;
+    n = nn;
+    g3 = ng3;
+    g4 = ng4;
+#pragma unroll
+    for (int k = 0; k < KD; ++k) uin[k] = nuin[k];
+  }
+}
+
 // ----------------------------------------------------------- backward: gather ---
 // Gp[b, kind, c] = sum_{n in chunk c of group(kind, src_b)} drop(kind, b, n) * dU[n]
 // (chunks of kGatherChunk members, ascending), then G[b, kind] = sum_c Gp[b, kind, c]
@@ -587,6 +683,19 @@ static int check(const msha_graph* g, const msha_groups* grp, int64_t B, const i
   return MSHA_OK;
 }
 
+static int ours_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 static OursArgs make_args(const msha_graph* g, const msha_groups* grp, int64_t B,
                           const int64_t* src, int32_t heads, int32_t feat, const void* h2,
                           const float* a3s, const float* a4s, float slope, float drop_p,
@@ -611,10 +720,22 @@ static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const 
   if (B > 0)
     hipLaunchKernelGGL(ours_prep_kernel<T>, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
                        g->col, g->rowflag, el, er, lse, bstat);
+  const int D = a.H * a.F;
+  if (B > 0 && B <= 64 && D <= 256) {
+    // the batch staged in LDS (ours_fwd_lds_kernel): a persistent grid, two blocks per CU
+    const size_t lds = (size_t)B * (D + 2 * a.H) * sizeof(float);
+    const dim3 grid(grid_for(g->n_rows, 4, 2 * ours_cu_count()));
+#define FWDL(kd) hipLaunchKernelGGL((ours_fwd_lds_kernel<T, kd>), grid, dim3(256), lds, s, a, \
+                                    (const float*)bstat, (const T*)u_inter, (T*)u_out)
+    if (D <= 64) FWDL(1);
+    else if (D <= 128) FWDL(2);
+    else FWDL(4);
+#undef FWDL
+    return;
+  }
   // B <= 64: waves walk ~4 nodes each (the batch's groups load once per wave, the next
   // node's loads overlap this node's gathers); otherwise one node per wave
   const dim3 grid(grid_for(g->n_rows, 4, B <= 64 ? 2048 : 1 << 16));
-  const int D = a.H * a.F;
 #define FWD(kd) hipLaunchKernelGGL((ours_fwd_kernel<T, kd>), grid, dim3(256), 0, s, a, \
                                    (const float*)bstat, (const T*)u_inter, (T*)u_out)
   if (D <= 64) FWD(1);

