@@ -835,6 +835,21 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
     return res
 
 
+def write_train_py_year(d):
+    """The shipped 2015 graph (tests/golden) as train.py's anonymous_data files under d."""
+    from msha_gnn_amd import trainpy
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
+    yz = np.load(os.path.join(ROOT, "tests", "golden", "years.npz"))
+    rows = np.repeat(np.arange(int(z["n"])), np.diff(z["rowptr"]))
+    flows = np.stack([np.repeat(rows, z["cnt"].astype(np.int64)),
+                      np.repeat(z["col"].astype(np.int64), z["cnt"].astype(np.int64))], 1)
+    trainpy.write_year(d, "2015", yz["2015.city"], yz["2015.prov"], yz["2015.gdp"], flows,
+                       int(z["m"]))
+    return dict(nodes=int(z["n"]), recipients=int(z["m"]), edges=int(len(z["col"])),
+                flows=int(len(flows)))
+
+
 def train_py_literal_leg(dev, model_kind="ablation3", steps=20, warmup=5):
     """train.py as written (train.py:180-232, msha_gnn_amd.trainpy): the zero-argument
     HigherDataset over the shipped 2015 data in anonymous_data format, its DataLoader
@@ -850,16 +865,10 @@ def train_py_literal_leg(dev, model_kind="ablation3", steps=20, warmup=5):
     msha_loader.load()
     from msha_gnn_amd import trainpy
 
-    z = np.load(os.path.join(ROOT, "tests", "golden", "r15_graph.npz"))
-    yz = np.load(os.path.join(ROOT, "tests", "golden", "years.npz"))
-    rows = np.repeat(np.arange(int(z["n"])), np.diff(z["rowptr"]))
-    flows = np.stack([np.repeat(rows, z["cnt"].astype(np.int64)),
-                      np.repeat(z["col"].astype(np.int64), z["cnt"].astype(np.int64))], 1)
     res = dict(model=model_kind, year="2015", dtype="float32", optimizer="torch.optim.Adam",
                loss="F.nll_loss(output[source_index], recipient_index)", hip_graph=False)
     with tempfile.TemporaryDirectory(prefix="msha_trainpy_") as d:
-        trainpy.write_year(d, "2015", yz["2015.city"], yz["2015.prov"], yz["2015.gdp"], flows,
-                           int(z["m"]))
+        sizes = write_train_py_year(d)
         with trainpy.namespace(d, dev) as ns:
             tp = trainpy.TrainPy(ns, dev, dropout=0.5, model_kind=model_kind)
             state = {"it": iter(tp.train_loader)}
@@ -885,8 +894,7 @@ def train_py_literal_leg(dev, model_kind="ablation3", steps=20, warmup=5):
             for _ in range(steps):
                 next_batch()
             loader = (time.perf_counter() - t0) / steps * 1e3
-            res.update(nodes=int(z["n"]), recipients=int(z["m"]),
-                       edges=int(len(z["col"])), flows=int(len(flows)))
+            res.update(sizes)
     res["ms_per_step_windows"] = [round(x, 4) for x in windows]
     res["ms_per_step"] = sorted(windows)[1]
     res["loader_ms_per_batch"] = loader

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 11
+#define MSHA_ABI_VERSION 12
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -480,10 +480,14 @@ MSHA_API int msha_bn_lrelu_bwd(int64_t rows, int32_t channels, int32_t dtype, co
  * x_i = G[gi[b]], x_j = G2[gj[b]] (gi / gj NULL: row b).
  * 'mlp' layer: out = act((x_i * x_j) @ W^T + bias), W an nn.Linear weight (N x K);
  * with G2 == NULL and gj == NULL the input is x_i alone (deeper predictor layers);
- * act bits: 1 bias, 2 relu, 4 dropout(drop_p, seed, offset), 8 sigmoid. */
+ * act bits: 1 bias, 2 relu, 4 dropout(drop_p, seed, offset), 8 sigmoid.
+ * g_rows / g2_rows: the row counts of G / G2 (every gi / gj index below them; 0 =
+ * unknown).  Known counts whose tables fit 4 GiB select the gather kernel with 32-bit
+ * buffer offsets (an index past the table then reads zeros). */
 MSHA_API int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const float* G, int64_t ldg,
                               const int64_t* gi, const float* G2, int64_t ldg2,
-                              const int64_t* gj, const float* W, const float* bias, int32_t act,
+                              const int64_t* gj, int64_t g_rows, int64_t g2_rows,
+                              const float* W, const float* bias, int32_t act,
                               float drop_p, uint64_t seed, uint64_t offset, float* out,
                               msha_stream_t stream);
 /* 'inner': out[b] = sigmoid(sum_f x_i[b,f] x_j[b,f]); feat a power of two in [4, 256]. */

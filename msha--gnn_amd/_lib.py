@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 11  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 12  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -155,8 +155,8 @@ SIGNATURES = {
     "msha_bn_lrelu_fwd": (C.c_int, [I64, I32, I32, P, P, P, F32, F32, I32, F32, P, P, P, P, P, P,
                                     SZ, P]),
     "msha_bn_lrelu_bwd": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, F32, P, P, P, P, SZ, P]),
-    "msha_pair_linear": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64, U64,
-                                   P, P]),
+    "msha_pair_linear": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, I64, I64, P, P, I32, F32,
+                                   U64, U64, P, P]),
     "msha_pair_inner_fwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
     "msha_pair_inner_fwd_bf16": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
     "msha_pair_linear_bf16": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64,

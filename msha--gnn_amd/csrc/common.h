@@ -327,7 +327,7 @@ int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, con
                    hipStream_t s);
 int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t ldg,
                        const int64_t* gi, const float* G2, int64_t ldg2, const int64_t* gj,
-                       const float* W, const float* bias, int act, const Dropout& dp, float* out,
+                       int64_t g_rows, int64_t g2_rows, const float* W, const float* bias, int act, const Dropout& dp, float* out,
                        hipStream_t s);
 int skinny_pair_linear_bf16(int64_t P, int64_t K, int64_t N, const void* G, int64_t ldg,
                             const int64_t* gi, const void* G2, int64_t ldg2, const int64_t* gj,

@@ -96,20 +96,21 @@ typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 // V elements of a T table row through a buffer descriptor (masked lanes: offset kOOB,
 // read 0 / store dropped), so every load and store of the row loop is unconditional and
 // the compiler's vmcnt waits stay exact across iterations
+// (soff: a wave-uniform byte offset in the instruction's SGPR field -- no VALU per row)
 template <typename T, int V>
-__device__ __forceinline__ void bld_row(rsrc_t r, uint32_t off, float (&x)[V]) {
+__device__ __forceinline__ void bld_row(rsrc_t r, uint32_t off, float (&x)[V], uint32_t soff = 0) {
   constexpr int B = V * (int)sizeof(T);
   uint32_t w[4] = {0, 0, 0, 0};
   if constexpr (B == 16) {
-    const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
     w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
   } else if constexpr (B == 8) {
-    const u32x2_t a = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    const u32x2_t a = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
     w[0] = a.x; w[1] = a.y;
   } else if constexpr (B == 4) {
-    w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0);
   } else {
-    w[0] = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+    w[0] = __builtin_amdgcn_raw_buffer_load_b16(r, off, soff, 0);
   }
 #pragma unroll
   for (int v = 0; v < V; ++v) {
@@ -118,7 +119,8 @@ __device__ __forceinline__ void bld_row(rsrc_t r, uint32_t off, float (&x)[V]) {
   }
 }
 template <typename T, int V>
-__device__ __forceinline__ void bst_row(rsrc_t r, uint32_t off, const float (&x)[V]) {
+__device__ __forceinline__ void bst_row(rsrc_t r, uint32_t off, const float (&x)[V],
+                                        uint32_t soff = 0) {
   constexpr int B = V * (int)sizeof(T);
   uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -133,72 +135,132 @@ __device__ __forceinline__ void bst_row(rsrc_t r, uint32_t off, const float (&x)
   if constexpr (B == 16) {
     u32x4_t a;
     a.x = w[0]; a.y = w[1]; a.z = w[2]; a.w = w[3];
-    __builtin_amdgcn_raw_buffer_store_b128(a, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(a, r, off, soff, 0);
   } else if constexpr (B == 8) {
     u32x2_t a;
     a.x = w[0]; a.y = w[1];
-    __builtin_amdgcn_raw_buffer_store_b64(a, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(a, r, off, soff, 0);
   } else if constexpr (B == 4) {
-    __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w[0], r, off, soff, 0);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w[0], r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w[0], r, off, soff, 0);
   }
 }
 
 // floats per block partial (16-byte aligned rows: the blocks store float4 pieces)
 __host__ __device__ constexpr int32_t part_stride(int32_t n) { return (n + 3) & ~3; }
 
-constexpr int kPD = 8;        // rows per group
-constexpr int kColPages = 4;  // a group's columns: <= kPD * 32 = 256 edges
+constexpr int kColPages = 4;  // a group's columns held in registers: 256 edges
 constexpr int kNCol = 64 * kColPages;
 constexpr int kRec = 72;      // slot records per wave: 64 slots + the pair loop's overrun
 
-// A group: rows [r0, r0 + kPD) of the wave's range.  rp lane t = rowptr[min(r0 + t, re)];
-// colv[p] lane q = column of edge E0 + 64 p + q; s0/s1/s2 lane t * H + h = el/lse/coef of
-// (row t, head h); flag lane t = rowflag; rows[.][t] = this lane's V elements of row
-// r0 + t of the streamed tables (hs, or dU and hs).  Rows past the range read as empty.
-template <int V, int NT>
+// Rows per group: every row's head scalars fit one lane each (PD * H <= 64), and the
+// streamed rows of one group (~8 KB over the streamed tables, 8..32 rows) are the bytes a
+// wave keeps in flight while it works on the previous group; larger groups also spread
+// the group's fixed instructions over more rows.  (8-row groups ran bf16 no faster than
+// fp32: rows, not bytes, were in flight.)
+template <int H, int D, typename T, int NT>
+constexpr int grp_rows() {
+  constexpr int rb = D * (int)sizeof(T) * (NT > 1 ? NT : 1);  // streamed bytes per row
+  constexpr int want = 8192 / rb < 8 ? 8 : (8192 / rb > 32 ? 32 : 8192 / rb);
+  return want < 64 / H ? want : 64 / H;
+}
+
+// a lane's V elements of a table row as loaded (RW 32-bit words; bf16 pairs stay packed
+// until their use: half the registers of a prefetched group)
+template <int V, typename T>
+constexpr int row_words() {
+  return V * (int)sizeof(T) / 4 > 0 ? V * (int)sizeof(T) / 4 : 1;
+}
+template <typename T, int V, int RW>
+__device__ __forceinline__ void raw_load(rsrc_t r, uint32_t off, uint32_t soff, uint32_t (&w)[RW]) {
+  constexpr int B = V * (int)sizeof(T);
+  if constexpr (B == 16) {
+    const u32x4_t a = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  } else if constexpr (B == 8) {
+    const u32x2_t a = __builtin_amdgcn_raw_buffer_load_b64(r, off, soff, 0);
+    w[0] = a.x; w[1] = a.y;
+  } else if constexpr (B == 4) {
+    w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0);
+  } else {
+    w[0] = __builtin_amdgcn_raw_buffer_load_b16(r, off, soff, 0);
+  }
+}
+template <typename T, int V, int RW>
+__device__ __forceinline__ void raw_unpack(const uint32_t (&w)[RW], float (&x)[V]) {
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    if constexpr (sizeof(T) == 4) x[v] = __uint_as_float(w[v]);
+    else x[v] = __uint_as_float(v % 2 == 0 ? w[v / 2] << 16 : w[v / 2] & 0xffff0000u);
+  }
+}
+
+// A group: rows [r0, r0 + PD) of the wave's range.  rp lane t (t <= PD) = rowptr[min(r0 +
+// t, re)]; colv[p] lane q = column of edge E0 + 64 p + q; s[k] lane t * H + h = row scalar
+// k (el / lse / coef) of (row t, head h); flag lane t = rowflag; rows[.][t] = this lane's
+// V elements of row r0 + t of the streamed tables (hs, or dU and hs).  Rows past the
+// wave's range read 0 (the descriptors end there).
+template <int RW, int NT, int NS, int PD>
 struct Grp {
   int32_t rp;
   int32_t colv[kColPages];
-  float s0, s1, s2;
+  float s[NS];
   uint32_t flag;
-  float rows[NT > 0 ? NT : 1][kPD][V];
+  uint32_t rows[NT > 0 ? NT : 1][PD][RW];
 };
 
+// Per-wave buffer descriptors, bounded at the wave's last row: a row, scalar or flag past
+// the range reads 0 and a store there is dropped, with no per-load mask arithmetic; the
+// group's row offsets go in the instructions' SGPR offset field.
 struct Srcs {
-  rsrc_t rp, col, flag, p0, p1, p2, t0, t1;
-  int32_t re;
+  rsrc_t rp, col, flag, sc[3], t[2];
+  uint32_t v_rp, v_col, v_s, v_flag, v_row;  // loop-invariant lane offsets (kOOB = unused lane)
+  int32_t re, rp_re;
 };
 
-__device__ __forceinline__ int32_t load_rp(const Srcs& S, int32_t r0, int lane) {
-  return buf_i32(S.rp, (uint32_t)min(r0 + lane, S.re) * 4u);
+template <int H, int V, int NT, int NS, int PD, typename T, int RW>
+__device__ __forceinline__ void load_grp(Grp<RW, NT, NS, PD>& g, const Srcs& S, int32_t r0,
+                                         int32_t rp, int lane) {
+  constexpr uint32_t RB = 64u * V * (uint32_t)sizeof(T);  // bytes per table row
+  g.rp = rp;
+  const int32_t E0 = rdlane(rp, 0);
+#pragma unroll
+  for (int p = 0; p < kColPages; ++p)
+    g.colv[p] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(S.col, S.v_col + 256u * p,
+                                                              (uint32_t)E0 * 4u, 0);
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+    g.s[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(S.sc[k], S.v_s,
+                                                                 (uint32_t)r0 * (4u * H), 0));
+  g.flag = __builtin_amdgcn_raw_buffer_load_b8(S.flag, S.v_flag, (uint32_t)r0, 0);
+#pragma unroll
+  for (int t = 0; t < PD; ++t) {
+    const uint32_t so = (uint32_t)(r0 + t) * RB;
+    if (NT > 0) raw_load<T, V, RW>(S.t[0], S.v_row, so, g.rows[0][t]);
+    if (NT > 1) raw_load<T, V, RW>(S.t[1], S.v_row, so, g.rows[NT > 1 ? 1 : 0][t]);
+  }
 }
 
-template <int H, int V, int NT, typename T>
-__device__ __forceinline__ void load_grp(Grp<V, NT>& g, const Srcs& S, int32_t r0, int32_t rp,
-                                         int lane) {
-  constexpr int D = 64 * V;
-  g.rp = rp;
-  const int32_t E0 = rdlane(rp, 0), nE = rdlane(rp, kPD) - E0;
-#pragma unroll
-  for (int p = 0; p < kColPages; ++p) {
-    const int32_t q = 64 * p + lane;
-    g.colv[p] = buf_i32(S.col, q < nE ? (uint32_t)(E0 + q) * 4u : kOOB);
-  }
-  const bool sl = lane < kPD * H && r0 + lane / H < S.re;
-  const uint32_t so = sl ? (uint32_t)(r0 * H + lane) * 4u : kOOB;
-  g.s0 = buf_f32(S.p0, so);
-  g.s1 = buf_f32(S.p1, so);
-  g.s2 = buf_f32(S.p2, so);
-  g.flag = buf_u8(S.flag, lane < kPD && r0 + lane < S.re ? (uint32_t)(r0 + lane) : kOOB);
-#pragma unroll
-  for (int t = 0; t < kPD; ++t) {
-    const uint32_t ro = r0 + t < S.re ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
-                                      : kOOB;
-    if (NT > 0) bld_row<T, V>(S.t0, ro, g.rows[0][t]);
-    if (NT > 1) bld_row<T, V>(S.t1, ro, g.rows[NT > 1 ? 1 : 0][t]);
-  }
+// rowptr[min(r0 + lane, re)] for lanes <= PD
+__device__ __forceinline__ int32_t load_rp(const Srcs& S, int32_t r0, int lane) {
+  const int32_t v = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(S.rp, S.v_rp, (uint32_t)r0 * 4u, 0);
+  return r0 + lane <= S.re ? v : S.rp_re;
+}
+
+__device__ __forceinline__ void make_srcs(Srcs& S, const int32_t* rowptr, const int32_t* col,
+                                          const uint8_t* rowflag, int32_t n_edges, int32_t re,
+                                          int H, int PD, uint32_t row_bytes, int lane) {
+  S.re = re;
+  S.rp_re = rowptr[re];
+  S.rp = make_rsrc(rowptr, (uint32_t)(re + 1) * 4u);
+  S.col = make_rsrc(col, (uint32_t)n_edges * 4u);
+  S.flag = make_rsrc(rowflag, (uint32_t)re);
+  S.v_rp = (uint32_t)lane * 4u;
+  S.v_col = (uint32_t)lane * 4u;
+  S.v_s = lane < PD * H ? (uint32_t)lane * 4u : kOOB;
+  S.v_flag = lane < PD ? (uint32_t)lane : kOOB;
+  S.v_row = (uint32_t)lane * row_bytes / 64u;
 }
 
 // all-reduce over the lanes of one head (lane % H): rotations inside 16-lane rows by
@@ -302,10 +364,10 @@ __device__ __forceinline__ float slot_keep(const Dropout& dp, uint64_t doff, int
 }
 
 // the sub-group after t0: rows while their edges fit W slots
-template <int W>
+template <int W, int PD>
 __device__ __forceinline__ int sub_end(int32_t rp, int t0, int lane) {
   const int32_t Es = rdlane(rp, t0);
-  const uint64_t fit = __ballot(lane > t0 && lane <= kPD && rp - Es <= W);
+  const uint64_t fit = __ballot(lane > t0 && lane <= PD && rp - Es <= W);
   return t0 + max(1, (int)__popcll(fit));
 }
 
@@ -316,24 +378,37 @@ struct Slot {
   bool valid;
 };
 
-template <int H>
-__device__ __forceinline__ Slot slot_geo(const int32_t (&srp)[kPD + 1], int32_t rp, int32_t Es,
-                                         int nEs, int32_t E0, const uint8_t* colb, int lane,
-                                         int M) {
+// t by binary search over the sub-group's rows [t0, t1) in the rp register (one
+// ds_bpermute per halving); colb holds the columns from edge cbase on
+template <int H, int PD>
+__device__ __forceinline__ Slot slot_geo(int32_t rp, int t0, int t1, int32_t Es, int nEs,
+                                         int32_t cbase, const uint8_t* colb, int lane, int M) {
   constexpr int W = 64 / H;
   Slot s;
   const int h = lane / W, k = lane % W;
   const int32_t x = Es + k;
-  int t = 0;
+  int t = t0;
 #pragma unroll
-  for (int u = 1; u < kPD; ++u) t += srp[u] <= x ? 1 : 0;
+  for (int st = PD / 2; st >= 1; st >>= 1) {
+    const int pr = t + st;
+    const int32_t v = __shfl(rp, min(pr, PD));
+    t = (pr < t1 && v <= x) ? pr : t;
+  }
   s.t = t;
   s.valid = k < nEs;
   const int32_t rs = __shfl(rp, t), re = __shfl(rp, t + 1);
   s.d = x - rs;
   s.endl = h * W + (re - Es) - 1;
-  s.j = min((int)colb[(x - E0) & (kNCol - 1)], M - 1);
+  s.j = min((int)colb[(x - cbase) & (kNCol - 1)], M - 1);
   return s;
+}
+
+// a sub-group whose edges run past the group's column pages (more than kNCol edges in
+// the group): its own page, loaded now
+__device__ __forceinline__ int32_t colb_refill(const Srcs& S, uint8_t* colb, int32_t Es,
+                                               int lane) {
+  colb[lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b32(S.col, S.v_col, (uint32_t)Es * 4u, 0);
+  return Es;
 }
 
 // ------------------------------------------------------------------------ forward ---
@@ -341,9 +416,9 @@ __device__ __forceinline__ Slot slot_geo(const int32_t (&srp)[kPD + 1], int32_t 
 // v_j = sum_e attd_e hs_i.  attd_e = softmax_row(lrelu(el_i + er_j))_e * keep_e.
 // Per sub-group: slot lanes compute scores, the row softmax (segmented max / sum scans)
 // and keep bits once, and leave one record {attd, byte offset of hc_j} per slot in LDS.
-// Element lanes then walk each row's edges: one record read, the hc_j read, u += attd hc_j,
-// and v_j += attd hs_i as LDS float adds into the wave's slab (one wave's adds land in
-// program order: deterministic).  The next group's loads are in flight meanwhile.
+// Element lanes then walk each row's edges two at a time: the records, hc_j from LDS,
+// u += attd hc_j in registers, v_j += attd hs_i into the wave's slab.  The next group's
+// loads are in flight meanwhile.
 template <int H, int F, typename T, bool HS, bool ATTD>
 __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
@@ -352,8 +427,10 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
     const T* __restrict__ hs, float slope, Dropout dp, T* __restrict__ u,
     T* __restrict__ u_lo, float* __restrict__ lse, float* __restrict__ attd,
     float* __restrict__ part) {
-  constexpr int D = H * F, V = D / 64, PD = kPD, WB = kWavesF, W = 64 / H;
+  constexpr int D = H * F, V = D / 64, WB = kWavesF, W = 64 / H;
   constexpr int NT = HS ? 1 : 0;
+  constexpr int PD = grp_rows<H, D, T, NT>(), RW = row_words<V, T>();
+  constexpr uint32_t RB = (uint32_t)D * sizeof(T);
   __shared__ __attribute__((aligned(16))) float tab[kMaxMD];
   __shared__ float ert[64];
   __shared__ __attribute__((aligned(16))) float slab[HS ? WB : 1][HS ? kMaxMD : 4];
@@ -379,52 +456,48 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
   const uint64_t doff = dp.active ? dropout_offset(dp, dp.offset) : 0;
   const int64_t Wt = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
   const int32_t rb = (int32_t)(w * n_rows / Wt), re = (int32_t)((w + 1) * n_rows / Wt);
-  const uint32_t TB = (uint32_t)n_rows * D * (uint32_t)sizeof(T);
   Srcs S;
-  S.rp = make_rsrc(rowptr, (uint32_t)(n_rows + 1) * 4u);
-  S.col = make_rsrc(col, (uint32_t)n_edges * 4u);
-  S.flag = make_rsrc(rowflag, (uint32_t)n_rows);
-  S.p0 = make_rsrc(el, (uint32_t)n_rows * H * 4u);
-  S.p1 = S.p2 = make_rsrc(nullptr, 0);
-  S.t0 = make_rsrc(HS ? hs : nullptr, TB);
-  S.t1 = make_rsrc(nullptr, 0);
-  S.re = re;
-  const rsrc_t r_u = make_rsrc(u, TB);
-  const rsrc_t r_ulo = make_rsrc(sizeof(T) == 2 ? u_lo : nullptr, TB);
-  const rsrc_t r_lse = make_rsrc(lse, (uint32_t)n_rows * H * 4u);
+  make_srcs(S, rowptr, col, rowflag, n_edges, re, H, PD, RB, lane);
+  S.sc[0] = make_rsrc(el, (uint32_t)re * H * 4u);
+  S.t[0] = make_rsrc(HS ? hs : nullptr, (uint32_t)re * RB);
+  const rsrc_t r_u = make_rsrc(u, (uint32_t)re * RB);
+  const rsrc_t r_ulo = make_rsrc(sizeof(T) == 2 ? u_lo : nullptr, (uint32_t)re * RB);
+  const rsrc_t r_lse = make_rsrc(lse, (uint32_t)re * H * 4u);
   const rsrc_t r_att = make_rsrc(ATTD ? attd : nullptr, (uint32_t)n_edges * H * 4u);
   const char* tabc = reinterpret_cast<const char*>(tab) + lane * V * 4;
   char* slabc = reinterpret_cast<char*>(&slab[wv][0]) + lane * V * 4;
   const float2* recl = &rec[wv][hl * W];
+  const uint32_t v_att0 = (uint32_t)((lane % W) * H + lane / W) * 4u;
   if (rb < re) {
-    using Gp = Grp<V, NT>;
+    using Gp = Grp<RW, NT, 1, PD>;
     const int ng = (re - rb + PD - 1) / PD;
     Gp nxt;
-    load_grp<H, V, NT, T>(nxt, S, rb, load_rp(S, rb, lane), lane);
+    load_grp<H, V, NT, 1, PD, T, RW>(nxt, S, rb, load_rp(S, rb, lane), lane);
     int32_t rp_n = load_rp(S, rb + PD, lane);
     for (int gi = 0; gi < ng; ++gi) {
       const int32_t r0 = rb + gi * PD;
       const Gp cur = nxt;  // this group's loads (issued one group ago)
-      load_grp<H, V, NT, T>(nxt, S, r0 + PD, rp_n, lane);
+      load_grp<H, V, NT, 1, PD, T, RW>(nxt, S, r0 + PD, rp_n, lane);
       rp_n = load_rp(S, r0 + 2 * PD, lane);
 
       int32_t srp[PD + 1];
 #pragma unroll
       for (int u = 0; u <= PD; ++u) srp[u] = rdlane(cur.rp, u);
-      const int32_t E0 = srp[0];
+      int32_t cbase = srp[0];
 #pragma unroll
       for (int p = 0; p < kColPages; ++p) colb[wv][64 * p + lane] = (uint8_t)cur.colv[p];
       const uint64_t vmask = __ballot(lane < PD && cur.flag != 0);
       lses[wv][lane] = -INFINITY;  // rows without edges (and no virtual row)
       for (int t0 = 0; t0 < PD;) {
-        const int t1 = sub_end<W>(cur.rp, t0, lane);
+        const int t1 = sub_end<W, PD>(cur.rp, t0, lane);
         const int32_t Es = rdlane(cur.rp, t0);
         const int nEs = min(W, rdlane(cur.rp, t1) - Es);
+        if (Es - cbase + nEs > kNCol) cbase = colb_refill(S, colb[wv], Es, lane);
         // (1) slot lanes: score, row softmax, keep, attention -> records
         {
-          const Slot sl = slot_geo<H>(srp, cur.rp, Es, nEs, E0, colb[wv], lane, M);
+          const Slot sl = slot_geo<H, PD>(cur.rp, t0, t1, Es, nEs, cbase, colb[wv], lane, M);
           const int h = lane / W, k = lane % W;
-          const float elv = __shfl(cur.s0, sl.t * H + h);
+          const float elv = __shfl(cur.s[0], sl.t * H + h);
           const bool virt = (vmask >> sl.t) & 1ull;
           const float sc = sl.valid ? (virt ? 0.f : lrelu(elv + ert[sl.j * H + h], slope))
                                     : -INFINITY;
@@ -435,16 +508,20 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
           const float ad = sl.valid ? pe / sm * slot_keep(dp, doff, elem) : 0.f;
           rec[wv][lane] = make_float2(ad, __int_as_float(sl.j * D * 4));
           if (sl.valid && lane == sl.endl) lses[wv][sl.t * H + h] = mx + __logf(sm);
-          if (ATTD) buf_store_f32(r_att, sl.valid ? (uint32_t)elem * 4u : kOOB, ad);
+          if (ATTD)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ad), r_att,
+                                                  sl.valid ? v_att0 : kOOB,
+                                                  (uint32_t)Es * (4u * H), 0);
         }
-        // (2) element lanes: per row, its edges' records; u in registers, v by LDS adds
+        // (2) element lanes: per row, its edges' records; u in registers, v slab
 #pragma unroll
         for (int t = 0; t < PD; ++t) {
           if (t >= t0 && t < t1) {
             const int32_t q0 = srp[t] - Es, q1 = srp[t + 1] - Es;
-            float acc[V];
+            float acc[V], hsr[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) acc[v] = 0.f;
+            if (HS) raw_unpack<T, V, RW>(cur.rows[0][t], hsr);
             // two edges a step: a row's columns are distinct, so both slab entries are
             // read before either is written (the next step's reads follow these writes)
             for (int32_t q = q0; q < q1; q += 2) {
@@ -465,29 +542,27 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
                 ld_row<V>(sp1, y1);
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
-                  y0[v] = fmaf(a0, cur.rows[0][t][v], y0[v]);
-                  y1[v] = fmaf(a1, cur.rows[0][t][v], y1[v]);
+                  y0[v] = fmaf(a0, hsr[v], y0[v]);
+                  y1[v] = fmaf(a1, hsr[v], y1[v]);
                 }
                 st_row<V>(sp0, y0);
                 if (two) st_row<V>(sp1, y1);
               }
             }
-            const uint32_t ro = r0 + t < re
-                                    ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
-                                    : kOOB;
-            bst_row<T, V>(r_u, ro, acc);
+            const uint32_t so = (uint32_t)(r0 + t) * RB;
+            bst_row<T, V>(r_u, S.v_row, acc, so);
             if (sizeof(T) == 2) {
               float res[V];
 #pragma unroll
               for (int v = 0; v < V; ++v) res[v] = acc[v] - (float)(bf16_t)acc[v];
-              bst_row<T, V>(r_ulo, ro, res);
+              bst_row<T, V>(r_ulo, S.v_row, res, so);
             }
           }
         }
         t0 = t1;
       }
-      const bool lr = lane < PD * H && r0 + lane / H < re;
-      buf_store_f32(r_lse, lr ? (uint32_t)(r0 * H + lane) * 4u : kOOB, lses[wv][lane]);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lses[wv][lane]), r_lse, S.v_s,
+                                            (uint32_t)r0 * (4u * H), 0);
     }
   }
   if (HS) {
@@ -512,9 +587,9 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
 //   ds_e = att_e (keep_e g_e - D_i),  de_e = ds_e lrelu'(pre_e),  d_el_i = sum_e de_e
 //   d_hs_i = sum_e attd_e dV_j;  block partials of d_hc_j = sum attd_e dU_i, d_er_j = sum de_e
 // Per sub-group: slot lanes give att, keep and the records; element lanes walk each
-// row's edges two at a time (g_e dots reduced together, d_hs in registers, d_hc as LDS
-// adds into the wave's slab, g_e back into the record); slot lanes finish D, de, d_el
-// (segmented scans) and add de into the wave's d_er slab (LDS adds).
+// row's edges two at a time (g_e dots reduced together, d_hs in registers, d_hc into the
+// wave's slab, g_e back into the record); slot lanes finish D, de, d_el (segmented
+// scans) and add de into the wave's d_er slab (one LDS float add per slot).
 template <int H, int F, typename T, bool HS, bool COEF>
 __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
@@ -523,8 +598,11 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
     const float* __restrict__ lse, const T* __restrict__ dU, const T* __restrict__ hs,
     const T* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
     float* __restrict__ d_el, T* __restrict__ d_hs, float* __restrict__ part) {
-  constexpr int D = H * F, V = D / 64, QH = F / V, PD = kPD, WB = kWavesB, W = 64 / H;
+  constexpr int D = H * F, V = D / 64, QH = F / V, WB = kWavesB, W = 64 / H;
   constexpr int NT = HS ? 2 : 1;
+  constexpr int PD = grp_rows<H, D, T, NT>(), RW = row_words<V, T>();
+  constexpr int NS = COEF ? 3 : 2;
+  constexpr uint32_t RB = (uint32_t)D * sizeof(T);
   __shared__ __attribute__((aligned(16))) float tab[HS ? 2 : 1][kMaxMD];  // hc, dV
   __shared__ float ert[64];
   __shared__ __attribute__((aligned(16))) float slab[WB][kMaxMD];  // d_hc
@@ -555,56 +633,53 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
   const uint64_t doff = dp.active ? dropout_offset(dp, dp.offset) : 0;
   const int64_t Wt = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
   const int32_t rb = (int32_t)(w * n_rows / Wt), re = (int32_t)((w + 1) * n_rows / Wt);
-  const uint32_t TB = (uint32_t)n_rows * D * (uint32_t)sizeof(T);
   Srcs S;
-  S.rp = make_rsrc(rowptr, (uint32_t)(n_rows + 1) * 4u);
-  S.col = make_rsrc(col, (uint32_t)n_edges * 4u);
-  S.flag = make_rsrc(rowflag, (uint32_t)n_rows);
-  S.p0 = make_rsrc(el, (uint32_t)n_rows * H * 4u);
-  S.p1 = make_rsrc(lse, (uint32_t)n_rows * H * 4u);
-  S.p2 = make_rsrc(COEF ? row_coef : nullptr, (uint32_t)n_rows * H * 4u);
-  S.t0 = make_rsrc(dU, TB);
-  S.t1 = make_rsrc(HS ? hs : nullptr, TB);
-  S.re = re;
-  const rsrc_t r_dhs = make_rsrc(HS ? d_hs : nullptr, TB);
-  const rsrc_t r_del = make_rsrc(d_el, (uint32_t)n_rows * H * 4u);
+  make_srcs(S, rowptr, col, rowflag, n_edges, re, H, PD, RB, lane);
+  S.sc[0] = make_rsrc(el, (uint32_t)re * H * 4u);
+  S.sc[1] = make_rsrc(lse, (uint32_t)re * H * 4u);
+  S.sc[2] = make_rsrc(COEF ? row_coef : nullptr, (uint32_t)re * H * 4u);
+  S.t[0] = make_rsrc(dU, (uint32_t)re * RB);
+  S.t[1] = make_rsrc(HS ? hs : nullptr, (uint32_t)re * RB);
+  const rsrc_t r_dhs = make_rsrc(HS ? d_hs : nullptr, (uint32_t)re * RB);
+  const rsrc_t r_del = make_rsrc(d_el, (uint32_t)re * H * 4u);
   const char* tabc = reinterpret_cast<const char*>(&tab[0][0]) + lane * V * 4;
   const char* tdvc = reinterpret_cast<const char*>(&tab[HS ? 1 : 0][0]) + lane * V * 4;
   char* slabc = reinterpret_cast<char*>(&slab[wv][0]) + lane * V * 4;
   float2* recl = &rec[wv][hl * W];
   if (rb < re) {
-    using Gp = Grp<V, NT>;
+    using Gp = Grp<RW, NT, NS, PD>;
     const int ng = (re - rb + PD - 1) / PD;
     Gp nxt;
-    load_grp<H, V, NT, T>(nxt, S, rb, load_rp(S, rb, lane), lane);
+    load_grp<H, V, NT, NS, PD, T, RW>(nxt, S, rb, load_rp(S, rb, lane), lane);
     int32_t rp_n = load_rp(S, rb + PD, lane);
     for (int gi = 0; gi < ng; ++gi) {
       const int32_t r0 = rb + gi * PD;
       const Gp cur = nxt;
-      load_grp<H, V, NT, T>(nxt, S, r0 + PD, rp_n, lane);
+      load_grp<H, V, NT, NS, PD, T, RW>(nxt, S, r0 + PD, rp_n, lane);
       rp_n = load_rp(S, r0 + 2 * PD, lane);
 
       int32_t srp[PD + 1];
 #pragma unroll
       for (int u = 0; u <= PD; ++u) srp[u] = rdlane(cur.rp, u);
-      const int32_t E0 = srp[0];
+      int32_t cbase = srp[0];
 #pragma unroll
       for (int p = 0; p < kColPages; ++p) colb[wv][64 * p + lane] = (uint8_t)cur.colv[p];
       const uint64_t vmask = __ballot(lane < PD && cur.flag != 0);
       dels[wv][lane] = 0.f;  // rows without edges (and no virtual row)
       for (int t0 = 0; t0 < PD;) {
-        const int t1 = sub_end<W>(cur.rp, t0, lane);
+        const int t1 = sub_end<W, PD>(cur.rp, t0, lane);
         const int32_t Es = rdlane(cur.rp, t0);
         const int nEs = min(W, rdlane(cur.rp, t1) - Es);
+        if (Es - cbase + nEs > kNCol) cbase = colb_refill(S, colb[wv], Es, lane);
         // (1) slot lanes: score, attention, keep -> records
-        const Slot sl = slot_geo<H>(srp, cur.rp, Es, nEs, E0, colb[wv], lane, M);
+        const Slot sl = slot_geo<H, PD>(cur.rp, t0, t1, Es, nEs, cbase, colb[wv], lane, M);
         const int h = lane / W, k = lane % W;
         const int rsl = sl.t * H + h;
         const bool virt = (vmask >> sl.t) & 1ull;
         // (the row scalars live on lanes t * H + h: every shuffle runs with all lanes
         // active -- ds_bpermute reads 0 from an inactive lane)
-        const float elq = __shfl(cur.s0, rsl), lsq = __shfl(cur.s1, rsl);
-        const float cfq = COEF ? __shfl(cur.s2, rsl) : 0.f;
+        const float elq = __shfl(cur.s[0], rsl), lsq = __shfl(cur.s[1], rsl);
+        const float cfq = COEF ? __shfl(cur.s[NS - 1], rsl) : 0.f;
         const float pre = elq + ert[sl.j * H + h];
         const float sc = virt ? 0.f : lrelu(pre, slope);
         const float att = sl.valid ? __expf(sc - lsq) : 0.f;
@@ -616,8 +691,9 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
         for (int t = 0; t < PD; ++t) {
           if (t >= t0 && t < t1) {
             const int32_t q0 = srp[t] - Es, q1 = srp[t + 1] - Es;
-            const float(&dUr)[V] = cur.rows[0][t];
-            const float(&hsr)[V] = cur.rows[NT - 1][t];
+            float dUr[V], hsr[V];
+            raw_unpack<T, V, RW>(cur.rows[0][t], dUr);
+            raw_unpack<T, V, RW>(cur.rows[NT - 1][t], hsr);
             float wacc[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) wacc[v] = 0.f;
@@ -672,12 +748,7 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
                 if (two) st_row<V>(sp1, z1);
               }
             }
-            if (HS) {
-              const uint32_t ro = r0 + t < re
-                                      ? ((uint32_t)(r0 + t) * D + lane * V) * (uint32_t)sizeof(T)
-                                      : kOOB;
-              bst_row<T, V>(r_dhs, ro, wacc);
-            }
+            if (HS) bst_row<T, V>(r_dhs, S.v_row, wacc, (uint32_t)(r0 + t) * RB);
           }
         }
         // (3) slot lanes: D_i, de_e, d_el_i, the d_er slab
@@ -695,8 +766,8 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
         }
         t0 = t1;
       }
-      const bool lr = lane < PD * H && r0 + lane / H < re;
-      buf_store_f32(r_del, lr ? (uint32_t)(r0 * H + lane) * 4u : kOOB, dels[wv][lane]);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dels[wv][lane]), r_del, S.v_s,
+                                            (uint32_t)r0 * (4u * H), 0);
     }
   }
   __syncthreads();

@@ -865,9 +865,10 @@ extern "C" int msha_add_head_outer(int64_t rows, int32_t heads, int32_t feat, co
 
 extern "C" int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const float* G,
                                 int64_t ldg, const int64_t* gi, const float* G2, int64_t ldg2,
-                                const int64_t* gj, const float* W, const float* bias,
-                                int32_t act, float drop_p, uint64_t seed, uint64_t offset,
-                                float* out, msha_stream_t stream) {
+                                const int64_t* gj, int64_t g_rows, int64_t g2_rows,
+                                const float* W, const float* bias, int32_t act, float drop_p,
+                                uint64_t seed, uint64_t offset, float* out,
+                                msha_stream_t stream) {
   MSHA_ARG_CHECK(n_pairs > 0 && K > 0 && N > 0, "pair_linear: bad sizes");
   MSHA_ARG_CHECK(G && W && out, "pair_linear: null pointer");
   MSHA_ARG_CHECK(!(act & ACT_BIAS) || bias, "pair_linear: bias missing");
@@ -878,8 +879,8 @@ extern "C" int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const flo
   p.act = act; p.bias = bias;
   p.dp = make_dropout(drop_p, seed, offset, (hipStream_t)stream);
   if (!p.dp.active) p.act &= ~ACT_DROPOUT;
-  if (!skinny_pair_linear(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, W, bias, p.act, p.dp, out,
-                          (hipStream_t)stream))
+  if (!skinny_pair_linear(n_pairs, K, N, G, ldg, gi, G2, ldg2, gj, g_rows, g2_rows, W, bias,
+                          p.act, p.dp, out, (hipStream_t)stream))
     launch<A_GATHER_HADAMARD, EPI_ACT, 0>(p, 1, (hipStream_t)stream);
   return check_launch("pair_linear");
 }

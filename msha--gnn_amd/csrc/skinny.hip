@@ -154,6 +154,21 @@ __device__ __forceinline__ void transpose_fill(float* Wl, const float* __restric
   transpose_store<K, N, NT>(Wl, p, tid);
 }
 
+// Line-major k order (PROJ_LINE=1, default): slot i of a lane group g holds the row's
+// columns [16 i + 4 g, +4) (fp32) / [32 i + 8 g, +8) (bf16), so one 16-byte load per lane
+// reads 64 contiguous bytes of each of the tile's 16 rows and slots 2j, 2j + 1 -- reloaded
+// together -- complete one 128-byte line.  PROJ_LINE=0: lane group g holds the row's
+// g-th K/4 quarter (every slot load touches 4 lines per row, 16 bytes of each, and a
+// slot-by-slot reload fetched each line from L2 once per slot).  The fp32 W image rows
+// follow the k order; the bf16 image stays [n][k] and only the read offsets move.
+#ifndef PROJ_LINE
+#define PROJ_LINE 1
+#endif
+template <int KL>
+__host__ __device__ constexpr int proj_img_row(int k) {  // fp32 image row of column k
+  return PROJ_LINE ? 4 * (4 * (k / 16) + k % 4) + (k % 16) / 4 : 4 * (k % KL) + k / KL;
+}
+
 // proj_kernel's block: PROJ_WPS waves per SIMD when the resident W and one staging
 // tile per wave fit the 160 KB of LDS, the staging tile narrowed to column halves when
 // the whole-width one would not fit (a head must not straddle the halves), else 2.
@@ -200,6 +215,9 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
   const int g = lane >> 4, r16 = lane & 15;
+  constexpr uint32_t kSlotB = PROJ_LINE ? 64u : 16u;      // bytes between a lane's slots
+  constexpr int kStepK = PROJ_LINE ? 32 : 8;              // bf16 k advance per MFMA step
+  static_assert(!PROJ_LINE || G::NLD % 2 == 0, "line-major slots come in pairs");
   TL_OPEN(1);  // marks: entry, W resident, per item (start, MFMAs done), exit
 
   // Work items of a wave, in order: whole 16-row tiles gw, gw + nw, ... for the R rounds
@@ -226,7 +244,8 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   const rsrc_t r_x = make_rsrc(X, (uint32_t)((int64_t)M * K * sizeof(T)));
   auto tile_off = [&](int t) -> uint32_t {
     const int row = t * 16 + r16;
-    return row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) + (uint32_t)(g * G::KL * sizeof(T))
+    return row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) +
+                         (uint32_t)(PROJ_LINE ? 16 * g : g * G::KL * (int)sizeof(T))
                    : kOOB;
   };
   // ---- W -> LDS once per block.  W's pieces load first, then the first item's rows:
@@ -245,7 +264,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   {
     const uint32_t off = n_items > 0 ? tile_off(item_tile(0)) : kOOB;
 #pragma unroll
-    for (int i = 0; i < G::NLD; ++i) buf[i] = buf_b128(r_x, off + 16u * i);
+    for (int i = 0; i < G::NLD; ++i) buf[i] = buf_b128(r_x, off + kSlotB * i);
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -254,7 +273,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
     if (!wp.ok(idx)) continue;
     if constexpr (G::F32) {
       const int k = idx / (N / 4), n4 = idx % (N / 4);
-      const int kr = 4 * (k % G::KL) + k / G::KL;
+      const int kr = proj_img_row<G::KL>(k);
       *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Wl) + kr * G::PW + 4 * n4) = wp.v[i];
     } else {
       const int k = idx / (N / 8), n8 = idx % (N / 8);
@@ -289,6 +308,17 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   // but not the launch: 42.2 vs 40.6 us at C4, the last item's epilogue and the start
   // dominate.  The two waves of a SIMD already overlap one's epilogue with the other's
   // MFMAs.)
+  // slot reloads: one slot after its last step (PROJ_LINE=0), or the two slots of a line
+  // after the second one's last step
+  auto reload = [&](int s, u32x4_t* cur, uint32_t noff) {
+    if (!PROJ_LINE) {
+      if ((s + 1) % SPL == 0) cur[s / SPL] = buf_b128(r_x, noff + 16u * (s / SPL));
+    } else if ((s + 1) % (2 * SPL) == 0) {
+      const int i = s / SPL - 1;
+      cur[i] = buf_b128(r_x, noff + 64u * i);
+      cur[i + 1] = buf_b128(r_x, noff + 64u * (i + 1));
+    }
+  };
   auto tile = [&](auto nbp_c, int t, int cb0, u32x4_t* cur, uint32_t noff) {
     constexpr int NBP = decltype(nbp_c)::value;
     TL_MARK();
@@ -314,12 +344,13 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
         for (int c = 0; c < NBP; ++c)
           acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if ((s + 1) % SPL == 0) cur[s / SPL] = buf_b128(r_x, noff + 16u * (s / SPL));
+        reload(s, cur, noff);
 #pragma unroll
         for (int c = 0; c < NBP; ++c) bc[c] = bn[c];
       }
     } else {
-      const bf16_t* Wb = reinterpret_cast<const bf16_t*>(Wl) + (r16 + cb0 * 16) * G::PW + g * G::KL;
+      const bf16_t* Wb = reinterpret_cast<const bf16_t*>(Wl) + (r16 + cb0 * 16) * G::PW +
+                         (PROJ_LINE ? 8 * g : g * G::KL);
       bf16x8 bc[NBP], bn[NBP];
 #pragma unroll
       for (int c = 0; c < NBP; ++c) bc[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW);
@@ -328,7 +359,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
         if (s + 1 < G::S) {
 #pragma unroll
           for (int c = 0; c < NBP; ++c)
-            bn[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW + 8 * (s + 1));
+            bn[c] = *reinterpret_cast<const bf16x8*>(Wb + c * 16 * G::PW + kStepK * (s + 1));
         }
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8 a = __builtin_bit_cast(bf16x8, cur[s]);
@@ -336,7 +367,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
         for (int c = 0; c < NBP; ++c)
           acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bc[c], acc[c], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if ((s + 1) % SPL == 0) cur[s / SPL] = buf_b128(r_x, noff + 16u * (s / SPL));
+        reload(s, cur, noff);
 #pragma unroll
         for (int c = 0; c < NBP; ++c) bc[c] = bn[c];
       }
@@ -545,6 +576,181 @@ __global__ void __launch_bounds__(64 * kProjWaves) pair_kernel(
     load_idx(t + 3 * nw, xa, xb);
     __builtin_amdgcn_sched_barrier(0);
     tile(t + nw, bi, bj);
+  }
+}
+
+// The fp32 pair scorer with ONE register set of rows (pair_kernel holds two: the tile in
+// use and the next one, 128 VGPRs of rows at K = 128, which left it at 2 waves per SIMD
+// with a spill).  A lane's row registers ci[i] / cj[i] feed steps [i SPL, (i + 1) SPL);
+// once those MFMAs have issued, slot i is reloaded with the NEXT tile's rows, so the next
+// tile's gathers are in flight under the rest of this tile (7/8 of a tile of lead for the
+// first slot).  The next tile's pair indices are loaded a whole tile earlier still.
+//   The waits must stay exact for that lead to exist, which decides the memory ops:
+//   - row gathers are buffer loads at 32-bit offsets from the table base (plain 64-bit
+//     loads let the register allocator rotate the row registers through copies at the
+//     loop latch, each copy waiting on its load);
+//   - the epilogue writes the MFMA C layout (row 4 g + i, column 16 c + r16) with
+//     buffer stores through a per-tile descriptor that ends at the batch's last row, so
+//     rows past it drop without a branch: every tile issues the same count of stores
+//     and the compiler's vmcnt at the next tile's first use counts them (a branch
+//     around the stores made it assume none and wait for every reload);
+//   - no staging tile: the LDS holds W alone, so WPS waves per SIMD fit.
+//   - line-major k: slot i of lane group g holds columns [16 i + 4 g, +4), so one load
+//     instruction reads 64 contiguous bytes of each of its 16 rows and slots 2j, 2j + 1
+//     (reloaded together) cover one 128-byte line.  (pair_kernel's k = g K/4 + s puts a
+//     lane group's 16 bytes of a slot in a different line for each g: reloaded a slot at
+//     a time, every line came from L2 eight times.)  The W image rows follow the same
+//     k order.
+// The host picks this kernel when both tables fit a buffer window (msha_pair_linear's
+// table_rows: rows x ldg x 4 < 4 GiB); the descriptors end at the tables' ends, so an
+// index past them reads zeros instead of faulting.  Same activation bits and dropout
+// keys (p * N + n) as pair_kernel; the k order differs, so the sums round differently.
+#ifndef PAIR32_WPS
+#define PAIR32_WPS 3
+#endif
+template <int K, int N, int WPS>
+__global__ void __launch_bounds__(256 * WPS) pair_roll_kernel(
+    int M, const float* __restrict__ G, int64_t ldg, const int64_t* __restrict__ gi,
+    const float* __restrict__ G2, int64_t ldg2, const int64_t* __restrict__ gj,
+    const float* __restrict__ Wlin, const float* __restrict__ bias, int act, Dropout dp,
+    float* __restrict__ out, uint32_t bytes_a, uint32_t bytes_b) {
+  using Gm = ProjGeo<float, K, N>;
+  constexpr int kWaves = 4 * WPS;
+  constexpr int SPL = Gm::S / Gm::NLD;  // MFMA steps fed by one 16-byte row register
+  __shared__ __attribute__((aligned(16))) float Wl[Gm::WBYTES / 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+
+  {  // B[k][n] = Wlin[n][k] -> image row 4 s + g for k = 16 (s / 4) + 4 g + s % 4
+    WPieces<K, N, 64 * kWaves> p;
+    p.load(Wlin, tid);
+#pragma unroll
+    for (int i = 0; i < p.IT; ++i) {
+      const int idx = tid + 64 * kWaves * i;
+      if (p.ok(idx)) {
+        const int n = idx / (K / 4), k4 = idx % (K / 4);
+        const uint32_t e[4] = {p.v[i].x, p.v[i].y, p.v[i].z, p.v[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = 4 * k4 + j;
+          const int row = 4 * (4 * (k / 16) + k % 4) + (k % 16) / 4;
+          Wl[row * Gm::PW + n] = __uint_as_float(e[j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  float bv[Gm::NB];
+#pragma unroll
+  for (int c = 0; c < Gm::NB; ++c) bv[c] = (act & SK_BIAS) ? bias[c * 16 + r16] : 0.f;
+  const uint64_t doff = (act & SK_DROPOUT) ? dropout_offset(dp, dp.offset) : 0;
+
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kWaves;
+  const int tiles = (M + 15) / 16;
+  if (gw >= tiles) return;
+
+  // the tables (G / G2 are non-null: checked on the host; make_rsrc's null test would put
+  // the descriptor in VGPRs and waterfall every load)
+  const rsrc_t r_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), 0, bytes_a, 0x00020000);
+  const rsrc_t r_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G2), 0, bytes_b, 0x00020000);
+  // rows past the batch (and tiles past the last) clamp to the last pair: valid
+  // addresses, never stored, so every reload is unconditional
+  auto load_idx = [&](int t, int64_t& a, int64_t& b) {
+    const int row = min(t * 16 + r16, M - 1);
+    a = gi[row];
+    b = gj[row];
+  };
+  // byte offsets of this lane's first 4 columns of the two rows (< 4 GiB: the host's check).
+  // An index outside [0, 2^31) maps past the window (reads zeros); the test also keeps
+  // the index's high word live, so the register allocator does not put the offset into
+  // the dead high half of the NEXT index load's destination (a write that would wait on
+  // that load: vmcnt(0) at every tile start)
+  auto offset_a = [&](int64_t a) -> uint32_t {
+    return (a >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((a * ldg + 4 * g) * 4);
+  };
+  auto offset_b = [&](int64_t b) -> uint32_t {
+    return (b >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((b * ldg2 + 4 * g) * 4);
+  };
+  auto mfma_tile = [&](int t, u32x4_t* ci, u32x4_t* cj, uint32_t na, uint32_t nb) {
+    f32x4 acc[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* Wf = Wl + g * Gm::PW + r16;
+    float bc[Gm::NB], bn[Gm::NB];
+#pragma unroll
+    for (int c = 0; c < Gm::NB; ++c) bc[c] = Wf[c * 16];
+#pragma unroll
+    for (int s = 0; s < Gm::S; ++s) {
+      if (s + 1 < Gm::S) {
+#pragma unroll
+        for (int c = 0; c < Gm::NB; ++c) bn[c] = Wf[4 * (s + 1) * Gm::PW + c * 16];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const float a = __uint_as_float(ci[s / 4][s % 4]) * __uint_as_float(cj[s / 4][s % 4]);
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bc[c], acc[c], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if ((s + 1) % (2 * SPL) == 0) {  // the two slots of one 128-byte line
+        const int i = s / SPL - 1;
+        ci[i] = buf_b128(r_a, na + 64u * i);
+        ci[i + 1] = buf_b128(r_a, na + 64u * (i + 1));
+        cj[i] = buf_b128(r_b, nb + 64u * i);
+        cj[i + 1] = buf_b128(r_b, nb + 64u * (i + 1));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c) bc[c] = bn[c];
+    }
+    // ---- epilogue on the C layout: element (row t 16 + 4 g + i, column 16 c + r16)
+    const int rows = min(16, M - t * 16);
+    const rsrc_t r_o = make_rsrc(out + (int64_t)t * 16 * N, (uint32_t)(rows * N * 4));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = t * 16 + 4 * g + i;
+#pragma unroll
+      for (int c = 0; c < Gm::NB; ++c) {
+        float x = acc[c][i] + bv[c];
+        if (act & SK_RELU) x = fmaxf(x, 0.f);
+        if (act & SK_DROPOUT)
+          x *= philox_x(dp.seed, doff, (uint64_t)row * N + c * 16 + r16) >= dp.threshold
+                   ? dp.scale
+                   : 0.f;
+        if (act & SK_SIGMOID) x = 1.f / (1.f + __expf(-x));
+        buf_store_f32(r_o, (uint32_t)(((4 * g + i) * N + c * 16 + r16) * 4), x);
+      }
+    }
+  };
+
+  u32x4_t ci[Gm::NLD], cj[Gm::NLD];
+  int64_t xa, xb;
+  load_idx(gw, xa, xb);
+  {
+    const uint32_t oa = offset_a(xa), ob = offset_b(xb);
+    // in slot order, as the loop reloads them: the wait counts at the loop head merge
+    // this path's (a reordered prologue let slot 0 look like one of the last loads and
+    // the loop then waited for nearly every reload at each tile start)
+#pragma unroll
+    for (int i = 0; i < Gm::NLD; i += 2) {
+      ci[i] = buf_b128(r_a, oa + 64u * i);
+      ci[i + 1] = buf_b128(r_a, oa + 64u * (i + 1));
+      cj[i] = buf_b128(r_b, ob + 64u * i);
+      cj[i + 1] = buf_b128(r_b, ob + 64u * (i + 1));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  load_idx(gw + nw, xa, xb);
+  for (int t = gw; t < tiles; t += nw) {
+    // the next tile's row offsets (its indices were loaded one tile ago), then the
+    // indices of the tile after it
+    const uint32_t oa = offset_a(xa), ob = offset_b(xb);
+    load_idx(t + 2 * nw, xa, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_tile(t, ci, cj, oa, ob);
   }
 }
 
@@ -1161,21 +1367,38 @@ template int skinny_project<float>(int64_t, int64_t, int, int, const void*, cons
 template int skinny_project<bf16_t>(int64_t, int64_t, int, int, const void*, const void*,
                                     const float*, const float*, void*, float*, float*, hipStream_t);
 
-// pair linear on the resident-W kernel: fp32, both gathers given, K and N in {64, 128},
-// 16-byte aligned rows; 0 = not covered (the caller runs the tiled GEMM)
+// pair linear on the resident-W kernels: fp32, both gathers given, K and N in {64, 128},
+// 16-byte aligned rows; 0 = not covered (the caller runs the tiled GEMM).  Tables with
+// known row counts inside a 4 GiB buffer window take pair_roll_kernel.
 int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t ldg,
                        const int64_t* gi, const float* G2, int64_t ldg2, const int64_t* gj,
-                       const float* W, const float* bias, int act, const Dropout& dp, float* out,
-                       hipStream_t s) {
+                       int64_t g_rows, int64_t g2_rows, const float* W, const float* bias,
+                       int act, const Dropout& dp, float* out, hipStream_t s) {
   if (!skinny_enabled() || P < 1024 || P >= (1ll << 31) || gi == nullptr || gj == nullptr) return 0;
-  if (G2 == nullptr) { G2 = G; ldg2 = ldg; }
+  if (G2 == nullptr) { G2 = G; ldg2 = ldg; g2_rows = g_rows; }
   if (ldg % 4 || ldg2 % 4 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)out | (uintptr_t)W) & 15))
     return 0;
+  static const int roll_env = [] {  // MSHA_PAIR_ROLL=0: always the two-register-set pair_kernel
+    const char* v = getenv("MSHA_PAIR_ROLL");
+    return v != nullptr && *v ? atoi(v) : 1;
+  }();
+  // table bytes up to the last row's K columns (the kernel reads no further)
+  auto span = [&](int64_t rows, int64_t ld) -> int64_t { return rows > 0 ? ((rows - 1) * ld + K) * 4 : -1; };
+  const int64_t ba = span(g_rows, ldg), bb = span(g2_rows, ldg2);
+  const bool roll = roll_env && ba > 0 && bb > 0 && ba <= 0xFFFFFFFFll && bb <= 0xFFFFFFFFll &&
+                    P * N * 4 < (1ll << 31);
   const dim3 grid(proj_grid(P)), block(64 * sk::kProjWaves);
+  constexpr int rw = 4 * PAIR32_WPS;
+  const dim3 rgrid(proj_grid(P, rw)), rblock(64 * rw);
 #define SKPL(k, n)                                                                              \
   if (K == k && N == n) {                                                                       \
-    hipLaunchKernelGGL((sk::pair_kernel<k, n>), grid, block, 0, s, (int)P, G, ldg, gi, G2,     \
-                       ldg2, gj, W, bias, act, dp, out);                                        \
+    if (roll)                                                                                   \
+      hipLaunchKernelGGL((sk::pair_roll_kernel<k, n, PAIR32_WPS>), rgrid, rblock, 0, s, (int)P, \
+                         G, ldg, gi, G2, ldg2, gj, W, bias, act, dp, out, (uint32_t)ba,         \
+                         (uint32_t)bb);                                                         \
+    else                                                                                        \
+      hipLaunchKernelGGL((sk::pair_kernel<k, n>), grid, block, 0, s, (int)P, G, ldg, gi, G2,   \
+                         ldg2, gj, W, bias, act, dp, out);                                      \
     return 1;                                                                                   \
   }
   SKPL(128, 128) SKPL(64, 128) SKPL(128, 64) SKPL(64, 64)

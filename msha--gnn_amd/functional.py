@@ -868,7 +868,8 @@ class _PairLayer(torch.autograd.Function):
         act = ACT_BIAS | ACT_RELU | (ACT_DROPOUT if p > 0 else 0) | (ACT_SIGMOID if sigmoid else 0)
         out = torch.empty(B, N, device=x_i.device, dtype=torch.float32)
         _lib.call("msha_pair_linear", B, K, N, x_i.data_ptr(), K, None, _lib.ptr(x_j), K, None,
-                  W.data_ptr(), b.data_ptr(), act, p, seed, 0, out.data_ptr(), _stream(x_i))
+                  B, B, W.data_ptr(), b.data_ptr(), act, p, seed, 0, out.data_ptr(),
+                  _stream(x_i))
         ctx.p, ctx.sigmoid = p, sigmoid
         ctx.has_xj = x_j is not None
         ctx.save_for_backward(x_i, x_j if x_j is not None else x_i.new_empty(0), W, out)
@@ -977,8 +978,9 @@ def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None, out_dtype=N
                   out.data_ptr(), s)
         return out
     out = torch.empty(P, N, device=h.device, dtype=torch.float32) if out is None else out
+    rows = (h.shape[0], h.shape[0]) if not bf else ()  # the fp32 entry takes the row counts
     _lib.call("msha_pair_linear_bf16" if bf else "msha_pair_linear", P, Fd, N, h.data_ptr(),
-              h.stride(0), src.data_ptr(), h.data_ptr(), h.stride(0), dst.data_ptr(),
+              h.stride(0), src.data_ptr(), h.data_ptr(), h.stride(0), dst.data_ptr(), *rows,
               W.data_ptr(), b.data_ptr(), ACT_BIAS | ACT_RELU | ACT_SIGMOID, 0.0, 0, 0,
               out.data_ptr(), s)
     return out

@@ -32,7 +32,10 @@ def timeit(fn, reps=int(os.environ.get("GEMM_AB_REPS", 50)), warm=2):
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    for shape in ((100000, 128, 8, 16), (39179, 128, 2, 64)):  # C4, R15 (configs[1])
+    shapes = [(100000, 128, 8, 16), (39179, 128, 2, 64)]  # C4, R15 (configs[1])
+    if os.environ.get("GEMM_AB_BIP1M"):
+        shapes.append((1000000, 128, 2, 64))  # bip1m's source table
+    for shape in shapes:
         run_shape(dev, g, *shape)
 
 

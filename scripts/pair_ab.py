@@ -42,8 +42,9 @@ def save(path):
         o = torch.empty(P, N, device=dev, dtype=torch.float32)
         fn = "msha_pair_linear_bf16" if ob is not None else "msha_pair_linear"
         s = torch.cuda.current_stream(dev).cuda_stream
+        rows = () if ob is not None else (h.shape[0], h.shape[0])
         _lib.call(fn, P, F, N, h.data_ptr(), h.stride(0), src.data_ptr(), h.data_ptr(),
-                  h.stride(0), dst.data_ptr(), W.data_ptr(), b.data_ptr(), 1 | 2 | 4 | 8, 0.5,
+                  h.stride(0), dst.data_ptr(), *rows, W.data_ptr(), b.data_ptr(), 1 | 2 | 4 | 8, 0.5,
                   1234, 7, o.data_ptr(), s)
         outs[tag + "_drop"] = o
     torch.save({k: v.cpu() for k, v in outs.items()}, path)

@@ -780,12 +780,14 @@ def test_edge_attention_fused_backward_slot_order(cuda, msha):
     tol_close(rt[1].cpu().numpy(), split[1].cpu().numpy(), 1e-5, 1e-5)
 
 
-@pytest.mark.parametrize("K,N", [(128, 128), (64, 128), (128, 64)])
+@pytest.mark.parametrize("K,N", [(128, 128), (64, 128), (128, 64), (64, 64)])
 def test_pair_linear_resident_w(cuda, msha, K, N):
-    """msha_pair_linear on the resident-W kernel (skinny.hip pair_kernel: fp32, both
-    gathers, P >= 1024): hadamard of the gathered rows @ W^T + b, ReLU, dropout keyed on
-    p * N + n (the library's Philox mask), sigmoid -- vs the oracle with that mask; a
-    ragged last tile (P % 16 != 0)."""
+    """msha_pair_linear on the resident-W kernels (skinny.hip, fp32, both gathers,
+    P >= 1024): hadamard of the gathered rows @ W^T + b, ReLU, dropout keyed on p * N + n
+    (the library's Philox mask), sigmoid -- vs the oracle with that mask; a ragged last
+    tile (P % 16 != 0).  Table row counts given -> pair_roll_kernel (one rolling row
+    set, buffer gathers, line-major k order); unknown (0) -> pair_kernel.  Both against
+    the oracle; they sum k in different orders, so they agree to rounding, not bits."""
     from msha_gnn_amd import _lib
     from msha_gnn_amd import functional as MF
 
@@ -793,19 +795,26 @@ def test_pair_linear_resident_w(cuda, msha, K, N):
     n, P, p, seed = 3000, 4099, 0.5, 123
     h = rng.standard_normal((n, K)).astype(np.float32)
     src, dst = rng.integers(0, n, P), rng.integers(0, n, P)
+    src[-1], dst[0] = n - 1, n - 1  # the tables' last rows (the buffer windows' ends)
     W = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
     b = rng.standard_normal(N).astype(np.float32)
     th, ts, td = t(h, cuda), t(src, cuda, torch.int64), t(dst, cuda, torch.int64)
     tW, tb = t(W, cuda), t(b, cuda)
-    out = torch.empty(P, N, device=cuda)
     act = MF.ACT_BIAS | MF.ACT_RELU | MF.ACT_DROPOUT | MF.ACT_SIGMOID
-    _lib.call("msha_pair_linear", P, K, N, th.data_ptr(), K, ts.data_ptr(), th.data_ptr(), K,
-              td.data_ptr(), tW.data_ptr(), tb.data_ptr(), act, p, seed, 0, out.data_ptr(),
-              _lib.stream_handle(cuda))
+    outs = []
+    for rows in (n, 0):
+        out = torch.full((P + 16, N), -7.0, device=cuda)  # 16 guard rows past the batch
+        _lib.call("msha_pair_linear", P, K, N, th.data_ptr(), K, ts.data_ptr(), th.data_ptr(),
+                  K, td.data_ptr(), rows, rows, tW.data_ptr(), tb.data_ptr(), act, p, seed, 0,
+                  out.data_ptr(), _lib.stream_handle(cuda))
+        o = out.cpu().numpy()
+        assert (o[P:] == -7.0).all(), "a store past the batch"
+        outs.append(o[:P])
     keep = MF.dropout_keep_mask(P * N, p, seed, cuda).cpu().numpy().reshape(P, N)
     z = np.maximum((h[src].astype(np.float64) * h[dst]) @ W.T.astype(np.float64) + b, 0)
     ref = 1 / (1 + np.exp(-(z * keep / (1 - p))))
-    tol_close(out.cpu().numpy(), ref, 1e-5, 1e-6)
+    for o in outs:
+        tol_close(o, ref, 1e-5, 1e-6)
 
 
 @pytest.mark.parametrize("M,H,F,two", [(100000, 8, 16, True), (50015, 2, 64, True),
