@@ -279,9 +279,13 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 // matches read LDS instead of a dependent global round trip each (the global-gather form
 // above took 43 us at the 2015 graph: ~5 nodes per wave, one L2 latency chain per node).
 // A persistent grid walks the nodes; the next node's group ids and u_in are loaded before
-// this node's matches run.  Same sums in the same order as ours_fwd_kernel.
+// this node's matches run.  Same sums in the same order as ours_fwd_kernel.  Blocks of 8
+// waves, 4 per CU (4 x 34 KB of LDS at B 64, D 128): ~5 nodes per wave at the 2015 graph
+// (2 blocks of 4 waves per CU left each wave ~19 dependent node steps: 60 us vs 43 us
+// for the global-gather form).
+constexpr int kOursFwdWaves = 8;
 template <typename T, int KD>
-__global__ void __launch_bounds__(256) ours_fwd_lds_kernel(OursArgs a,
+__global__ void __launch_bounds__(64 * kOursFwdWaves) ours_fwd_lds_kernel(OursArgs a,
                                                            const float* __restrict__ bstat,
                                                            const T* __restrict__ u_in,
                                                            T* __restrict__ u_out) {
@@ -291,11 +295,11 @@ __global__ void __launch_bounds__(256) ours_fwd_lds_kernel(OursArgs a,
   const int B = (int)a.B;
   float* w3s = sx + B * D;
   float* w4s = w3s + B * H;
-  for (int b = wv; b < B; b += 4) {
+  for (int b = wv; b < B; b += kOursFwdWaves) {
     const int64_t ib = a.src[b];
     for (int d = lane; d < D; d += 64) sx[b * D + d] = ldt<T>(a.h2, ib * D + d);
   }
-  for (int i = threadIdx.x; i < B * H; i += 256) {
+  for (int i = threadIdx.x; i < B * H; i += 64 * kOursFwdWaves) {
     w3s[i] = bstat[(int64_t)i * BS_N + BS_W3];
     w4s[i] = bstat[(int64_t)i * BS_N + BS_W4];
   }
@@ -722,10 +726,10 @@ static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const 
                        g->col, g->rowflag, el, er, lse, bstat);
   const int D = a.H * a.F;
   if (B > 0 && B <= 64 && D <= 256) {
-    // the batch staged in LDS (ours_fwd_lds_kernel): a persistent grid, two blocks per CU
+    // the batch staged in LDS (ours_fwd_lds_kernel): a persistent grid, four blocks per CU
     const size_t lds = (size_t)B * (D + 2 * a.H) * sizeof(float);
-    const dim3 grid(grid_for(g->n_rows, 4, 2 * ours_cu_count()));
-#define FWDL(kd) hipLaunchKernelGGL((ours_fwd_lds_kernel<T, kd>), grid, dim3(256), lds, s, a, \
+    const dim3 grid(grid_for(g->n_rows, kOursFwdWaves, 4 * ours_cu_count()));
+#define FWDL(kd) hipLaunchKernelGGL((ours_fwd_lds_kernel<T, kd>), grid, dim3(64 * kOursFwdWaves), lds, s, a, \
                                     (const float*)bstat, (const T*)u_inter, (T*)u_out)
     if (D <= 64) FWDL(1);
     else if (D <= 128) FWDL(2);
