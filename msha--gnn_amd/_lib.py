@@ -237,9 +237,22 @@ def raise_for(rc: int, name: str):
     raise RuntimeError(f"{name} failed ({rc}): {msg}")
 
 
+_FNS: dict = {}  # name -> typed ctypes function (one getattr per name)
+
+
+def fn(name: str):
+    f = _FNS.get(name)
+    if f is None:
+        f = _FNS[name] = getattr(load(), name)
+    return f
+
+
 def call(name: str, *args):
     """Invoke an ABI function; raise on a non-zero status with the library message."""
-    rc = getattr(load(), name)(*args)
+    f = _FNS.get(name)
+    if f is None:
+        f = fn(name)
+    rc = f(*args)
     if rc != MSHA_OK:
         raise_for(rc, name)
     return rc
@@ -252,7 +265,23 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle(device=None) -> int:
+    """The current HIP stream of ``device`` (torch.device, index or None = current) as
+    an integer handle -- the raw-stream query, without building a torch Stream object
+    per call (the ops issue one per launch)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            if isinstance(device, str):
+                device = torch.device(device)
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -8,6 +8,10 @@
 """
 from __future__ import annotations
 
+import ctypes
+import functools
+import struct
+
 import torch
 
 from . import _lib
@@ -94,6 +98,31 @@ def _stream(t):
     return _lib.stream_handle(t.device)
 
 
+# Host-side caches for the per-call work around each launch (the eager train.py step is
+# host-bound: ~40 launches behind ~1 ms of Python per step).
+_WS: dict = {}  # (device index, stream) -> uint8 scratch tensor
+
+
+def _workspace(dev, nbytes: int):
+    """A scratch buffer of at least ``nbytes`` for one call's launches, shared by every
+    call on the same device and stream (the library's workspaces are transient within a
+    call; stream order keeps consecutive users apart)."""
+    key = (dev.index, _lib.stream_handle(dev))
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = _WS[key] = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+    return t
+
+
+def _memo(obj, key, make):
+    """Per-object memo (a graph's capability answers and workspace sizes)."""
+    d = obj.__dict__.setdefault("_msha_memo", {})
+    v = d.get(key)
+    if v is None:
+        v = d[key] = make()
+    return v
+
+
 class _EdgeAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, el, er, hc, hs, graph: Graph, p: float, seed: int, slope: float, ar=None):
@@ -113,7 +142,7 @@ class _EdgeAttention(torch.autograd.Function):
             u = torch.empty(n, H, F, device=dev, dtype=dt)
             lse = torch.empty(n, H, device=dev, dtype=torch.float32)
             v = torch.empty(m, H, F, device=dev, dtype=dt) if hs is not None else None
-            ws = _bip_ws(g, H, F, dev)
+            ws = _bip_ws(graph, H, F, dev)
             ev = _timed("bip_attention_fwd")
             _lib.call("msha_bip_attention_fwd", g, H, F, _code(dt), el.data_ptr(),
                       er.data_ptr(), hc.data_ptr(), _lib.ptr(hs), slope, p, seed, 0,
@@ -232,13 +261,14 @@ def bip_ok(graph, H, F, dtype) -> bool:
     """The bipartite kernels cover the graph: the library's shape rule (M <= 32,
     M * H <= 64, M * H * F <= 4096) and rows with distinct columns, at most 64 / H each
     (every graph from_dense builds; checked on the host for from_csr)."""
-    return bool(BIP and graph.distinct_cols and graph.max_deg * H <= 64
-                and _lib.load().msha_bip_supported(graph.desc, H, F, _code(dtype)))
+    return bool(BIP and graph.distinct_cols and graph.max_deg * H <= 64 and _memo(
+        graph, ("bip", H, F, _code(dtype)),
+        lambda: bool(_lib.fn("msha_bip_supported")(graph.desc, H, F, _code(dtype)))))
 
 
-def _bip_ws(g, H, F, dev):
-    return torch.empty(int(_lib.load().msha_bip_workspace_size(g, H, F)), dtype=torch.uint8,
-                       device=dev)
+def _bip_ws(graph, H, F, dev):
+    return _workspace(dev, _memo(graph, ("bip_ws", H, F), lambda: int(
+        _lib.fn("msha_bip_workspace_size")(graph.desc, H, F))))
 
 
 def _bip_bwd(ctx, dU, dV):
@@ -258,7 +288,7 @@ def _bip_bwd(ctx, dU, dV):
     d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
     d_hc = torch.empty(m, H, F, device=dev, dtype=dt)
     d_hs = torch.empty(n, H, F, device=dev, dtype=dt) if use_dv else None
-    ws = _bip_ws(g, H, F, dev)
+    ws = _bip_ws(ctx.graph, H, F, dev)
     ev = _timed("bip_attention_bwd")
     _lib.call("msha_bip_attention_bwd", g, H, F, _code(dt), el.data_ptr(), er.data_ptr(),
               hc.data_ptr(), lse.data_ptr(), dU.data_ptr(), hs.data_ptr() if use_dv else None,
@@ -554,8 +584,7 @@ class _ProjectScores(torch.autograd.Function):
         el = torch.empty(M, heads, device=dev, dtype=torch.float32) if al is not None else None
         er = torch.empty(M, heads, device=dev, dtype=torch.float32) if ar is not None else None
         # a small table (the 32 recipients of R15): one single-workgroup launch each way
-        ctx.small = dt == torch.float32 and bool(
-            _lib.load().msha_project_small_supported(M, K, heads, feat))
+        ctx.small = dt == torch.float32 and _project_small(M, K, heads, feat)
         fn = ("msha_project_small" if ctx.small else
               "msha_project_scores_bf16" if dt == BF16 else "msha_project_scores")
         _lib.call(fn, M, K, heads, feat, X.data_ptr(), W.data_ptr(), _lib.ptr(al), _lib.ptr(ar),
@@ -629,8 +658,7 @@ class _ProjectScores(torch.autograd.Function):
             d2 = terms[1][0] if len(terms) > 1 else None
             o1 = torch.empty(H, Fd, device=dev, dtype=torch.float32)
             o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
-            wsb = int(_lib.load().msha_head_colsum_workspace_size(M, H, Fd))
-            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+            ws = _workspace(dev, int(_lib.fn("msha_head_colsum_workspace_size")(M, H, Fd)))
             d1, d2 = _f32c(d1), _f32c(d2)  # held until the launch (see bn_lrelu)
             _lib.call("msha_head_colsum", M, H, Fd, _code(dt), d1.data_ptr(),
                       _lib.ptr(d2), h.data_ptr(), o1.data_ptr(), _lib.ptr(o2),
@@ -664,23 +692,33 @@ def _wgrad_colsum(X, dh, outer, h):
     splits = _splits_for(M, K, N)
     dev = X.device
     dW = torch.empty(K, N, device=dev, dtype=torch.float32)
-    ws = torch.empty(int(_lib.load().msha_gemm_workspace_size(K, N, splits)), dtype=torch.uint8,
-                     device=dev)
-    cws = torch.empty(int(_lib.load().msha_head_outer_colsum_workspace_size(N)),
-                      dtype=torch.uint8, device=dev)
+    # the GEMM's and the colsum's scratch as two aligned parts of the shared workspace
+    wsb = (int(_lib.fn("msha_gemm_workspace_size")(K, N, splits)) + 255) // 256 * 256
+    cwsb = int(_lib.fn("msha_head_outer_colsum_workspace_size")(N))
+    buf = _workspace(dev, wsb + cwsb)
     o1 = torch.empty(H, Fd, device=dev, dtype=torch.float32)
     o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
     A = X.t()
-    rc = _lib.load().msha_gemm_f32_head_outer_colsum(
+    rc = _lib.fn("msha_gemm_f32_head_outer_colsum")(
         K, N, M, A.data_ptr(), A.stride(0), A.stride(1), dh.data_ptr(), dh.stride(0),
-        dh.stride(1), dW.data_ptr(), dW.stride(0), splits, ws.data_ptr(), ws.numel(), H, Fd,
+        dh.stride(1), dW.data_ptr(), dW.stride(0), splits, buf.data_ptr(), wsb, H, Fd,
         d1.data_ptr(), a1.data_ptr(), _lib.ptr(d2), _lib.ptr(a2), h.data_ptr(), o1.data_ptr(),
-        _lib.ptr(o2), cws.data_ptr(), cws.numel(), _stream(X))
+        _lib.ptr(o2), buf.data_ptr() + wsb, cwsb, _stream(X))
     if rc == _lib.MSHA_ERR_UNSUPPORTED:
         return None
     if rc != 0:
         _lib.raise_for(rc, "msha_gemm_f32_head_outer_colsum")
     return dW, o1, o2
+
+
+@functools.lru_cache(maxsize=256)
+def _project_small(M, K, heads, feat) -> bool:
+    return bool(_lib.fn("msha_project_small_supported")(M, K, heads, feat))
+
+
+@functools.lru_cache(maxsize=256)
+def _row_order(M, K, heads, feat, code) -> bool:
+    return bool(_lib.fn("msha_project_scores_row_order")(M, K, heads, feat, code))
 
 
 def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = None):
@@ -699,8 +737,7 @@ def project_scores(X, W, al=None, ar=None, heads: int = 1, feat: int | None = No
         # it (msha_project_scores_row_order): edge_attention(..., ar=) then reads this er
         # where it needs er_j per column instead of recomputing it (the same bits)
         M, K = X.shape
-        out[-1]._msha_row_order = bool(_lib.load().msha_project_scores_row_order(
-            M, K, heads, feat, _code(_table_dtype(X, W))))
+        out[-1]._msha_row_order = _row_order(M, K, heads, feat, _code(_table_dtype(X, W)))
     return out
 
 
@@ -1012,7 +1049,7 @@ class _OursAttention(torch.autograd.Function):
         v = torch.empty(m, H, Fd, device=dev, dtype=dt)
         if bip:
             # u, v and the attention export in one pass (msha_bip_attention_fwd)
-            ws = _bip_ws(g, H, Fd, dev)
+            ws = _bip_ws(graph, H, Fd, dev)
             _lib.call("msha_bip_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
                       er.data_ptr(), h1.data_ptr(), h2.data_ptr(), slope, p, seed, 0,
                       u_inter.data_ptr(), None, lse.data_ptr(), attd.data_ptr(), v.data_ptr(),
@@ -1059,8 +1096,8 @@ class _OursAttention(torch.autograd.Function):
         args = (g, gr, B, src.data_ptr(), H, Fd, _code(dt), h2.data_ptr(), a3s.data_ptr(),
                 a4s.data_ptr(),
                 bstat.data_ptr(), dU.data_ptr())
-        wsb = int(_lib.load().msha_ours_workspace_size(gr, B, H, Fd))
-        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        ws = _workspace(dev, _memo(groups, ("ours_ws", B, H, Fd), lambda: int(
+            _lib.fn("msha_ours_workspace_size")(gr, B, H, Fd))))
         _lib.call("msha_ours_intra_bwd", *args, 0, ctx.slope, ctx.p, ctx.seed, 0, G.data_ptr(),
                   bgrad.data_ptr(), row_coef.data_ptr(), da3s.data_ptr(), da4s.data_ptr(), None,
                   ws.data_ptr(), ws.numel(), s)
@@ -1071,7 +1108,7 @@ class _OursAttention(torch.autograd.Function):
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
         if ctx.bip:
             # row and column gradients of the inter attention in one pass
-            ws = _bip_ws(g, H, Fd, dev)
+            ws = _bip_ws(graph, H, Fd, dev)
             _lib.call("msha_bip_attention_bwd", g, H, Fd, _code(dt), el.data_ptr(),
                       er.data_ptr(), h1.data_ptr(), lse.data_ptr(), dU.data_ptr(),
                       h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p,
@@ -1118,13 +1155,31 @@ def head_supported(graph: Graph, heads: int, feat: int) -> bool:
     return bool(_lib.load().msha_head_supported(graph.n_cols, heads, feat))
 
 
-def _head_params(H, F, eps, momentum, slope, ptrs):
-    hp = _lib.MshaHeadParams()
-    hp.heads, hp.feat, hp.eps, hp.momentum, hp.slope = H, F, eps, momentum, slope
-    for name, lst in ptrs.items():
+_HP_CACHE: dict = {}
+
+
+def _head_params(H, F, eps, momentum, slope, ptrs, dyn=None):
+    """msha_head_params from pointer lists: the ``ptrs`` part is built once per distinct
+    set of pointers (the parameters and buffers stay put across steps) and copied; the
+    ``dyn`` part (this call's gradient outputs) is written into the copy."""
+    key = (H, F, eps, momentum, slope, tuple((k, None if v is None else tuple(v))
+                                            for k, v in ptrs.items()))
+    base = _HP_CACHE.get(key)
+    if base is None:
+        if len(_HP_CACHE) > 64:
+            _HP_CACHE.clear()
+        base = _lib.MshaHeadParams()
+        base.heads, base.feat, base.eps, base.momentum, base.slope = H, F, eps, momentum, slope
+        for name, lst in ptrs.items():
+            arr = getattr(base, name)
+            for h in range(len(lst) if lst is not None else H):
+                arr[h] = lst[h] if lst is not None else None
+        _HP_CACHE[key] = base
+    hp = _lib.MshaHeadParams.from_buffer_copy(base)
+    for name, lst in (dyn or {}).items():
         arr = getattr(hp, name)
-        for h in range(len(lst) if lst is not None else H):
-            arr[h] = lst[h] if lst is not None else None
+        for h, v in enumerate(lst):
+            arr[h] = v
     return hp
 
 
@@ -1192,8 +1247,8 @@ class _ModelHead(torch.autograd.Function):
         stats = torch.empty(4 * H * F + H * F * M, device=dev, dtype=torch.float32)
         out = torch.empty(N, M, device=dev, dtype=dt)
         g = graph.desc
-        wsb = int(_lib.load().msha_head_workspace_size(g, H, F)) if training else 0
-        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        ws = _workspace(dev, _memo(graph, ("head_ws", H, F), lambda: int(
+            _lib.fn("msha_head_workspace_size")(g, H, F))) if training else 0)
         _lib.call("msha_head_fwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
                   W32.data_ptr(), int(training), px, sx, pa, sa, stats.data_ptr(),
                   out.data_ptr(), ws.data_ptr(), ws.numel(), s)
@@ -1224,16 +1279,18 @@ class _ModelHead(torch.autograd.Function):
         dW = torch.empty_like(W32)
         dp = torch.empty(4, H, F, device=dev, dtype=torch.float32)
         ptr = lambda lst: [_lib.ptr(t) for t in lst]  # noqa: E731
+        base = dp.data_ptr()
+        step = 4 * F  # dp (4, H, F): gradient k of head h at base + 4 (k H + h) F
         hp = _head_params(H, F, eps, momentum, slope, {
             "u_weight": ptr(p32[0:H]), "u_bias": ptr(p32[H:2 * H]),
             "v_weight": ptr(p32[2 * H:3 * H]), "v_bias": ptr(p32[3 * H:4 * H]),
-            "du_weight": ptr(dp[0].unbind(0)), "du_bias": ptr(dp[1].unbind(0)),
-            "dv_weight": ptr(dp[2].unbind(0)), "dv_bias": ptr(dp[3].unbind(0)),
             "u_running_mean": None, "u_running_var": None, "v_running_mean": None,
-            "v_running_var": None})
+            "v_running_var": None}, dyn={
+            name: [base + step * (k * H + h) for h in range(H)]
+            for k, name in enumerate(("du_weight", "du_bias", "dv_weight", "dv_bias"))})
         g = graph.desc
-        wsb = int(_lib.load().msha_head_workspace_size(g, H, F))
-        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        ws = _workspace(dev, _memo(graph, ("head_ws", H, F), lambda: int(
+            _lib.fn("msha_head_workspace_size")(g, H, F))))
         shape, adt, adev = ctx.a_meta
         da = torch.empty(shape, dtype=torch.float32, device=adev)  # zeroed by the reduce
         _lib.call("msha_head_bwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
@@ -1294,18 +1351,25 @@ def model_head(graph: Graph, u, v, bns, out_W, out_a, p: float = 0.0, training: 
 
 
 # ------------------------------------------------- parameter packing / feature dropout ---
+_SEG_FMT = struct.Struct("<QQQqqqqqf4xQQii")  # struct msha_segment (checked at import)
+assert _SEG_FMT.size == ctypes.sizeof(_lib.MshaSegment)
+
+
 def _segments(segs, stream):
     """msha_segments launches: segs = [(a, dst, rows, cols, lda, ldd, b, ldb, p, seed
     [, a_dtype, dst_dtype])] (pointers as ints, a / b may be None; dtypes as torch dtypes,
-    fp32 when omitted), MSHA_MAX_SEGMENTS per launch."""
+    fp32 when omitted), MSHA_MAX_SEGMENTS per launch.  The records are packed bytes
+    (one struct.pack_into each) viewed as the ctypes array."""
     for lo in range(0, len(segs), _lib.MAX_SEGMENTS):
         part = segs[lo:lo + _lib.MAX_SEGMENTS]
-        arr = (_lib.MshaSegment * len(part))()
+        buf = bytearray(_SEG_FMT.size * len(part))
         for k, sg in enumerate(part):
             a, dst, rows, cols, lda, ldd, b, ldb, p, seed = sg[:10]
             adt, ddt = (sg[10], sg[11]) if len(sg) > 10 else (torch.float32, torch.float32)
-            arr[k] = _lib.MshaSegment(a, b, dst, rows, cols, lda, ldb, ldd, p, seed, 0,
-                                      _code(adt), _code(ddt))
+            _SEG_FMT.pack_into(buf, k * _SEG_FMT.size, a or 0, b or 0, dst, rows, cols, lda,
+                               ldb, ldd, p, seed, 0, 1 if adt == BF16 else 0,
+                               1 if ddt == BF16 else 0)
+        arr = (_lib.MshaSegment * len(part)).from_buffer(buf)
         _lib.call("msha_segments", len(part), C_byref(arr), stream)
 
 
@@ -1324,6 +1388,41 @@ def _cast_many(pairs, stream):
         _segments(segs, stream)
 
 
+def _fd_fwd(S, R, p, s_seed, r_seed):
+    """Segments + outputs of dropout(S), dropout(R) (one Philox mask each)."""
+    S, R = S.contiguous(), R.contiguous()
+    So, Ro = torch.empty_like(S), torch.empty_like(R)
+    segs = [(S.data_ptr(), So.data_ptr(), S.shape[0], S.shape[1], S.shape[1], S.shape[1],
+             None, 0, p, s_seed, S.dtype, S.dtype),
+            (R.data_ptr(), Ro.data_ptr(), R.shape[0], R.shape[1], R.shape[1], R.shape[1],
+             None, 0, p, r_seed, R.dtype, R.dtype)]
+    return segs, So, Ro
+
+
+def _fd_bwd(leaves, grads, p, seeds, needs):
+    """Segments + gradients of the two feature dropouts (the masks regenerated).  A leaf
+    registered with ``optim.Adam.fuse_dropout_grad`` gets no gradient: its optimizer step
+    reads the output gradient and the mask seed instead."""
+    from .optim import fused_optimizer_of
+
+    segs, outs = [], []
+    for k, (d, seed) in enumerate(zip(grads, seeds)):
+        leaf = leaves[k]
+        opt = fused_optimizer_of(leaf) if d is not None else None
+        if opt is not None and needs[k]:
+            opt.stash_dropout_grad(leaf, d, p, seed)
+            d = None
+        if d is None:
+            outs.append(None)
+            continue
+        d = d.contiguous()
+        g = torch.empty_like(d)
+        segs.append((d.data_ptr(), g.data_ptr(), d.shape[0], d.shape[1], d.shape[1],
+                     d.shape[1], None, 0, p, seed, d.dtype, d.dtype))
+        outs.append(g)
+    return segs, outs
+
+
 class _FeatureDropout(torch.autograd.Function):
     """dropout(Sfeatures), dropout(Rfeatures) (Ablation.py:296-297, Ours.py:161-162) in one
     launch; the backward regenerates both Philox masks in one launch.  A table registered
@@ -1333,35 +1432,14 @@ class _FeatureDropout(torch.autograd.Function):
     @staticmethod
     def forward(ctx, S, R, p, s_seed, r_seed):
         ctx.params = (S, R)  # the leaves themselves (a fused optimizer updates them)
-        S, R = S.contiguous(), R.contiguous()
-        So, Ro = torch.empty_like(S), torch.empty_like(R)
-        _segments([(S.data_ptr(), So.data_ptr(), S.shape[0], S.shape[1], S.shape[1], S.shape[1],
-                    None, 0, p, s_seed, S.dtype, S.dtype),
-                   (R.data_ptr(), Ro.data_ptr(), R.shape[0], R.shape[1], R.shape[1], R.shape[1],
-                    None, 0, p, r_seed, R.dtype, R.dtype)], _stream(S))
+        segs, So, Ro = _fd_fwd(S, R, p, s_seed, r_seed)
+        _segments(segs, _stream(S))
         ctx.p, ctx.seeds = p, (s_seed, r_seed)
         return So, Ro
 
     @staticmethod
     def backward(ctx, dSo, dRo):
-        from .optim import fused_optimizer_of
-
-        segs, outs = [], []
-        for k, (d, seed) in enumerate(((dSo, ctx.seeds[0]), (dRo, ctx.seeds[1]))):
-            leaf = ctx.params[k]
-            opt = fused_optimizer_of(leaf) if d is not None else None
-            if opt is not None and ctx.needs_input_grad[k]:
-                # no gradient tensor for this leaf: its optimizer step reads d + the mask
-                opt.stash_dropout_grad(leaf, d, ctx.p, seed)
-                d = None
-            if d is None:
-                outs.append(None)
-                continue
-            d = d.contiguous()
-            g = torch.empty_like(d)
-            segs.append((d.data_ptr(), g.data_ptr(), d.shape[0], d.shape[1], d.shape[1],
-                         d.shape[1], None, 0, ctx.p, seed, d.dtype, d.dtype))
-            outs.append(g)
+        segs, outs = _fd_bwd(ctx.params, (dSo, dRo), ctx.p, ctx.seeds, ctx.needs_input_grad)
         if segs:
             _segments(segs, _stream(outs[0] if outs[0] is not None else outs[1]))
         return outs[0], outs[1], None, None, None
@@ -1373,12 +1451,92 @@ def feature_dropout(S, R, p: float, training: bool):
     outputs rounded once from the fp32 product), F.dropout otherwise."""
     if not training or p <= 0:
         return S, R
-    ok = (torch.float32, BF16)
-    if S.dtype not in ok or R.dtype not in ok or S.dim() != 2 or R.dim() != 2:
+    if not _fd_ok(S, R):
         return (torch.nn.functional.dropout(S, p, training=True),
                 torch.nn.functional.dropout(R, p, training=True))
     _lib.require_cuda(S, R)
     return _FeatureDropout.apply(S, R, float(p), new_seed(), new_seed())
+
+
+def _fd_ok(S, R):
+    ok = (torch.float32, BF16)
+    return S.dtype in ok and R.dtype in ok and S.dim() == 2 and R.dim() == 2
+
+
+def _ph_fwd(H, intra, params):
+    """Segments + outputs of the head packing: W1 / W2 (K, H*F) in the parameters' dtype,
+    a_r / a_l (H, F) fp32 [, a3s, a4s = a3[:F] + a3[F:], a4[:F] + a4[F:]]."""
+    W1s, W2s, As = params[:H], params[H:2 * H], params[2 * H:3 * H]
+    K, Fd = W1s[0].shape
+    dev = W1s[0].device
+    pdt = W1s[0].dtype
+    es = W1s[0].element_size()
+    W1 = torch.empty(K, H * Fd, device=dev, dtype=pdt)
+    W2 = torch.empty(K, H * Fd, device=dev, dtype=pdt)
+    ar = torch.empty(H, Fd, device=dev)
+    al = torch.empty(H, Fd, device=dev)
+    outs = [W1, W2, ar, al]
+    f32 = torch.float32
+    segs = []
+    w1p, w2p, arp, alp = W1.data_ptr(), W2.data_ptr(), ar.data_ptr(), al.data_ptr()
+    for h in range(H):
+        segs.append((W1s[h].data_ptr(), w1p + es * h * Fd, K, Fd, Fd, H * Fd, None, 0, 0.0, 0,
+                     pdt, pdt))
+        segs.append((W2s[h].data_ptr(), w2p + es * h * Fd, K, Fd, Fd, H * Fd, None, 0, 0.0, 0,
+                     pdt, pdt))
+        pa = As[h].data_ptr()
+        segs.append((pa, arp + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0, pdt, f32))
+        segs.append((pa + es * Fd, alp + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0, pdt, f32))
+    if intra:
+        a3s = torch.empty(H, Fd, device=dev)
+        a4s = torch.empty(H, Fd, device=dev)
+        outs += [a3s, a4s]
+        for h in range(H):
+            for src, dst in ((params[3 * H + h], a3s), (params[4 * H + h], a4s)):
+                pa = src.data_ptr()
+                segs.append((pa, dst.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, pa + es * Fd, Fd,
+                             0.0, 0, pdt, f32))
+    return segs, outs, (H, intra, K, Fd, pdt)
+
+
+def _ph_bwd(meta, dW1, dW2, dar, dal, da3s=None, da4s=None):
+    """Segments + per-head parameter gradients of the head packing (cast to the
+    parameters' dtype); a missing packed gradient writes zeros."""
+    H, intra, K, Fd, pdt = meta
+    some = next(t for t in (dW1, dW2, dar, dal, da3s, da4s) if t is not None)
+    dev = some.device
+    c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+    dW1, dW2, dar, dal, da3s, da4s = map(c, (dW1, dW2, dar, dal, da3s, da4s))
+    # a missing gradient writes zeros (NULL a); its dtype code is then irrelevant
+    dty = lambda t: pdt if t is None else t.dtype  # noqa: E731
+    ptr = lambda t, off=0: None if t is None else t.data_ptr() + off * t.element_size()  # noqa: E731
+    gW1 = [torch.empty(K, Fd, device=dev, dtype=pdt) for _ in range(H)]
+    gW2 = [torch.empty(K, Fd, device=dev, dtype=pdt) for _ in range(H)]
+    gA = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
+    ge = gA[0].element_size()
+    segs = []
+    for h in range(H):
+        o = h * Fd
+        segs.append((ptr(dW1, o), gW1[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0,
+                     dty(dW1), pdt))
+        segs.append((ptr(dW2, o), gW2[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0,
+                     dty(dW2), pdt))
+        segs.append((ptr(dar, o), gA[h].data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                     dty(dar), pdt))
+        segs.append((ptr(dal, o), gA[h].data_ptr() + ge * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                     dty(dal), pdt))
+    g3 = g4 = []
+    if intra:
+        g3 = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
+        g4 = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
+        for h in range(H):
+            o = h * Fd
+            for d, g in ((da3s, g3[h]), (da4s, g4[h])):  # sum backward: both halves
+                segs.append((ptr(d, o), g.data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0,
+                             dty(d), pdt))
+                segs.append((ptr(d, o), g.data_ptr() + ge * Fd, 1, Fd, Fd, Fd, None, 0, 0.0,
+                             0, dty(d), pdt))
+    return segs, [*gW1, *gW2, *gA, *g3, *g4], dev
 
 
 class _PackHeads(torch.autograd.Function):
@@ -1391,78 +1549,26 @@ class _PackHeads(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, H, intra, *params):
-        W1s, W2s, As = params[:H], params[H:2 * H], params[2 * H:3 * H]
-        K, Fd = W1s[0].shape
-        dev = W1s[0].device
-        pdt = W1s[0].dtype
-        es = W1s[0].element_size()
-        W1 = torch.empty(K, H * Fd, device=dev, dtype=pdt)
-        W2 = torch.empty(K, H * Fd, device=dev, dtype=pdt)
-        ar = torch.empty(H, Fd, device=dev)
-        al = torch.empty(H, Fd, device=dev)
-        outs = [W1, W2, ar, al]
-        f32 = torch.float32
-        segs = []
-        for h in range(H):
-            segs.append((W1s[h].data_ptr(), W1.data_ptr() + es * h * Fd, K, Fd, Fd, H * Fd,
-                         None, 0, 0.0, 0, pdt, pdt))
-            segs.append((W2s[h].data_ptr(), W2.data_ptr() + es * h * Fd, K, Fd, Fd, H * Fd,
-                         None, 0, 0.0, 0, pdt, pdt))
-            pa = As[h].data_ptr()
-            segs.append((pa, ar.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0, pdt, f32))
-            segs.append((pa + es * Fd, al.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0,
-                         pdt, f32))
-        if intra:
-            a3s = torch.empty(H, Fd, device=dev)
-            a4s = torch.empty(H, Fd, device=dev)
-            outs += [a3s, a4s]
-            for h in range(H):
-                for src, dst in ((params[3 * H + h], a3s), (params[4 * H + h], a4s)):
-                    pa = src.data_ptr()
-                    segs.append((pa, dst.data_ptr() + 4 * h * Fd, 1, Fd, Fd, Fd, pa + es * Fd, Fd,
-                                 0.0, 0, pdt, f32))
-        _segments(segs, _stream(W1))
-        ctx.H, ctx.intra, ctx.K, ctx.Fd, ctx.pdt = H, intra, K, Fd, pdt
+        segs, outs, ctx.meta = _ph_fwd(H, intra, params)
+        _segments(segs, _stream(outs[0]))
         return tuple(outs)
 
     @staticmethod
-    def backward(ctx, dW1, dW2, dar, dal, da3s=None, da4s=None):
-        H, K, Fd, pdt = ctx.H, ctx.K, ctx.Fd, ctx.pdt
-        dev = (dW1 if dW1 is not None else dW2).device if (dW1 is not None or dW2 is not None) \
-            else dar.device
-        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
-        dW1, dW2, dar, dal, da3s, da4s = map(c, (dW1, dW2, dar, dal, da3s, da4s))
-        # a missing gradient writes zeros (NULL a); its dtype code is then irrelevant
-        dty = lambda t: pdt if t is None else t.dtype  # noqa: E731
-        ptr = lambda t, off=0: None if t is None else t.data_ptr() + off * t.element_size()  # noqa: E731
-        gW1 = [torch.empty(K, Fd, device=dev, dtype=pdt) for _ in range(H)]
-        gW2 = [torch.empty(K, Fd, device=dev, dtype=pdt) for _ in range(H)]
-        gA = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
-        ge = gA[0].element_size()
-        segs = []
-        for h in range(H):
-            o = h * Fd
-            segs.append((ptr(dW1, o), gW1[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0,
-                         dty(dW1), pdt))
-            segs.append((ptr(dW2, o), gW2[h].data_ptr(), K, Fd, H * Fd, Fd, None, 0, 0.0, 0,
-                         dty(dW2), pdt))
-            segs.append((ptr(dar, o), gA[h].data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0,
-                         dty(dar), pdt))
-            segs.append((ptr(dal, o), gA[h].data_ptr() + ge * Fd, 1, Fd, Fd, Fd, None, 0, 0.0, 0,
-                         dty(dal), pdt))
-        g3 = g4 = []
-        if ctx.intra:
-            g3 = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
-            g4 = [torch.empty(2 * Fd, 1, device=dev, dtype=pdt) for _ in range(H)]
-            for h in range(H):
-                o = h * Fd
-                for d, g in ((da3s, g3[h]), (da4s, g4[h])):  # sum backward: both halves
-                    segs.append((ptr(d, o), g.data_ptr(), 1, Fd, Fd, Fd, None, 0, 0.0, 0,
-                                 dty(d), pdt))
-                    segs.append((ptr(d, o), g.data_ptr() + ge * Fd, 1, Fd, Fd, Fd, None, 0, 0.0,
-                                 0, dty(d), pdt))
+    def backward(ctx, *grads):
+        segs, gs, dev = _ph_bwd(ctx.meta, *grads)
         _segments(segs, _lib.stream_handle(dev))
-        return (None, None, *gW1, *gW2, *gA, *g3, *g4)
+        return (None, None, *gs)
+
+
+def _pack_params(heads, intra):
+    names = ["W1", "W2", "a"] + (["a3", "a4"] if intra else [])
+    return [getattr(h, n) for n in names for h in heads]
+
+
+def _ph_ok(H, params):
+    pdt = params[0].dtype
+    return H <= 4 and pdt in (torch.float32, BF16) and all(
+        p.dtype == pdt and p.is_contiguous() and p.is_cuda for p in params)
 
 
 def pack_heads(heads, intra: bool):
@@ -1470,13 +1576,52 @@ def pack_heads(heads, intra: bool):
     None when the one-launch packing does not apply (mixed or non-fp32/bf16 dtypes,
     non-contiguous parameters, more than 4 heads)."""
     H = len(heads)
-    names = ["W1", "W2", "a"] + (["a3", "a4"] if intra else [])
-    params = [getattr(h, n) for n in names for h in heads]
-    pdt = params[0].dtype
-    if H > 4 or pdt not in (torch.float32, BF16) or any(
-            p.dtype != pdt or not p.is_contiguous() or not p.is_cuda for p in params):
+    params = _pack_params(heads, intra)
+    if not _ph_ok(H, params):
         return None
     return _PackHeads.apply(H, intra, *params)
+
+
+class _Prologue(torch.autograd.Function):
+    """feature_dropout + pack_heads as ONE launch each way (and one autograd node): the
+    models' step starts with both (Ablation.py:296-297 + :262-267, Ours.py:161-162 +
+    :58-75) and their segments fit one msha_segments batch."""
+
+    @staticmethod
+    def forward(ctx, p, s_seed, r_seed, H, intra, S, R, *params):
+        ctx.leaves = (S, R)
+        fsegs, So, Ro = _fd_fwd(S, R, p, s_seed, r_seed)
+        psegs, outs, ctx.meta = _ph_fwd(H, intra, params)
+        _segments(fsegs + psegs, _stream(So))
+        ctx.p, ctx.seeds = p, (s_seed, r_seed)
+        return (So, Ro, *outs)
+
+    @staticmethod
+    def backward(ctx, dSo, dRo, *dpacked):
+        fsegs, fouts = _fd_bwd(ctx.leaves, (dSo, dRo), ctx.p, ctx.seeds,
+                               ctx.needs_input_grad[5:7])
+        if any(d is not None for d in dpacked):
+            psegs, gs, dev = _ph_bwd(ctx.meta, *dpacked)
+        else:
+            psegs, gs = [], [None] * (len(ctx.needs_input_grad) - 7)
+        if fsegs or psegs:
+            dev = next(t for t in (*fouts, *gs) if t is not None).device
+            _segments(fsegs + psegs, _lib.stream_handle(dev))
+        return (None, None, None, None, None, fouts[0], fouts[1], *gs)
+
+
+def model_prologue(S, R, p: float, training: bool, heads, intra: bool):
+    """(dropout(S), dropout(R), packed heads) -- feature_dropout and pack_heads in one
+    launch each way when both apply (training with dropout, packable heads); otherwise
+    the two separately (packed None where pack_heads does not apply)."""
+    H = len(heads)
+    params = _pack_params(heads, intra)
+    if training and p > 0 and _fd_ok(S, R) and _ph_ok(H, params):
+        _lib.require_cuda(S, R)
+        outs = _Prologue.apply(float(p), new_seed(), new_seed(), H, intra, S, R, *params)
+        return outs[0], outs[1], tuple(outs[2:])
+    s_in, r_in = feature_dropout(S, R, p, training)
+    return s_in, r_in, pack_heads(heads, intra)
 
 
 # ------------------------------------------------------------- loss on gathered rows ---

@@ -204,15 +204,17 @@ def _tail_unfused(model, graph: Graph, u, v):
     return F.log_softmax(x, dim=1)
 
 
-def _attention_uv3(heads, s_input, r_input, graph: Graph, training):
-    """OursLayer3 inter attention of all heads: (u (N, H, F), v (M, H, F))."""
+def _attention_uv3(heads, s_input, r_input, graph: Graph, training, packed=False):
+    """OursLayer3 inter attention of all heads: (u (N, H, F), v (M, H, F)).  ``packed``:
+    the heads' packed parameters when the caller already has them (model_prologue)."""
     H = len(heads)
     Fd = heads[0].out_features
     n, m = s_input.shape[0], r_input.shape[0]
     if graph.n_cols != m or graph.n_rows != n:
         raise ValueError(f"inter_adj is {graph.n_rows}x{graph.n_cols}, features are {n} "
                          f"sources x {m} recipients")
-    packed = MF.pack_heads(heads, intra=False)
+    if packed is False:
+        packed = MF.pack_heads(heads, intra=False)
     if packed is not None:  # one launch (and one in the backward)
         W1, W2, a_r, a_l = packed
     else:
@@ -255,9 +257,11 @@ class ablation3(nn.Module):  # noqa: N801  (reference class name)
 
     def forward(self, inter_adj, city_adj, province_adj, source_index):
         g = _graph(inter_adj)
-        s_input, r_input = MF.feature_dropout(self.Sfeatures, self.Rfeatures, self.dropout,
-                                              self.training)
-        u, v = _attention_uv3(self.attentions, s_input, r_input, g, self.training)
+        # feature dropout + head packing: one launch (and one autograd node) each way
+        s_input, r_input, packed = MF.model_prologue(self.Sfeatures, self.Rfeatures,
+                                                     self.dropout, self.training,
+                                                     self.attentions, intra=False)
+        u, v = _attention_uv3(self.attentions, s_input, r_input, g, self.training, packed)
         if _head_fusable(self.attentions, g, self.training):
             return _model_tail(self, g, u, v)
         return _tail_unfused(self, g, u, v)
@@ -336,7 +340,7 @@ def fused_ours_layer(heads, s_input, r_input, graph: Graph, city_adj, province_a
 
 def _attention_uv(heads, s_input, r_input, graph: Graph, city_adj, province_adj,
                   source_index, training, record=False, Coeff12=None, Coeff3=None,
-                  Coeff4=None):
+                  Coeff4=None, packed=False):
     """OursLayer inter + intra attention of all heads: (u (N, H, F), v (M, H, F))."""
     H = len(heads)
     Fd = heads[0].out_features
@@ -346,7 +350,8 @@ def _attention_uv(heads, s_input, r_input, graph: Graph, city_adj, province_adj,
                          f"sources x {m} recipients")
     groups = groups_for(city_adj, province_adj, s_input.device)
     # e3 = lrelu(cat(h2_b, h2_b) @ a3) = lrelu(h2_b . (a3[:F] + a3[F:]))  (Ours.py:74-75)
-    packed = MF.pack_heads(heads, intra=True)
+    if packed is False:
+        packed = MF.pack_heads(heads, intra=True)
     if packed is not None:  # one launch (and one in the backward)
         W1, W2, a_r, a_l, a3s, a4s = packed
     else:
@@ -426,10 +431,12 @@ class Ours(nn.Module):
     def forward(self, inter_adj, city_adj, province_adj, source_index, record=False,
                 Coeff12=None, Coeff3=None, Coeff4=None):
         g = _graph(inter_adj)
-        s_input, r_input = MF.feature_dropout(self.Sfeatures, self.Rfeatures, self.dropout,
-                                              self.training)
+        s_input, r_input, packed = MF.model_prologue(self.Sfeatures, self.Rfeatures,
+                                                     self.dropout, self.training,
+                                                     self.attentions, intra=True)
         u, v = _attention_uv(self.attentions, s_input, r_input, g, city_adj, province_adj,
-                             source_index, self.training, record, Coeff12, Coeff3, Coeff4)
+                             source_index, self.training, record, Coeff12, Coeff3, Coeff4,
+                             packed)
         if _head_fusable(self.attentions, g, self.training):
             return _model_tail(self, g, u, v)
         return _tail_unfused(self, g, u, v)

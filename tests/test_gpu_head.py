@@ -294,6 +294,40 @@ def test_feature_dropout_masks_and_grad(cuda, msha, dtype):
     assert torch.equal(R.grad, (kR.float() * 6.0).to(dtype))
 
 
+@pytest.mark.parametrize("intra", [False, True])
+def test_model_prologue_matches_separate_launches(cuda, msha, intra):
+    """model_prologue (feature dropout + head packing in one launch each way, one autograd
+    node) == feature_dropout then pack_heads with the same seeds: outputs and every
+    gradient bit-identical (the same segment records, one batch)."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd import layers
+
+    torch.manual_seed(0)
+    cls = layers.OursLayer if intra else layers.OursLayer3
+    heads = [cls(128, 64, 0.5).to(cuda) for _ in range(2)]
+    gen = torch.Generator(device=cuda).manual_seed(5)
+    S = torch.rand(1000, 128, device=cuda, generator=gen).requires_grad_(True)
+    R = torch.rand(32, 128, device=cuda, generator=gen).requires_grad_(True)
+    params = [S, R] + [p for h in heads for p in h.parameters()]
+    torch.manual_seed(11)
+    s1, r1, packed = MF.model_prologue(S, R, 0.5, True, heads, intra)
+    torch.manual_seed(11)
+    s2, r2 = MF.feature_dropout(S, R, 0.5, True)
+    ref = MF.pack_heads(heads, intra)
+    outs1, outs2 = [s1, r1, *packed], [s2, r2, *ref]
+    ws = [torch.randn(t.shape, device=cuda, generator=gen) for t in outs1]
+    for a, b in zip(outs1, outs2):
+        assert torch.equal(a, b)
+    g1 = torch.autograd.grad(sum((t * w).sum() for t, w in zip(outs1, ws)), params,
+                             allow_unused=True)
+    g2 = torch.autograd.grad(sum((t * w).sum() for t, w in zip(outs2, ws)), params,
+                             allow_unused=True)
+    for a, b in zip(g1, g2):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a, b)
+
+
 def test_cast_segments_round_to_nearest_even(cuda, msha):
     """msha_segments as a dtype cast (ABI 8): fp32 -> bf16 rounds like torch's .to(),
     bf16 -> fp32 is exact, strided rows, and several pairs in one launch."""

@@ -166,3 +166,20 @@ def test_from_csr_records_what_the_bipartite_kernels_need(msha):
     assert (g.distinct_cols, g.max_deg) == (False, 2)
     g = Graph.from_csr(np.array([0, 2, 5]), np.array([1, 3, 0, 2, 3]), 4, "cpu")
     assert (g.distinct_cols, g.max_deg) == (True, 3)
+
+
+def test_segment_records_pack_as_the_struct(msha):
+    """_segments' packed records (struct.pack_into) are byte-identical to ctypes
+    MshaSegment records built field by field."""
+    import ctypes
+
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+
+    rec = (0x7f0012345600, 0x7f0012349900, 17, 129, 129, 256, None, 0, 0.5, 2**61 + 3,
+           torch.bfloat16, torch.float32)
+    a, dst, rows, cols, lda, ldd, b, ldb, p, seed, adt, ddt = rec
+    ref = _lib.MshaSegment(a, b, dst, rows, cols, lda, ldb, ldd, p, seed, 0, 1, 0)
+    buf = bytearray(MF._SEG_FMT.size)
+    MF._SEG_FMT.pack_into(buf, 0, a, b or 0, dst, rows, cols, lda, ldb, ldd, p, seed, 0, 1, 0)
+    assert bytes(buf) == ctypes.string_at(ctypes.addressof(ref), ctypes.sizeof(ref))
