@@ -154,20 +154,49 @@ __device__ __forceinline__ void transpose_fill(float* Wl, const float* __restric
   transpose_store<K, N, NT>(Wl, p, tid);
 }
 
-// Line-major k order (PROJ_LINE=1, default): slot i of a lane group g holds the row's
+// Line-major k order (PROJ_LINE=1): slot i of a lane group g holds the row's
 // columns [16 i + 4 g, +4) (fp32) / [32 i + 8 g, +8) (bf16), so one 16-byte load per lane
 // reads 64 contiguous bytes of each of the tile's 16 rows and slots 2j, 2j + 1 -- reloaded
 // together -- complete one 128-byte line.  PROJ_LINE=0: lane group g holds the row's
 // g-th K/4 quarter (every slot load touches 4 lines per row, 16 bytes of each, and a
 // slot-by-slot reload fetched each line from L2 once per slot).  The fp32 W image rows
 // follow the k order; the bf16 image stays [n][k] and only the read offsets move.
+// Measured 1-2 % at C4 / bip1m, and it changes the bf16 projection's summation order
+// (ablation3's bf16 gradient check sits at its reference-bf16 bar): off by default; the
+// fp32 projection runs the split-bf16 form below, whose rows are line-major anyway.
 #ifndef PROJ_LINE
-#define PROJ_LINE 1
+#define PROJ_LINE 0
 #endif
 template <int KL>
 __host__ __device__ constexpr int proj_img_row(int k) {  // fp32 image row of column k
   return PROJ_LINE ? 4 * (4 * (k / 16) + k % 4) + (k % 16) / 4 : 4 * (k % KL) + k / KL;
 }
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+__device__ __forceinline__ Split3 split3(const float (&x)[8]) {
+  Split3 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bf16_t h = (bf16_t)x[e];
+    const float r1 = x[e] - (float)h;
+    const bf16_t m = (bf16_t)r1;
+    const float r2 = r1 - (float)m;
+    r.h[e] = h;
+    r.m[e] = m;
+    r.l[e] = (bf16_t)r2;
+  }
+  return r;
+}
+// fp32 projections on the split-bf16 products (PROJ_X3=1, default; see pair_x3_kernel for
+// the error argument): W is held as three bf16 [n][k] images, each k-chunk of 32 runs six
+// v_mfma_f32_16x16x32_bf16 per column block instead of eight v_mfma_f32_16x16x4_f32, the
+// rows are read line-major (step s of lane group g: columns [32 s + 8 g, +8), two slots
+// per step, reloaded right after the step).  PROJ_X3=0: the exact-fp32 MFMA.
+#ifndef PROJ_X3
+#define PROJ_X3 1
+#endif
 
 // proj_kernel's block: PROJ_WPS waves per SIMD when the resident W and one staging
 // tile per wave fit the 160 KB of LDS, the staging tile narrowed to column halves when
@@ -176,13 +205,19 @@ __host__ __device__ constexpr int proj_img_row(int k) {  // fp32 image row of co
 #ifndef PROJ_WPS
 #define PROJ_WPS 2
 #endif
-template <typename T, int K, int N, int FE>
+template <typename T, int K, int N, int FE, bool SPLIT = false>
 struct ProjStage {
   using G = ProjGeo<T, K, N>;
   static constexpr int kLds = 160 * 1024;
-  static constexpr int bytes(int waves, int sw) { return G::WBYTES + waves * 16 * (sw + 4) * 4 + 8 * N; }
   static constexpr bool HALF_OK = (FE == 0 || FE <= N / 2) && (N / 2) % (16 / (int)sizeof(T)) == 0 &&
                                   64 % ((N / 2) / (16 / (int)sizeof(T))) == 0;
+  // split-bf16 W images (fp32 only, when they fit beside the narrowest staging tiles)
+  static constexpr int XPW = K + 8;                     // bf16 image pitch
+  static constexpr int XIMG = N * XPW;                  // elements per image
+  static constexpr bool X3 = SPLIT && sizeof(T) == 4 && PROJ_X3 &&
+                             3 * XIMG * 2 + 4 * PROJ_WPS * 16 * ((HALF_OK ? N / 2 : N) + 4) * 4 + 8 * N <= kLds;
+  static constexpr int WB = X3 ? 3 * XIMG * 2 : G::WBYTES;  // W image bytes
+  static constexpr int bytes(int waves, int sw) { return WB + waves * 16 * (sw + 4) * 4 + 8 * N; }
   static constexpr int W3 = 4 * PROJ_WPS;
   static constexpr bool FULL3 = bytes(W3, N) <= kLds;
   static constexpr bool HALF3 = !FULL3 && HALF_OK && bytes(W3, N / 2) <= kLds;
@@ -199,18 +234,19 @@ struct ProjStage {
   static_assert(bytes(WAVES, SW) <= kLds, "proj_kernel LDS");
 };
 
-template <typename T, int K, int N, int FE>
-__global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_kernel(
+template <typename T, int K, int N, int FE, bool SPLIT>
+__global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE, SPLIT>::WAVES)) proj_kernel(
     int M, const T* __restrict__ X, const T* __restrict__ W, const float* __restrict__ al,
     const float* __restrict__ ar, T* __restrict__ h, float* __restrict__ el,
     float* __restrict__ er, int H) {
   using G = ProjGeo<T, K, N>;
-  using S = ProjStage<T, K, N, FE>;
+  using S = ProjStage<T, K, N, FE, SPLIT>;
   constexpr int kWaves = S::WAVES;
+  constexpr bool X3 = S::X3;
   // W image | per-wave staging tiles | score vectors al, ar (read in the epilogue)
-  __shared__ __attribute__((aligned(16))) char smem[G::WBYTES + kWaves * S::SBYTES + 8 * N];
+  __shared__ __attribute__((aligned(16))) char smem[S::WB + kWaves * S::SBYTES + 8 * N];
   T* Wl = reinterpret_cast<T*>(smem);
-  float* als = reinterpret_cast<float*>(smem + G::WBYTES + kWaves * S::SBYTES);
+  float* als = reinterpret_cast<float*>(smem + S::WB + kWaves * S::SBYTES);
   float* ars = als + N;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loop control
@@ -218,6 +254,8 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   constexpr uint32_t kSlotB = PROJ_LINE ? 64u : 16u;      // bytes between a lane's slots
   constexpr int kStepK = PROJ_LINE ? 32 : 8;              // bf16 k advance per MFMA step
   static_assert(!PROJ_LINE || G::NLD % 2 == 0, "line-major slots come in pairs");
+  // byte offset of slot i from the lane's base (X3: step i / 2's 32 bytes, two halves)
+  auto slot_b = [&](int i) -> uint32_t { return X3 ? 128u * (i >> 1) + 16u * (i & 1) : kSlotB * i; };
   TL_OPEN(1);  // marks: entry, W resident, per item (start, MFMAs done), exit
 
   // Work items of a wave, in order: whole 16-row tiles gw, gw + nw, ... for the R rounds
@@ -245,7 +283,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   auto tile_off = [&](int t) -> uint32_t {
     const int row = t * 16 + r16;
     return row < M ? (uint32_t)row * (K * (uint32_t)sizeof(T)) +
-                         (uint32_t)(PROJ_LINE ? 16 * g : g * G::KL * (int)sizeof(T))
+                         (uint32_t)(X3 ? 32 * g : PROJ_LINE ? 16 * g : g * G::KL * (int)sizeof(T))
                    : kOOB;
   };
   // ---- W -> LDS once per block.  W's pieces load first, then the first item's rows:
@@ -264,14 +302,29 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
   {
     const uint32_t off = n_items > 0 ? tile_off(item_tile(0)) : kOOB;
 #pragma unroll
-    for (int i = 0; i < G::NLD; ++i) buf[i] = buf_b128(r_x, off + kSlotB * i);
+    for (int i = 0; i < G::NLD; ++i) buf[i] = buf_b128(r_x, off + slot_b(i));
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < wp.IT; ++i) {
     const int idx = tid + 64 * kWaves * i;
     if (!wp.ok(idx)) continue;
-    if constexpr (G::F32) {
+    if constexpr (X3) {  // W[k][4 n4 .. +3] -> the three bf16 images at [n][k]
+      const int k = idx / (N / 4), n4 = idx % (N / 4);
+      const uint32_t e4[4] = {wp.v[i].x, wp.v[i].y, wp.v[i].z, wp.v[i].w};
+      bf16_t* Wx = reinterpret_cast<bf16_t*>(Wl);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = __uint_as_float(e4[j]);
+        const bf16_t hb = (bf16_t)x;
+        const float r1 = x - (float)hb;
+        const bf16_t mb = (bf16_t)r1;
+        const int o = (4 * n4 + j) * S::XPW + k;
+        Wx[o] = hb;
+        Wx[S::XIMG + o] = mb;
+        Wx[2 * S::XIMG + o] = (bf16_t)(r1 - (float)mb);
+      }
+    } else if constexpr (G::F32) {
       const int k = idx / (N / 4), n4 = idx % (N / 4);
       const int kr = proj_img_row<G::KL>(k);
       *reinterpret_cast<uint4*>(reinterpret_cast<float*>(Wl) + kr * G::PW + 4 * n4) = wp.v[i];
@@ -295,7 +348,7 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
     return;
   }
 
-  float* Tw = reinterpret_cast<float*>(smem + G::WBYTES) + w * 16 * S::TPS;
+  float* Tw = reinterpret_cast<float*>(smem + S::WB) + w * 16 * S::TPS;
   // A register i of a tile feeds steps [i SPL, (i + 1) SPL): once they have issued, it is
   // reloaded with the next item's (one register buffer, a whole tile of lead time)
   constexpr int SPL = G::S / G::NLD;
@@ -325,7 +378,62 @@ __global__ void __launch_bounds__((64 * ProjStage<T, K, N, FE>::WAVES)) proj_ker
     f32x4 acc[NBP];
 #pragma unroll
     for (int c = 0; c < NBP; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (G::F32) {
+    if constexpr (X3) {
+      constexpr int XI = S::XIMG;
+      const bf16_t* Wb = reinterpret_cast<const bf16_t*>(Wl) + (r16 + cb0 * 16) * S::XPW + 8 * g;
+      // the six products of a column block, small terms first
+      auto six = [&](f32x4& ac, const Split3& a, const bf16_t* wc) {
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(wc);
+        const bf16x8 mb = *reinterpret_cast<const bf16x8*>(wc + XI);
+        const bf16x8 lb = *reinterpret_cast<const bf16x8*>(wc + 2 * XI);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, hb, ac, 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, lb, ac, 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, mb, ac, 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, mb, ac, 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, hb, ac, 0, 0, 0);
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, hb, ac, 0, 0, 0);
+      };
+#pragma unroll
+      for (int st = 0; st < K / 32; ++st) {
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = __uint_as_float(cur[2 * st][e]);
+          x[4 + e] = __uint_as_float(cur[2 * st + 1][e]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        cur[2 * st] = buf_b128(r_x, noff + slot_b(2 * st));  // both slots free: next item's
+        cur[2 * st + 1] = buf_b128(r_x, noff + slot_b(2 * st + 1));
+        __builtin_amdgcn_sched_barrier(0);
+        const Split3 a = split3(x);
+        const bf16_t* ws = Wb + 32 * st;
+        // column blocks in pairs: a block's dependent MFMAs alternate with its partner's
+#pragma unroll
+        for (int c = 0; c + 1 < NBP; c += 2) {
+          const bf16_t* w0 = ws + c * 16 * S::XPW;
+          const bf16_t* w1 = w0 + 16 * S::XPW;
+          const bf16x8 h0 = *reinterpret_cast<const bf16x8*>(w0);
+          const bf16x8 h1 = *reinterpret_cast<const bf16x8*>(w1);
+          const bf16x8 m0 = *reinterpret_cast<const bf16x8*>(w0 + XI);
+          const bf16x8 m1 = *reinterpret_cast<const bf16x8*>(w1 + XI);
+          const bf16x8 l0 = *reinterpret_cast<const bf16x8*>(w0 + 2 * XI);
+          const bf16x8 l1 = *reinterpret_cast<const bf16x8*>(w1 + 2 * XI);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, h0, acc[c], 0, 0, 0);
+          acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, h1, acc[c + 1], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, l0, acc[c], 0, 0, 0);
+          acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, l1, acc[c + 1], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, m0, acc[c], 0, 0, 0);
+          acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, m1, acc[c + 1], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, m0, acc[c], 0, 0, 0);
+          acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, m1, acc[c + 1], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, h0, acc[c], 0, 0, 0);
+          acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, h1, acc[c + 1], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, h0, acc[c], 0, 0, 0);
+          acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, h1, acc[c + 1], 0, 0, 0);
+        }
+        if constexpr (NBP % 2 == 1) six(acc[NBP - 1], a, ws + (NBP - 1) * 16 * S::XPW);
+      }
+    } else if constexpr (G::F32) {
       const float* Wf = reinterpret_cast<const float*>(Wl) + g * G::PW + r16 + cb0 * 16;
       float bc[NBP], bn[NBP];
 #pragma unroll
@@ -747,6 +855,189 @@ __global__ void __launch_bounds__(256 * WPS) pair_roll_kernel(
   for (int t = gw; t < tiles; t += nw) {
     // the next tile's row offsets (its indices were loaded one tile ago), then the
     // indices of the tile after it
+    const uint32_t oa = offset_a(xa), ob = offset_b(xb);
+    load_idx(t + 2 * nw, xa, xb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_tile(t, ci, cj, oa, ob);
+  }
+}
+
+// ------------------------------------------- fp32 pair scorer on split bf16 MFMA ---
+// The same resident-W rolling-row structure with the fp32 products computed on the bf16
+// matrix pipe (16x the fp32 MFMA rate): every fp32 operand is split into three bf16
+// terms, x = x_h + x_m + x_l (x_h = bf16(x), x_m = bf16(x - x_h), x_l = bf16(x - x_h -
+// x_m); both subtractions exact in fp32, |x - sum| <= 2^-27 |x|), and each k-chunk runs
+// the six products whose weight reaches fp32's 2^-24: hh, hm, mh, mm, hl, lh (the dropped
+// ml, lm, ll are <= 2^-26 |x w| each).  Each bf16 x bf16 product is exact in fp32 and the
+// MFMA accumulates in fp32, so a score carries fp32-level error (the same order as the
+// exact-fp32 MFMA's; tests/test_gpu_kernels.py holds both kernels to 1e-5 of fp64).
+// Cost per 32-wide k-chunk and 16 x 16 block: 6 x 16 cycles on the bf16 pipe against
+// 8 x 32 cycles of v_mfma_f32_16x16x4_f32.  The hadamard x_i * x_j is rounded to fp32
+// first (the reference's fp32 product), then split.  W is split once into three bf16
+// [n][k] images (3 x 34 KB at K = N = 128).  Rows: line-major, step s of lane group g
+// reads columns [32 s + 8 g, +8) -- 32 contiguous bytes, a full 128-byte line per row
+// per step -- and both of a step's slots are reloaded with the next tile's rows right
+// after that step's MFMAs.
+#ifndef PAIR_X3_WPS
+#define PAIR_X3_WPS 3
+#endif
+template <int K, int N>
+struct X3Geo {
+  static constexpr int NB = N / 16;    // 16-column MFMA blocks
+  static constexpr int S = K / 32;     // k-chunks (MFMA steps)
+  static constexpr int PW = K + 8;     // image pitch (bf16 elements)
+  static constexpr int IMG = N * PW;   // elements per image
+  static_assert(K % 64 == 0 && N % 32 == 0 && K <= 128 && N <= 128, "x3 pair shape");
+};
+template <int K, int N, int WPS>
+__global__ void __launch_bounds__(256 * WPS) pair_x3_kernel(
+    int M, const float* __restrict__ G, int64_t ldg, const int64_t* __restrict__ gi,
+    const float* __restrict__ G2, int64_t ldg2, const int64_t* __restrict__ gj,
+    const float* __restrict__ Wlin, const float* __restrict__ bias, int act, Dropout dp,
+    float* __restrict__ out, uint32_t bytes_a, uint32_t bytes_b) {
+  using Gx = X3Geo<K, N>;
+  constexpr int kWaves = 4 * WPS;
+  __shared__ __attribute__((aligned(16))) bf16_t Wl[3 * Gx::IMG];  // hi | mid | lo
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+
+  {  // W (N, K) row-major fp32 -> three bf16 [n][k] images
+    WPieces<K, N, 64 * kWaves> p;
+    p.load(Wlin, tid);
+#pragma unroll
+    for (int i = 0; i < p.IT; ++i) {
+      const int idx = tid + 64 * kWaves * i;
+      if (p.ok(idx)) {
+        const int n = idx / (K / 4), k4 = idx % (K / 4);
+        const float x[4] = {__uint_as_float(p.v[i].x), __uint_as_float(p.v[i].y),
+                            __uint_as_float(p.v[i].z), __uint_as_float(p.v[i].w)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16_t h = (bf16_t)x[j];
+          const float r1 = x[j] - (float)h;
+          const bf16_t m = (bf16_t)r1;
+          const int o = n * Gx::PW + 4 * k4 + j;
+          Wl[o] = h;
+          Wl[Gx::IMG + o] = m;
+          Wl[2 * Gx::IMG + o] = (bf16_t)(r1 - (float)m);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  float bv[Gx::NB];
+#pragma unroll
+  for (int c = 0; c < Gx::NB; ++c) bv[c] = (act & SK_BIAS) ? bias[c * 16 + r16] : 0.f;
+  const uint64_t doff = (act & SK_DROPOUT) ? dropout_offset(dp, dp.offset) : 0;
+
+  const int nblk = gridDim.x;
+  const int gw = (w >> 2) * (nblk * 4) + blockIdx.x * 4 + (w & 3);
+  const int nw = nblk * kWaves;
+  const int tiles = (M + 15) / 16;
+  if (gw >= tiles) return;
+
+  // (G / G2 non-null, host-checked: a null test would put the descriptors in VGPRs)
+  const rsrc_t r_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G), 0, bytes_a, 0x00020000);
+  const rsrc_t r_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G2), 0, bytes_b, 0x00020000);
+  auto load_idx = [&](int t, int64_t& a, int64_t& b) {
+    const int row = min(t * 16 + r16, M - 1);
+    a = gi[row];
+    b = gj[row];
+  };
+  // this lane's first 8 columns of each row (index outside [0, 2^31): past the window;
+  // the test keeps the index's high word live, see pair_roll_kernel)
+  auto offset_a = [&](int64_t a) -> uint32_t {
+    return (a >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((a * ldg + 8 * g) * 4);
+  };
+  auto offset_b = [&](int64_t b) -> uint32_t {
+    return (b >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((b * ldg2 + 8 * g) * 4);
+  };
+  // slot 2 s + j: step s's columns [32 s + 8 g + 4 j, +4) at byte 128 s + 16 j
+  auto slot_off = [](int i) -> uint32_t { return 128u * (i >> 1) + 16u * (i & 1); };
+  constexpr int NS = 2 * Gx::S;  // 16-byte slots per lane and row
+  auto mfma_tile = [&](int t, u32x4_t* ci, u32x4_t* cj, uint32_t na, uint32_t nb) {
+    f32x4 acc[Gx::NB];
+#pragma unroll
+    for (int c = 0; c < Gx::NB; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* Wb = Wl + r16 * Gx::PW + 8 * g;
+#pragma unroll
+    for (int s = 0; s < Gx::S; ++s) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[e] = __uint_as_float(ci[2 * s][e]) * __uint_as_float(cj[2 * s][e]);
+        x[4 + e] = __uint_as_float(ci[2 * s + 1][e]) * __uint_as_float(cj[2 * s + 1][e]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // both of this step's slots are free: the next tile's rows go out now
+      ci[2 * s] = buf_b128(r_a, na + slot_off(2 * s));
+      ci[2 * s + 1] = buf_b128(r_a, na + slot_off(2 * s + 1));
+      cj[2 * s] = buf_b128(r_b, nb + slot_off(2 * s));
+      cj[2 * s + 1] = buf_b128(r_b, nb + slot_off(2 * s + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      const Split3 a = split3(x);
+      // column blocks in pairs (dependent MFMAs two apart); per pair the B terms in the
+      // order h (hh, mh, lh), m (hm, mm), l (hl)
+#pragma unroll
+      for (int c = 0; c < Gx::NB; c += 2) {
+        const bf16_t* w0 = Wb + c * 16 * Gx::PW + 32 * s;
+        const bf16_t* w1 = w0 + 16 * Gx::PW;
+        const bf16x8 h0 = *reinterpret_cast<const bf16x8*>(w0);
+        const bf16x8 h1 = *reinterpret_cast<const bf16x8*>(w1);
+        const bf16x8 m0 = *reinterpret_cast<const bf16x8*>(w0 + Gx::IMG);
+        const bf16x8 m1 = *reinterpret_cast<const bf16x8*>(w1 + Gx::IMG);
+        const bf16x8 l0 = *reinterpret_cast<const bf16x8*>(w0 + 2 * Gx::IMG);
+        const bf16x8 l1 = *reinterpret_cast<const bf16x8*>(w1 + 2 * Gx::IMG);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, h0, acc[c], 0, 0, 0);
+        acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, h1, acc[c + 1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, l0, acc[c], 0, 0, 0);
+        acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, l1, acc[c + 1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, m0, acc[c], 0, 0, 0);
+        acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, m1, acc[c + 1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, m0, acc[c], 0, 0, 0);
+        acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, m1, acc[c + 1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, h0, acc[c], 0, 0, 0);
+        acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, h1, acc[c + 1], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, h0, acc[c], 0, 0, 0);
+        acc[c + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, h1, acc[c + 1], 0, 0, 0);
+      }
+    }
+    // ---- epilogue on the C layout: element (row t 16 + 4 g + i, column 16 c + r16)
+    const int rows = min(16, M - t * 16);
+    const rsrc_t r_o = make_rsrc(out + (int64_t)t * 16 * N, (uint32_t)(rows * N * 4));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = t * 16 + 4 * g + i;
+#pragma unroll
+      for (int c = 0; c < Gx::NB; ++c) {
+        float x = acc[c][i] + bv[c];
+        if (act & SK_RELU) x = fmaxf(x, 0.f);
+        if (act & SK_DROPOUT)
+          x *= philox_x(dp.seed, doff, (uint64_t)row * N + c * 16 + r16) >= dp.threshold
+                   ? dp.scale
+                   : 0.f;
+        if (act & SK_SIGMOID) x = 1.f / (1.f + __expf(-x));
+        buf_store_f32(r_o, (uint32_t)(((4 * g + i) * N + c * 16 + r16) * 4), x);
+      }
+    }
+  };
+
+  u32x4_t ci[NS], cj[NS];
+  int64_t xa, xb;
+  load_idx(gw, xa, xb);
+  {
+    const uint32_t oa = offset_a(xa), ob = offset_b(xb);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      ci[i] = buf_b128(r_a, oa + slot_off(i));
+      cj[i] = buf_b128(r_b, ob + slot_off(i));
+      if (i & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  load_idx(gw + nw, xa, xb);
+  for (int t = gw; t < tiles; t += nw) {
     const uint32_t oa = offset_a(xa), ob = offset_b(xb);
     load_idx(t + 2 * nw, xa, xb);
     __builtin_amdgcn_sched_barrier(0);
@@ -1346,10 +1637,22 @@ int skinny_project(int64_t M, int64_t K, int heads, int feat, const void* X, con
   const bool score = al != nullptr || ar != nullptr;
   const int minfe = 16 / (int)sizeof(T);
   if (score && (feat < minfe || N % feat != 0)) return 0;
+  // fp32: the split-bf16 form from 64k rows (1M rows: 292 vs 368 us, C4's 100k: 36.6 vs
+  // 39.4 us); below it the three-image W fill outweighs the faster steps (R15's 39k rows:
+  // 24.9 vs 20.8 us), so the exact-fp32 MFMA runs there
+  constexpr bool kF32 = std::is_same<T, float>::value;
+  const bool split = kF32 && M >= 65536;
 #define SKP(k, n, fe)                                                                           \
   if (K == k && N == n && (score ? feat == fe : fe == 0)) {                                    \
-    constexpr int wv = sk::ProjStage<T, k, n, fe>::WAVES;                                      \
-    hipLaunchKernelGGL((sk::proj_kernel<T, k, n, fe>), dim3(proj_grid(M, wv)), dim3(64 * wv),  \
+    if (split) {                                                                                \
+      constexpr int wv = sk::ProjStage<T, k, n, fe, kF32>::WAVES;                               \
+      hipLaunchKernelGGL((sk::proj_kernel<T, k, n, fe, kF32>), dim3(proj_grid(M, wv)),         \
+                         dim3(64 * wv), 0, s, (int)M, (const T*)X, (const T*)W, al, ar, (T*)h,  \
+                         el, er, heads);                                                        \
+      return 1;                                                                                 \
+    }                                                                                           \
+    constexpr int wv = sk::ProjStage<T, k, n, fe, false>::WAVES;                                \
+    hipLaunchKernelGGL((sk::proj_kernel<T, k, n, fe, false>), dim3(proj_grid(M, wv)), dim3(64 * wv), \
                        0, s, (int)M, (const T*)X, (const T*)W, al, ar, (T*)h, el, er, heads);   \
     return 1;                                                                                   \
   }
@@ -1378,9 +1681,11 @@ int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t 
   if (G2 == nullptr) { G2 = G; ldg2 = ldg; g2_rows = g_rows; }
   if (ldg % 4 || ldg2 % 4 || (((uintptr_t)G | (uintptr_t)G2 | (uintptr_t)out | (uintptr_t)W) & 15))
     return 0;
-  static const int roll_env = [] {  // MSHA_PAIR_ROLL=0: always the two-register-set pair_kernel
+  // MSHA_PAIR_ROLL: 2 (default) split-bf16 pair_x3_kernel, 1 the exact-fp32 rolling
+  // pair_roll_kernel, 0 always the two-register-set pair_kernel
+  static const int roll_env = [] {
     const char* v = getenv("MSHA_PAIR_ROLL");
-    return v != nullptr && *v ? atoi(v) : 1;
+    return v != nullptr && *v ? atoi(v) : 2;
   }();
   // table bytes up to the last row's K columns (the kernel reads no further)
   auto span = [&](int64_t rows, int64_t ld) -> int64_t { return rows > 0 ? ((rows - 1) * ld + K) * 4 : -1; };
@@ -1388,11 +1693,16 @@ int skinny_pair_linear(int64_t P, int64_t K, int64_t N, const float* G, int64_t 
   const bool roll = roll_env && ba > 0 && bb > 0 && ba <= 0xFFFFFFFFll && bb <= 0xFFFFFFFFll &&
                     P * N * 4 < (1ll << 31);
   const dim3 grid(proj_grid(P)), block(64 * sk::kProjWaves);
-  constexpr int rw = 4 * PAIR32_WPS;
+  constexpr int rw = 4 * PAIR32_WPS, xw = 4 * PAIR_X3_WPS;
   const dim3 rgrid(proj_grid(P, rw)), rblock(64 * rw);
+  const dim3 xgrid(proj_grid(P, xw)), xblock(64 * xw);
 #define SKPL(k, n)                                                                              \
   if (K == k && N == n) {                                                                       \
-    if (roll)                                                                                   \
+    if (roll && roll_env == 2)                                                                  \
+      hipLaunchKernelGGL((sk::pair_x3_kernel<k, n, PAIR_X3_WPS>), xgrid, xblock, 0, s, (int)P,  \
+                         G, ldg, gi, G2, ldg2, gj, W, bias, act, dp, out, (uint32_t)ba,         \
+                         (uint32_t)bb);                                                         \
+    else if (roll)                                                                              \
       hipLaunchKernelGGL((sk::pair_roll_kernel<k, n, PAIR32_WPS>), rgrid, rblock, 0, s, (int)P, \
                          G, ldg, gi, G2, ldg2, gj, W, bias, act, dp, out, (uint32_t)ba,         \
                          (uint32_t)bb);                                                         \
