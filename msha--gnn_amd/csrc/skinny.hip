@@ -214,11 +214,13 @@ struct ProjStage {
   // split-bf16 W images (fp32 only, when they fit beside the narrowest staging tiles)
   static constexpr int XPW = K + 8;                     // bf16 image pitch
   static constexpr int XIMG = N * XPW;                  // elements per image
+  // the split form runs 3 waves per SIMD (C4 34.2 vs 36.4 us, 1M rows 264 vs 279 us at 2);
+  // the exact-fp32 and bf16 forms PROJ_WPS (R15 fp32: 20.5 us at 2, 23.3 at 3)
   static constexpr bool X3 = SPLIT && sizeof(T) == 4 && PROJ_X3 &&
-                             3 * XIMG * 2 + 4 * PROJ_WPS * 16 * ((HALF_OK ? N / 2 : N) + 4) * 4 + 8 * N <= kLds;
+                             3 * XIMG * 2 + 12 * 16 * ((HALF_OK ? N / 2 : N) + 4) * 4 + 8 * N <= kLds;
   static constexpr int WB = X3 ? 3 * XIMG * 2 : G::WBYTES;  // W image bytes
   static constexpr int bytes(int waves, int sw) { return WB + waves * 16 * (sw + 4) * 4 + 8 * N; }
-  static constexpr int W3 = 4 * PROJ_WPS;
+  static constexpr int W3 = 4 * (X3 ? 3 : PROJ_WPS);
   static constexpr bool FULL3 = bytes(W3, N) <= kLds;
   static constexpr bool HALF3 = !FULL3 && HALF_OK && bytes(W3, N / 2) <= kLds;
   static constexpr int WAVES = FULL3 || HALF3 ? W3 : kProjWaves;
