@@ -295,9 +295,31 @@ __global__ void __launch_bounds__(64 * kOursFwdWaves) ours_fwd_lds_kernel(OursAr
   const int B = (int)a.B;
   float* w3s = sx + B * D;
   float* w4s = w3s + B * H;
-  for (int b = wv; b < B; b += kOursFwdWaves) {
-    const int64_t ib = a.src[b];
-    for (int d = lane; d < D; d += 64) sx[b * D + d] = ldt<T>(a.h2, ib * D + d);
+  {  // every row this wave stages, loads first: one gather latency, not one per row
+    constexpr int RPW = 64 / kOursFwdWaves;  // B <= 64
+    int64_t ib[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int b = wv + kOursFwdWaves * r;
+      ib[r] = b < B ? a.src[b] : 0;
+    }
+    float xv[RPW][KD];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        xv[r][k] = d < D ? ldt<T>(a.h2, ib[r] * D + d) : 0.f;
+      }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int b = wv + kOursFwdWaves * r;
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        if (b < B && d < D) sx[b * D + d] = xv[r][k];
+      }
+    }
   }
   for (int i = threadIdx.x; i < B * H; i += 64 * kOursFwdWaves) {
     w3s[i] = bstat[(int64_t)i * BS_N + BS_W3];
@@ -341,22 +363,41 @@ __global__ void __launch_bounds__(64 * kOursFwdWaves) ours_fwd_lds_kernel(OursAr
       uint64_t bal = kind == 0 ? bal3 : bal4;
       const uint32_t kbk = kind == 0 ? kb3 : kb4;
       const float* ws = kind == 0 ? w3s : w4s;
+      // matches two at a time: both matches' LDS reads leave before the first fma (the
+      // sums stay in bit order); the keep bits come by readlane (the match index is
+      // wave-uniform), not a bpermute round trip through LDS
       while (bal) {
-        const int bit = __ffsll((long long)bal) - 1;
+        const int bit0 = __ffsll((long long)bal) - 1;
         bal &= bal - 1;
-        const uint32_t kbits = __shfl(kbk, bit);
+        const bool two = bal != 0;
+        const int bit1 = two ? __ffsll((long long)bal) - 1 : bit0;
+        if (two) bal &= bal - 1;
+        const int bits[2] = {bit0, bit1};
+        float wv2[2][KD], xv2[2][KD];
 #pragma unroll
-        for (int k = 0; k < KD; ++k) {
-          const int d = min(lane + 64 * k, D - 1);
-          const int h = hk[k];
-          float drop = 1.f;
-          if (a.dp.active)
-            drop = h < 32 ? (((kbits >> h) & 1u) ? a.dp.scale : 0.f)
-                          : intra_drop(a.dp, kind, h, (uint64_t)bit * a.N + n);
-          const float w = ws[bit * H + h] * drop;
-          const float x = sx[bit * D + d];
-          if (kind == 0) acc3[k] = fmaf(w, x, acc3[k]);
-          else acc4[k] = fmaf(w, x, acc4[k]);
+        for (int q = 0; q < 2; ++q) {
+          const int bit = bits[q];
+          const uint32_t kbits = __builtin_amdgcn_readlane(kbk, bit);
+#pragma unroll
+          for (int k = 0; k < KD; ++k) {
+            const int d = min(lane + 64 * k, D - 1);
+            const int h = hk[k];
+            float drop = 1.f;
+            if (a.dp.active)
+              drop = h < 32 ? (((kbits >> h) & 1u) ? a.dp.scale : 0.f)
+                            : intra_drop(a.dp, kind, h, (uint64_t)bit * a.N + n);
+            wv2[q][k] = ws[bit * H + h] * drop;
+            xv2[q][k] = sx[bit * D + d];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (q == 1 && !two) break;
+#pragma unroll
+          for (int k = 0; k < KD; ++k) {
+            if (kind == 0) acc3[k] = fmaf(wv2[q][k], xv2[q][k], acc3[k]);
+            else acc4[k] = fmaf(wv2[q][k], xv2[q][k], acc4[k]);
+          }
         }
       }
     }

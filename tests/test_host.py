@@ -183,3 +183,60 @@ def test_segment_records_pack_as_the_struct(msha):
     buf = bytearray(MF._SEG_FMT.size)
     MF._SEG_FMT.pack_into(buf, 0, a, b or 0, dst, rows, cols, lda, ldb, ldd, p, seed, 0, 1, 0)
     assert bytes(buf) == ctypes.string_at(ctypes.addressof(ref), ctypes.sizeof(ref))
+
+
+def _bf16(x):
+    """Round fp32 -> bf16 (round to nearest even), returned as fp32 (numpy emulation of
+    v_cvt_pk_bf16_f32 for finite values)."""
+    import numpy as np
+
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def test_split_bf16_products_reach_fp32_accuracy():
+    """The split-bf16 fp32 GEMM scheme of skinny.hip (pair_x3_kernel, the split proj_kernel):
+    x = x_h + x_m + x_l with x_h = bf16(x), x_m = bf16(x - x_h), x_l = bf16(x - x_h - x_m);
+    the six products hh, hm, mh, mm, hl, lh summed in fp32 give each product within a few
+    fp32 ulps, and a 128-term dot within the fp32 forward-error bound of the exact-fp32
+    MFMA (n 2^-24 sum|x w|)."""
+    import numpy as np
+
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(200000) * np.exp(rng.uniform(-8, 8, 200000))).astype(np.float32)
+    w = (rng.standard_normal(200000) * np.exp(rng.uniform(-8, 8, 200000))).astype(np.float32)
+
+    def split(a):
+        h = _bf16(a)
+        r1 = (a - h).astype(np.float32)  # exact in fp32
+        m = _bf16(r1)
+        r2 = (r1 - m).astype(np.float32)  # exact in fp32
+        return h, m, _bf16(r2)
+
+    xh, xm, xl = split(x)
+    wh, wm, wl = split(w)
+    # the three terms carry x to 2^-27 of |x| (fp32 has 24 bits)
+    assert np.all(np.abs((xh.astype(np.float64) + xm + xl) - x) <= 2.0 ** -26 * np.abs(x))
+    # each bf16 x bf16 product is exact in fp32
+    for a, b in ((xh, wh), (xm, wl), (xl, wm)):
+        assert np.array_equal((a * b).astype(np.float64), a.astype(np.float64) * b)
+    # six products (small terms first, as the kernels order them), fp32 accumulation
+    terms = (xl * wh, xh * wl, xm * wm, xh * wm, xm * wh, xh * wh)
+    acc = np.zeros_like(x)
+    for t in terms:
+        acc = (acc + t).astype(np.float32)
+    exact = x.astype(np.float64) * w.astype(np.float64)
+    rel = np.abs(acc - exact) / np.abs(exact)
+    assert rel.max() <= 2.0 ** -21, rel.max()  # a few fp32 ulps (the dropped ml, lm, ll)
+    # a 128-term dot product: within the exact-fp32 MFMA's error bound
+    X = x[:128 * 1000].reshape(1000, 128)
+    Wv = w[:128 * 1000].reshape(1000, 128)
+    sX, sW = split(X), split(Wv)
+    pairs = ((2, 0), (0, 2), (1, 1), (0, 1), (1, 0), (0, 0))  # lh, hl, mm, hm, mh, hh
+    dot = np.zeros(1000, np.float32)
+    for i, j in pairs:
+        dot = (dot + (sX[i] * sW[j]).astype(np.float32).sum(1, dtype=np.float32)).astype(np.float32)
+    ref = (X.astype(np.float64) * Wv.astype(np.float64)).sum(1)
+    bound = 128 * 6 * 2.0 ** -24 * (np.abs(X.astype(np.float64) * Wv)).sum(1)
+    assert np.all(np.abs(dot - ref) <= bound)
