@@ -535,7 +535,8 @@ MSHA_API int msha_ours_intra_fwd(const msha_graph* g, const msha_groups* grp, in
                                  msha_stream_t stream);
 /* Backward, two stages around msha_edge_attention_bwd_rows:
  *   stage 0: G (B, 2, heads*feat) = group sums of dropout * dU; bgrad (B, heads, 4);
- *            row_coef (n_rows, heads; zero-filled by the caller) = dL/dSUM per batch row;
+ *            row_coef (n_rows, heads; written in full) = dL/dSUM at the batch rows, 0
+ *            elsewhere;
  *            da3s, da4s (heads, feat).
  *   stage 1: d_hs[src_b] += the intra gradient of h2's batch rows.
  * Per-row sums follow batch order (deterministic).  Stage 0 needs a workspace of

@@ -37,6 +37,8 @@ namespace bip {
 constexpr int kMaxMD = 4096;  // floats of one (M, H*F) LDS table: M = 32 at H*F = 128
 constexpr int kWavesF = 8;    // fwd: 16 KB table + 8 x (16 KB v slab + 1.1 KB) = 153 KB
 constexpr int kWavesB = 7;    // bwd: two 16 KB tables + 7 x (d_hc slab + 1.6 KB) = 153 KB
+// (F = 64 with several heads runs head-split: one head per block (grid.y), every table
+// 1/H as large, so twice the waves per CU -- see fwd_waves / bwd_waves)
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) {
   return __builtin_amdgcn_readlane(v, l);
@@ -219,10 +221,11 @@ struct Srcs {
   int32_t re, rp_re;
 };
 
-template <int H, int V, int NT, int NS, int PD, typename T, int RW>
+template <int H, int V, int NT, int NS, int PD, typename T, int RW, int HT = H>
 __device__ __forceinline__ void load_grp(Grp<RW, NT, NS, PD>& g, const Srcs& S, int32_t r0,
                                          int32_t rp, int lane) {
-  constexpr uint32_t RB = 64u * V * (uint32_t)sizeof(T);  // bytes per table row
+  // bytes per table row (HT > H: this launch's heads are a slice of HT-head rows)
+  constexpr uint32_t RB = 64u * V * (uint32_t)sizeof(T) * HT / H;
   g.rp = rp;
   const int32_t E0 = rdlane(rp, 0);
 #pragma unroll
@@ -232,7 +235,7 @@ __device__ __forceinline__ void load_grp(Grp<RW, NT, NS, PD>& g, const Srcs& S, 
 #pragma unroll
   for (int k = 0; k < NS; ++k)
     g.s[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(S.sc[k], S.v_s,
-                                                                 (uint32_t)r0 * (4u * H), 0));
+                                                                 (uint32_t)r0 * (4u * HT), 0));
   g.flag = __builtin_amdgcn_raw_buffer_load_b8(S.flag, S.v_flag, (uint32_t)r0, 0);
 #pragma unroll
   for (int t = 0; t < PD; ++t) {
@@ -250,7 +253,9 @@ __device__ __forceinline__ int32_t load_rp(const Srcs& S, int32_t r0, int lane) 
 
 __device__ __forceinline__ void make_srcs(Srcs& S, const int32_t* rowptr, const int32_t* col,
                                           const uint8_t* rowflag, int32_t n_edges, int32_t re,
-                                          int H, int PD, uint32_t row_bytes, int lane) {
+                                          int H, int PD, uint32_t row_bytes, int lane,
+                                          int HT = 0, int h0 = 0, uint32_t head_bytes = 0) {
+  if (HT == 0) HT = H;
   S.re = re;
   S.rp_re = rowptr[re];
   S.rp = make_rsrc(rowptr, (uint32_t)(re + 1) * 4u);
@@ -258,9 +263,10 @@ __device__ __forceinline__ void make_srcs(Srcs& S, const int32_t* rowptr, const 
   S.flag = make_rsrc(rowflag, (uint32_t)re);
   S.v_rp = (uint32_t)lane * 4u;
   S.v_col = (uint32_t)lane * 4u;
-  S.v_s = lane < PD * H ? (uint32_t)lane * 4u : kOOB;
+  // row scalar (row t, head h) of lane t H + h at element t HT + h0 + h of an HT-head table
+  S.v_s = lane < PD * H ? (uint32_t)((lane / H) * HT + h0 + lane % H) * 4u : kOOB;
   S.v_flag = lane < PD ? (uint32_t)lane : kOOB;
-  S.v_row = (uint32_t)lane * row_bytes / 64u;
+  S.v_row = (uint32_t)lane * row_bytes / 64u + (uint32_t)h0 * head_bytes;
 }
 
 // all-reduce over the lanes of one head (lane % H): rotations inside 16-lane rows by
@@ -419,33 +425,42 @@ __device__ __forceinline__ int32_t colb_refill(const Srcs& S, uint8_t* colb, int
 // Element lanes then walk each row's edges two at a time: the records, hc_j from LDS,
 // u += attd hc_j in registers, v_j += attd hs_i into the wave's slab.  The next group's
 // loads are in flight meanwhile.
-template <int H, int F, typename T, bool HS, bool ATTD>
-__global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
+// HT > H: the head-split form -- blockIdx.y picks heads [h0, h0 + H) of HT-head tables
+// (strided rows, scalars and attention), so a block holds one head's column table and
+// slabs (half the LDS of both heads at HT = 2) and twice the waves fit a CU.
+constexpr int kWavesF2 = 16;
+template <int H, int HT>
+constexpr int fwd_waves() { return HT > H ? kWavesF2 : kWavesF; }
+template <int H, int F, typename T, bool HS, bool ATTD, int HT = H>
+__global__ void __launch_bounds__((fwd_waves<H, HT>() * 64)) bip_fwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
     const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
     const T* __restrict__ hs, float slope, Dropout dp, T* __restrict__ u,
     T* __restrict__ u_lo, float* __restrict__ lse, float* __restrict__ attd,
     float* __restrict__ part) {
-  constexpr int D = H * F, V = D / 64, WB = kWavesF, W = 64 / H;
+  constexpr int D = H * F, V = D / 64, WB = fwd_waves<H, HT>(), W = 64 / H;
+  constexpr int DT = HT * F;  // floats per table row
+  constexpr int MDX = kMaxMD * H / HT;
   constexpr int NT = HS ? 1 : 0;
   constexpr int PD = grp_rows<H, D, T, NT>(), RW = row_words<V, T>();
-  constexpr uint32_t RB = (uint32_t)D * sizeof(T);
-  __shared__ __attribute__((aligned(16))) float tab[kMaxMD];
+  constexpr uint32_t RB = (uint32_t)DT * sizeof(T);  // row stride in bytes
+  const int h0 = HT > H ? (int)blockIdx.y * H : 0;
+  __shared__ __attribute__((aligned(16))) float tab[MDX];
   __shared__ float ert[64];
-  __shared__ __attribute__((aligned(16))) float slab[HS ? WB : 1][HS ? kMaxMD : 4];
+  __shared__ __attribute__((aligned(16))) float slab[HS ? WB : 1][HS ? MDX : 4];
   __shared__ __attribute__((aligned(16))) float2 rec[WB][kRec];
   __shared__ uint8_t colb[WB][kNCol];
   __shared__ float lses[WB][64];
   const int M = n_cols, MD = M * D;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid * 4; i < MD; i += WB * 256) {
+  for (int i = tid * 4; i < MD; i += WB * 256) {  // this launch's heads of hc (D of DT)
     float x[4];
-    ld_row<4>(hc + i, x);
+    ld_row<4>(hc + (i / D) * DT + h0 * F + i % D, x);
     st_row<4>(tab + i, x);
   }
-  for (int i = tid; i < M * H; i += WB * 64) ert[i] = er[i];
+  for (int i = tid; i < M * H; i += WB * 64) ert[i] = er[(i / H) * HT + h0 + i % H];
   if (HS)
     for (int i = lane * 4; i < MD; i += 256)
       *reinterpret_cast<float4*>(&slab[wv][i]) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -457,27 +472,28 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
   const int64_t Wt = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
   const int32_t rb = (int32_t)(w * n_rows / Wt), re = (int32_t)((w + 1) * n_rows / Wt);
   Srcs S;
-  make_srcs(S, rowptr, col, rowflag, n_edges, re, H, PD, RB, lane);
-  S.sc[0] = make_rsrc(el, (uint32_t)re * H * 4u);
+  make_srcs(S, rowptr, col, rowflag, n_edges, re, H, PD, (uint32_t)D * sizeof(T), lane, HT, h0,
+            (uint32_t)F * sizeof(T));
+  S.sc[0] = make_rsrc(el, (uint32_t)re * HT * 4u);
   S.t[0] = make_rsrc(HS ? hs : nullptr, (uint32_t)re * RB);
   const rsrc_t r_u = make_rsrc(u, (uint32_t)re * RB);
   const rsrc_t r_ulo = make_rsrc(sizeof(T) == 2 ? u_lo : nullptr, (uint32_t)re * RB);
-  const rsrc_t r_lse = make_rsrc(lse, (uint32_t)re * H * 4u);
-  const rsrc_t r_att = make_rsrc(ATTD ? attd : nullptr, (uint32_t)n_edges * H * 4u);
+  const rsrc_t r_lse = make_rsrc(lse, (uint32_t)re * HT * 4u);
+  const rsrc_t r_att = make_rsrc(ATTD ? attd : nullptr, (uint32_t)n_edges * HT * 4u);
   const char* tabc = reinterpret_cast<const char*>(tab) + lane * V * 4;
   char* slabc = reinterpret_cast<char*>(&slab[wv][0]) + lane * V * 4;
   const float2* recl = &rec[wv][hl * W];
-  const uint32_t v_att0 = (uint32_t)((lane % W) * H + lane / W) * 4u;
+  const uint32_t v_att0 = (uint32_t)((lane % W) * HT + h0 + lane / W) * 4u;
   if (rb < re) {
     using Gp = Grp<RW, NT, 1, PD>;
     const int ng = (re - rb + PD - 1) / PD;
     Gp nxt;
-    load_grp<H, V, NT, 1, PD, T, RW>(nxt, S, rb, load_rp(S, rb, lane), lane);
+    load_grp<H, V, NT, 1, PD, T, RW, HT>(nxt, S, rb, load_rp(S, rb, lane), lane);
     int32_t rp_n = load_rp(S, rb + PD, lane);
     for (int gi = 0; gi < ng; ++gi) {
       const int32_t r0 = rb + gi * PD;
       const Gp cur = nxt;  // this group's loads (issued one group ago)
-      load_grp<H, V, NT, 1, PD, T, RW>(nxt, S, r0 + PD, rp_n, lane);
+      load_grp<H, V, NT, 1, PD, T, RW, HT>(nxt, S, r0 + PD, rp_n, lane);
       rp_n = load_rp(S, r0 + 2 * PD, lane);
 
       int32_t srp[PD + 1];
@@ -504,14 +520,14 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
           const float mx = __shfl(seg_scan<W, true>(sc, lane, sl.d), sl.endl);
           const float pe = sl.valid ? __expf(sc - mx) : 0.f;
           const float sm = __shfl(seg_scan<W, false>(pe, lane, sl.d), sl.endl);
-          const int64_t elem = (int64_t)(Es + k) * H + h;
+          const int64_t elem = (int64_t)(Es + k) * HT + h0 + h;
           const float ad = sl.valid ? pe / sm * slot_keep(dp, doff, elem) : 0.f;
           rec[wv][lane] = make_float2(ad, __int_as_float(sl.j * D * 4));
           if (sl.valid && lane == sl.endl) lses[wv][sl.t * H + h] = mx + __logf(sm);
           if (ATTD)
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ad), r_att,
                                                   sl.valid ? v_att0 : kOOB,
-                                                  (uint32_t)Es * (4u * H), 0);
+                                                  (uint32_t)Es * (4u * HT), 0);
         }
         // (2) element lanes: per row, its edges' records; u in registers, v slab
 #pragma unroll
@@ -562,12 +578,12 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
         t0 = t1;
       }
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lses[wv][lane]), r_lse, S.v_s,
-                                            (uint32_t)r0 * (4u * H), 0);
+                                            (uint32_t)r0 * (4u * HT), 0);
     }
   }
   if (HS) {
     __syncthreads();
-    float* dst = part + (int64_t)blockIdx.x * MD;
+    float* dst = part + ((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * MD;  // [block][head]
     for (int i = tid * 4; i < MD; i += WB * 256) {
       float4 a = *reinterpret_cast<const float4*>(&slab[0][i]);
 #pragma unroll
@@ -590,22 +606,31 @@ __global__ void __launch_bounds__(kWavesF * 64) bip_fwd_kernel(
 // row's edges two at a time (g_e dots reduced together, d_hs in registers, d_hc into the
 // wave's slab, g_e back into the record); slot lanes finish D, de, d_el (segmented
 // scans) and add de into the wave's d_er slab (one LDS float add per slot).
-template <int H, int F, typename T, bool HS, bool COEF>
-__global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
+// (HT > H: the head-split form, as bip_fwd_kernel's; 12 waves (three per SIMD, 168 VGPRs)
+// beside the two 8 KB tables of one head, 8 for the bf16 form with hs, which needs ~190)
+constexpr int kWavesB2 = 12;
+template <int H, int HT, typename T, bool HS>
+constexpr int bwd_waves() {
+  return HT > H ? (sizeof(T) == 2 && HS ? 8 : kWavesB2) : kWavesB;
+}
+template <int H, int F, typename T, bool HS, bool COEF, int HT = H>
+__global__ void __launch_bounds__((bwd_waves<H, HT, T, HS>() * 64)) bip_bwd_kernel(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, int32_t n_rows, int32_t n_cols, int32_t n_edges,
     const float* __restrict__ el, const float* __restrict__ er, const T* __restrict__ hc,
     const float* __restrict__ lse, const T* __restrict__ dU, const T* __restrict__ hs,
     const T* __restrict__ dV, const float* __restrict__ row_coef, float slope, Dropout dp,
     float* __restrict__ d_el, T* __restrict__ d_hs, float* __restrict__ part) {
-  constexpr int D = H * F, V = D / 64, QH = F / V, WB = kWavesB, W = 64 / H;
+  constexpr int D = H * F, V = D / 64, QH = F / V, WB = bwd_waves<H, HT, T, HS>(), W = 64 / H;
+  constexpr int DT = HT * F, MDX = kMaxMD * H / HT;
   constexpr int NT = HS ? 2 : 1;
   constexpr int PD = grp_rows<H, D, T, NT>(), RW = row_words<V, T>();
   constexpr int NS = COEF ? 3 : 2;
-  constexpr uint32_t RB = (uint32_t)D * sizeof(T);
-  __shared__ __attribute__((aligned(16))) float tab[HS ? 2 : 1][kMaxMD];  // hc, dV
+  constexpr uint32_t RB = (uint32_t)DT * sizeof(T);  // row stride in bytes
+  const int h0 = HT > H ? (int)blockIdx.y * H : 0;
+  __shared__ __attribute__((aligned(16))) float tab[HS ? 2 : 1][MDX];  // hc, dV
   __shared__ float ert[64];
-  __shared__ __attribute__((aligned(16))) float slab[WB][kMaxMD];  // d_hc
+  __shared__ __attribute__((aligned(16))) float slab[WB][MDX];  // d_hc
   __shared__ float sder[WB][64];                                  // d_er, lane j * H + h
   __shared__ __attribute__((aligned(16))) float2 rec[WB][kRec];
   __shared__ uint8_t colb[WB][kNCol];
@@ -613,16 +638,17 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
   const int M = n_cols, MD = M * D, MH = M * H;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid * 4; i < MD; i += WB * 256) {
+  for (int i = tid * 4; i < MD; i += WB * 256) {  // this launch's heads of hc, dV
+    const int src = (i / D) * DT + h0 * F + i % D;
     float x[4];
-    ld_row<4>(hc + i, x);
+    ld_row<4>(hc + src, x);
     st_row<4>(&tab[0][i], x);
     if (HS) {
-      ld_row<4>(dV + i, x);
+      ld_row<4>(dV + src, x);
       st_row<4>(&tab[HS ? 1 : 0][i], x);
     }
   }
-  for (int i = tid; i < MH; i += WB * 64) ert[i] = er[i];
+  for (int i = tid; i < MH; i += WB * 64) ert[i] = er[(i / H) * HT + h0 + i % H];
   for (int i = lane * 4; i < MD; i += 256)
     *reinterpret_cast<float4*>(&slab[wv][i]) = make_float4(0.f, 0.f, 0.f, 0.f);
   sder[wv][lane] = 0.f;
@@ -634,14 +660,15 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
   const int64_t Wt = (int64_t)gridDim.x * WB, w = (int64_t)blockIdx.x * WB + wv;
   const int32_t rb = (int32_t)(w * n_rows / Wt), re = (int32_t)((w + 1) * n_rows / Wt);
   Srcs S;
-  make_srcs(S, rowptr, col, rowflag, n_edges, re, H, PD, RB, lane);
-  S.sc[0] = make_rsrc(el, (uint32_t)re * H * 4u);
-  S.sc[1] = make_rsrc(lse, (uint32_t)re * H * 4u);
-  S.sc[2] = make_rsrc(COEF ? row_coef : nullptr, (uint32_t)re * H * 4u);
+  make_srcs(S, rowptr, col, rowflag, n_edges, re, H, PD, (uint32_t)D * sizeof(T), lane, HT, h0,
+            (uint32_t)F * sizeof(T));
+  S.sc[0] = make_rsrc(el, (uint32_t)re * HT * 4u);
+  S.sc[1] = make_rsrc(lse, (uint32_t)re * HT * 4u);
+  S.sc[2] = make_rsrc(COEF ? row_coef : nullptr, (uint32_t)re * HT * 4u);
   S.t[0] = make_rsrc(dU, (uint32_t)re * RB);
   S.t[1] = make_rsrc(HS ? hs : nullptr, (uint32_t)re * RB);
   const rsrc_t r_dhs = make_rsrc(HS ? d_hs : nullptr, (uint32_t)re * RB);
-  const rsrc_t r_del = make_rsrc(d_el, (uint32_t)re * H * 4u);
+  const rsrc_t r_del = make_rsrc(d_el, (uint32_t)re * HT * 4u);
   const char* tabc = reinterpret_cast<const char*>(&tab[0][0]) + lane * V * 4;
   const char* tdvc = reinterpret_cast<const char*>(&tab[HS ? 1 : 0][0]) + lane * V * 4;
   char* slabc = reinterpret_cast<char*>(&slab[wv][0]) + lane * V * 4;
@@ -650,12 +677,12 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
     using Gp = Grp<RW, NT, NS, PD>;
     const int ng = (re - rb + PD - 1) / PD;
     Gp nxt;
-    load_grp<H, V, NT, NS, PD, T, RW>(nxt, S, rb, load_rp(S, rb, lane), lane);
+    load_grp<H, V, NT, NS, PD, T, RW, HT>(nxt, S, rb, load_rp(S, rb, lane), lane);
     int32_t rp_n = load_rp(S, rb + PD, lane);
     for (int gi = 0; gi < ng; ++gi) {
       const int32_t r0 = rb + gi * PD;
       const Gp cur = nxt;
-      load_grp<H, V, NT, NS, PD, T, RW>(nxt, S, r0 + PD, rp_n, lane);
+      load_grp<H, V, NT, NS, PD, T, RW, HT>(nxt, S, r0 + PD, rp_n, lane);
       rp_n = load_rp(S, r0 + 2 * PD, lane);
 
       int32_t srp[PD + 1];
@@ -683,7 +710,7 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
         const float pre = elq + ert[sl.j * H + h];
         const float sc = virt ? 0.f : lrelu(pre, slope);
         const float att = sl.valid ? __expf(sc - lsq) : 0.f;
-        const float kf = slot_keep(dp, doff, (int64_t)(Es + k) * H + h);
+        const float kf = slot_keep(dp, doff, (int64_t)(Es + k) * HT + h0 + h);
         const float ad = att * kf;
         rec[wv][lane] = make_float2(ad, __int_as_float(sl.j * D * 4));
         // (2) element lanes: g_e (into the record), d_hs, the d_hc slab
@@ -767,11 +794,14 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
         t0 = t1;
       }
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dels[wv][lane]), r_del, S.v_s,
-                                            (uint32_t)r0 * (4u * H), 0);
+                                            (uint32_t)r0 * (4u * HT), 0);
     }
   }
   __syncthreads();
-  float* dst = part + (int64_t)blockIdx.x * part_stride(MD + MH);
+  // the block's partial: [d_hc: head blk (M D)][d_er: head blk (M H)] over all HT heads,
+  // each head block writing its own slices
+  const int nh = HT / H, hb = HT > H ? (int)blockIdx.y : 0;
+  float* dst = part + (int64_t)blockIdx.x * part_stride(nh * (MD + MH));
   for (int i = tid * 4; i < MD; i += WB * 256) {
     float4 a = *reinterpret_cast<const float4*>(&slab[0][i]);
 #pragma unroll
@@ -779,13 +809,13 @@ __global__ void __launch_bounds__(kWavesB * 64) bip_bwd_kernel(
       const float4 b = *reinterpret_cast<const float4*>(&slab[q][i]);
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
-    *reinterpret_cast<float4*>(dst + i) = a;
+    *reinterpret_cast<float4*>(dst + hb * MD + i) = a;
   }
   for (int i = tid; i < MH; i += WB * 64) {
     float a = sder[0][i];
 #pragma unroll
     for (int q = 1; q < WB; ++q) a += sder[q][i];
-    dst[MD + i] = a;
+    dst[nh * MD + hb * MH + i] = a;
   }
 }
 
@@ -798,7 +828,10 @@ template <typename T>
 __global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restrict__ part,
                                                           int32_t nb, int32_t stride, int32_t n,
                                                           int32_t n_t, T* __restrict__ out_t,
-                                                          float* __restrict__ out_f) {
+                                                          float* __restrict__ out_f,
+                                                          int32_t seg, int32_t seg_stride,
+                                                          int32_t blk, int32_t blk_off,
+                                                          int32_t fblk, int32_t fstride) {
   __shared__ float red[64][17];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = lane & 15, st = wv * 4 + (lane >> 4);  // entry in the slice, stream
@@ -814,8 +847,11 @@ __global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restric
     float sum = red[0][c];
 #pragma unroll 8
     for (int q = 1; q < 64; ++q) sum += red[q][c];
-    if (i < n_t) out_t[i] = from_f32<T>(sum);
-    else out_f[i - n_t] = sum;
+    // (a head-split launch's partials are [head blk][column seg]: entry i lands at column
+    // (i % blk) / seg, head i / blk of the HT-head table)
+    if (i < n_t)
+      out_t[((i % blk) / seg) * seg_stride + (i / blk) * blk_off + i % seg] = from_f32<T>(sum);
+    else out_f[((i - n_t) % fblk) * fstride + (i - n_t) / fblk] = sum;
   }
 }
 
@@ -869,26 +905,50 @@ extern "C" size_t msha_bip_workspace_size(const msha_graph* g, int32_t heads, in
   return (size_t)bip::cu_count() * rec * sizeof(float) + 256;
 }
 
+// the forward's head-split form (one head per block, blockIdx.y) where a head's row slice
+// is 64 elements: twice the waves per CU (MSHA_BIP_SPLIT=0: both heads per block)
+static bool bip_split_enabled() {
+  static const int on = [] {
+    const char* v = getenv("MSHA_BIP_SPLIT");
+    return v != nullptr && *v ? atoi(v) : 1;
+  }();
+  return on != 0;
+}
+
 template <int H, int F, typename T>
 static void bip_launch_fwd(const msha_graph* g, const float* el, const float* er, const void* hc,
                            const void* hs, float slope, const Dropout& dp, void* u, void* u_lo,
                            float* lse, float* attd, void* v, float* part, int nb, hipStream_t s) {
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(bip::kWavesF * 64), 0, s, g->rowptr, g->col,
+  constexpr bool kSplit = H > 1 && F == 64;
+  const bool split = kSplit && bip_split_enabled();
+  auto go = [&](auto kern, dim3 grid, int waves) {
+    hipLaunchKernelGGL(kern, grid, dim3(waves * 64), 0, s, g->rowptr, g->col,
                        g->rowflag, (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges,
                        el, er, (const T*)hc, (const T*)hs, slope, dp, (T*)u, (T*)u_lo, lse, attd,
                        part);
   };
+  const dim3 g1(nb), gs(nb, H);
+  constexpr int w1 = bip::kWavesF, ws = bip::kWavesF2;
   if (hs != nullptr) {
-    if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, true, true>);
-    else go(bip::bip_fwd_kernel<H, F, T, true, false>);
-    const int32_t MD = (int32_t)(g->n_cols * H * F);
+    if (split) {
+      if constexpr (kSplit) {
+        if (attd != nullptr) go(bip::bip_fwd_kernel<1, F, T, true, true, H>, gs, ws);
+        else go(bip::bip_fwd_kernel<1, F, T, true, false, H>, gs, ws);
+      }
+    } else if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, true, true>, g1, w1);
+    else go(bip::bip_fwd_kernel<H, F, T, true, false>, g1, w1);
+    const int32_t MD = (int32_t)(g->n_cols * H * F), MDh = (int32_t)(g->n_cols * F);
+    // partials [block][head][column][F] (split) or [block][column][H F]
     hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + 15) / 16), dim3(1024), 0, s, part,
-                       nb, MD, MD, MD, (T*)v, (float*)nullptr);
-  } else {
-    if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, false, true>);
-    else go(bip::bip_fwd_kernel<H, F, T, false, false>);
-  }
+                       nb, MD, MD, MD, (T*)v, (float*)nullptr, split ? F : MD,
+                       split ? H * F : 0, split ? MDh : MD, split ? F : 0, 1, 1);
+  } else if (split) {
+    if constexpr (kSplit) {
+      if (attd != nullptr) go(bip::bip_fwd_kernel<1, F, T, false, true, H>, gs, ws);
+      else go(bip::bip_fwd_kernel<1, F, T, false, false, H>, gs, ws);
+    }
+  } else if (attd != nullptr) go(bip::bip_fwd_kernel<H, F, T, false, true>, g1, w1);
+  else go(bip::bip_fwd_kernel<H, F, T, false, false>, g1, w1);
 }
 
 template <int H, int F, typename T>
@@ -897,21 +957,40 @@ static void bip_launch_bwd(const msha_graph* g, const float* el, const float* er
                            const float* row_coef, float slope, const Dropout& dp, float* d_el,
                            float* d_er, void* d_hc, void* d_hs, float* part, int nb,
                            hipStream_t s) {
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(bip::kWavesB * 64), 0, s, g->rowptr, g->col,
+  constexpr bool kSplit = H > 1 && F == 64;
+  const bool split = kSplit && bip_split_enabled();
+  auto go = [&](auto kern, dim3 grid, int waves) {
+    hipLaunchKernelGGL(kern, grid, dim3(waves * 64), 0, s, g->rowptr, g->col,
                        g->rowflag, (int32_t)g->n_rows, (int32_t)g->n_cols, (int32_t)g->n_edges,
                        el, er, (const T*)hc,
                        lse, (const T*)dU, (const T*)hs, (const T*)dV, row_coef, slope, dp, d_el,
                        (T*)d_hs, part);
   };
   const bool hsb = dV != nullptr, cf = row_coef != nullptr;
-  if (hsb && cf) go(bip::bip_bwd_kernel<H, F, T, true, true>);
-  else if (hsb) go(bip::bip_bwd_kernel<H, F, T, true, false>);
-  else if (cf) go(bip::bip_bwd_kernel<H, F, T, false, true>);
-  else go(bip::bip_bwd_kernel<H, F, T, false, false>);
+  if (split) {
+    if constexpr (kSplit) {
+      const dim3 gs(nb, H);
+      constexpr int w1 = bip::bwd_waves<1, H, T, true>(), w0 = bip::bwd_waves<1, H, T, false>();
+      if (hsb && cf) go(bip::bip_bwd_kernel<1, F, T, true, true, H>, gs, w1);
+      else if (hsb) go(bip::bip_bwd_kernel<1, F, T, true, false, H>, gs, w1);
+      else if (cf) go(bip::bip_bwd_kernel<1, F, T, false, true, H>, gs, w0);
+      else go(bip::bip_bwd_kernel<1, F, T, false, false, H>, gs, w0);
+    }
+  } else {
+    const dim3 g1(nb);
+    constexpr int w1 = bip::kWavesB;
+    if (hsb && cf) go(bip::bip_bwd_kernel<H, F, T, true, true>, g1, w1);
+    else if (hsb) go(bip::bip_bwd_kernel<H, F, T, true, false>, g1, w1);
+    else if (cf) go(bip::bip_bwd_kernel<H, F, T, false, true>, g1, w1);
+    else go(bip::bip_bwd_kernel<H, F, T, false, false>, g1, w1);
+  }
   const int32_t MD = (int32_t)(g->n_cols * H * F), MH = (int32_t)(g->n_cols * H);
+  const int32_t MDh = (int32_t)(g->n_cols * F), M = (int32_t)g->n_cols;
+  // partials [block][d_hc (split: [head][column][F])][d_er (split: [head][column])]
   hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + MH + 15) / 16), dim3(1024), 0, s, part,
-                     nb, bip::part_stride(MD + MH), MD + MH, MD, (T*)d_hc, d_er);
+                     nb, bip::part_stride(MD + MH), MD + MH, MD, (T*)d_hc, d_er,
+                     split ? F : MD, split ? H * F : 0, split ? MDh : MD, split ? F : 0,
+                     split ? M : MH, split ? H : 1);
 }
 
 extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,

@@ -510,9 +510,16 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_kernel(OursArgs a,
     }
 }
 
+// (also zero-fills row_coef (nz floats), which the finish kernel after it writes at the
+// batch rows: one launch fewer than a separate fill)
 __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, int D, int nck,
                                                                      const float* __restrict__ Gp,
-                                                                     float* __restrict__ G) {
+                                                                     float* __restrict__ G,
+                                                                     float* __restrict__ zf,
+                                                                     int64_t nz) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nz;
+       t += (int64_t)gridDim.x * blockDim.x)
+    zf[t] = 0.f;
   const int64_t total = 2 * B * D;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -836,7 +843,7 @@ static void launch_bwd(const OursArgs& a, int stage, int64_t B, int nck, int hea
 #undef GATHER
     hipLaunchKernelGGL(ours_bwd_gather_reduce_kernel,
                        dim3(grid_for(2 * B * heads * feat, 256, 4096)), dim3(256), 0, s, B,
-                       heads * feat, nck, (const float*)Gp, G);
+                       heads * feat, nck, (const float*)Gp, G, row_coef, a.N * heads);
     hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(1), dim3(1024), 0, s, a, 0, bstat,
                        (const float*)G, bgrad, row_coef, da3s, da4s, (T*)nullptr);
   } else {
@@ -869,7 +876,8 @@ extern "C" int msha_ours_intra_bwd(const msha_graph* g, const msha_groups* grp, 
   if (B == 0) {
     if (stage == 0) {
       if (hipMemsetAsync(da3s, 0, sizeof(float) * heads * feat, s) != hipSuccess ||
-          hipMemsetAsync(da4s, 0, sizeof(float) * heads * feat, s) != hipSuccess)
+          hipMemsetAsync(da4s, 0, sizeof(float) * heads * feat, s) != hipSuccess ||
+          hipMemsetAsync(row_coef, 0, sizeof(float) * a.N * heads, s) != hipSuccess)
         return check_launch("ours_intra_bwd memset");
     }
     return MSHA_OK;

@@ -1090,7 +1090,7 @@ class _OursAttention(torch.autograd.Function):
         dV = torch.zeros(m, H, Fd, device=dev, dtype=dt) if dV is None else _tc(dV, dt)
         G = torch.empty(max(B, 1), 2, H * Fd, device=dev, dtype=torch.float32)
         bgrad = torch.empty(max(B, 1), H, 4, device=dev, dtype=torch.float32)
-        row_coef = torch.zeros(n, H, device=dev, dtype=torch.float32)
+        row_coef = torch.empty(n, H, device=dev, dtype=torch.float32)  # zeroed by stage 0
         da3s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
         da4s = torch.empty(H, Fd, device=dev, dtype=torch.float32)
         args = (g, gr, B, src.data_ptr(), H, Fd, _code(dt), h2.data_ptr(), a3s.data_ptr(),

@@ -23,6 +23,7 @@ CASES = [
     (300, 16, 2, 128, 7, dict(empty_rows=(5,))),                      # V = 4
     (257, 16, 4, 32, 3, dict()),
     (5000, 32, 2, 64, 2, dict()),                                     # groups capped by rows
+    (600, 16, 4, 64, 6, dict(empty_rows=(2,))),                       # four head blocks
 ]
 
 
