@@ -37,8 +37,8 @@ namespace bip {
 constexpr int kMaxMD = 4096;  // floats of one (M, H*F) LDS table: M = 32 at H*F = 128
 constexpr int kWavesF = 8;    // fwd: 16 KB table + 8 x (16 KB v slab + 1.1 KB) = 153 KB
 constexpr int kWavesB = 7;    // bwd: two 16 KB tables + 7 x (d_hc slab + 1.6 KB) = 153 KB
-// (F = 64 with several heads runs head-split: one head per block (grid.y), every table
-// 1/H as large, so twice the waves per CU -- see fwd_waves / bwd_waves)
+// (MSHA_BIP_SPLIT=1, F = 64 with several heads: head-split, one head per block (grid.y),
+// every table 1/H as large, so twice the waves per CU -- see fwd_waves / bwd_waves)
 
 __device__ __forceinline__ int32_t rdlane(int32_t v, int l) {
   return __builtin_amdgcn_readlane(v, l);
@@ -905,12 +905,15 @@ extern "C" size_t msha_bip_workspace_size(const msha_graph* g, int32_t heads, in
   return (size_t)bip::cu_count() * rec * sizeof(float) + 256;
 }
 
-// the forward's head-split form (one head per block, blockIdx.y) where a head's row slice
-// is 64 elements: twice the waves per CU (MSHA_BIP_SPLIT=0: both heads per block)
+// the head-split form (one head per block, blockIdx.y) where a head's row slice is 64
+// elements: twice the waves per CU, but every row's CSR walk, column bytes and scalar
+// control run once per head.  Off by default (MSHA_BIP_SPLIT=1 turns it on): the
+// kernels are issue-bound on that per-row control, and the A/B at bip1m fp32 was fwd
+// 290 -> 316 us, bwd 466 -> 663 us; R15 bip_fwd + bip_bwd 56 -> 86 us.
 static bool bip_split_enabled() {
   static const int on = [] {
     const char* v = getenv("MSHA_BIP_SPLIT");
-    return v != nullptr && *v ? atoi(v) : 1;
+    return v != nullptr && *v ? atoi(v) : 0;
   }();
   return on != 0;
 }

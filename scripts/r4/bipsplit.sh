@@ -9,7 +9,7 @@ $T 700 python -u -m pytest -x -q -s --timeout 300 --timeout-method thread tests/
   "tests/test_gpu_parity_full.py::test_bip1m_ourslayer3_core_every_row" tests/test_gpu_ours.py tests/test_gpu_head.py tests/test_gpu_modules.py \
   > gpurun_out/r4/bipsplit_tests.log 2>&1 || { tail -40 gpurun_out/r4/bipsplit_tests.log; exit 1; }
 grep -E "bip1m|passed|failed" gpurun_out/r4/bipsplit_tests.log | tail -14
-MSHA_BIP_SPLIT=0 $T 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_bip.py \
+MSHA_BIP_SPLIT=1 $T 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_bip.py \
   > gpurun_out/r4/bipsplit_off.log 2>&1 || { tail -40 gpurun_out/r4/bipsplit_off.log; exit 1; }
 tail -2 gpurun_out/r4/bipsplit_off.log
 for SP in 1 0; do
