@@ -25,7 +25,9 @@ LIBDIR = os.path.join(PKG, "lib")
 # timeline, msha_debug_timeline; lib/libmsha_gnn_timeline.so, selected with MSHA_GNN_LIB)
 VARIANTS = {"": [], "timeline": ["-DSK_TIMELINE"],
             # gather-layout forward A/Bs (edge_geo.h knobs)
-            "nopf": ["-DGL_PREFETCH_F32=0", "-DGL_PREFETCH_BF16=0", "-DGL_EPL_F32=2"]}
+            "nopf": ["-DGL_PREFETCH_F32=0", "-DGL_PREFETCH_BF16=0", "-DGL_EPL_F32=2"],
+            # bipartite kernels' streamed bytes per row group (edge_bip.hip grp_rows)
+            "bipg16": ["-DBIP_GRP_BYTES=16384"]}
 OBJDIR = os.path.join(LIBDIR, "obj")
 LIB = os.path.join(LIBDIR, "libmsha_gnn.so")
 ARCH = os.environ.get("MSHA_OFFLOAD_ARCH", "gfx950")

@@ -161,10 +161,14 @@ constexpr int kRec = 72;      // slot records per wave: 64 slots + the pair loop
 // wave keeps in flight while it works on the previous group; larger groups also spread
 // the group's fixed instructions over more rows.  (8-row groups ran bf16 no faster than
 // fp32: rows, not bytes, were in flight.)
+#ifndef BIP_GRP_BYTES
+#define BIP_GRP_BYTES 8192
+#endif
 template <int H, int D, typename T, int NT>
 constexpr int grp_rows() {
   constexpr int rb = D * (int)sizeof(T) * (NT > 1 ? NT : 1);  // streamed bytes per row
-  constexpr int want = 8192 / rb < 8 ? 8 : (8192 / rb > 32 ? 32 : 8192 / rb);
+  constexpr int gb = BIP_GRP_BYTES;
+  constexpr int want = gb / rb < 8 ? 8 : (gb / rb > 32 ? 32 : gb / rb);
   return want < 64 / H ? want : 64 / H;
 }
 
