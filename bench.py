@@ -136,19 +136,68 @@ def kernel_source_id() -> str:
     return h.hexdigest()[:16]
 
 
+def _source_files():
+    import glob
+
+    return sorted(glob.glob(os.path.join(ROOT, "msha--gnn_amd", "csrc", "*.hip"))
+                  + glob.glob(os.path.join(ROOT, "msha--gnn_amd", "csrc", "*.h"))
+                  + glob.glob(os.path.join(ROOT, "include", "*.h")))
+
+
+def kernel_source_files() -> dict:
+    """Per-file identity of the sources (basename -> sha256[:16]), recorded with each
+    profile beside kernel_source_id: a profile stays valid for a kernel while the file
+    that defines it and every header are unchanged."""
+    import hashlib
+
+    return {os.path.basename(f): hashlib.sha256(open(f, "rb").read()).hexdigest()[:16]
+            for f in _source_files()}
+
+
+def _kernel_defs() -> dict:
+    """__global__ kernel name -> the .hip file defining it."""
+    import re
+
+    out = {}
+    for f in _source_files():
+        if f.endswith(".hip"):
+            for m in re.finditer(r"__global__[\s\S]{0,200}?\b(\w+_kernel)\s*\(", open(f).read()):
+                out.setdefault(m.group(1), os.path.basename(f))
+    return out
+
+
+def _same_sources(meta: dict, kernels) -> bool:
+    """Whether a profile (its _meta) measured this build's code for ``kernels`` (profile
+    kernel names): the whole-tree id matches, or the per-file ids of every header and of
+    the files defining those kernels do."""
+    if meta.get("source_id") == kernel_source_id():
+        return True
+    files = meta.get("source_files")
+    if not files:
+        return False
+    cur, defs = kernel_source_files(), _kernel_defs()
+    need = {f for f in cur if f.endswith(".h")}
+    for k in kernels:
+        hit = [n for n in defs if n in k]
+        if not hit:
+            return False
+        need.add(defs[max(hit, key=len)])
+    return all(files.get(f) == cur[f] for f in need)
+
+
 def pmc_lookup(patterns, glob_pat, profiles_dir=None):
     """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction) summed over
     the kernels matching ``patterns`` (regexes; each must match a kernel of the same
     summary, several matches of one pattern are averaged) in the newest committed profile matching ``glob_pat``
     (profiles/<glob>/pmc_summary.json, written by scripts/summarize_profile.py from
     separate rocprofv3 --pmc passes) whose recorded source id is this build's
-    (kernel_source_id).  (None, None) if absent; (None, note) if only profiles of other
-    sources exist."""
+    (kernel_source_id), or whose per-file ids match for the headers and the files that
+    define the matched kernels (_same_sources).  (None, None) if absent; (None, note) if
+    only profiles of other sources exist."""
     import glob
     import re
 
     pats = [re.compile(p) for p in patterns]
-    sid = kernel_source_id()
     stale = None
     pdir = profiles_dir or os.path.join(ROOT, "profiles")
     for path in sorted(glob.glob(os.path.join(pdir, glob_pat, "pmc_summary.json")),
@@ -157,7 +206,8 @@ def pmc_lookup(patterns, glob_pat, profiles_dir=None):
             summ = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if summ.get("_meta", {}).get("source_id") != sid:
+        keys = [k for k in summ if any(p.search(k) for p in pats)]
+        if not _same_sources(summ.get("_meta", {}), keys):
             stale = stale or os.path.relpath(path, ROOT)
             continue
         tot, ok = 0.0, True

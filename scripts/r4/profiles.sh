@@ -13,6 +13,7 @@ run() {  # name, bench args
   local OUT="$R/gpurun_out/prof_r4${TAG}_$1"; shift
   mkdir -p "$OUT"
   (cd "$R" && python3 -c "import bench; print(bench.kernel_source_id())") > "$OUT/source_id.txt" || return 2
+  (cd "$R" && python3 -c "import bench, json; print(json.dumps(bench.kernel_source_files()))") > "$OUT/source_files.json" || return 2
   local B="$R/bench.py $*"
   (cd /tmp && TMPDIR=/tmp timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 $B) \
     > "$OUT/bench_trace.log" 2>&1 || { echo "$OUT trace failed"; tail -5 "$OUT/bench_trace.log"; return 3; }

@@ -81,6 +81,34 @@ def test_pmc_traffic_only_from_this_build(tmp_path):
     assert len(bench.kernel_source_id()) == 16
 
 
+def test_pmc_traffic_per_file_identity(tmp_path):
+    """A profile of another whole-tree id still serves a kernel whose defining file and
+    every header are unchanged (_meta.source_files), and no kernel whose file changed."""
+    import json
+
+    files = bench.kernel_source_files()
+    assert bench._kernel_defs()["bip_fwd_kernel"] == "edge_bip.hip"
+    bip = "void msha::bip::bip_fwd_kernel<2, 64, float, true, false>"
+    pair = "void msha::sk::pair_x3_kernel<128, 128, 3>"
+    d = tmp_path / "round4_link_v1"
+    d.mkdir()
+    edited = dict(files, **{"edge_bip.hip": "0" * 16})
+    json.dump({bip: {"hbm_bytes_per_launch_corrected": 1e9},
+               pair: {"hbm_bytes_per_launch_corrected": 2e9},
+               "_meta": {"source_id": "0123456789abcdef", "source_files": edited}},
+              open(d / "pmc_summary.json", "w"))
+    tr, src = bench.pmc_lookup([r"pair_x3_kernel<"], "*link*", profiles_dir=str(tmp_path))
+    assert tr == 2e9
+    tr, src = bench.pmc_lookup([r"bip_fwd_kernel<"], "*link*", profiles_dir=str(tmp_path))
+    assert tr is None and "other sources" in src
+    hdr = dict(files, **{"common.h": "0" * 16})  # a header change invalidates every kernel
+    json.dump({pair: {"hbm_bytes_per_launch_corrected": 2e9},
+               "_meta": {"source_id": "0123456789abcdef", "source_files": hdr}},
+              open(d / "pmc_summary.json", "w"))
+    tr, _ = bench.pmc_lookup([r"pair_x3_kernel<"], "*link*", profiles_dir=str(tmp_path))
+    assert tr is None
+
+
 def test_gpus_flag_launches_ranks():
     """``bench.py --gpus 2`` without WORLD_SIZE starts two ranks itself (torch.distributed.run
     on 127.0.0.1); --dry-run runs them over gloo on the CPU: both ranks report, the sharded
