@@ -857,7 +857,7 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
         model.train()
         sr_s = torch.empty(2, 64, dtype=torch.int64, device=dev)
         si_s, ri_s = sr_s[0], sr_s[1]
-        one = torch.ones((), device=dev)  # dL/dL, made once (not a fill node per step)
+        unit = torch.ones((), device=dev)  # dL/dL, made once (not a fill node per step)
 
         def body():
             opt.zero_grad(set_to_none=True)
@@ -865,7 +865,7 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
             # train.py:229 F.nll_loss(output[source_index], recipient_index) as one launch
             # each way (msha_nll_rows_fwd/_bwd) instead of ~12 ATen launches
             loss = MF.nll_loss_rows(out, si_s, ri_s)
-            loss.backward(one)
+            loss.backward(unit)
             opt.step()
             return loss
 
