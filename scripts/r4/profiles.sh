@@ -34,6 +34,7 @@ echo ALL_DONE
 else
 run bip1m --workload bip1m --steps 5 --warmup 2 --no-cpu-baseline --no-dropout-leg &&
 bash scripts/pmc_bip_sq.sh r4${TAG} > gpurun_out/prof_r4${TAG}_bip_sq.txt 2>&1 &&
+bash scripts/pmc_step_sq.sh r4${TAG} > gpurun_out/prof_r4${TAG}_step_sq.txt 2>&1 &&
 NROWS=40 bash scripts/trace_train_step.sh r4${TAG}_ours32 Ours 2015 float32 > gpurun_out/prof_r4${TAG}_step_ours32.txt 2>&1 &&
 NROWS=40 bash scripts/trace_train_step.sh r4${TAG}_abl32 ablation3 2015 float32 > gpurun_out/prof_r4${TAG}_step_abl32.txt 2>&1 &&
 NROWS=40 bash scripts/trace_train_step.sh r4${TAG}_ours16 Ours 2015 bfloat16 > gpurun_out/prof_r4${TAG}_step_ours16.txt 2>&1 &&
