@@ -3,7 +3,7 @@
 # timeout; counters in separate --pmc passes): C4 headline (+ bf16, dropout and link
 # legs), syn2m, bip1m (+ SQ passes over the bipartite kernels), the configs[1] steps.
 # Usage: scripts/r4/profiles.sh [tag] [a|b]  -> gpurun_out/prof_r4<tag>_*
-#   a: C4 + syn2m; b: bip1m + its SQ passes + the configs[1] step traces
+#   a: C4 + syn2m; b: bip1m + its SQ passes + the configs[1] step traces; c: bip1m alone
 TAG=${1:-v1}; SET=${2:-a}
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 cd "$R" && mkdir -p gpurun_out
@@ -27,12 +27,16 @@ run() {  # name, bench args
 ( while true; do date > "$R/gpurun_out/prof_r4${TAG}_heartbeat"; sleep 60; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-if [ "$SET" = a ]; then
+if [ "$SET" = c ]; then  # bip1m alone (the R15 legs share its kernel names)
+run bip1m --workload bip1m --steps 5 --warmup 2 --no-cpu-baseline --no-dropout-leg --no-r15 &&
+bash scripts/pmc_bip_sq.sh r4${TAG}c > gpurun_out/prof_r4${TAG}_bip_sq.txt 2>&1 &&
+echo ALL_DONE
+elif [ "$SET" = a ]; then
 run syn100k --workload syn100k --steps 10 --warmup 3 --no-cpu-baseline --no-r15 --no-syn2m --no-bip1m &&
 run syn2m --workload syn2m --steps 3 --warmup 1 --no-cpu-baseline --no-link-score --no-r15 --no-bip1m --no-dropout-leg &&
 echo ALL_DONE
 else
-run bip1m --workload bip1m --steps 5 --warmup 2 --no-cpu-baseline --no-dropout-leg &&
+run bip1m --workload bip1m --steps 5 --warmup 2 --no-cpu-baseline --no-dropout-leg --no-r15 &&
 bash scripts/pmc_bip_sq.sh r4${TAG} > gpurun_out/prof_r4${TAG}_bip_sq.txt 2>&1 &&
 bash scripts/pmc_step_sq.sh r4${TAG} > gpurun_out/prof_r4${TAG}_step_sq.txt 2>&1 &&
 NROWS=40 bash scripts/trace_train_step.sh r4${TAG}_ours32 Ours 2015 float32 > gpurun_out/prof_r4${TAG}_step_ours32.txt 2>&1 &&
