@@ -307,8 +307,8 @@ MSHA_API int msha_edge_attention_bwd_fused_ex(
  * heads*feat*sizeof <= 1024 B; tables under 2 GiB); MSHA_ERR_UNSUPPORTED otherwise. */
 MSHA_API int msha_edge_attention_row_scores_supported(const msha_graph* g, int32_t heads,
                                                       int32_t feat, int32_t dtype);
-/* whether the library's default is to use them (fp32 tables; bf16 tables once the er
- * table outgrows L2); MSHA_ROW_SCORES=0/1 in the environment forces it */
+/* whether the library's default is to use them (wherever supported, fp32 and bf16,
+ * since round 4); MSHA_ROW_SCORES=0/1 in the environment forces it */
 MSHA_API int msha_edge_attention_row_scores_preferred(const msha_graph* g, int32_t heads,
                                                       int32_t feat, int32_t dtype);
 MSHA_API int msha_edge_attention_fwd_rs(const msha_graph* g, int32_t heads, int32_t feat,

@@ -1664,13 +1664,14 @@ extern "C" int msha_edge_attention_row_scores_supported(const msha_graph* g, int
   return fwd_bat_ok(g, heads, feat, dtype) ? 1 : 0;
 }
 
-// MSHA_ROW_SCORES: 1 = whenever supported, 0 = never (A/B).  Default: fp32 tables always
-// (C4 forward 174 -> 161 us, syn2m 3900 -> 3652 us); bf16 tables once the er table
-// outgrows an XCD's L2 (RS_BF16_MIN_BYTES): the bf16 forward is issue-bound and at C4
-// (3.2 MB er, L2-resident) the V extra fmas per gathered piece cost more (98 -> 111 us)
-// than the gather they replace.
+// MSHA_ROW_SCORES: 1 = whenever supported, 0 = never (A/B).  Default: whenever supported.
+// fp32: C4 forward 174 -> 149 us, syn2m 3900 -> 3652 us.  bf16: in round 3 the C4 forward
+// (3.2 MB er, L2-resident) ran slower on row scores (98 -> 111 us) and took them only
+// once the er table outgrew an XCD's L2; on the round-4 gather-layout forward they win
+// there too (C4 bf16 forward 101 -> 94 us, step 0.325 -> 0.318 ms,
+// profiles/round4_rs_bf16_ab/), and the er gather's extra traffic is gone.
 #ifndef RS_BF16_MIN_BYTES
-#define RS_BF16_MIN_BYTES (16ll << 20)
+#define RS_BF16_MIN_BYTES 0ll
 #endif
 extern "C" int msha_edge_attention_row_scores_preferred(const msha_graph* g, int32_t heads,
                                                         int32_t feat, int32_t dtype) {

@@ -966,9 +966,17 @@ struct HeadLayout {
 };
 
 // rows per wave and waves of the backward row pass (msha_head_bwd launches exactly these)
+// rows per wave of the backward row pass (at least kHeadRowsPerWave; MSHA_HEAD_RPW
+// overrides the floor, A/B).  Every wave is a block holding the whole backward LDS
+// image, so the floor also sets how many rounds of blocks the row scan takes.
 static int64_t head_bwd_rpw(int64_t N) {
+  static const int64_t floor_rpw = [] {
+    const char* v = getenv("MSHA_HEAD_RPW");
+    const int64_t x = v != nullptr && *v ? atoll(v) : 0;
+    return x > 0 ? x : (int64_t)kHeadRowsPerWave;
+  }();
   int64_t rpw = (N + kHeadBwdWaves - 1) / kHeadBwdWaves;
-  return rpw < kHeadRowsPerWave ? kHeadRowsPerWave : rpw;
+  return rpw < floor_rpw ? floor_rpw : rpw;
 }
 static int head_bwd_waves(int64_t N) {
   const int64_t rpw = head_bwd_rpw(N);

@@ -184,7 +184,7 @@ def test_c4_row_scores_every_row(cuda, c4, dt):
     got = {}
     for rt in ("0", "1"):
         os.environ["MSHA_ROWTERMS"] = rt
-        os.environ["MSHA_ROW_SCORES"] = "1"  # bf16 at C4 defaults to the er gather
+        os.environ["MSHA_ROW_SCORES"] = "1"  # (the default too; pinned against the knob)
         try:
             el_l = el.detach().clone().requires_grad_(True)
             er_l = torch.zeros_like(er).requires_grad_(True)  # not read on this path

@@ -25,7 +25,7 @@ EMB_RTOL = 1e-5
 
 def _rs_grads(MF, graph, el, hc, ar, dU, p, seed, dev, dtype, rowterms, er_hint=None):
     os.environ["MSHA_ROWTERMS"] = "1" if rowterms else "0"
-    os.environ["MSHA_ROW_SCORES"] = "1"  # wherever supported (the default skips small bf16)
+    os.environ["MSHA_ROW_SCORES"] = "1"  # wherever supported (the default; pinned)
     try:
         tel = t(el, dev).requires_grad_(True)
         H, F = ar.shape
