@@ -1329,6 +1329,11 @@ def main():
     dist = world > 1
     if args.dry_run:
         return dry_run(world, rank)
+    # stdout carries exactly the one JSON line: what libraries write to fd 1 (RCCL's
+    # version banner at communicator setup) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if dist:
         import torch.distributed as tdist
 
@@ -1478,7 +1483,8 @@ def main():
         if cpu_bip1m is not None:
             cb["bip1m"] = cpu_bip1m
         out["cpu_baseline"] = cb
-    print(json.dumps(out), flush=True)
+    sys.stdout.flush()
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist:
         tdist.destroy_process_group()
 
