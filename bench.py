@@ -490,9 +490,10 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
         "msha_edge_attention_bwd_rows": [tmpl("edge_attn_bwd_rows(_gl)?_kernel")],
         "msha_csc_aggregate": [tmpl("csc_aggregate_kernel")],
-        "msha_bip_attention_fwd": [tmpl("bip_fwd_kernel") + (rf"(ELb{int(lay.v_branch)}E|, bool, E, false>)"
+        # (<H, F, T, HS, ATTD, HT>: profiles before the HT flag end at ATTD)
+        "msha_bip_attention_fwd": [tmpl("bip_fwd_kernel") + (rf"(Lb{int(lay.v_branch)}E|, bool, E, false(, \d+)?>)"
                                                              if bf else
-                                                             rf", {str(lay.v_branch).lower()}, false>")],
+                                                             rf", {str(lay.v_branch).lower()}, false(, \d+)?>")],
         "msha_bip_attention_bwd": [tmpl("bip_bwd_kernel")],
     }
     out = []
@@ -539,8 +540,8 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
         fb = bip_fwd_bytes(n, m, e, H, F, s, hs=lay.v_branch)
         # (<H, F, T, HS, ATTD>; rocprofv3 demangles some bf16 instances as "bool _Accum")
         bpat = ((rf"bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(lay.v_branch)}E|<{H}, {F}, bool _Accum, "
-                 rf"bool, E, false>)") if s == 2 else
-                rf"bip_fwd_kernel<{H}, {F}, float, {str(lay.v_branch).lower()}, false>")
+                 rf"bool, E, false(, \d+)?>)") if s == 2 else
+                rf"bip_fwd_kernel<{H}, {F}, float, {str(lay.v_branch).lower()}, false(, \d+)?>")
         tr, src = pmc_lookup([bpat], f"*{workload}_v*") if workload else (None, None)
     else:
         fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
