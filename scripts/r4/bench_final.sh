@@ -9,4 +9,4 @@ tail -1 gpurun_out/r4f/smoke2.log
 timeout -k 10 600 python -u bench.py > gpurun_out/r4f/bench_final.json 2> gpurun_out/r4f/bench_final.err \
   || { tail -20 gpurun_out/r4f/bench_final.err; exit 1; }
 wc -l gpurun_out/r4f/bench_final.json
-python scripts/bench_brief.py gpurun_out/r4f/bench_final.json | head -24
+python scripts/bench_brief.py gpurun_out/r4f/bench_final.json
