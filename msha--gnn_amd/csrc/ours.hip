@@ -551,6 +551,7 @@ __global__ void __launch_bounds__(256) ours_bwd_gather_reduce_kernel(int64_t B, 
 //   tree; the batch sources sit in LDS for the repeated-source scans.
 constexpr int kFinishLds = 2048;
 constexpr int kFinishKB = 8;  // items per wave whose loads are issued together
+constexpr int kFinishBg = 4096;  // floats of bgrad staged in LDS between the mode-0 phases
 
 template <typename T>
 __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
@@ -560,9 +561,45 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
   __shared__ int64_t s_src[kFinishLds];
   __shared__ int32_t s_next[kFinishLds];  // next batch entry with the same source, -1 = none
   __shared__ int32_t s_first[kFinishLds];  // first batch entry of its source
+  __shared__ float s_bg[kFinishBg];         // mode 0: bgrad between the phases
   const int H = a.H, F = a.F, D = H * F;
   const int64_t B = a.B;
   const bool in_lds = B <= kFinishLds;
+  // Mode 0 is one workgroup walking a chain of dependent phases; the loads that depend on
+  // no phase are issued here, so their latencies (the group-size lookups are two deep)
+  // overlap the batch-source staging instead of adding to the chain: the scalar chain's
+  // per-(b, h) statistics and group sizes (a thread per item), and the h2 values of the
+  // da3s / da4s sums (a wave per output, a lane per batch entry).
+  const int nwv = (int)blockDim.x >> 6, lid = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bool pre2 = mode == 0 && B * H <= (int64_t)blockDim.x;
+  const bool pre4 = mode == 0 && B <= 64 && D <= nwv * kFinishKB;
+  float pS = 0.f, pE3 = 0.f, pE4 = 0.f, pP3 = 0.f, pP4 = 0.f, pc3 = 0.f, pc4 = 0.f;
+  if (pre2 && threadIdx.x < B * H) {
+    const int64_t b = threadIdx.x / H;
+    const int64_t i = a.src[b];
+    const float* st = bstat + (int64_t)threadIdx.x * BS_N;
+    pS = st[BS_SUM];
+    pE3 = st[BS_E3];
+    pE4 = st[BS_E4];
+    pP3 = st[BS_PRE3];
+    pP4 = st[BS_PRE4];
+    const int32_t g3 = a.gid3[i], g4 = a.gid4[i];
+    pc3 = (float)(a.gptr3[g3 + 1] - a.gptr3[g3]);
+    pc4 = (float)(a.gptr4[g4 + 1] - a.gptr4[g4]);
+  }
+  float px[kFinishKB];
+#pragma unroll
+  for (int k = 0; k < kFinishKB; ++k) px[k] = 0.f;
+  if (pre4 && lid < B) {
+    const int64_t ib = a.src[lid];
+#pragma unroll
+    for (int k = 0; k < kFinishKB; ++k) {
+      const int t = wid + k * nwv;
+      if (t < D) px[k] = ldt<T>(a.h2, ib * D + t);
+    }
+  }
+  const bool bg_lds = mode == 0 && B * H * 4 <= kFinishBg;
+  float* const bg = bg_lds ? s_bg : bgrad;
   if (in_lds)
     for (int64_t t = threadIdx.x; t < B; t += blockDim.x) {
       s_src[t] = a.src[t];
@@ -632,8 +669,8 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
         const float dw4 = wave_xor_sum<1>(d4[k]);
         const int64_t t = t0 + (int64_t)k * nw;
         if (lane == 0 && t < nt) {
-          bgrad[t * 4 + 0] = dw3;
-          bgrad[t * 4 + 1] = dw4;
+          bg[t * 4 + 0] = dw3;
+          bg[t * 4 + 1] = dw4;
         }
       }
     }
@@ -643,28 +680,36 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     for (int64_t t = threadIdx.x; t < nt; t += blockDim.x) {
       const int64_t b = t / H;
       const int h = (int)(t % H);
-      const int64_t i = SRC(b);
-      const float dw3 = bgrad[t * 4 + 0], dw4 = bgrad[t * 4 + 1];
-      const float* st = bstat + (b * H + h) * BS_N;
-      const float sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
-      const float c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
-      const float c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
+      const float dw3 = bg[t * 4 + 0], dw4 = bg[t * 4 + 1];
+      float sum, E3, E4, c3, c4, p3, p4;
+      if (pre2) {
+        sum = pS, E3 = pE3, E4 = pE4, c3 = pc3, c4 = pc4, p3 = pP3, p4 = pP4;
+      } else {
+        const int64_t i = SRC(b);
+        const float* st = bstat + (b * H + h) * BS_N;
+        sum = st[BS_SUM], E3 = st[BS_E3], E4 = st[BS_E4];
+        c3 = (float)(a.gptr3[a.gid3[i] + 1] - a.gptr3[a.gid3[i]]);
+        c4 = (float)(a.gptr4[a.gid4[i] + 1] - a.gptr4[a.gid4[i]]);
+        p3 = st[BS_PRE3], p4 = st[BS_PRE4];
+      }
       const float dsum = -(dw3 * E3 + dw4 * E4) / (sum * sum);
       const float dE3 = dw3 / sum + dsum * c3;
       const float dE4 = dw4 / sum + dsum * c4;
-      const float p3 = st[BS_PRE3], p4 = st[BS_PRE4];
-      float* o = bgrad + t * 4;
+      float* o = bg + t * 4;
       o[0] = dE3 * E3 * (p3 > 0.f ? 1.f : a.slope);
       o[1] = dE4 * E4 * (p4 > 0.f ? 1.f : a.slope);
       o[2] = dsum;
+      o[3] = 0.f;
     }
     __syncthreads();
+    if (bg_lds)  // the (B, H, 4) output, for mode 1
+      for (int64_t t = threadIdx.x; t < nt * 4; t += blockDim.x) bgrad[t] = s_bg[t];
     for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
       const int64_t b = t / H;
       const int h = (int)(t % H);
       if (!is_first(b)) continue;
       float s = 0.f;
-      for (int64_t q = b; q >= 0; q = next_same(q)) s += bgrad[(q * H + h) * 4 + 2];
+      for (int64_t q = b; q >= 0; q = next_same(q)) s += bg[(q * H + h) * 4 + 2];
       row_coef[SRC(b) * H + h] = s;
     }
     // da3s[t] = sum_b dpre3_b h2_b[t] (da4s): a wave per output, lanes across b,
@@ -681,9 +726,10 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
           const int64_t t = t0 + (int64_t)k * nw;
           const bool ok = t < D;
           const int h = ok ? (int)(t / F) : 0;
-          x[k] = ok ? ldt<T>(a.h2, ib * D + t) : 0.f;
-          w3[k] = ok ? bgrad[(b * H + h) * 4 + 0] : 0.f;
-          w4[k] = ok ? bgrad[(b * H + h) * 4 + 1] : 0.f;
+          // (pre4: one pass, t0 = wave, b = lane: the values loaded at entry)
+          x[k] = pre4 ? px[k] : ok ? ldt<T>(a.h2, ib * D + t) : 0.f;
+          w3[k] = ok ? bg[(b * H + h) * 4 + 0] : 0.f;
+          w4[k] = ok ? bg[(b * H + h) * 4 + 1] : 0.f;
         }
 #pragma unroll
         for (int k = 0; k < kFinishKB; ++k) {
