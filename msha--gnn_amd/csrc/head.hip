@@ -916,34 +916,41 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
   constexpr int U = 4;  // elements per thread whose loads are in flight together
   for (int64_t e0 = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; e0 < total;
        e0 += U * stride) {
-    float4 x[U], dz[U];
+    float4 x[U];
     uint8_t nz[U];
+    int64_t ri[U];
+    int rc[U];
 #pragma unroll
     for (int t = 0; t < U; ++t) {
       const int64_t e = e0 + t * stride;
-      const int64_t i = e < total ? e / q : 0;
+      // (row, channel) of element e: a 32-bit division where e fits (a 64-bit one is a
+      // ~100-instruction sequence, and there is one per float4)
+      const int64_t i = e >= total ? 0 : total < (int64_t)INT32_MAX ? (int64_t)((uint32_t)e / (uint32_t)q)
+                                                                      : e / q;
       const int c = 4 * (int)(e - i * q);
+      ri[t] = i;
+      rc[t] = c;
       x[t] = e < total ? ld4(u + i * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       nz[t] = e < total ? ws.rflag[i] : 0;
-      // dz of a zero row is never written: loaded anyway (in flight with the rest) and
-      // not used
-      dz[t] = e < total ? *reinterpret_cast<const float4*>(ws.dz + i * HF + c)
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int t = 0; t < U; ++t) {
       const int64_t e = e0 + t * stride;
       if (e >= total) break;
-      const int64_t i = e / q;
-      const int c = 4 * (int)(e - i * q);
+      const int64_t i = ri[t];
+      const int c = rc[t];
       const float xs[4] = {x[t].x, x[t].y, x[t].z, x[t].w};
-      const float dzs[4] = {dz[t].x, dz[t].y, dz[t].z, dz[t].w};
+      // dz exists only for the rows the loss reaches (64 of ~39k at R15): read for those
+      // alone (a dz pass over every row was a third of the kernel's bytes)
+      const float4 d4 = nz[t] ? *reinterpret_cast<const float4*>(ws.dz + i * HF + c)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float dzs[4] = {d4.x, d4.y, d4.z, d4.w};
       float r[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ch = c + k;
         const float xh = (xs[k] - cf[ch]) * cf[HF + ch];
-        r[k] = cf[2 * HF + ch] * ((nz[t] ? dzs[k] : 0.f) - cf[3 * HF + ch] - xh * cf[4 * HF + ch]);
+        r[k] = cf[2 * HF + ch] * (dzs[k] - cf[3 * HF + ch] - xh * cf[4 * HF + ch]);
       }
       st4(du + i * HF + c, make_float4(r[0], r[1], r[2], r[3]));
     }
