@@ -866,8 +866,12 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
   const float* sdb = red + nW + nV;
   const float* sdbx = sdb + HF;
   const float* st = a.stats;
+  // one LDS image for both roles (block 0: v and d v_out; the row blocks: coefficients),
+  // so the row blocks are not sized by block 0's staging: 32 KB a block, 5 per CU
+  __shared__ __attribute__((aligned(16))) float sm[2 * kHeadVStage];
   if (blockIdx.x == 0) {
-    __shared__ float vs[kHeadVStage], gs[kHeadVStage];
+    float* vs = sm;
+    float* gs = sm + kHeadVStage;
     const bool staged = M * HF <= kHeadVStage;
     if (staged) {
       lds_copy(vs, v, M * HF);
@@ -900,7 +904,7 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
     return;
   }
   // per-channel coefficients in LDS: mean, invstd, w * invstd, sum dz / N, sum dz xhat / N
-  __shared__ float cf[5 * 512];
+  float* cf = sm;  // 5 * HF <= 2560 floats
   const float invN = 1.f / (float)a.N;
   for (int c = threadIdx.x; c < HF; c += blockDim.x) {
     cf[c] = st[c];
@@ -913,7 +917,7 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
   const int q = HF / 4;  // float4 groups per row (HF % 4 == 0, checked by the caller)
   const int64_t total = a.N * q;
   const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
-  constexpr int U = 4;  // elements per thread whose loads are in flight together
+  constexpr int U = 8;  // elements per thread whose loads are in flight together
   for (int64_t e0 = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; e0 < total;
        e0 += U * stride) {
     float4 x[U];
@@ -1185,7 +1189,7 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
   hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 255) / 256)), dim3(256), 0, s, a,
                      w, nw, dW, dzero, dzero != nullptr ? n_zero : 0);
-  const dim3 ga(1 + grid_for(a.N * a.HF / 4, 256 * 4, 1024));
+  const dim3 ga(1 + grid_for(a.N * a.HF / 4, 256 * 8, 1024));
   if (bf)
     hipLaunchKernelGGL(head_bwd_apply_kernel<bf16_t>, ga, dim3(256), 0, s, a, (const bf16_t*)u,
                        (const bf16_t*)v, w, (bf16_t*)du, (bf16_t*)dv);
