@@ -801,40 +801,42 @@ __global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBw
   if (blockIdx.x == 0)  // the out_att score vector's (exactly zero) gradient
     for (int64_t e = threadIdx.x; e < n_zero; e += blockDim.x) dzero[e] = 0.f;
   __shared__ int list[kHeadBwdWaves];
-  __shared__ int cnt[257];
-  // ordered compaction of the wave flags (each thread a contiguous slice of them)
-  const int per = (nw + 255) / 256;
+  __shared__ int wsum[4];
+  // ordered compaction of the wave flags: each thread a contiguous slice of them (its
+  // flags loaded together into a bit mask), the slice counts scanned by wave shuffles
+  // (a serial scan over 256 counts on one lane was a chain of LDS round trips)
+  const int per = (nw + 255) / 256;  // <= kHeadBwdWaves / 256 = 16
   const int b0 = threadIdx.x * per;
-  int c = 0;
-  for (int b = b0; b < b0 + per && b < nw; ++b) c += ws.wflag[b];
-  cnt[threadIdx.x] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int q = 0; q < 256; ++q) {
-      const int x = cnt[q];
-      cnt[q] = run;
-      run += x;
-    }
-    cnt[256] = run;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t bits = 0;
+  for (int q = 0; q < per; ++q)
+    if (b0 + q < nw && ws.wflag[b0 + q]) bits |= 1u << q;
+  const int c = __popc(bits);
+  int x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
+  if (lane == 63) wsum[w] = x;
   __syncthreads();
-  int pos = cnt[threadIdx.x];
-  for (int b = b0; b < b0 + per && b < nw; ++b)
-    if (ws.wflag[b]) list[pos++] = b;
+  int pos = x - c;
+  for (int q = 0; q < w; ++q) pos += wsum[q];
+  for (int q = 0; q < per; ++q)
+    if ((bits >> q) & 1u) list[pos++] = b0 + q;
   __syncthreads();
-  const int nl = cnt[256];
+  const int nl = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= PT) return;
   float sum = 0.f;
   int l = 0;
-  for (; l + 8 <= nl; l += 8) {  // 8 partials in flight, added in list order
-    float v[8];
+  for (; l + 16 <= nl; l += 16) {  // 16 partials in flight, added in list order
+    float v[16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = ws.part[(int64_t)list[l + q] * PT + t];
+    for (int q = 0; q < 16; ++q) v[q] = ws.part[(int64_t)list[l + q] * PT + t];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) sum += v[q];
+    for (int q = 0; q < 16; ++q) sum += v[q];
   }
   for (; l < nl; ++l) sum += ws.part[(int64_t)list[l] * PT + t];
   ws.red[t] = sum;
