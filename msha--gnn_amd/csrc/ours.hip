@@ -610,8 +610,11 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
   if (in_lds) {
     // every (b, q) pair of the batch at once (one LDS min per match), instead of a
     // serial scan per entry: next = the smallest later entry with b's source
-    for (int64_t t = threadIdx.x; t < B * B; t += blockDim.x) {
-      const int64_t b = t / B, q = t % B;
+    // (32-bit index math here and below: B <= kFinishLds, B * H < 2^31 (check()); a
+    // 64-bit division is a ~100-instruction sequence and these phases are issue-bound)
+    const int Bi = (int)B;
+    for (int t = threadIdx.x; t < Bi * Bi; t += blockDim.x) {
+      const int b = t / Bi, q = t - b * Bi;
       if (q != b && s_src[q] == s_src[b]) {
         if (q < b) s_first[b] = 0;
         else atomicMin(&s_next[b], (int32_t)q);
@@ -651,8 +654,9 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
         for (int k = 0; k < kFinishKB; ++k) {
           const int64_t t = t0 + (int64_t)k * nw;
           const bool ok = t < nt && f < F;
-          const int64_t b = ok ? t / H : 0;
-          const int h = ok ? (int)(t % H) : 0;
+          const int ti = ok ? (int)t : 0;
+          const int64_t b = ti / H;
+          const int h = ti - (int)b * H;
           x[k] = ok ? ldt<T>(a.h2, SRC(b) * D + h * F + f) : 0.f;
           g3[k] = ok ? G[(b * 2 + 0) * D + h * F + f] : 0.f;
           g4[k] = ok ? G[(b * 2 + 1) * D + h * F + f] : 0.f;
@@ -678,8 +682,8 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     // the scalar chain, a thread per (b, h) (its dependent group-size loads overlap
     // across threads; on one lane per wave they ran one item after another)
     for (int64_t t = threadIdx.x; t < nt; t += blockDim.x) {
-      const int64_t b = t / H;
-      const int h = (int)(t % H);
+      const int64_t b = (int)t / H;
+      const int h = (int)t - (int)b * H;
       const float dw3 = bg[t * 4 + 0], dw4 = bg[t * 4 + 1];
       float sum, E3, E4, c3, c4, p3, p4;
       if (pre2) {
@@ -705,8 +709,8 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     if (bg_lds)  // the (B, H, 4) output, for mode 1
       for (int64_t t = threadIdx.x; t < nt * 4; t += blockDim.x) bgrad[t] = s_bg[t];
     for (int64_t t = threadIdx.x; t < B * H; t += blockDim.x) {
-      const int64_t b = t / H;
-      const int h = (int)(t % H);
+      const int64_t b = (int)t / H;
+      const int h = (int)t - (int)b * H;
       if (!is_first(b)) continue;
       float s = 0.f;
       for (int64_t q = b; q >= 0; q = next_same(q)) s += bg[(q * H + h) * 4 + 2];
@@ -725,7 +729,7 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
         for (int k = 0; k < kFinishKB; ++k) {
           const int64_t t = t0 + (int64_t)k * nw;
           const bool ok = t < D;
-          const int h = ok ? (int)(t / F) : 0;
+          const int h = ok ? (int)t / F : 0;
           // (pre4: one pass, t0 = wave, b = lane: the values loaded at entry)
           x[k] = pre4 ? px[k] : ok ? ldt<T>(a.h2, ib * D + t) : 0.f;
           w3[k] = ok ? bg[(b * H + h) * 4 + 0] : 0.f;
@@ -777,6 +781,7 @@ static int check(const msha_graph* g, const msha_groups* grp, int64_t B, const i
                      grp->gmem4 && grp->n_nodes == g->n_rows,
                  "ours: group CSR missing or not over the graph's rows");
   MSHA_ARG_CHECK(B >= 0 && (B == 0 || src), "ours: batch missing");
+  MSHA_ARG_CHECK(B * (int64_t)heads < INT32_MAX, "ours: batch * heads must be < 2^31");
   MSHA_ARG_CHECK(heads > 0 && feat > 0 && heads * feat <= kMaxD, "ours: heads*feat must be <= 512");
   return MSHA_OK;
 }
