@@ -1295,6 +1295,133 @@ def _world1_group(dev):
     return done
 
 
+LINE_MAX_BYTES = 12 * 1024  # the stdout line; the driver keeps only a tail of stdout
+
+
+def _finite(o):
+    """A copy of ``o`` with every non-finite float replaced by None (strict JSON)."""
+    if isinstance(o, float):
+        return o if np.isfinite(o) else None
+    if isinstance(o, dict):
+        return {k: _finite(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_finite(v) for v in o]
+    if isinstance(o, (np.floating, np.integer)):
+        return _finite(o.item())
+    return o
+
+
+def _sig(x, digits=4):
+    """Float rounded to ``digits`` significant digits (None for missing / non-finite)."""
+    if x is None:
+        return None
+    x = float(x)
+    if not np.isfinite(x):
+        return None
+    if x == 0.0:
+        return 0.0
+    return float(f"{x:.{digits}g}")
+
+
+def dumps_line(obj) -> str:
+    """Strict single-line JSON (no NaN/Infinity tokens)."""
+    return json.dumps(_finite(obj), separators=(",", ":"), allow_nan=False)
+
+
+_KSHORT = {"msha_edge_attention_fwd": "fwd", "msha_edge_attention_bwd_fused": "bwd",
+           "msha_edge_attention_bwd_rows": "bwd_rows", "msha_csc_aggregate": "csc",
+           "msha_bip_attention_fwd": "bip_fwd", "msha_bip_attention_bwd": "bip_bwd"}
+
+
+def compact_line(out: dict, detail_path: str) -> dict:
+    """The stdout line: the contract keys, the headline roofline and CPU baseline, and a
+    compact ``legs`` map (per leg value / ms_per_step / frac / traffic) plus each leg's
+    edge-kernel HBM fractions; everything else stays in ``detail_path``."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+    line = {k: out[k] for k in keep if k in out}
+    line["value"], line["ms_per_step"] = _sig(out["value"], 6), _sig(out["ms_per_step"], 5)
+    rk = out.get("ranks") or {}
+    line["ranks"] = {"world_size": rk.get("world_size"), "backend": rk.get("backend"),
+                     "ranks": [{k: r.get(k) for k in ("rank", "local_rank", "device",
+                                                      "pci_bus_id") if k in r}
+                               for r in rk.get("ranks", [])]}
+    ro = out.get("roofline") or {}
+    line["roofline"] = {k: (_sig(ro.get(k)) if isinstance(ro.get(k), float) else ro.get(k))
+                        for k in ("kernel", "bound", "achieved", "peak", "unit", "frac",
+                                  "traffic", "algorithmic_bytes_per_launch", "avg_launch_us")}
+    legs, kfrac = {}, {}
+
+    def leg(name, d, unit=None):
+        if not d:
+            return
+        r = d.get("roofline") or {}
+        legs[name] = {"value": _sig(d.get("value")), "ms_per_step": _sig(d.get("ms_per_step")),
+                      "frac": _sig(r.get("frac"), 3), "traffic": _sig(r.get("traffic"))}
+        if unit:
+            legs[name]["unit"] = unit
+        ks = {_KSHORT.get(k["kernel"], k["kernel"]): _sig(k.get("frac"), 3)
+              for k in d.get("edge_kernels", [])}
+        if ks:
+            kfrac[name] = ks
+
+    leg("c4_f32", out)
+    leg("c4_f32_dropout", out.get("dropout_p05"))
+    leg("c4_bf16", out.get("bf16"))
+    for big in ("syn2m", "bip1m"):
+        for tag, d in (out.get(big) or {}).items():
+            leg(f"{big}_{tag}", d)
+    ls = out.get("link_score")
+    for tag, d in (("f32", ls), ("bf16", (ls or {}).get("bf16"))):
+        if not d:
+            continue
+        for mode in ("mlp", "inner"):
+            r = d.get(f"roofline_{mode}") or {}
+            legs[f"link_{mode}_{tag}"] = {
+                "value": _sig(d.get(f"pairs_per_sec_{mode}")),
+                "ms_per_step": _sig(d.get(f"ms_per_batch_{mode}")),
+                "frac": _sig(r.get("frac"), 3),
+                "traffic": _sig((r.get("memory") or {}).get("traffic")), "unit": "pairs/s"}
+            for v in ("overlapped", "amortised"):
+                legs[f"link_{mode}_{tag}_{v}"] = {
+                    "value": _sig(d.get(f"pairs_per_sec_{mode}_{v}")),
+                    "ms_per_step": _sig(d.get(f"ms_per_batch_{mode}_{v}")), "unit": "pairs/s"}
+        legs[f"link_allgather_{tag}"] = {"ms_per_step": _sig(d.get("allgather_ms")),
+                                         "world": d.get("world")}
+    for key, tag in (("train_step_configs1", "graphed"), ("train_step_configs2", "graphed")):
+        for r in (out.get(key) or {}).get("runs", []):
+            dt = "bf16" if "bfloat16" in str(r.get("dtype")) else "f32"
+            legs[f"step_{r['model']}_{r['year']}_{dt}"] = {
+                "value": _sig(r.get("edges_per_sec")), "ms_per_step": _sig(r.get("ms_per_step")),
+                "ms_eager": _sig(r.get("ms_per_step_eager"))}
+    for r in (out.get("train_py_literal") or {}).get("runs", []):
+        legs[f"trainpy_{r['model']}"] = {"value": _sig(r.get("edges_per_sec")),
+                                         "ms_per_step": _sig(r.get("ms_per_step"))}
+    line["legs"] = legs
+    line["kernel_frac"] = kfrac
+    cb = out.get("cpu_baseline")
+    if cb:
+        c = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample")}
+        c["value"] = _sig(c["value"])
+        c["host"] = (cb.get("host") or {}).get("model")
+        other = {}
+        if cb.get("configs1_ablation3"):
+            other["configs1_ablation3"] = {"value": _sig(cb["configs1_ablation3"]["value"]),
+                                           "unit": "s/step"}
+        if cb.get("link_score"):
+            other["link_mlp"] = {"value": _sig(cb["link_score"]["pairs_per_sec_mlp"]),
+                                 "unit": "pairs/s"}
+            other["link_inner"] = {"value": _sig(cb["link_score"]["pairs_per_sec_inner"]),
+                                   "unit": "pairs/s"}
+        if cb.get("bip1m"):
+            other["bip1m"] = {"value": _sig(cb["bip1m"]["value"]), "unit": "edges/s"}
+        if other:
+            c["other"] = other
+        line["cpu_baseline"] = c
+    line["detail"] = detail_path
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1311,6 +1438,8 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="report the eager launches (no HIP-graph replay of the timed steps)")
     ap.add_argument("--no-dropout-leg", action="store_true")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where the full per-leg detail goes (stdout carries the compact line)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: rehearse the rank launch and the sharded table exchange over "
                          "gloo on the CPU (tests)")
@@ -1484,8 +1613,15 @@ def main():
         if cpu_bip1m is not None:
             cb["bip1m"] = cpu_bip1m
         out["cpu_baseline"] = cb
+    detail = args.detail
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+        with open(detail, "w") as fh:
+            json.dump(_finite(out), fh, indent=1)
+    except OSError as ex:
+        print(f"bench.py: could not write {detail}: {ex}", file=sys.stderr)
     sys.stdout.flush()
-    os.write(json_fd, (json.dumps(out) + "\n").encode())
+    os.write(json_fd, (dumps_line(compact_line(out, detail)) + "\n").encode())
     if dist:
         tdist.destroy_process_group()
 

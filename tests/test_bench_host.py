@@ -157,3 +157,51 @@ def test_gpus_flag_mismatch_fails():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--dry-run"], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
+
+
+def _maximal_out():
+    """The round-4 builder line (every leg present, 23 KB) widened to 8 ranks with a NaN
+    and an infinity planted: the largest dict main() can hand to compact_line."""
+    import copy
+    import json
+
+    d = json.load(open(os.path.join(ROOT, "profiles", "round4_final", "bench_line.json")))
+    d = copy.deepcopy(d)
+    r0 = d["ranks"]["ranks"][0]
+    d["ranks"] = {"world_size": 8, "backend": "nccl (RCCL)",
+                  "ranks": [dict(r0, rank=i, local_rank=i, device=f"cuda:{i}",
+                                 pci_bus_id=f"0000:{0x10 + i:02x}:00") for i in range(8)]}
+    d["roofline"]["traffic"] = float("nan")
+    d["bip1m"]["f32"]["roofline"]["frac"] = float("inf")
+    return d
+
+
+def test_bench_line_is_small_strict_json():
+    """the stdout line stays <= 12 KB, is strict JSON (no NaN/Infinity
+    tokens) and carries the contract keys, roofline, cpu_baseline and the compact legs."""
+    import json
+
+    out = _maximal_out()
+    s = bench.dumps_line(bench.compact_line(out, "gpurun_out/bench_detail.json"))
+    assert "\n" not in s
+    assert len(s.encode()) <= bench.LINE_MAX_BYTES, len(s)
+    assert len(s.encode()) <= 8 * 1024  # the driver's stdout tail
+
+    def bad(tok):
+        raise ValueError(tok)
+
+    line = json.loads(s, parse_constant=bad)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype",
+              "config", "ranks", "roofline", "cpu_baseline", "legs", "higher_is_better",
+              "scaling", "vs_baseline", "data"):
+        assert k in line, k
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    assert line["roofline"]["traffic"] is None  # the planted NaN
+    assert len(line["ranks"]["ranks"]) == 8
+    legs = line["legs"]
+    for k in ("c4_f32", "c4_bf16", "syn2m_f32", "syn2m_bf16", "bip1m_f32", "bip1m_bf16",
+              "link_mlp_f32", "link_inner_bf16_overlapped", "step_Ours_2015_f32",
+              "step_ablation3_2015_f32", "step_Ours_2018_bf16", "trainpy_Ours"):
+        assert k in legs, k
+    assert legs["bip1m_f32"]["frac"] is None  # the planted infinity
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
