@@ -483,7 +483,8 @@ MSHA_API int msha_bn_lrelu_bwd(int64_t rows, int32_t channels, int32_t dtype, co
  * act bits: 1 bias, 2 relu, 4 dropout(drop_p, seed, offset), 8 sigmoid.
  * g_rows / g2_rows: the row counts of G / G2 (every gi / gj index below them; 0 =
  * unknown).  Known counts whose tables fit 4 GiB select the gather kernel with 32-bit
- * buffer offsets (an index past the table then reads zeros). */
+ * buffer offsets (an index outside [0, rows) then reads zeros: negative indices are not
+ * wrapped as torch indexing would wrap them, so callers pass valid indices). */
 MSHA_API int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const float* G, int64_t ldg,
                               const int64_t* gi, const float* G2, int64_t ldg2,
                               const int64_t* gj, int64_t g_rows, int64_t g2_rows,

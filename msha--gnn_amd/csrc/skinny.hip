@@ -775,15 +775,19 @@ __global__ void __launch_bounds__(256 * WPS) pair_roll_kernel(
     b = gj[row];
   };
   // byte offsets of this lane's first 4 columns of the two rows (< 4 GiB: the host's check).
-  // An index outside [0, 2^31) maps past the window (reads zeros); the test also keeps
+  // An index outside [0, rows) maps past the window (reads zeros); the test also keeps
   // the index's high word live, so the register allocator does not put the offset into
   // the dead high half of the NEXT index load's destination (a write that would wait on
   // that load: vmcnt(0) at every tile start)
+  // (the row counts behind the windows: an index at or past them, or negative, reads
+  // zeros instead of wrapping its byte offset past 4 GiB back into the table)
+  const uint64_t rows_a = ((uint64_t)bytes_a - 4 * K) / (4 * (uint64_t)ldg) + 1;
+  const uint64_t rows_b = ((uint64_t)bytes_b - 4 * K) / (4 * (uint64_t)ldg2) + 1;
   auto offset_a = [&](int64_t a) -> uint32_t {
-    return (a >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((a * ldg + 4 * g) * 4);
+    return (uint64_t)a >= rows_a ? 0xFFFFFFF0u : (uint32_t)((a * ldg + 4 * g) * 4);
   };
   auto offset_b = [&](int64_t b) -> uint32_t {
-    return (b >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((b * ldg2 + 4 * g) * 4);
+    return (uint64_t)b >= rows_b ? 0xFFFFFFF0u : (uint32_t)((b * ldg2 + 4 * g) * 4);
   };
   auto mfma_tile = [&](int t, u32x4_t* ci, u32x4_t* cj, uint32_t na, uint32_t nb) {
     f32x4 acc[Gm::NB];
@@ -948,13 +952,15 @@ __global__ void __launch_bounds__(256 * WPS) pair_x3_kernel(
     a = gi[row];
     b = gj[row];
   };
-  // this lane's first 8 columns of each row (index outside [0, 2^31): past the window;
+  // this lane's first 8 columns of each row (index outside [0, rows): past the window;
   // the test keeps the index's high word live, see pair_roll_kernel)
+  const uint64_t rows_a = ((uint64_t)bytes_a - 4 * K) / (4 * (uint64_t)ldg) + 1;
+  const uint64_t rows_b = ((uint64_t)bytes_b - 4 * K) / (4 * (uint64_t)ldg2) + 1;
   auto offset_a = [&](int64_t a) -> uint32_t {
-    return (a >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((a * ldg + 8 * g) * 4);
+    return (uint64_t)a >= rows_a ? 0xFFFFFFF0u : (uint32_t)((a * ldg + 8 * g) * 4);
   };
   auto offset_b = [&](int64_t b) -> uint32_t {
-    return (b >> 31) != 0 ? 0xFFFFFFF0u : (uint32_t)((b * ldg2 + 8 * g) * 4);
+    return (uint64_t)b >= rows_b ? 0xFFFFFFF0u : (uint32_t)((b * ldg2 + 8 * g) * 4);
   };
   // slot 2 s + j: step s's columns [32 s + 8 g + 4 j, +4) at byte 128 s + 16 j
   auto slot_off = [](int i) -> uint32_t { return 128u * (i >> 1) + 16u * (i & 1); };

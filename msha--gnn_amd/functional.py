@@ -106,7 +106,14 @@ _WS: dict = {}  # (device index, stream) -> uint8 scratch tensor
 def _workspace(dev, nbytes: int):
     """A scratch buffer of at least ``nbytes`` for one call's launches, shared by every
     call on the same device and stream (the library's workspaces are transient within a
-    call; stream order keeps consecutive users apart)."""
+    call; stream order keeps consecutive users apart).
+
+    Under HIP-graph capture every call gets a fresh buffer from the graph's private pool:
+    a cached buffer recorded into a graph could later be replaced (and freed) by a larger
+    eager request while replays still write to it, and capture streams are pooled handles
+    whose keys can collide with an eager stream's."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
     key = (dev.index, _lib.stream_handle(dev))
     t = _WS.get(key)
     if t is None or t.numel() < nbytes:

@@ -109,8 +109,21 @@ class Adam(torch.optim.Optimizer):
                       float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
                       self._workspace(dev).data_ptr(), _lib.stream_handle(dev))
 
+    def _check_groups(self):
+        # a loaded torch.optim.Adam state_dict may carry flags this kernel does not run
+        for g in self.param_groups:
+            bad = [k for k in ("amsgrad", "maximize", "differentiable") if g.get(k)]
+            if bad:
+                raise NotImplementedError(f"msha Adam: {', '.join(bad)} set in a parameter "
+                                          "group (loaded state_dict?)")
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._check_groups()
+
     @torch.no_grad()
     def step(self, closure=None):
+        self._check_groups()
         loss = None
         if closure is not None:
             with torch.enable_grad():

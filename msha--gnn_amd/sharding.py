@@ -58,7 +58,9 @@ class ShardedTable:
         self.fulls = [torch.empty(self.R * world, feat, device=device, dtype=dtype)
                       for _ in range(max(1, buffers))]
         self.cur = 0
-        if _group_ready(group, world):
+        if dist.is_available() and dist.is_initialized() and (group is not None or world > 1):
+            # world 1 without a group may copy its rows inside a larger job; any other table
+            # must match the group it will gather over
             gw = dist.get_world_size(group)
             if gw != world:
                 raise ValueError(f"ShardedTable: world {world} but the process group has {gw}")

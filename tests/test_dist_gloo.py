@@ -88,6 +88,13 @@ def _worker(rank, world, port, q):
         solo = sharding.ShardedTable(n, F, 1, 0, "cpu")
         solo.set_local(torch.as_tensor(h))
         ok = ok and solo.path() == "copy" and torch.equal(solo.gather(), torch.as_tensor(h))
+        # a world > 1 table that does not match the default group fails at construction
+        # with the world-size message, not later in path()
+        try:
+            sharding.ShardedTable(n, F, world + 1, rank, "cpu")
+            ok = False
+        except ValueError as ex:
+            ok = ok and "process group has" in str(ex)
         # bench.py's timing reduction: the max over ranks
         t = torch.tensor([0.5 + rank])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

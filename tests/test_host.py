@@ -229,14 +229,32 @@ def test_split_bf16_products_reach_fp32_accuracy():
     exact = x.astype(np.float64) * w.astype(np.float64)
     rel = np.abs(acc - exact) / np.abs(exact)
     assert rel.max() <= 2.0 ** -21, rel.max()  # a few fp32 ulps (the dropped ml, lm, ll)
-    # a 128-term dot product: within the exact-fp32 MFMA's error bound
+    # a 128-term dot product accumulated sequentially in fp32 in the kernels' order (per k,
+    # the six products small terms first): within the exact-fp32 dot's n u A bound with
+    # n = 128 -- the 768 split terms add no more error than the 128 fp32 products would
     X = x[:128 * 1000].reshape(1000, 128)
     Wv = w[:128 * 1000].reshape(1000, 128)
     sX, sW = split(X), split(Wv)
     pairs = ((2, 0), (0, 2), (1, 1), (0, 1), (1, 0), (0, 0))  # lh, hl, mm, hm, mh, hh
     dot = np.zeros(1000, np.float32)
-    for i, j in pairs:
-        dot = (dot + (sX[i] * sW[j]).astype(np.float32).sum(1, dtype=np.float32)).astype(np.float32)
+    for k in range(128):
+        for i, j in pairs:
+            dot = (dot + (sX[i][:, k] * sW[j][:, k]).astype(np.float32)).astype(np.float32)
     ref = (X.astype(np.float64) * Wv.astype(np.float64)).sum(1)
-    bound = 128 * 6 * 2.0 ** -24 * (np.abs(X.astype(np.float64) * Wv)).sum(1)
+    bound = 128 * 2.0 ** -24 * (np.abs(X.astype(np.float64) * Wv)).sum(1)
     assert np.all(np.abs(dot - ref) <= bound)
+
+
+def test_adam_rejects_loaded_unsupported_flags(msha):
+    """a torch.optim.Adam state_dict saved with amsgrad / maximize must not
+    silently run plain Adam after load_state_dict."""
+    import pytest
+    import torch
+
+    from msha_gnn_amd.optim import Adam
+
+    p = torch.nn.Parameter(torch.zeros(4))
+    ref = torch.optim.Adam([torch.nn.Parameter(torch.zeros(4))], amsgrad=True)
+    opt = Adam([p])
+    with pytest.raises(NotImplementedError, match="amsgrad"):
+        opt.load_state_dict(ref.state_dict())
