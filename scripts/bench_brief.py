@@ -19,8 +19,11 @@ def main(*paths):
 
 
 def brief(path):
-    lines = [ln for ln in open(path) if ln.startswith("{")]
-    d = json.loads(lines[-1])
+    text = open(path).read()
+    try:  # bench.py --detail file (indented JSON) or a log whose last '{' line is the line
+        d = json.loads(text)
+    except ValueError:
+        d = json.loads([ln for ln in text.splitlines() if ln.startswith("{")][-1])
     leg("head", d)
     for key in ("dropout_p05", "bf16"):
         if key in d:

@@ -140,3 +140,47 @@ def test_two_graphed_steps_keep_their_counters(cuda, msha):
     a.close()
     assert MF.rng_counter(cuda) is None
     assert msha._lib.load().msha_get_rng_counter(cuda.index) is None
+
+
+def test_captured_workspaces_survive_cache_growth(cuda, msha):
+    """workspaces recorded into a HIP graph belong to the graph's pool.  Two
+    graphs of different workspace needs, captured on one stream, replay the eager results
+    after an eager call on that stream grows (replaces) the shared scratch buffer and the
+    freed memory is scribbled over."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph
+
+    rng = np.random.default_rng(11)
+    s = torch.cuda.Stream()
+    cases = []
+    for n in (300, 20000):
+        c = random_counts(rng, n, 32, 20)
+        graph = Graph.from_dense(t(c, cuda))
+        el, er = t(rng.standard_normal((n, 2)), cuda), t(rng.standard_normal((32, 2)), cuda)
+        hc = t(rng.standard_normal((32, 2, 64)), cuda)
+        hs = t(rng.standard_normal((n, 2, 64)), cuda)
+        cases.append((graph, el, er, hc, hs))
+    s.wait_stream(torch.cuda.current_stream())
+    refs, graphs, outs = [], [], []
+    with torch.cuda.stream(s):
+        for graph, el, er, hc, hs in cases:
+            refs.append([x.clone() for x in MF.edge_attention(graph, el, er, hc, hs=hs)])
+    for graph, el, er, hc, hs in cases:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            assert torch.cuda.is_current_stream_capturing()
+            ws = MF._workspace(cuda, 1 << 20)
+            assert all(ws.data_ptr() != w.data_ptr() for w in MF._WS.values())
+            outs.append(MF.edge_attention(graph, el, er, hc, hs=hs))
+        graphs.append(g)
+    with torch.cuda.stream(s):
+        big = MF._workspace(cuda, 256 << 20)  # replaces the stream's cached buffer
+        big.fill_(0xFF)
+        junk = [torch.full((1 << 20,), float("nan"), device=cuda) for _ in range(8)]
+    torch.cuda.current_stream().wait_stream(s)
+    for g, o, r in zip(graphs, outs, refs):
+        g.replay()
+        torch.cuda.synchronize()
+        for a, b in zip(o, r):
+            assert torch.equal(a, b)
+    del junk
