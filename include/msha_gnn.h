@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 12
+#define MSHA_ABI_VERSION 13
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -85,6 +85,10 @@ typedef struct msha_graph {
    * (large graphs): the column pass writes it contiguously and the row pass gathers it
    * through this map (ABI 3). */
   const int32_t* csr_slot;
+  /* n_rows, graphs with n_cols <= 32 (ABI 13; nullable): bit j of rowmask[i] is set when
+   * row i has an edge to column j (virtual full rows: every column).  Built from the CSR
+   * by msha_graph_rowmask; the bipartite kernels walk these masks instead of col. */
+  const uint32_t* rowmask;
 } msha_graph;
 
 /* Same-group adjacency of the full MSHA layer (city and province, dataset.py:260-277
@@ -148,6 +152,9 @@ MSHA_API size_t msha_graph_workspace_size(int64_t n_rows, int64_t n_cols);
 MSHA_API int msha_graph_count(const float* adj, int64_t n_rows, int64_t n_cols, int32_t* rowptr,
                      int32_t* colptr, uint8_t* rowflag, void* ws, size_t ws_bytes,
                      msha_stream_t stream);
+/* rowmask[i] = OR over row i's CSR edges of (1 << col) for a graph with n_cols <= 32
+ * (g->rowptr, g->col; g->rowmask is not read).  ABI 13. */
+MSHA_API int msha_graph_rowmask(const msha_graph* g, uint32_t* rowmask, msha_stream_t stream);
 MSHA_API int msha_graph_fill(const float* adj, int64_t n_rows, int64_t n_cols, const int32_t* rowptr,
                     const int32_t* colptr, const uint8_t* rowflag, int32_t* col,
                     int32_t* csc_row, int32_t* csc_eid, void* ws, size_t ws_bytes,

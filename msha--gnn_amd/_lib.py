@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 12  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 13  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -31,7 +31,7 @@ class MshaGraph(C.Structure):
         ("n_chunks", C.c_int64), ("chunk_col", C.c_void_p), ("chunk_start", C.c_void_p),
         ("chunk_end", C.c_void_p),
         ("n_multi", C.c_int64), ("multi_col", C.c_void_p), ("multi_first", C.c_void_p),
-        ("multi_count", C.c_void_p), ("csr_slot", C.c_void_p),
+        ("multi_count", C.c_void_p), ("csr_slot", C.c_void_p), ("rowmask", C.c_void_p),
     ]
 
 
@@ -102,6 +102,7 @@ SIGNATURES = {
     "msha_inter_adjacency": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
     "msha_normalize_adjacency": (C.c_int, [P, I64, I64, P, P, P]),
     "msha_graph_workspace_size": (SZ, [I64, I64]),
+    "msha_graph_rowmask": (C.c_int, [GP, P, P]),
     "msha_graph_count": (C.c_int, [P, I64, I64, P, P, P, P, SZ, P]),
     "msha_graph_fill": (C.c_int, [P, I64, I64, P, P, P, P, P, P, P, SZ, P]),
     "msha_edge_attention_supported": (C.c_int, [I32, I32]),

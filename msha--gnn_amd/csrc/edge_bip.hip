@@ -859,6 +859,27 @@ __global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restric
   }
 }
 
+}  // namespace bip
+
+// (edge_bip2.hip) block partials -> v or d_hc + d_er, un-split layout
+int bip_reduce(const float* part, int32_t nb, int32_t stride, int32_t n, int32_t n_t, void* out_t,
+               bool bf16, float* out_f, int32_t fblk, hipStream_t s) {
+  const dim3 grid((n + 15) / 16), block(1024);
+  if (bf16)
+    hipLaunchKernelGGL(bip::bip_reduce_kernel<bf16_t>, grid, block, 0, s, part, nb, stride, n, n_t,
+                       (bf16_t*)out_t, out_f, n_t, 0, n_t, 0, fblk, 1);
+  else
+    hipLaunchKernelGGL(bip::bip_reduce_kernel<float>, grid, block, 0, s, part, nb, stride, n, n_t,
+                       (float*)out_t, out_f, n_t, 0, n_t, 0, fblk, 1);
+  return 1;
+}
+bool bip2_ok(const msha_graph* g, int heads, int feat, float slope);
+int bip2_fwd(const msha_graph* g, int dtype, const float* el, const float* er, const void* hc,
+             const void* hs, float slope, const Dropout& dp, void* u, float* lse, float* attd,
+             void* v, float* part, int nb, hipStream_t s);
+
+namespace bip {
+
 static int cu_count() {
   static int cached[64] = {0};
   int dev = 0;
@@ -1019,6 +1040,9 @@ extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_
                    "bip_attention_fwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
+  if (u_lo == nullptr && bip2_ok(g, heads, feat, neg_slope) &&
+      bip2_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s))
+    return check_launch("bip_attention_fwd");
   bool done = false;
 #define X(h, f)                                                                                  \
   if (heads == h && feat == f) {                                                                 \

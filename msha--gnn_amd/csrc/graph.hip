@@ -307,9 +307,31 @@ static size_t graph_ws_layout(int64_t n_rows, int64_t n_cols, void* base, GraphW
   return off;
 }
 
+// one lane per row: OR of the row's columns (n_cols <= 32)
+__global__ void __launch_bounds__(256) rowmask_kernel(const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ col,
+                                                      int64_t n_rows, uint32_t* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rows) return;
+  uint32_t m = 0;
+  for (int32_t e = rowptr[r], e1 = rowptr[r + 1]; e < e1; ++e) m |= 1u << (col[e] & 31);
+  out[r] = m;
+}
+
 }  // namespace msha
 
 using namespace msha;
+
+extern "C" int msha_graph_rowmask(const msha_graph* g, uint32_t* rowmask, msha_stream_t stream) {
+  MSHA_ARG_CHECK(g != nullptr && rowmask != nullptr && g->rowptr != nullptr,
+                 "graph_rowmask: null pointer");
+  MSHA_ARG_CHECK(g->n_rows > 0 && g->n_cols > 0 && g->n_cols <= 32 && g->n_rows < (1ll << 31),
+                 "graph_rowmask: needs 1 <= n_cols <= 32");
+  MSHA_ARG_CHECK(g->n_edges == 0 || g->col != nullptr, "graph_rowmask: col missing");
+  hipLaunchKernelGGL(rowmask_kernel, dim3((unsigned)((g->n_rows + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, g->rowptr, g->col, g->n_rows, rowmask);
+  return check_launch("graph_rowmask");
+}
 
 extern "C" int msha_inter_adjacency(const int64_t* source, const int64_t* recipient,
                                     int64_t n_flows, int64_t n_rows, int64_t n_cols, float* adj,

@@ -92,6 +92,12 @@ class Graph:
                     self.csr_slot[self.csc_eid.long()] = torch.arange(
                         self.n_edges, dtype=torch.int32, device=self.device)
                     d.csr_slot = _lib.ptr(self.csr_slot)
+            if self.n_cols <= 32 and self.n_rows > 0:
+                # per-row column bit masks: what the bipartite kernels walk (ABI 13)
+                self.rowmask = torch.empty(self.n_rows, dtype=torch.int32, device=self.device)
+                _lib.call("msha_graph_rowmask", d, self.rowmask.data_ptr(),
+                          _lib.stream_handle(self.device))
+                d.rowmask = _lib.ptr(self.rowmask)
             self._desc = d
         return self._desc
 

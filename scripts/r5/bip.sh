@@ -1,0 +1,18 @@
+#!/bin/bash
+# bipartite kernels: parity suites, then the bip1m leg with the mask kernels (MSHA_BIP2=1)
+# and the CSR-walk kernels (MSHA_BIP2=0) for A/B.  Output under gpurun_out/r5_bip${TAG}/.
+set -o pipefail
+O=gpurun_out/r5_bip${TAG}
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+T="timeout -k 10"
+$T 600 python -u -m pytest ${TESTS:-tests/test_gpu_bip.py tests/test_gpu_ours.py tests/test_gpu_graph.py} -m gpu -x -q \
+  --timeout 240 --timeout-method thread -p no:cacheprovider ${PYK:+-k "$PYK"} > $O/tests.log 2>&1 \
+  || { grep -E "passed|failed|Error|error|assert" $O/tests.log | tail -30; tail -60 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for v in 1 0; do
+  MSHA_BIP2=$v $T 300 python -u bench.py --workload bip1m --steps 10 --warmup 3 --no-cpu-baseline \
+    --no-r15 --no-dropout-leg --detail $O/bip1m_$v.json > $O/bip1m_$v.line 2> $O/bip1m_$v.err \
+    || { tail -20 $O/bip1m_$v.err; exit 1; }
+  python scripts/bench_brief.py $O/bip1m_$v.json | grep -E "bip|head"
+done
