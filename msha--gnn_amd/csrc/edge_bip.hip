@@ -874,6 +874,10 @@ int bip_reduce(const float* part, int32_t nb, int32_t stride, int32_t n, int32_t
   return 1;
 }
 bool bip2_ok(const msha_graph* g, int heads, int feat, float slope);
+int bip2_bwd(const msha_graph* g, int dtype, const float* el, const float* er, const void* hc,
+             const float* lse, const void* dU, const void* hs, const void* dV,
+             const float* row_coef, float slope, const Dropout& dp, float* d_el, float* d_er,
+             void* d_hc, void* d_hs, float* part, int nb, hipStream_t s);
 int bip2_fwd(const msha_graph* g, int dtype, const float* el, const float* er, const void* hc,
              const void* hs, float slope, const Dropout& dp, void* u, float* lse, float* attd,
              void* v, float* part, int nb, hipStream_t s);
@@ -1084,6 +1088,10 @@ extern "C" int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_
   const int nb = bip::cu_count();
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
+  if (bip2_ok(g, heads, feat, neg_slope) &&
+      bip2_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
+               d_hs, (float*)ws, nb, s))
+    return check_launch("bip_attention_bwd");
   bool done = false;
 #define X(h, f)                                                                                  \
   if (heads == h && feat == f) {                                                                 \
