@@ -44,17 +44,22 @@ def tol_close(a, b, rtol, atol_rel):
 U32 = 2.0 ** -24  # fp32 unit roundoff
 
 
-def bounded_close(got, ref, absterms, nterms, rtol, frac=None, name=""):
-    """fp32 sums against an fp64 reference, elementwise:
+STAT_C = 4.0  # standard deviations of the rounding-error random walk allowed
 
-    * every element within the forward-error bound of an n-term fp32 sum,
-      |got - ref| <= rtol |ref| + n 2^-24 A, where A = the sum of the absolute values of
-      the terms (incl. the magnitudes inside each term, e.g. |g| + |D| of a score
-      gradient) and n = the number of terms plus the ops inside a term and the block
-      reduce levels (``nterms``, scalar or per element);
-    * with ``frac``: at least that fraction of the elements within rtol |ref| alone
-      (elementwise relative, no max-based floor).
-    Returns (max err / bound, fraction within rtol) for reporting."""
+
+def bounded_close(got, ref, absterms, nterms, rtol, name=""):
+    """Sums against an fp64 reference, EVERY element (no fraction clause):
+
+        |got - ref| <= rtol |ref| + 4 sqrt(n) 2^-24 A
+
+    A = the sum of the absolute values of the terms (incl. the magnitudes inside each
+    term, e.g. |g| + |D| of a score gradient), n = the number of terms plus the ops
+    inside a term and the reduce levels (``nterms``, scalar or per element).  The
+    rounding errors of an n-term fp32 sum are a random walk of n steps of at most
+    u |partial| each, so 4 sqrt(n) u A is a four-sigma statistical bound (the worst-case
+    n u A is ~sqrt(n) times looser: 2e-3 A for the 70k-edge bip1m columns).  A small
+    element is held to its own terms, never to the tensor's largest.
+    Returns (max err / bound, fraction within rtol |ref| alone) for reporting."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
     A = np.broadcast_to(np.asarray(absterms, np.float64), ref.shape)
@@ -63,15 +68,27 @@ def bounded_close(got, ref, absterms, nterms, rtol, frac=None, name=""):
         n = n.reshape((-1,) + (1,) * (ref.ndim - 1))
     n = np.broadcast_to(n, ref.shape)
     err = np.abs(got - ref)
-    bound = rtol * np.abs(ref) + n * U32 * A + 1e-300
+    bound = rtol * np.abs(ref) + STAT_C * np.sqrt(n) * U32 * A + 1e-300
     worst = float((err / bound).max()) if err.size else 0.0
     assert np.all(err <= bound), (
-        f"{name}: {int((err > bound).sum())} of {err.size} elements beyond rtol|ref| + n u A "
-        f"(worst {worst:.3g}x the bound)")
+        f"{name}: {int((err > bound).sum())} of {err.size} elements beyond "
+        f"rtol|ref| + 4 sqrt(n) u A (worst {worst:.3g}x the bound)")
     inside = float(np.mean(err <= rtol * np.abs(ref))) if err.size else 1.0
-    if frac is not None:
-        assert inside >= frac, f"{name}: {inside:.4%} of elements within rtol {rtol} (< {frac})"
     return worst, inside
+
+
+def rel_close(got, ref, rtol, floor, name=""):
+    """Elementwise relative check above a stated magnitude floor: every element within
+    rtol max(|ref|, floor) -- the floor is an absolute magnitude of the quantity (not a
+    fraction of the tensor's largest element)."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    bound = rtol * np.maximum(np.abs(ref), floor)
+    worst = float((err / bound).max()) if err.size else 0.0
+    assert np.all(err <= bound), (f"{name}: {int((err > bound).sum())} of {err.size} elements "
+                                  f"beyond {rtol} max(|ref|, {floor}) (worst {worst:.3g}x)")
+    return worst
 
 
 def _seg_sum(x, ptr):

@@ -168,8 +168,8 @@ def test_edge_attention_fwd_bwd(cuda, msha, case, p):
     # score gradients: the fp32 forward-error bound of their sums (the softmax backward
     # cancels, sum_j att (g - D) = 0 before lrelu'; gpu_helpers.bounded_close)
     A = edge_abs_terms(rowptr, col, ref, hc, dU, hs=hs, dV=dV, keep=keep, p=p)
-    bounded_close(tel.grad.cpu().numpy(), bw["d_el"], A["d_el"], A["n_row"], 1e-5, None, "d_el")
-    bounded_close(ter.grad.cpu().numpy(), bw["d_er"], A["d_er"], A["n_col"], 1e-5, None, "d_er")
+    bounded_close(tel.grad.cpu().numpy(), bw["d_el"], A["d_el"], A["n_row"], 1e-5, "d_el")
+    bounded_close(ter.grad.cpu().numpy(), bw["d_er"], A["d_er"], A["n_col"], 1e-5, "d_er")
     tol_close(thc.grad.cpu().numpy(), bw["d_hc"], EMB_RTOL, 1e-5)
     tol_close(ths.grad.cpu().numpy(), bw["d_hs"], EMB_RTOL, 1e-5)
 
