@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import functional as MF
+from . import replay
 import math
 
 from .graph import Graph, graph_for, graph_of, groups_for
@@ -256,6 +257,13 @@ class ablation3(nn.Module):  # noqa: N801  (reference class name)
         self.out_att = GraphAttentionLayer(n_classes * n_heads, n_classes, dropout=dropout)
 
     def forward(self, inter_adj, city_adj, province_adj, source_index):
+        if replay.eligible(self, source_index):  # one graph replay each way (replay.py)
+            return replay.run(self, lambda s: self._forward(inter_adj, city_adj, province_adj,
+                                                             s),
+                              (inter_adj, city_adj, province_adj), source_index)
+        return self._forward(inter_adj, city_adj, province_adj, source_index)
+
+    def _forward(self, inter_adj, city_adj, province_adj, source_index):
         g = _graph(inter_adj)
         # feature dropout + head packing: one launch (and one autograd node) each way
         s_input, r_input, packed = MF.model_prologue(self.Sfeatures, self.Rfeatures,
@@ -430,6 +438,15 @@ class Ours(nn.Module):
 
     def forward(self, inter_adj, city_adj, province_adj, source_index, record=False,
                 Coeff12=None, Coeff3=None, Coeff4=None):
+        if not record and replay.eligible(self, source_index):  # replay.py
+            return replay.run(self, lambda s: self._forward(inter_adj, city_adj, province_adj,
+                                                             s),
+                              (inter_adj, city_adj, province_adj), source_index)
+        return self._forward(inter_adj, city_adj, province_adj, source_index, record, Coeff12,
+                             Coeff3, Coeff4)
+
+    def _forward(self, inter_adj, city_adj, province_adj, source_index, record=False,
+                 Coeff12=None, Coeff3=None, Coeff4=None):
         g = _graph(inter_adj)
         s_input, r_input, packed = MF.model_prologue(self.Sfeatures, self.Rfeatures,
                                                      self.dropout, self.training,

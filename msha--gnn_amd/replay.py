@@ -1,0 +1,121 @@
+"""Per-model HIP-graph replay of the drop-in models' training forward and backward.
+
+``train.py`` as written (train.py:221-232) runs the model eagerly every iteration:
+torch's Adam, ``F.nll_loss(output[source_index], ...)``, ``loss.item()``.  The GPU work of
+one ablation3 / Ours iteration is ~0.3-0.4 ms, but ~40 library launches issued from
+Python around ~30 autograd nodes cost more than that on the host.  Here the model's
+whole training forward is captured ONCE into a HIP graph (torch.cuda.CUDAGraph on a
+side stream, static batch buffer), its whole backward into a second graph (static
+output-gradient buffer, the parameters' gradients into static buffers), and every
+later call is one autograd node whose forward is a 512-byte batch copy + one graph
+replay and whose backward is one output-gradient copy + one replay.  train.py's own
+statements (the loss, ``.item()``, torch's Adam) run unchanged around it.
+
+* Dropout stays fresh: the library draws its Philox masks at (seed, offset + counter
+  << 32); the model's own device counter is installed while its graphs are captured
+  (so the captured launches read it) and incremented as the forward graph's first node.
+  The backward graph reads the same counter value, so it regenerates the forward's
+  masks (include/msha_gnn.h, msha_set_rng_counter).
+* The untimed warm-up passes that settle the caches before capture would also move the
+  BatchNorm running statistics; those buffers are restored before the first replay, so
+  the statistics see exactly one update per iteration, as in the eager model.
+* Gradients come back as the static buffers (no copies); with ``zero_grad()`` setting
+  ``.grad`` to None (torch's default, train.py:226) the AccumulateGrad nodes adopt them,
+  as with ``torch.cuda.make_graphed_callables``.
+* Not replayed (the eager path runs): eval mode, no grad mode, record mode, an outer
+  graph capture (``step.GraphedStep``), a parameter registered with
+  ``optim.Adam.fuse_dropout_grad``, or ``MSHA_MODEL_REPLAY=0``.
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+
+import torch
+
+from . import functional as MF
+
+REPLAY = os.environ.get("MSHA_MODEL_REPLAY", "1") != "0"
+WARMUP = 2  # eager passes on the side stream before capture (graph views, workspaces)
+MAX_GRAPHS = 4  # per model: batch sizes / adjacency versions kept
+
+
+def eligible(model, source_index) -> bool:
+    return bool(REPLAY and model.training and torch.is_grad_enabled()
+                and isinstance(source_index, torch.Tensor) and source_index.is_cuda
+                and not torch.cuda.is_current_stream_capturing()
+                and all(getattr(p, "_msha_fused_adam", None) is None
+                        for p in model.parameters()))
+
+
+class _ModelGraphs:
+    """The captured forward / backward of one (model, adjacencies, batch shape)."""
+
+    def __init__(self, fwd, params, buffers, src, keep):
+        dev = src.device
+        self.params = params
+        self.keep = keep  # the adjacencies the captured launches read: kept alive
+        self.src = src.detach().clone()
+        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        snaps = [b.detach().clone() for b in buffers]
+        prev = MF.set_rng_counter(self.counter, dev.index)
+        try:
+            cur = torch.cuda.current_stream(dev)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                for _ in range(WARMUP):
+                    self.counter.add_(1)
+                    out = fwd(self.src)
+                    torch.autograd.grad(out, params, torch.zeros_like(out), allow_unused=True)
+                    del out
+            cur.wait_stream(side)
+            for b, s in zip(buffers, snaps):  # undo the warm-ups' BatchNorm updates
+                b.copy_(s)
+            self.fwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.fwd):
+                self.counter.add_(1)
+                self.out = fwd(self.src)
+            self.dout = torch.empty_like(self.out)
+            self.bwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.bwd, pool=self.fwd.pool()):
+                self.grads = torch.autograd.grad(self.out, params, self.dout, allow_unused=True)
+        finally:
+            MF.set_rng_counter(prev, dev.index)
+        self.out = self.out.detach()
+
+
+class _Replay(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, graphs, src, *params):
+        graphs.src.copy_(src)
+        graphs.fwd.replay()
+        ctx.graphs = graphs
+        return graphs.out.detach()
+
+    @staticmethod
+    def backward(ctx, dout):
+        g = ctx.graphs
+        g.dout.copy_(dout)
+        g.bwd.replay()
+        return (None, None) + tuple(x.detach() if x is not None else None for x in g.grads)
+
+
+def run(model, fwd, consts, source_index):
+    """``fwd(src)`` (the model's eager training forward over the fixed inputs ``consts``:
+    adjacencies, group structures) through the model's captured graphs for this set of
+    inputs and batch shape (captured on first use)."""
+    cache = model.__dict__.setdefault("_msha_graphs", OrderedDict())
+    params = [p for p in model.parameters() if p.requires_grad]
+    key = (tuple((id(c), getattr(c, "_version", None)) for c in consts),
+           tuple(source_index.shape), source_index.dtype, model.dropout,
+           tuple((p.data_ptr(), p.dtype) for p in params))
+    g = cache.get(key)
+    if g is None:
+        g = _ModelGraphs(fwd, params, list(model.buffers()), source_index, tuple(consts))
+        cache[key] = g
+        while len(cache) > MAX_GRAPHS:
+            cache.popitem(last=False)
+    else:
+        cache.move_to_end(key)
+    return _Replay.apply(g, source_index, *params)

@@ -184,3 +184,56 @@ def test_captured_workspaces_survive_cache_growth(cuda, msha):
         for a, b in zip(o, r):
             assert torch.equal(a, b)
     del junk
+
+
+@pytest.mark.parametrize("kind", ["Ours", "ablation3"])
+def test_model_replay_matches_eager(cuda, msha, kind):
+    """replay.py: the drop-in model's training forward / backward replayed from its own
+    HIP graphs under train.py's loop (torch Adam, F.nll_loss(output[src]), .item())
+    gives the eager losses, parameters and BatchNorm running statistics (dropout 0), and
+    draws fresh dropout masks per replay (dropout 0.5)."""
+    from msha_gnn_amd import layers, replay
+    from msha_gnn_amd.data import GroupAdjacency
+
+    z = golden("ours_small.npz")
+    inter = msha.normalize_adjacency_matrix(t(z["counts"], cuda))
+    city = GroupAdjacency(torch.as_tensor(z["city"], device=cuda))
+    prov = GroupAdjacency(torch.as_tensor(z["prov"], device=cuda))
+    src = torch.as_tensor(z["source_index"], device=cuda)
+    tgt = torch.as_tensor(np.arange(src.numel()) % z["counts"].shape[1], device=cuda)
+    n, m = z["counts"].shape
+    cls = layers.Ours if kind == "Ours" else layers.ablation3
+
+    def make(p):
+        torch.manual_seed(0)
+        return cls(16, 8, m, 2, p, {i: 0.1 * i for i in range(n)}, n, m).to(cuda)
+
+    runs = {}
+    for rp in (False, True):
+        replay.REPLAY = rp
+        try:
+            model = make(0.0)
+            opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=5e-4)
+            model.train()
+            losses = []
+            for _ in range(4):
+                opt.zero_grad()
+                out = model(inter, city, prov, src)
+                loss = F.nll_loss(out[src], tgt)
+                losses.append(loss.item())
+                loss.backward()
+                opt.step()
+            if rp:
+                assert model.__dict__.get("_msha_graphs"), "replay path not taken"
+            runs[rp] = (losses, {k: v.detach().clone() for k, v in model.state_dict().items()})
+        finally:
+            replay.REPLAY = True
+    np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=1e-6)
+    for k, v in runs[False][1].items():
+        torch.testing.assert_close(runs[True][1][k], v, rtol=1e-5, atol=1e-6, msg=k)
+    # dropout: every replay draws new masks
+    model = make(0.5)
+    model.train()
+    outs = [model(inter, city, prov, src).detach().clone() for _ in range(3)]
+    assert model.__dict__.get("_msha_graphs")
+    assert not torch.equal(outs[1], outs[2]) and torch.isfinite(outs[2]).all()
