@@ -773,6 +773,9 @@ __host__ __device__ constexpr int rec_stride(int H) {
   while (s < 3 * H) s <<= 1;
   return REC_PAD ? s : 3 * H;
 }
+// the padded record also carries the row's virtual flag (float 0 / 1 at 3H): the column
+// pass reads it from the record line it fetches anyway instead of a random byte gather
+__host__ __device__ constexpr bool rec_has_flag(int H) { return rec_stride(H) > 3 * H; }
 
 // RT: the forward's row terms are given (uc, qc; see edge_attn_fwd_bat_kernel), so the
 // same pass also finishes d_el_i = dU_i . uc_i - D_i qc_i (0 on virtual rows) and the
@@ -837,6 +840,8 @@ __global__ void __launch_bounds__(256) bwd_row_stats_kernel(
           r[h] = el[row * H + h];
           r[H + h] = lse[row * H + h];
           r[2 * H + h] = dk;
+          if (rec_has_flag(H) && h == 0)
+            r[3 * H] = rowflag != nullptr && rowflag[row] != 0 ? 1.f : 0.f;
           if (RT) {
             const bool virt = rowflag != nullptr && rowflag[row] != 0;
             d_el[row * H + h] = virt ? 0.f : fmaf(-dk, qc[row * H + h], dc);
@@ -1070,6 +1075,9 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
   const rsrc_t r_dU = make_rsrc(dU, (uint32_t)(n_rows * G::D * sizeof(T)));
   const rsrc_t r_de = make_rsrc(de, (uint32_t)(n_edges * 4 * H));
   const uint32_t h_off = h_s * F * sizeof(T);
+  // the CSR edge id serves the dropout stream and an edge-ordered de only: otherwise its
+  // load stays off the memory system (kOOB)
+  const bool need_eid = dp.active || (de != nullptr && !slot_de);
 
   int64_t c = wave;
   if (c >= n_chunks) return;
@@ -1110,12 +1118,15 @@ __global__ void __launch_bounds__(256) bwd_cols_eh_kernel(
 #pragma unroll
         for (int k = 0; k < NV; ++k)
           dUv[g][k] = pk_load_buf(r_dU, row_off + (valid ? k * 16u : 0u), (T*)nullptr);
-        eid[g] = buf_i32(r_eid, valid ? (uint32_t)(cs + g * G::CE + e_s) * 4u : kOOB);
+        eid[g] = buf_i32(r_eid, valid && need_eid ? (uint32_t)(cs + g * G::CE + e_s) * 4u : kOOB);
         const uint32_t rec_off = valid ? (uint32_t)ii[g] * (4u * rec_stride(H)) + h_s * 4u : kOOB;
         r_el[g] = buf_f32(r_rec, rec_off);
         r_lse[g] = buf_f32(r_rec, valid ? rec_off + 4u * H : kOOB);
         Dsi[g] = buf_f32(r_rec, valid ? rec_off + 8u * H : kOOB);
-        vflag[g] = buf_u8(r_flag, valid ? (uint32_t)ii[g] : kOOB);
+        if constexpr (rec_has_flag(H))
+          vflag[g] = __float_as_uint(buf_f32(r_rec, valid ? rec_off - h_s * 4u + 12u * H : kOOB));
+        else
+          vflag[g] = buf_u8(r_flag, valid ? (uint32_t)ii[g] : kOOB);
       }
       // CSC rows of the next trip
 #pragma unroll
