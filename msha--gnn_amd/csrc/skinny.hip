@@ -1775,6 +1775,10 @@ int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, 
 // dW (128 x 128, fp32) = X^T D' over K rows: A = X^T given as (A, sAm = 1, sAk = ldx),
 // B = D' = D (+ head outer) given as (B, sBk = ldd, sBn = 1).  Uses the caller's split-K
 // workspace (splits x 128 x 128 fp32) for the block partials; 0 = not covered.
+int wgrad_x3(int64_t K, const float* X, int64_t ldx, const float* D, int64_t ldd, int hH, int hF,
+             const float* de, const float* a, const float* de2, const float* a2, float* slab,
+             int nb, const float* cs_tab, float* cs_part, hipStream_t s);
+
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
@@ -1793,7 +1797,9 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
                           (de2 != nullptr) != (cs_out2 != nullptr) || ((uintptr_t)cs_tab & 7)))
     return 0;
   float* slab = (float*)ws;
-  if (cs_tab != nullptr)
+  if (wgrad_x3(K, A, sAk, B, sBk, hH, hF, de, a, de2, a2, slab, (int)nb, cs_tab, cs_part, s)) {
+    // split-bf16 (wgrad_x3.hip): same slab / partial layout
+  } else if (cs_tab != nullptr)
     hipLaunchKernelGGL((sk::wgrad_kernel<true, true>), dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s,
                        (int)K, A, sAk, B, sBk, de, a, de2, a2, hH, hF, slab, cs_tab, cs_part);
   else if (de != nullptr)
