@@ -47,7 +47,10 @@ U32 = 2.0 ** -24  # fp32 unit roundoff
 STAT_C = 4.0  # standard deviations of the rounding-error random walk allowed
 
 
-def bounded_close(got, ref, absterms, nterms, rtol, name=""):
+BF16_U = 2.0 ** -8  # bf16 unit roundoff with one extra bit of slack (stored bf16 values)
+
+
+def bounded_close(got, ref, absterms, nterms, rtol, name="", u=U32):
     """Sums against an fp64 reference, EVERY element (no fraction clause):
 
         |got - ref| <= rtol |ref| + 4 sqrt(n) 2^-24 A
@@ -58,7 +61,9 @@ def bounded_close(got, ref, absterms, nterms, rtol, name=""):
     rounding errors of an n-term fp32 sum are a random walk of n steps of at most
     u |partial| each, so 4 sqrt(n) u A is a four-sigma statistical bound (the worst-case
     n u A is ~sqrt(n) times looser: 2e-3 A for the 70k-edge bip1m columns).  A small
-    element is held to its own terms, never to the tensor's largest.
+    element is held to its own terms, never to the tensor's largest.  ``u``: the unit
+    roundoff of the arithmetic or storage (fp32 2^-24; paths that round operands or
+    results to bf16 pass BF16_U).
     Returns (max err / bound, fraction within rtol |ref| alone) for reporting."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
@@ -68,7 +73,7 @@ def bounded_close(got, ref, absterms, nterms, rtol, name=""):
         n = n.reshape((-1,) + (1,) * (ref.ndim - 1))
     n = np.broadcast_to(n, ref.shape)
     err = np.abs(got - ref)
-    bound = rtol * np.abs(ref) + STAT_C * np.sqrt(n) * U32 * A + 1e-300
+    bound = rtol * np.abs(ref) + STAT_C * np.sqrt(n) * u * A + 1e-300
     worst = float((err / bound).max()) if err.size else 0.0
     assert np.all(err <= bound), (
         f"{name}: {int((err > bound).sum())} of {err.size} elements beyond "

@@ -19,6 +19,18 @@ from gpu_helpers import random_counts, t, tol_close
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _eager_models(msha):
+    """These tests compare optimizers on identically seeded eager models (the same
+    Philox seeds, hence the same dropout masks); the drop-in models' graph replay
+    (replay.py) draws its masks from a replay counter instead, so it is off here."""
+    from msha_gnn_amd import replay
+
+    prev, replay.REPLAY = replay.REPLAY, False
+    yield
+    replay.REPLAY = prev
+
+
 def test_adam_matches_torch_on_same_grads(cuda, msha):
     from msha_gnn_amd.optim import Adam
 
