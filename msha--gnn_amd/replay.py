@@ -41,11 +41,11 @@ MAX_GRAPHS = 4  # per model: batch sizes / adjacency versions kept
 
 
 def eligible(model, source_index) -> bool:
+    """Cheap per-call checks; the parameters' fused-optimizer marks are checked when a
+    graph is captured (``run`` falls back to the eager forward then)."""
     return bool(REPLAY and model.training and torch.is_grad_enabled()
                 and isinstance(source_index, torch.Tensor) and source_index.is_cuda
-                and not torch.cuda.is_current_stream_capturing()
-                and all(getattr(p, "_msha_fused_adam", None) is None
-                        for p in model.parameters()))
+                and not torch.cuda.is_current_stream_capturing())
 
 
 class _ModelGraphs:
@@ -105,13 +105,20 @@ def run(model, fwd, consts, source_index):
     """``fwd(src)`` (the model's eager training forward over the fixed inputs ``consts``:
     adjacencies, group structures) through the model's captured graphs for this set of
     inputs and batch shape (captured on first use)."""
-    cache = model.__dict__.setdefault("_msha_graphs", OrderedDict())
-    params = [p for p in model.parameters() if p.requires_grad]
+    d = model.__dict__
+    cache = d.get("_msha_graphs")
+    if cache is None:
+        cache = d["_msha_graphs"] = OrderedDict()
+    params = d.get("_msha_params")
+    if params is None or len(params) != sum(1 for _ in model.parameters()):
+        params = d["_msha_params"] = [p for p in model.parameters() if p.requires_grad]
     key = (tuple((id(c), getattr(c, "_version", None)) for c in consts),
-           tuple(source_index.shape), source_index.dtype, model.dropout,
-           tuple((p.data_ptr(), p.dtype) for p in params))
+           source_index.shape, source_index.dtype, model.dropout,
+           tuple([p.data_ptr() for p in params]))
     g = cache.get(key)
     if g is None:
+        if any(getattr(p, "_msha_fused_adam", None) is not None for p in params):
+            return fwd(source_index)  # optim.Adam consumes a dropout gradient: eager
         g = _ModelGraphs(fwd, params, list(model.buffers()), source_index, tuple(consts))
         cache[key] = g
         while len(cache) > MAX_GRAPHS:
