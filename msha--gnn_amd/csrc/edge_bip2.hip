@@ -35,7 +35,7 @@ typedef float f32x32 __attribute__((ext_vector_type(32)));
 constexpr int kF = 64, kD = 128;   // 2 heads x 64: one element of each head per lane
 constexpr int kWaves = 8;          // 16.5 KB table + 8 x 16.5 KB slabs
 constexpr int kTile = 32;          // rows per tile: phase A lane = row + 32 head
-constexpr int kBlk = 16;           // rows per element block (hs one block ahead)
+constexpr int kBlk = 8;            // rows per element block (hs one block ahead)
 constexpr int kRows = 33;          // LDS table / slab rows: 32 columns + the pair's dummy
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -84,13 +84,13 @@ __device__ __forceinline__ uint32_t bitmask(uint32_t m, int j) {
 // Phase A: lane (t, h) -> s[j] = attention of (row t, column j, head h) (0 where row t has
 // no edge j), lse of (t, h).  elv = el[t][h], flag = virtual full row (score 0 everywhere).
 template <bool VIRT>
-__device__ __forceinline__ float row_softmax(uint32_t mk, float elv, bool virt, const f32x32& erv,
+__device__ __forceinline__ float row_softmax(uint32_t mk, float elv, bool virt, const float* erl,
                                              float slope, f32x32& s) {
   constexpr float NINF = -INFINITY;
   float mx = NINF;
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
-    float x = elv + erv[j];
+    float x = elv + erl[2 * j];  // er[j][h]: LDS broadcast reads (no 32-register copy)
     x = fmaxf(x, x * slope);  // lrelu, slope in [0, 1]
     if (VIRT) x = virt ? 0.f : x;
     const uint32_t b = bitmask(mk, j);
@@ -137,9 +137,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip2_fwd_kernel(
   __syncthreads();
 
   const int t = lane & 31, h = lane >> 5;
-  f32x32 erv;  // this lane's head: er[j][h]
-#pragma unroll
-  for (int j = 0; j < 32; ++j) erv[j] = ert[j * 2 + h];
+  const float* erl = ert + h;  // er[j][h] = erl[2 j]
   const bool drop = dp.active;
   const uint64_t doff = drop ? dropout_offset(dp, dp.offset) : 0;
   const bool need_rp = ATTD || drop;
@@ -191,8 +189,8 @@ __global__ void __launch_bounds__(kWaves * 64) bip2_fwd_kernel(
       f32x32 s;
       const bool virt = fl != 0;
       float ls;
-      if (__builtin_amdgcn_ballot_w64(virt) != 0) ls = row_softmax<true>(mk, elv, virt, erv, slope, s);
-      else ls = row_softmax<false>(mk, elv, virt, erv, slope, s);
+      if (__builtin_amdgcn_ballot_w64(virt) != 0) ls = row_softmax<true>(mk, elv, virt, erl, slope, s);
+      else ls = row_softmax<false>(mk, elv, virt, erl, slope, s);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ls), r_lse, v_el, (uint32_t)r0 * 8u, 0);
       if (drop || ATTD) {
         // tile edges [E0, E1): rows r0 .. min(re, r0 + 32) - 1 are contiguous in the CSR
