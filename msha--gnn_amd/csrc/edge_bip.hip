@@ -1088,7 +1088,14 @@ extern "C" int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_
   const int nb = bip::cu_count();
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
-  if (bip2_ok(g, heads, feat, neg_slope) &&
+  // the mask backward wins on large graphs (bip1m: 450 -> 380-416 us) but not on the shipped
+  // ones (R15: 36.6 vs 31.7 us, rocprof, profiles/round5_step_r15_v1): rows per wave too few
+  // to amortise its per-wave d_er and slab epilogue.  MSHA_BIP2_BWD_MIN_ROWS moves the cut.
+  static const int64_t min_rows = [] {
+    const char* v = getenv("MSHA_BIP2_BWD_MIN_ROWS");
+    return v != nullptr && *v ? (int64_t)atoll(v) : (int64_t)131072;
+  }();
+  if (g->n_rows >= min_rows && bip2_ok(g, heads, feat, neg_slope) &&
       bip2_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
                d_hs, (float*)ws, nb, s))
     return check_launch("bip_attention_bwd");

@@ -674,6 +674,18 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
   int* fl = nullptr;
   float *P = nullptr, *PW = nullptr, *Pvo = nullptr, *Pdb = nullptr, *Pdbx = nullptr;
   bool any = false;
+  // fast form (the shipped shapes: M <= 32, H M <= 64, H F <= 128, F a multiple of 64):
+  // the wave's partials live in registers -- lane k owns W[k][.] and dW[k][.], lane c (and
+  // c + 64) owns v_out[c][.] and its partial -- and the per-column vectors travel by
+  // v_readlane, so a flagged row costs ~200 VALU instead of ~100 LDS read-modify-write
+  // round trips in two serial j loops (the slow form, kept for other shapes)
+  const bool fast = QM == 1 && M <= 32 && KX <= 64 && HF <= 128 && F % 64 == 0;
+  // (W and v_out are read from column-major copies in the unused partial area: lane k / c
+  // reads consecutive words, conflict free)
+  float rPW[32], rPvo[2][32], rPdb[2] = {0.f, 0.f}, rPdbx[2] = {0.f, 0.f};
+  float *Wt = nullptr, *vot = nullptr;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) rPW[j] = rPvo[0][j] = rPvo[1][j] = 0.f;
   // 64 rows per pass: each lane reads one row's dout (all loads in flight together);
   // the nonzero rows are then processed in ascending order
   for (int64_t base = r0; base < r1; base += 64) {
@@ -718,8 +730,22 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
       Pvo = PW + (int64_t)KX * M;
       Pdb = Pvo + (int64_t)HF * M;
       Pdbx = Pdb + HF;
-      for (int64_t t = lane; t < PT; t += 64) P[t] = 0.f;
+      if (!fast)
+        for (int64_t t = lane; t < PT; t += 64) P[t] = 0.f;
       __syncthreads();
+      if (fast) {  // Wt[j][k] (32 x 64), vot[j][c] (32 x 128), zero-padded
+        Wt = P;
+        vot = P + 32 * 64;
+        for (int t = lane; t < 32 * 64; t += 64) {
+          const int j = t >> 6, k = t & 63;
+          Wt[t] = k < KX && j < M ? s.W[k * M + j] : 0.f;
+        }
+        for (int t = lane; t < 32 * 128; t += 64) {
+          const int j = t >> 7, c = t & 127;
+          vot[t] = c < HF && j < M ? s.vo[c * M + j] : 0.f;
+        }
+        __syncthreads();
+      }
     }
     while (mask != 0ull) {
     const int bit = __builtin_ctzll(mask);
@@ -738,6 +764,57 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
 #pragma unroll
     for (int q = 0; q < QM; ++q) sdo += dov[q];
     sdo = wave_xor_sum<1>(sdo);
+    if (fast) {
+      // lane j < M: this row's gradient at the GAL output column j
+      float dh = 0.f;
+      if (lane < M) {
+        const float dy = dov[0] - __expf(y[0] - lse) * sdo;
+        const float z = at[0] * hg[0];
+        const float g = elu1(z);
+        dh = dy * delu1(g) * delu1(z) * at[0];
+      }
+      // lane k < KX: dx_k = sum_j dh_j W[k][j]; dW partial += x_k dh_j
+      const float xk = lane < KX ? xs[lane] : 0.f;
+      float dx = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dh), j));
+        dx = fmaf(d, Wt[j * 64 + lane], dx);
+        rPW[j] = fmaf(xk, d, rPW[j]);
+      }
+      float dck = 0.f;
+      if (lane < KX) {
+        const float keep = dropout_factor(a.dx, (uint64_t)i * KX + lane);
+        dck = dx * keep * delu1(cp[lane]);
+      }
+      // lanes c, c + 64 < HF (head h = c / F, uniform per half): d u_out[c], its BN input
+      // gradient and the v_out / BatchNorm partials
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int c = lane + 64 * pp;
+        const int hb = (64 * pp / F) * M;  // first lane of this head's dcv
+        const float uc = c < HF ? uo[c] : 0.f;
+        float duo = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const float d = j < M ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dck),
+                                                                          min(hb + j, 63)))
+                                : 0.f;
+          duo = fmaf(d, vot[j * 128 + c], duo);
+          rPvo[pp][j] = fmaf(d, uc, rPvo[pp][j]);
+        }
+        if (c < HF) {
+          const float xhat = (to_f32(u[i * HF + c]) - s.mu[c]) * s.su[c];
+          const float zb = fmaf(s.g[c], xhat, s.b[c]);
+          const float dz = duo * (zb > 0.f ? 1.f : a.slope);
+          rPdb[pp] += dz;
+          rPdbx[pp] = fmaf(dz, xhat, rPdbx[pp]);
+          ws.dz[i * HF + c] = dz;
+        }
+      }
+      wave_sync();  // uo / xs / cp reads done before the next row's head_row_fwd writes
+      continue;
+    }
 #pragma unroll
     for (int q = 0; q < QM; ++q) {
       const int j = lane + 64 * q;
@@ -788,7 +865,25 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
   if (lane == 0) ws.wflag[blockIdx.x] = any ? 1 : 0;
   if (any) {
     float* dst = ws.part + (int64_t)blockIdx.x * PT;
-    for (int64_t t = lane; t < PT; t += 64) dst[t] = P[t];
+    if (fast) {  // the register partials in the slow form's layout
+      if (lane < KX)
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (j < M) dst[lane * M + j] = rPW[j];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int c = lane + 64 * pp;
+        if (c < HF) {
+#pragma unroll
+          for (int j = 0; j < 32; ++j)
+            if (j < M) dst[(int64_t)KX * M + c * M + j] = rPvo[pp][j];
+          dst[(int64_t)KX * M + (int64_t)HF * M + c] = rPdb[pp];
+          dst[(int64_t)KX * M + (int64_t)HF * M + HF + c] = rPdbx[pp];
+        }
+      }
+    } else {
+      for (int64_t t = lane; t < PT; t += 64) dst[t] = P[t];
+    }
   }
 }
 
@@ -970,8 +1065,9 @@ static size_t fwd_lds(int HF, int KX, int M) {
                           (kHeadThreads / 64) * (size_t)(HF + KX + M));
 }
 static size_t bwd_lds(int HF, int KX, int M) {
-  return sizeof(float) * ((size_t)HF * M + (size_t)KX * M + 4 * HF + HF + 3 * (size_t)KX + 2 * M +
-                          (size_t)head_pt(HF, KX, M));
+  // (the partial area also holds head_bwd_rows' fast-form W / v_out copies: 32 x 192)
+  const size_t pt = (size_t)head_pt(HF, KX, M) > 32 * 192 ? (size_t)head_pt(HF, KX, M) : 32 * 192;
+  return sizeof(float) * ((size_t)HF * M + (size_t)KX * M + 4 * HF + HF + 3 * (size_t)KX + 2 * M + pt);
 }
 
 struct HeadLayout {
