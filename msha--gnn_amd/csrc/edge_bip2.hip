@@ -454,6 +454,16 @@ __global__ void __launch_bounds__(kWavesB * 64) bip2_bwd_kernel(
           float2 dhs = make_float2(0.f, 0.f);
           // lanes (tr, h) of G: rows 0 / 2 of the reduced pair hold edge 0's g when tr < 16
           const bool mine = (lane & 31) == tr;
+          if (m != 0u && (m & (m - 1u)) == 0u) {
+            // a one-edge row: att = 1, so ds = attd g (1 - att) = 0 whatever g is; only the
+            // dV / d_hc products remain (the reference's softmax backward gives exactly 0)
+            const int j0 = __builtin_ctz(m);
+            m = 0u;
+            const float s0 = s[j0];
+            const float2 a = make_float2(rdl(s0, tr), rdl(s0, tr + 32));
+            if (HS) dhs = fma2(a, tdvl[j0 * 64], dhs);
+            slabl[j0 * 64] = fma2(a, du, slabl[j0 * 64]);
+          }
           while (m) {
             const int j0 = __builtin_ctz(m);
             m &= m - 1;

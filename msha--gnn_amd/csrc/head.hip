@@ -54,6 +54,7 @@ struct HeadArgs {
   const float* W;  // (KX, M)
   Dropout dx, dg;
   float* stats;    // [u mean | u invstd | v mean | v invstd] (HF each) | vo_t (HF x M)
+  int slow_bwd;    // head_bwd_rows: the general (LDS partial) form for every shape
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -679,7 +680,7 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
   // c + 64) owns v_out[c][.] and its partial -- and the per-column vectors travel by
   // v_readlane, so a flagged row costs ~200 VALU instead of ~100 LDS read-modify-write
   // round trips in two serial j loops (the slow form, kept for other shapes)
-  const bool fast = QM == 1 && M <= 32 && KX <= 64 && HF <= 128 && F % 64 == 0;
+  const bool fast = !a.slow_bwd && QM == 1 && M <= 32 && KX <= 64 && HF <= 128 && F % 64 == 0;
   // (W and v_out are read from column-major copies in the unused partial area: lane k / c
   // reads consecutive words, conflict free)
   float rPW[32], rPvo[2][32], rPdb[2] = {0.f, 0.f}, rPdbx[2] = {0.f, 0.f};
@@ -1275,6 +1276,11 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
   const bool bf = dtype == MSHA_DTYPE_BF16;
   const size_t lds = bwd_lds(a.HF, a.KX, a.M);
   const int qm = (a.M + 63) / 64;
+  static const int slow = [] {
+    const char* v = getenv("MSHA_HEAD_BWD_SLOW");
+    return v != nullptr && *v ? atoi(v) : 0;
+  }();
+  a.slow_bwd = slow;
 #define HEAD_BWD(T, QM)                                                                     \
   hipLaunchKernelGGL((head_bwd_rows_kernel<T, QM>), dim3(nw), dim3(64), lds, s, a,          \
                      (const T*)u, (const T*)dout, w, rpw)
