@@ -9,13 +9,15 @@
 // unbiased variance), y = lrelu(weight * (x - mean) * invstd + bias).
 // Backward: dz = dy * lrelu'(z) (z recomputed from x), dbias = sum dz,
 // dweight = sum dz * xhat, dx = weight * invstd * (dz - dbias / R - xhat * dweight / R).
-// Rows <= kBnRows: one workgroup does statistics and the elementwise pass in one
+// Rows <= kBnSingle: one workgroup does statistics and the elementwise pass in one
 // launch (the recipient side v, 32 rows); otherwise partials + finalize + apply.
 #include "common.h"
 
 namespace msha {
 
-constexpr int kBnRows = 256;  // rows per partial block
+constexpr int kBnSingle = 256;  // up to this many rows: the one-workgroup path
+constexpr int kBnRows = 64;  // rows per partial block (256: 153 blocks at R15's 39k rows,
+                             // 16 serial load rounds per thread, 11.5 us)
 #ifndef BN_U
 #define BN_U 8  // rows per thread whose loads are in flight together
 #endif
@@ -96,7 +98,7 @@ __device__ __forceinline__ void bn_apply_elem(const BnArgs& a, const T* x, T* y,
   y[i] = from_f32<T>(z > 0.f ? z : z * a.slope);
 }
 
-// one workgroup: statistics + running update + elementwise (rows <= kBnRows)
+// one workgroup: statistics + running update + elementwise (rows <= kBnSingle)
 template <typename T>
 __global__ void __launch_bounds__(kBnThreads) bn_fwd_small_kernel(BnArgs a, int training,
                                                                  const T* __restrict__ x,
@@ -155,7 +157,15 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(BnArgs a, int nblk,
   const int lane = threadIdx.x & 63;
   if (c >= a.C) return;
   Wf w{0.f, 0.f, 0.f};
-  for (int b = lane; b < nblk; b += 64) w = wf_combine(w, part[(int64_t)b * a.C + c]);
+  int b = lane;  // partials lane, lane + 64, ... in order, 8 loads in flight at a time
+  for (; b + 7 * 64 < nblk; b += 8 * 64) {
+    Wf pb[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pb[q] = part[(int64_t)(b + q * 64) * a.C + c];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w = wf_combine(w, pb[q]);
+  }
+  for (; b < nblk; b += 64) w = wf_combine(w, part[(int64_t)b * a.C + c]);
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) w = wf_combine(w, wf_shfl_xor(w, o));
   if (lane == 0) bn_finalize_channel(a, c, w, true);
@@ -361,7 +371,7 @@ int64_t bn_stats_blocks(int64_t rows) { return bn_blocks(rows); }
 using namespace msha;
 
 extern "C" size_t msha_bn_workspace_size(int64_t rows, int32_t channels) {
-  if (rows <= kBnRows) return 0;
+  if (rows <= kBnSingle) return 0;
   const size_t nb = (size_t)bn_blocks(rows);
   const size_t f = nb * (size_t)channels * sizeof(Wf);
   const size_t b = nb * (size_t)channels * sizeof(float2) + (size_t)channels * sizeof(float2);
@@ -385,8 +395,8 @@ extern "C" int msha_bn_lrelu_fwd(int64_t rows, int32_t channels, int32_t dtype, 
   a.mean = mean; a.invstd = invstd;
   hipStream_t s = (hipStream_t)stream;
   const bool bf = dtype == MSHA_DTYPE_BF16;
-  if (rows <= kBnRows || !training) {
-    if (rows <= kBnRows) {
+  if (rows <= kBnSingle || !training) {
+    if (rows <= kBnSingle) {
       if (bf)
         hipLaunchKernelGGL(bn_fwd_small_kernel<bf16_t>, dim3(1), dim3(kBnThreads), 0, s, a,
                            training, (const bf16_t*)x, (bf16_t*)y);
@@ -432,7 +442,7 @@ extern "C" int msha_bn_lrelu_bwd(int64_t rows, int32_t channels, int32_t dtype, 
   a.mean = mean; a.invstd = invstd; a.dweight = dweight; a.dbias = dbias;
   hipStream_t s = (hipStream_t)stream;
   const bool bf = dtype == MSHA_DTYPE_BF16;
-  if (rows <= kBnRows) {
+  if (rows <= kBnSingle) {
     if (bf)
       hipLaunchKernelGGL(bn_bwd_small_kernel<bf16_t>, dim3(1), dim3(kBnThreads), 0, s, a,
                          (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx);

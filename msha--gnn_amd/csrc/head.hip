@@ -162,7 +162,17 @@ __global__ void __launch_bounds__(256) head_prep_kernel(HeadArgs a, int training
       return;
     }
     Wf w{0.f, 0.f, 0.f};
-    for (int b = lane; b < nbu; b += 64) w = wf_combine(w, part[(int64_t)b * HF + c]);
+    // partials lane, lane + 64, ... combined in that order; 8 loads in flight at a time
+    // (one dependent L2 round trip per partial was the kernel's time at ~600 partials)
+    int b = lane;
+    for (; b + 7 * 64 < nbu; b += 8 * 64) {
+      Wf pb[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) pb[q] = part[(int64_t)(b + q * 64) * HF + c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w = wf_combine(w, pb[q]);
+    }
+    for (; b < nbu; b += 64) w = wf_combine(w, part[(int64_t)b * HF + c]);
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1)
       w = wf_combine(w, Wf{__shfl_xor(w.n, o), __shfl_xor(w.mean, o), __shfl_xor(w.m2, o)});
@@ -656,8 +666,14 @@ struct HeadBwdWs {
   float* dz;       // N x HF: BN-input-side gradient of nonzero rows
   uint8_t* rflag;  // N
   float* red;      // PT reduced
+  uint64_t* wmask; // ceil(N / 64): rows with a nonzero dout, 64 a word (split form)
 };
 
+// head_bwd_rows' register form: the shipped shapes (M <= 32, H M <= 64, H F <= 128, F a
+// multiple of 64), one 64-column block of the output row
+__host__ __device__ inline bool head_bwd_fast(int QM, int M, int KX, int HF, int F, int slow) {
+  return !slow && QM == 1 && M <= 32 && KX <= 64 && HF <= 128 && F % 64 == 0;
+}
 __host__ __device__ inline int64_t head_pt(int HF, int KX, int M) { return (int64_t)KX * M + (int64_t)HF * M + 2 * HF; }
 
 template <typename T, int QM>
@@ -680,7 +696,7 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
   // c + 64) owns v_out[c][.] and its partial -- and the per-column vectors travel by
   // v_readlane, so a flagged row costs ~200 VALU instead of ~100 LDS read-modify-write
   // round trips in two serial j loops (the slow form, kept for other shapes)
-  const bool fast = !a.slow_bwd && QM == 1 && M <= 32 && KX <= 64 && HF <= 128 && F % 64 == 0;
+  const bool fast = head_bwd_fast(QM, M, KX, HF, F, a.slow_bwd);
   // (W and v_out are read from column-major copies in the unused partial area: lane k / c
   // reads consecutive words, conflict free)
   float rPW[32], rPvo[2][32], rPdb[2] = {0.f, 0.f}, rPdbx[2] = {0.f, 0.f};
@@ -888,12 +904,305 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
   }
 }
 
+// Split form of the backward row pass for the shipped shapes (head_bwd_fast): a scan
+// launch flags the rows whose dout is nonzero (rflag, and one 64-row bit mask a word),
+// then G single-wave blocks take the flagged rows k = b, b + G, ... (ascending row order).
+// In the one-launch form a flagged row's wave first scanned its 32 rows behind ~1200
+// LDS-heavy waves and then loaded the tables; here the G blocks load the tables while
+// locating their rows, and only they hold the LDS image.
+template <typename T>
+__global__ void __launch_bounds__(256) head_bwd_scan_kernel(const T* __restrict__ dout,
+                                                            int64_t N, int M,
+                                                            uint8_t* __restrict__ rflag,
+                                                            uint64_t* __restrict__ wmask) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int nzi = 0;
+  if (i < N) {
+    const T* dr = dout + i * M;
+    if (M % 4 == 0) {
+      int j = 0;
+      for (; j + 32 <= M; j += 32) {
+        float4 q[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) q[t] = ld4(dr + j + 4 * t);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          nzi |= (q[t].x != 0.f) | (q[t].y != 0.f) | (q[t].z != 0.f) | (q[t].w != 0.f);
+      }
+      for (; j < M; j += 4) {
+        const float4 q = ld4(dr + j);
+        nzi |= (q.x != 0.f) | (q.y != 0.f) | (q.z != 0.f) | (q.w != 0.f);
+      }
+    } else {
+      for (int j = 0; j < M; ++j) nzi |= to_f32(dr[j]) != 0.f;
+    }
+    rflag[i] = nzi ? 1 : 0;
+  }
+  const uint64_t bits = __ballot(nzi != 0);
+  if ((threadIdx.x & 63) == 0 && i < N) wmask[i >> 6] = bits;
+}
+
+// diagnostic build (-DSK_TIMELINE): lane 0 of each rows2 block stamps (wall clock, shader
+// clock) pairs at its marks into slot blockIdx.x of the buffer msha_debug_head_timeline
+// installs (scripts/head_timeline.py); marks compile to nothing in the shipped build
+#ifdef SK_TIMELINE
+__device__ uint64_t* g_head_tl = nullptr;
+#define HTL_MARK(k)                                                                   \
+  do {                                                                                \
+    if (g_head_tl != nullptr && (threadIdx.x & 63) == 0 && (k) < 31) {                \
+      const int sl_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);           \
+      g_head_tl[sl_ * 64 + 2 * (k)] = __builtin_amdgcn_s_memrealtime();               \
+      g_head_tl[sl_ * 64 + 2 * (k) + 1] = __builtin_amdgcn_s_memtime();               \
+    }                                                                                 \
+  } while (0)
+#else
+#define HTL_MARK(k) \
+  do {              \
+  } while (0)
+#endif
+
+template <typename T>
+__global__ void __launch_bounds__(256) head_bwd_rows2_kernel(HeadArgs a, const T* __restrict__ u,
+                                                             const T* __restrict__ dout,
+                                                             HeadBwdWs ws, int nwords) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int HF = a.HF, M = a.M, KX = a.KX, F = a.F;
+  const int64_t PT = head_pt(HF, KX, M);
+  // 4 waves a block: they stage the tables together (a one-wave block spent ~12 us of its
+  // ~30 us there, its LDS transposes one dependent round trip per element), then each
+  // takes the flagged rows slot, slot + 4 G, ... with its own scratch and partial slot
+  const int G = (int)gridDim.x, b = (int)blockIdx.x, slot = 4 * b + wv;
+  HTL_MARK(0);
+  // flagged rows per lane's mask words, and their prefix over the lanes
+  const int per = (nwords + 63) / 64;
+  const int w0 = lane * per;
+  int cnt = 0;
+  for (int q0 = 0; q0 < per; q0 += 8) {
+    uint64_t mw[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) mw[q] = q0 + q < per && w0 + q0 + q < nwords ? ws.wmask[w0 + q0 + q] : 0ull;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cnt += __popcll(mw[q]);
+  }
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  const int nl = __shfl(incl, 63);
+  HTL_MARK(1);
+  if (4 * b >= nl) {  // (uniform over the block)
+    if (lane == 0) ws.wflag[slot] = 0;
+    return;
+  }
+  // the k-th flagged row: the lane whose words hold it walks them, 8 words a round trip
+  auto locate = [&](int k) -> int64_t {
+    const int L = __builtin_ctzll(__ballot(incl > k));
+    int row = 0;
+    if (lane == L) {
+      int r = k - (incl - cnt);
+      for (int q0 = 0; q0 < per; q0 += 8) {
+        uint64_t mw[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) mw[q] = q0 + q < per && w0 + q0 + q < nwords ? ws.wmask[w0 + q0 + q] : 0ull;
+        bool found = false;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int pc = __popcll(mw[q]);
+          if (!found && r < pc) {
+            uint64_t m = mw[q];
+            for (int t = 0; t < r; ++t) m &= m - 1ull;
+            row = (w0 + q0 + q) * 64 + __builtin_ctzll(m);
+            found = true;
+          }
+          if (!found) r -= pc;
+        }
+        if (found) break;
+      }
+    }
+    return __builtin_amdgcn_readlane(row, L);
+  };
+  // a row's global inputs, loaded ahead: its GAL adjacency row (rowptr, columns), dout row,
+  // u row (lanes c, c + 64).  The first row's loads are in flight while the tables stage.
+  struct Pre {
+    int32_t lo, hi, col;
+    float dov, u0, u1;
+  };
+  auto prefetch = [&](int64_t i, Pre& p) {
+    p.lo = a.rowptr[i];
+    p.hi = a.rowptr[i + 1];
+    p.dov = lane < M ? to_f32(dout[i * M + lane]) : 0.f;
+    p.u0 = lane < HF ? to_f32(u[i * HF + lane]) : 0.f;
+    p.u1 = lane + 64 < HF ? to_f32(u[i * HF + 64 + lane]) : 0.f;
+    p.col = lane < p.hi - p.lo ? a.col[p.lo + lane] : 0;
+  };
+  int64_t i_nx = slot < nl ? locate(slot) : 0;
+  Pre pre{};
+  if (slot < nl) prefetch(i_nx, pre);
+  const HeadShared s = head_shared_load(a, smem);
+  // W / v_out column-major (lane k / c then reads consecutive words), zero-padded
+  float* Wt = s.su + HF;
+  float* vot = Wt + 32 * 64;
+  float* uo = vot + 32 * 128 + wv * (HF + 3 * KX + 2 * M);  // this wave's scratch
+  float* xs = uo + HF;
+  float* cp = xs + KX;
+  int* fl = reinterpret_cast<int*>(cp + 2 * KX + M);
+  __syncthreads();
+  for (int t = threadIdx.x; t < 32 * 64; t += 256) {
+    const int j = t >> 6, k = t & 63;
+    Wt[t] = k < KX && j < M ? s.W[k * M + j] : 0.f;
+  }
+  for (int t = threadIdx.x; t < 32 * 128; t += 256) {
+    const int j = t >> 7, c = t & 127;
+    vot[t] = c < HF && j < M ? s.vo[c * M + j] : 0.f;
+  }
+  __syncthreads();
+  HTL_MARK(2);
+  if (slot >= nl) {  // (no barrier after this point)
+    if (lane == 0) ws.wflag[slot] = 0;
+    return;
+  }
+  float rPW[32], rPvo[2][32], rPdb[2] = {0.f, 0.f}, rPdbx[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 32; ++j) rPW[j] = rPvo[0][j] = rPvo[1][j] = 0.f;
+  int tlk = 3;
+  for (int k = slot; k < nl; k += 4 * G) {
+    const int64_t i = i_nx;
+    const Pre cur = pre;
+    if (k + 4 * G < nl) {  // the next row's loads go out before this row's work
+      i_nx = locate(k + 4 * G);
+      prefetch(i_nx, pre);
+    }
+    HTL_MARK(tlk);
+    // the row's forward up to the log-softmax inputs (head_row_fwd, QM = 1, on the
+    // prefetched inputs)
+    const float dov = cur.dov;
+    float y[1], hg[1], at[1];
+    {
+      const int deg = cur.hi - cur.lo;
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int c = lane + 64 * pp;
+        if (c < HF) {
+          const float z = fmaf(s.g[c] * s.su[c], (pp ? cur.u1 : cur.u0) - s.mu[c], s.b[c]);
+          uo[c] = z > 0.f ? z : z * a.slope;
+        }
+      }
+      if (lane < M) fl[lane] = 0;
+      wave_sync();
+      if (lane < deg) fl[cur.col] = 1;
+      if (lane < KX) {
+        const int h = lane / M, j = lane - h * M;
+        const float* uh = uo + h * F;
+        const float* vh = s.vo + (int64_t)h * F * M + j;
+        float c = 0.f;
+#pragma unroll 8
+        for (int f = 0; f < F; ++f) c = fmaf(uh[f], vh[f * M], c);
+        cp[lane] = c;
+        xs[lane] = elu1(c) * dropout_factor(a.dx, (uint64_t)i * KX + lane);
+      }
+      wave_sync();
+      const float inv = deg > 0 ? 1.f / (float)deg : 0.f;
+      y[0] = -INFINITY;
+      hg[0] = 0.f;
+      at[0] = 0.f;
+      if (lane < M) {
+        float hv = 0.f;
+#pragma unroll 8
+        for (int kk = 0; kk < KX; ++kk) hv = fmaf(xs[kk], s.W[kk * M + lane], hv);
+        const float av = (fl[lane] ? inv : 0.f) * dropout_factor(a.dg, (uint64_t)i * M + lane);
+        hg[0] = hv;
+        at[0] = av;
+        y[0] = elu1(elu1(av * hv));
+      }
+    }
+    HTL_MARK(tlk + 1);
+    const float lse = row_lse<1>(y);
+    const float sdo = wave_xor_sum<1>(dov);
+    // lane j < M: this row's gradient at the GAL output column j
+    float dh = 0.f;
+    if (lane < M) {
+      const float dy = dov - __expf(y[0] - lse) * sdo;
+      const float z = at[0] * hg[0];
+      const float g = elu1(z);
+      dh = dy * delu1(g) * delu1(z) * at[0];
+    }
+    // lane k < KX: dx_k = sum_j dh_j W[k][j]; dW partial += x_k dh_j
+    const float xk = lane < KX ? xs[lane] : 0.f;
+    float dx = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dh), j));
+      dx = fmaf(d, Wt[j * 64 + lane], dx);
+      rPW[j] = fmaf(xk, d, rPW[j]);
+    }
+    float dck = 0.f;
+    if (lane < KX) {
+      const float keep = dropout_factor(a.dx, (uint64_t)i * KX + lane);
+      dck = dx * keep * delu1(cp[lane]);
+    }
+    // lanes c, c + 64 < HF (head h = c / F, uniform per half): d u_out[c], its BN input
+    // gradient and the v_out / BatchNorm partials
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int c = lane + 64 * pp;
+      const int hb = (64 * pp / F) * M;  // first lane of this head's dcv
+      const float uc = c < HF ? uo[c] : 0.f;
+      float duo = 0.f;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const float d = j < M ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dck),
+                                                                        min(hb + j, 63)))
+                              : 0.f;
+        duo = fmaf(d, vot[j * 128 + c], duo);
+        rPvo[pp][j] = fmaf(d, uc, rPvo[pp][j]);
+      }
+      if (c < HF) {
+        const float xhat = ((pp ? cur.u1 : cur.u0) - s.mu[c]) * s.su[c];
+        const float zb = fmaf(s.g[c], xhat, s.b[c]);
+        const float dz = duo * (zb > 0.f ? 1.f : a.slope);
+        rPdb[pp] += dz;
+        rPdbx[pp] = fmaf(dz, xhat, rPdbx[pp]);
+        ws.dz[i * HF + c] = dz;
+      }
+    }
+    wave_sync();  // uo / xs / cp reads done before the next row's writes
+    HTL_MARK(tlk + 2);
+    tlk += 3;
+  }
+  if (lane == 0) ws.wflag[slot] = 1;
+  // column-major W / v_out blocks ([j][k], [j][c]: the lanes' stores coalesce; the
+  // row-major form put each store's 64 lanes on 64 lines), head_bwd_reduce(tr = 1) maps back
+  float* dst = ws.part + (int64_t)slot * PT;
+  if (lane < KX)
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (j < M) dst[j * KX + lane] = rPW[j];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int c = lane + 64 * pp;
+    if (c < HF) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (j < M) dst[(int64_t)KX * M + j * HF + c] = rPvo[pp][j];
+      dst[(int64_t)KX * M + (int64_t)HF * M + c] = rPdb[pp];
+      dst[(int64_t)KX * M + (int64_t)HF * M + HF + c] = rPdbx[pp];
+    }
+  }
+  HTL_MARK(30);
+}
+
 // reduced[t] = sum over flagged waves (ascending) of part[w][t]; dW and the u-side
 // BatchNorm weight / bias gradients written out
+// tr: partials in the split form's layout (W and v_out blocks column-major: [j][k] and
+// [j][c], so that its lanes' stores were coalesced); the reduced vector is row-major either way
 __global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBwdWs ws, int nw,
                                                               float* __restrict__ dW,
                                                               float* __restrict__ dzero,
-                                                              int64_t n_zero) {
+                                                              int64_t n_zero, int tr) {
   if (blockIdx.x == 0)  // the out_att score vector's (exactly zero) gradient
     for (int64_t e = threadIdx.x; e < n_zero; e += blockDim.x) dzero[e] = 0.f;
   __shared__ int list[kHeadBwdWaves];
@@ -935,12 +1244,19 @@ __global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBw
     for (int q = 0; q < 16; ++q) sum += v[q];
   }
   for (; l < nl; ++l) sum += ws.part[(int64_t)list[l] * PT + t];
-  ws.red[t] = sum;
   const int64_t nW = (int64_t)a.KX * a.M, nV = (int64_t)a.HF * a.M;
-  if (t < nW) {
-    dW[t] = sum;
-  } else if (t >= nW + nV) {
-    const int64_t r = t - nW - nV;
+  int64_t o = t;
+  if (tr && t < nW) {
+    o = (t % a.KX) * a.M + t / a.KX;
+  } else if (tr && t < nW + nV) {
+    const int64_t r = t - nW;
+    o = nW + (r % a.HF) * a.M + r / a.HF;
+  }
+  ws.red[o] = sum;
+  if (o < nW) {
+    dW[o] = sum;
+  } else if (o >= nW + nV) {
+    const int64_t r = o - nW - nV;
     const int ch = (int)(r % a.HF);
     float* const* dst = r < a.HF ? a.dub : a.duw;  // sdb = d bias, sdbx = d weight
     float* d = dst[ch / a.F];
@@ -1001,9 +1317,57 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
     }
     return;
   }
+  const float invN = 1.f / (float)a.N;
+  const int q = HF / 4;  // float4 groups per row (HF % 4 == 0, checked by the caller)
+  const int64_t total = a.N * q;
+  const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
+  constexpr int U = 8;  // elements per thread whose loads are in flight together
+  if (blockDim.x % q == 0) {
+    // every element of this thread has the same 4 channels (the grid stride is a multiple
+    // of q): their 20 coefficients live in registers (read per element from LDS they were
+    // 20 stride-4 LDS reads per float4: 17.8 -> 15.3 us at R15)
+    const int c = 4 * (int)(threadIdx.x % q);
+    float cm[4], ci[4], cw[4], c1[4], c2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      cm[k] = st[c + k];
+      ci[k] = st[HF + c + k];
+      cw[k] = pw(a.uw, c + k, F, 1.f) * ci[k];
+      c1[k] = sdb[c + k] * invN;
+      c2[k] = sdbx[c + k] * invN;
+    }
+    const int64_t rs = stride / q;  // rows between a thread's consecutive elements
+    for (int64_t i0 = ((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x) / q;
+         i0 < a.N; i0 += U * rs) {
+      float4 x[U];
+      uint8_t nz[U];
+#pragma unroll
+      for (int t = 0; t < U; ++t) {
+        const int64_t i = i0 + t * rs;
+        x[t] = i < a.N ? ld4(u + i * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        nz[t] = i < a.N ? ws.rflag[i] : 0;
+      }
+#pragma unroll
+      for (int t = 0; t < U; ++t) {
+        const int64_t i = i0 + t * rs;
+        if (i >= a.N) break;
+        const float xs[4] = {x[t].x, x[t].y, x[t].z, x[t].w};
+        const float4 d4 = nz[t] ? *reinterpret_cast<const float4*>(ws.dz + i * HF + c)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float dzs[4] = {d4.x, d4.y, d4.z, d4.w};
+        float r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float xh = (xs[k] - cm[k]) * ci[k];
+          r[k] = cw[k] * (dzs[k] - c1[k] - xh * c2[k]);
+        }
+        st4(du + i * HF + c, make_float4(r[0], r[1], r[2], r[3]));
+      }
+    }
+    return;
+  }
   // per-channel coefficients in LDS: mean, invstd, w * invstd, sum dz / N, sum dz xhat / N
   float* cf = sm;  // 5 * HF <= 2560 floats
-  const float invN = 1.f / (float)a.N;
   for (int c = threadIdx.x; c < HF; c += blockDim.x) {
     cf[c] = st[c];
     cf[HF + c] = st[HF + c];
@@ -1012,10 +1376,6 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
     cf[4 * HF + c] = sdbx[c] * invN;
   }
   __syncthreads();
-  const int q = HF / 4;  // float4 groups per row (HF % 4 == 0, checked by the caller)
-  const int64_t total = a.N * q;
-  const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
-  constexpr int U = 8;  // elements per thread whose loads are in flight together
   for (int64_t e0 = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; e0 < total;
        e0 += U * stride) {
     float4 x[U];
@@ -1072,7 +1432,7 @@ static size_t bwd_lds(int HF, int KX, int M) {
 }
 
 struct HeadLayout {
-  size_t part_u, part_b, wflag, dz, rflag, red, total;
+  size_t part_u, part_b, wflag, dz, rflag, red, wmask, total;
 };
 
 // rows per wave and waves of the backward row pass (msha_head_bwd launches exactly these)
@@ -1101,7 +1461,7 @@ static HeadLayout head_layout(int64_t N, int M, int H, int F) {
   const size_t fwd = al256((size_t)bn_stats_blocks(N) * HF * sizeof(Wf));
   // backward regions (the forward's partials are dead by then: they alias); one partial
   // slab per wave the row pass launches (<= kHeadBwdWaves)
-  const size_t nw = (size_t)head_bwd_waves(N);
+  const size_t nw = (size_t)head_bwd_waves(N) > 4 ? (size_t)head_bwd_waves(N) : 4;
   L.part_b = 0;
   off = al256(nw * head_pt(HF, KX, M) * sizeof(float));
   L.wflag = off;
@@ -1112,6 +1472,8 @@ static HeadLayout head_layout(int64_t N, int M, int H, int F) {
   off += al256((size_t)N);
   L.red = off;
   off += al256((size_t)head_pt(HF, KX, M) * sizeof(float));
+  L.wmask = off;
+  off += al256((size_t)((N + 63) / 64) * sizeof(uint64_t));
   L.total = off > fwd ? off : fwd;
   return L;
 }
@@ -1271,6 +1633,7 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
   w.dz = (float*)(base + L.dz);
   w.rflag = (uint8_t*)(base + L.rflag);
   w.red = (float*)(base + L.red);
+  w.wmask = (uint64_t*)(base + L.wmask);
   const int64_t rpw = head_bwd_rpw(a.N);
   const int nw = head_bwd_waves(a.N);
   const bool bf = dtype == MSHA_DTYPE_BF16;
@@ -1281,18 +1644,47 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
     return v != nullptr && *v ? atoi(v) : 0;
   }();
   a.slow_bwd = slow;
+  // the split form (scan + G row blocks) for the shipped shapes; MSHA_HEAD_BWD_SPLIT=0: the
+  // one-launch row pass (A/B)
+  static const int split_env = [] {
+    const char* v = getenv("MSHA_HEAD_BWD_SPLIT");
+    return v != nullptr && *v ? atoi(v) : 1;
+  }();
+  const bool split = split_env != 0 && head_bwd_fast(qm, a.M, a.KX, a.HF, a.F, slow) &&
+                     a.N < (int64_t)INT32_MAX / 2;
+  int nblk = nw;
+  if (split) {
+    const int64_t nwords = (a.N + 63) / 64;
+    const int g2 = nw / 4 < 64 ? (nw / 4 > 0 ? nw / 4 : 1) : 64;  // 4 slots a block
+    nblk = 4 * g2;
+    const size_t lds2 = sizeof(float) * ((size_t)a.HF * a.M + (size_t)a.KX * a.M + 4 * (size_t)a.HF +
+                                         32 * 192 + 4 * ((size_t)a.HF + 3 * (size_t)a.KX + 2 * (size_t)a.M));
+    const dim3 gs((unsigned)((a.N + 255) / 256));
+    if (bf) {
+      hipLaunchKernelGGL(head_bwd_scan_kernel<bf16_t>, gs, dim3(256), 0, s, (const bf16_t*)dout,
+                         a.N, a.M, w.rflag, w.wmask);
+      hipLaunchKernelGGL(head_bwd_rows2_kernel<bf16_t>, dim3(g2), dim3(256), lds2, s, a,
+                         (const bf16_t*)u, (const bf16_t*)dout, w, (int)nwords);
+    } else {
+      hipLaunchKernelGGL(head_bwd_scan_kernel<float>, gs, dim3(256), 0, s, (const float*)dout,
+                         a.N, a.M, w.rflag, w.wmask);
+      hipLaunchKernelGGL(head_bwd_rows2_kernel<float>, dim3(g2), dim3(256), lds2, s, a,
+                         (const float*)u, (const float*)dout, w, (int)nwords);
+    }
+  } else {
 #define HEAD_BWD(T, QM)                                                                     \
   hipLaunchKernelGGL((head_bwd_rows_kernel<T, QM>), dim3(nw), dim3(64), lds, s, a,          \
                      (const T*)u, (const T*)dout, w, rpw)
-  if (bf) {
-    if (qm == 1) HEAD_BWD(bf16_t, 1); else if (qm == 2) HEAD_BWD(bf16_t, 2); else HEAD_BWD(bf16_t, 4);
-  } else {
-    if (qm == 1) HEAD_BWD(float, 1); else if (qm == 2) HEAD_BWD(float, 2); else HEAD_BWD(float, 4);
-  }
+    if (bf) {
+      if (qm == 1) HEAD_BWD(bf16_t, 1); else if (qm == 2) HEAD_BWD(bf16_t, 2); else HEAD_BWD(bf16_t, 4);
+    } else {
+      if (qm == 1) HEAD_BWD(float, 1); else if (qm == 2) HEAD_BWD(float, 2); else HEAD_BWD(float, 4);
+    }
 #undef HEAD_BWD
+  }
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
   hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 255) / 256)), dim3(256), 0, s, a,
-                     w, nw, dW, dzero, dzero != nullptr ? n_zero : 0);
+                     w, nblk, dW, dzero, dzero != nullptr ? n_zero : 0, split ? 1 : 0);
   const dim3 ga(1 + grid_for(a.N * a.HF / 4, 256 * 8, 1024));
   if (bf)
     hipLaunchKernelGGL(head_bwd_apply_kernel<bf16_t>, ga, dim3(256), 0, s, a, (const bf16_t*)u,
@@ -1301,4 +1693,19 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
     hipLaunchKernelGGL(head_bwd_apply_kernel<float>, ga, dim3(256), 0, s, a, (const float*)u,
                        (const float*)v, w, (float*)du, (float*)dv);
   return check_launch("head_bwd");
+}
+
+// Diagnostic: install (buf != NULL: >= 256 slots x 64 uint64 words, device memory) or
+// remove the head_bwd_rows2 timeline buffer; MSHA_ERR_UNSUPPORTED unless built with
+// -DSK_TIMELINE (build.py --variant timeline).
+extern "C" int msha_debug_head_timeline(void* buf) {
+#ifdef SK_TIMELINE
+  uint64_t* p = (uint64_t*)buf;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::g_head_tl), &p, sizeof(p)) != hipSuccess)
+    return msha::fail(MSHA_ERR_HIP, "debug_head_timeline: hipMemcpyToSymbol failed");
+  return MSHA_OK;
+#else
+  (void)buf;
+  return msha::fail(MSHA_ERR_UNSUPPORTED, "debug_head_timeline: library built without SK_TIMELINE");
+#endif
 }
