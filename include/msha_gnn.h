@@ -112,7 +112,7 @@ MSHA_API const char* msha_last_error(void);
  * -DSK_TIMELINE records (build.py --variant timeline); otherwise MSHA_ERR_UNSUPPORTED. */
 MSHA_API int msha_debug_timeline(void* buf, int64_t slots);
 /* Diagnostic: the model head's split backward row pass (head_bwd_rows2) stamps per-block
- * marks into buf (>= 1024 x 64 uint64, device memory; NULL removes it).  Same build
+ * marks into buf (>= 2048 x 64 uint64, device memory; NULL removes it).  Same build
  * condition as msha_debug_timeline. */
 MSHA_API int msha_debug_head_timeline(void* buf);
 

@@ -667,6 +667,8 @@ struct HeadBwdWs {
   uint8_t* rflag;  // N
   float* red;      // PT reduced
   uint64_t* wmask; // ceil(N / 64): rows with a nonzero dout, 64 a word (split form)
+  float* coef;     // 5 x HF: the apply's u-side coefficients (mean, invstd, w invstd,
+                   // sum dz / N, sum dz xhat / N), written by head_bwd_reduce
 };
 
 // head_bwd_rows' register form: the shipped shapes (M <= 32, H M <= 64, H F <= 128, F a
@@ -955,9 +957,20 @@ __device__ uint64_t* g_head_tl = nullptr;
       g_head_tl[sl_ * 64 + 2 * (k) + 1] = __builtin_amdgcn_s_memtime();               \
     }                                                                                 \
   } while (0)
+// head_bwd_apply: slot 1024 + block, lane 0 of thread 0
+#define HTL_MARKA(k)                                                                  \
+  do {                                                                                \
+    if (g_head_tl != nullptr && threadIdx.x == 0 && (k) < 31) {                       \
+      g_head_tl[(1024 + blockIdx.x) * 64 + 2 * (k)] = __builtin_amdgcn_s_memrealtime(); \
+      g_head_tl[(1024 + blockIdx.x) * 64 + 2 * (k) + 1] = __builtin_amdgcn_s_memtime(); \
+    }                                                                                 \
+  } while (0)
 #else
 #define HTL_MARK(k) \
   do {              \
+  } while (0)
+#define HTL_MARKA(k) \
+  do {               \
   } while (0)
 #endif
 
@@ -1258,6 +1271,16 @@ __global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBw
   } else if (o >= nW + nV) {
     const int64_t r = o - nW - nV;
     const int ch = (int)(r % a.HF);
+    const float invN = 1.f / (float)a.N;
+    if (r < a.HF) {
+      const float* st = a.stats;
+      ws.coef[ch] = st[ch];
+      ws.coef[a.HF + ch] = st[a.HF + ch];
+      ws.coef[2 * a.HF + ch] = pw(a.uw, ch, a.F, 1.f) * st[a.HF + ch];
+      ws.coef[3 * a.HF + ch] = sum * invN;
+    } else {
+      ws.coef[4 * a.HF + ch] = sum * invN;
+    }
     float* const* dst = r < a.HF ? a.dub : a.duw;  // sdb = d bias, sdbx = d weight
     float* d = dst[ch / a.F];
     if (d != nullptr) d[ch % a.F] = sum;
@@ -1280,73 +1303,94 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
   const float* sdb = red + nW + nV;
   const float* sdbx = sdb + HF;
   const float* st = a.stats;
-  // one LDS image for both roles (block 0: v and d v_out; the row blocks: coefficients),
-  // so the row blocks are not sized by block 0's staging: 32 KB a block, 5 per CU
-  __shared__ __attribute__((aligned(16))) float sm[2 * kHeadVStage];
-  if (blockIdx.x == 0) {
-    float* vs = sm;
-    float* gs = sm + kHeadVStage;
-    const bool staged = M * HF <= kHeadVStage;
-    if (staged) {
-      lds_copy(vs, v, M * HF);
-      lds_copy(gs, dvo, M * HF);
-      __syncthreads();
+  HTL_MARKA(0);
+  // blocks [0, nvb): the v side's BatchNorm backward, 32 channels a block, 8 row groups a
+  // channel (row sums: the 8 groups' partials added in group order through LDS); a single
+  // block walking every channel's M rows twice was this kernel's tail (12.6 us at R15)
+  const int nvb = (HF + 31) / 32;
+  __shared__ float2 vred[8][32];
+  if ((int)blockIdx.x < nvb) {
+    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int c = (int)blockIdx.x * 32 + cl;
+    const bool live = c < HF;
+    const float mean = live ? st[2 * HF + c] : 0.f, inv = live ? st[3 * HF + c] : 0.f;
+    const float gw = live ? pw(a.vw, c, F, 1.f) : 0.f, gb = live ? pw(a.vb, c, F, 0.f) : 0.f;
+    constexpr int RJ = 32;  // rows per thread (M <= 256 = 8 RJ)
+    float xh[RJ], dz[RJ];
+    float db = 0.f, dw = 0.f;
+#pragma unroll
+    for (int r = 0; r < RJ; ++r) {
+      const int j = g + 8 * r;
+      xh[r] = 0.f;
+      dz[r] = 0.f;
+      if (live && j < M) {
+        xh[r] = (to_f32(v[(int64_t)j * HF + c]) - mean) * inv;
+        dz[r] = dvo[(int64_t)c * M + j] * (fmaf(gw, xh[r], gb) > 0.f ? 1.f : a.slope);
+        db += dz[r];
+        dw = fmaf(dz[r], xh[r], dw);
+      }
     }
-    for (int c = threadIdx.x; c < HF; c += blockDim.x) {
-      const float mean = st[2 * HF + c], inv = st[3 * HF + c];
-      const float g = pw(a.vw, c, F, 1.f), b = pw(a.vb, c, F, 0.f);
-      auto xv = [&](int j) { return staged ? vs[j * HF + c] : to_f32(v[(int64_t)j * HF + c]); };
-      auto gv = [&](int j) { return staged ? gs[c * M + j] : dvo[(int64_t)c * M + j]; };
-      float db = 0.f, dw = 0.f;
-      for (int j = 0; j < M; ++j) {
-        const float xh = (xv(j) - mean) * inv;
-        const float dz = gv(j) * (fmaf(g, xh, b) > 0.f ? 1.f : a.slope);
-        db += dz;
-        dw = fmaf(dz, xh, dw);
-      }
-      const float invR = 1.f / (float)M;
-      for (int j = 0; j < M; ++j) {
-        const float xh = (xv(j) - mean) * inv;
-        const float dz = gv(j) * (fmaf(g, xh, b) > 0.f ? 1.f : a.slope);
-        dv[(int64_t)j * HF + c] = from_f32<T>(g * inv * (dz - db * invR - xh * dw * invR));
-      }
+    vred[g][cl] = make_float2(db, dw);
+    __syncthreads();
+    db = 0.f;
+    dw = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      db += vred[q][cl].x;
+      dw += vred[q][cl].y;
+    }
+    const float invR = 1.f / (float)M;
+#pragma unroll
+    for (int r = 0; r < RJ; ++r) {
+      const int j = g + 8 * r;
+      if (live && j < M)
+        dv[(int64_t)j * HF + c] = from_f32<T>(gw * inv * (dz[r] - db * invR - xh[r] * dw * invR));
+    }
+    if (live && g == 0) {
       float* dwp = a.dvw[c / F];
       float* dbp = a.dvb[c / F];
       if (dwp != nullptr) dwp[c % F] = dw;
       if (dbp != nullptr) dbp[c % F] = db;
     }
+    HTL_MARKA(30);
     return;
   }
+  __shared__ __attribute__((aligned(16))) float sm[5 * 512];
   const float invN = 1.f / (float)a.N;
   const int q = HF / 4;  // float4 groups per row (HF % 4 == 0, checked by the caller)
   const int64_t total = a.N * q;
-  const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
+  const int64_t stride = (int64_t)(gridDim.x - nvb) * blockDim.x;
   constexpr int U = 8;  // elements per thread whose loads are in flight together
   if (blockDim.x % q == 0) {
     // every element of this thread has the same 4 channels (the grid stride is a multiple
-    // of q): their 20 coefficients live in registers (read per element from LDS they were
-    // 20 stride-4 LDS reads per float4: 17.8 -> 15.3 us at R15)
+    // of q): their 20 coefficients (written by head_bwd_reduce: mean, invstd, w invstd,
+    // sum dz / N, sum dz xhat / N) are 5 float4 loads, in flight with the rows' loads
     const int c = 4 * (int)(threadIdx.x % q);
-    float cm[4], ci[4], cw[4], c1[4], c2[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      cm[k] = st[c + k];
-      ci[k] = st[HF + c + k];
-      cw[k] = pw(a.uw, c + k, F, 1.f) * ci[k];
-      c1[k] = sdb[c + k] * invN;
-      c2[k] = sdbx[c + k] * invN;
-    }
     const int64_t rs = stride / q;  // rows between a thread's consecutive elements
-    for (int64_t i0 = ((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x) / q;
-         i0 < a.N; i0 += U * rs) {
-      float4 x[U];
-      uint8_t nz[U];
+    const int64_t i00 = ((int64_t)(blockIdx.x - nvb) * blockDim.x + threadIdx.x) / q;
+    float4 x[U];
+    uint8_t nz[U];
 #pragma unroll
-      for (int t = 0; t < U; ++t) {
-        const int64_t i = i0 + t * rs;
-        x[t] = i < a.N ? ld4(u + i * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-        nz[t] = i < a.N ? ws.rflag[i] : 0;
-      }
+    for (int t = 0; t < U; ++t) {
+      const int64_t i = i00 + t * rs;
+      x[t] = i < a.N ? ld4(u + i * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      nz[t] = i < a.N ? ws.rflag[i] : 0;
+    }
+    float cm[4], ci[4], cw[4], c1[4], c2[4];
+    {
+      const float4 k0 = *reinterpret_cast<const float4*>(ws.coef + c);
+      const float4 k1 = *reinterpret_cast<const float4*>(ws.coef + HF + c);
+      const float4 k2 = *reinterpret_cast<const float4*>(ws.coef + 2 * HF + c);
+      const float4 k3 = *reinterpret_cast<const float4*>(ws.coef + 3 * HF + c);
+      const float4 k4 = *reinterpret_cast<const float4*>(ws.coef + 4 * HF + c);
+      cm[0] = k0.x; cm[1] = k0.y; cm[2] = k0.z; cm[3] = k0.w;
+      ci[0] = k1.x; ci[1] = k1.y; ci[2] = k1.z; ci[3] = k1.w;
+      cw[0] = k2.x; cw[1] = k2.y; cw[2] = k2.z; cw[3] = k2.w;
+      c1[0] = k3.x; c1[1] = k3.y; c1[2] = k3.z; c1[3] = k3.w;
+      c2[0] = k4.x; c2[1] = k4.y; c2[2] = k4.z; c2[3] = k4.w;
+    }
+    HTL_MARKA(1);
+    for (int64_t i0 = i00;; ) {
 #pragma unroll
       for (int t = 0; t < U; ++t) {
         const int64_t i = i0 + t * rs;
@@ -1363,7 +1407,17 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
         }
         st4(du + i * HF + c, make_float4(r[0], r[1], r[2], r[3]));
       }
+      HTL_MARKA(2);
+      i0 += U * rs;
+      if (i0 >= a.N) break;
+#pragma unroll
+      for (int t = 0; t < U; ++t) {
+        const int64_t i = i0 + t * rs;
+        x[t] = i < a.N ? ld4(u + i * HF + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        nz[t] = i < a.N ? ws.rflag[i] : 0;
+      }
     }
+    HTL_MARKA(30);
     return;
   }
   // per-channel coefficients in LDS: mean, invstd, w * invstd, sum dz / N, sum dz xhat / N
@@ -1376,7 +1430,7 @@ __global__ void __launch_bounds__(256) head_bwd_apply_kernel(HeadArgs a, const T
     cf[4 * HF + c] = sdbx[c] * invN;
   }
   __syncthreads();
-  for (int64_t e0 = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; e0 < total;
+  for (int64_t e0 = (int64_t)(blockIdx.x - nvb) * blockDim.x + threadIdx.x; e0 < total;
        e0 += U * stride) {
     float4 x[U];
     uint8_t nz[U];
@@ -1432,7 +1486,7 @@ static size_t bwd_lds(int HF, int KX, int M) {
 }
 
 struct HeadLayout {
-  size_t part_u, part_b, wflag, dz, rflag, red, wmask, total;
+  size_t part_u, part_b, wflag, dz, rflag, red, wmask, coef, total;
 };
 
 // rows per wave and waves of the backward row pass (msha_head_bwd launches exactly these)
@@ -1474,6 +1528,8 @@ static HeadLayout head_layout(int64_t N, int M, int H, int F) {
   off += al256((size_t)head_pt(HF, KX, M) * sizeof(float));
   L.wmask = off;
   off += al256((size_t)((N + 63) / 64) * sizeof(uint64_t));
+  L.coef = off;
+  off += al256((size_t)5 * HF * sizeof(float));
   L.total = off > fwd ? off : fwd;
   return L;
 }
@@ -1634,6 +1690,7 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
   w.rflag = (uint8_t*)(base + L.rflag);
   w.red = (float*)(base + L.red);
   w.wmask = (uint64_t*)(base + L.wmask);
+  w.coef = (float*)(base + L.coef);
   const int64_t rpw = head_bwd_rpw(a.N);
   const int nw = head_bwd_waves(a.N);
   const bool bf = dtype == MSHA_DTYPE_BF16;
@@ -1685,7 +1742,7 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
   hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 255) / 256)), dim3(256), 0, s, a,
                      w, nblk, dW, dzero, dzero != nullptr ? n_zero : 0, split ? 1 : 0);
-  const dim3 ga(1 + grid_for(a.N * a.HF / 4, 256 * 8, 1024));
+  const dim3 ga((a.HF + 31) / 32 + grid_for(a.N * a.HF / 4, 256 * 8, 1024));
   if (bf)
     hipLaunchKernelGGL(head_bwd_apply_kernel<bf16_t>, ga, dim3(256), 0, s, a, (const bf16_t*)u,
                        (const bf16_t*)v, w, (bf16_t*)du, (bf16_t*)dv);

@@ -25,15 +25,15 @@ msha_loader.load()
 from msha_gnn_amd import _lib  # noqa: E402
 
 dev = torch.device("cuda:0")
-buf = torch.zeros(1024 * 64, dtype=torch.int64, device=dev)
+buf = torch.zeros(2048 * 64, dtype=torch.int64, device=dev)
 _lib.call("msha_debug_head_timeline", buf.data_ptr())
 bench.train_step_leg(dev, "2015", "Ours", steps=2, warmup=2)
 torch.cuda.synchronize()
 _lib.call("msha_debug_head_timeline", None)
-raw = buf.view(1024, 64).cpu().numpy().view(np.uint64).astype(np.int64)
+raw = buf.view(2048, 64).cpu().numpy().view(np.uint64).astype(np.int64)
 t0 = raw[:, 0][raw[:, 0] > 0].min()
 act = []
-for b in range(1024):
+for b in range(1024):  # rows2 slots
     r = raw[b]
     if r[0] == 0:
         continue
@@ -44,5 +44,23 @@ idle = [m for b, m in act if 2 not in m]
 print(f"blocks stamped {len(act)}, without rows {len(idle)}; "
       f"idle exit (mark 1) median {np.median([m[1] for m in idle]):.2f} us" if idle else "")
 for b, m in act:
-    if 2 in m:
+    if 2 in m and b < 8:
         print(b, " ".join(f"{k}:{v:.2f}" for k, v in sorted(m.items())))
+
+# head_bwd_apply blocks (slots 1024 + block): 0 entry, 1 coefficients loaded, 2 row pass
+# issued, 30 exit (block 0: the v side)
+ap = raw[1024:]
+ap = ap[ap[:, 0] > 0]
+if len(ap):
+    t0a = ap[:, 0].min()
+    w = (ap[:, 0::2] - t0a) / 100.0
+    def col(k):
+        v = w[:, k][ap[:, 2 * k] > 0]
+        return v
+    print(f"apply blocks {len(ap)}: entry min/med/max {col(0).min():.2f}/{np.median(col(0)):.2f}/{col(0).max():.2f} us")
+    for k in (1, 2, 30):
+        v = col(k)
+        if len(v):
+            print(f"  mark {k}: min/med/max {v.min():.2f}/{np.median(v):.2f}/{v.max():.2f} us (n={len(v)})")
+    b0 = raw[1024]
+    print("  block 0 (v side):", " ".join(f"{k}:{(b0[2*k]-t0a)/100:.2f}" for k in range(31) if b0[2*k] > 0))
