@@ -468,6 +468,24 @@ class Clock:
         return dt_, k, len(events)
 
 
+def bip_kernel_patterns(H, F, bf, hs):
+    """rocprofv3 names of the bipartite forward / backward kernels: the mask kernels
+    (edge_bip2.hip, <T, HS, ATTD> / <T, HS, COEF, DROP>) or the CSR-walk ones (edge_bip.hip,
+    <H, F, T, HS, ATTD, HT> / <H, F, T, ...>), whichever the library chose; bf16
+    instances stay mangled (DF16b) or demangle the type as "bool _Accum"."""
+    h = str(bool(hs)).lower()
+    if bf:
+        fwd = (rf"(bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(hs)}E|<{H}, {F}, bool _Accum, "
+               rf"bool, E, false(, \d+)?>)|bip2_fwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum, {h}|<__bf16, {h}))")
+        bwd = (rf"(bip_bwd_kernel(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)"
+               rf"|bip2_bwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum, {h}|<__bf16, {h}))")
+    else:
+        fwd = (rf"(bip_fwd_kernel<{H}, {F}, float, {h}, false(, \d+)?>"
+               rf"|bip2_fwd_kernel<float, {h}, (true|false)>)")
+        bwd = rf"(bip_bwd_kernel<{H}, {F}, float|bip2_bwd_kernel<float, {h},)"
+    return fwd, bwd
+
+
 def edge_kernels(lay, n, m, e, H, F, s, workload=None):
     """Rooflines of the edge kernels of the step (HIP events, same run): the forward and
     either the fused backward or bwd_rows + csc_aggregate; PMC traffic per launch from
@@ -490,11 +508,8 @@ def edge_kernels(lay, n, m, e, H, F, s, workload=None):
         + ([] if rt else [rf"bwd_row_sum_kernel(<{H}>|ILi{H}E)"]),
         "msha_edge_attention_bwd_rows": [tmpl("edge_attn_bwd_rows(_gl)?_kernel")],
         "msha_csc_aggregate": [tmpl("csc_aggregate_kernel")],
-        # (<H, F, T, HS, ATTD, HT>: profiles before the HT flag end at ATTD)
-        "msha_bip_attention_fwd": [tmpl("bip_fwd_kernel") + (rf"(Lb{int(lay.v_branch)}E|, bool, E, false(, \d+)?>)"
-                                                             if bf else
-                                                             rf", {str(lay.v_branch).lower()}, false(, \d+)?>")],
-        "msha_bip_attention_bwd": [tmpl("bip_bwd_kernel")],
+        "msha_bip_attention_fwd": [bip_kernel_patterns(H, F, bf, lay.v_branch)[0]],
+        "msha_bip_attention_bwd": [bip_kernel_patterns(H, F, bf, lay.v_branch)[1]],
     }
     out = []
     v = lay.v_branch
@@ -538,10 +553,7 @@ def layer_leg(clock, dev, label, rowptr, col, n, m, fin, H, F, steps, warmup, wo
     dt = dtg if dtg is not None else dte
     if lay.bip:
         fb = bip_fwd_bytes(n, m, e, H, F, s, hs=lay.v_branch)
-        # (<H, F, T, HS, ATTD>; rocprofv3 demangles some bf16 instances as "bool _Accum")
-        bpat = ((rf"bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(lay.v_branch)}E|<{H}, {F}, bool _Accum, "
-                 rf"bool, E, false(, \d+)?>)") if s == 2 else
-                rf"bip_fwd_kernel<{H}, {F}, float, {str(lay.v_branch).lower()}, false(, \d+)?>")
+        bpat = bip_kernel_patterns(H, F, s == 2, lay.v_branch)[0]
         tr, src = pmc_lookup([bpat], f"*{workload}_v*") if workload else (None, None)
     else:
         fb = fwd_bytes(n, m, e, H, F, s, lay.rowterms, lay.row_scores, attd=lay.v_branch)
