@@ -476,9 +476,9 @@ def bip_kernel_patterns(H, F, bf, hs):
     h = str(bool(hs)).lower()
     if bf:
         fwd = (rf"(bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(hs)}E|<{H}, {F}, bool _Accum, "
-               rf"bool, E, false(, \d+)?>)|bip2_fwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum, {h}|<__bf16, {h}))")
+               rf"bool, E, false(, \d+)?>)|bip2_fwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum|<__bf16, {h}))")
         bwd = (rf"(bip_bwd_kernel(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)"
-               rf"|bip2_bwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum, {h}|<__bf16, {h}))")
+               rf"|bip2_bwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum|<__bf16, {h}))")
     else:
         fwd = (rf"(bip_fwd_kernel<{H}, {F}, float, {h}, false(, \d+)?>"
                rf"|bip2_fwd_kernel<float, {h}, (true|false)>)")
