@@ -1245,18 +1245,28 @@ __global__ void __launch_bounds__(256) head_bwd_reduce_kernel(HeadArgs a, HeadBw
   __syncthreads();
   const int nl = wsum[0] + wsum[1] + wsum[2] + wsum[3];
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= PT) return;
+  // 64 entries a block, 4 threads an entry: thread quarter w sums list entries
+  // [w nl / 4, (w + 1) nl / 4) in order (16 in flight), then the 4 sums add in quarter
+  // order (one round of loads per thread at 64 flagged slots instead of four)
+  __shared__ float qsum[4][64];
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
   float sum = 0.f;
-  int l = 0;
-  for (; l + 16 <= nl; l += 16) {  // 16 partials in flight, added in list order
-    float v[16];
+  if (t < PT) {
+    const int l0 = w * nl / 4, l1 = (w + 1) * nl / 4;
+    int l = l0;
+    for (; l + 16 <= l1; l += 16) {
+      float v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = ws.part[(int64_t)list[l + q] * PT + t];
+      for (int q = 0; q < 16; ++q) v[q] = ws.part[(int64_t)list[l + q] * PT + t];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) sum += v[q];
+      for (int q = 0; q < 16; ++q) sum += v[q];
+    }
+    for (; l < l1; ++l) sum += ws.part[(int64_t)list[l] * PT + t];
   }
-  for (; l < nl; ++l) sum += ws.part[(int64_t)list[l] * PT + t];
+  qsum[w][lane] = sum;
+  __syncthreads();
+  if (w != 0 || t >= PT) return;
+  sum = ((qsum[0][lane] + qsum[1][lane]) + qsum[2][lane]) + qsum[3][lane];
   const int64_t nW = (int64_t)a.KX * a.M, nV = (int64_t)a.HF * a.M;
   int64_t o = t;
   if (tr && t < nW) {
@@ -1740,7 +1750,7 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
 #undef HEAD_BWD
   }
   const int64_t PT = head_pt(a.HF, a.KX, a.M);
-  hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 255) / 256)), dim3(256), 0, s, a,
+  hipLaunchKernelGGL(head_bwd_reduce_kernel, dim3((unsigned)((PT + 63) / 64)), dim3(256), 0, s, a,
                      w, nblk, dW, dzero, dzero != nullptr ? n_zero : 0, split ? 1 : 0);
   const dim3 ga((a.HF + 31) / 32 + grid_for(a.N * a.HF / 4, 256 * 8, 1024));
   if (bf)
