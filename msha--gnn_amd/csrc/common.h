@@ -319,6 +319,21 @@ __device__ __forceinline__ float dropout_factor(const Dropout& d, uint64_t idx) 
   return philox_x(d.seed, dropout_offset(d, d.offset), idx) >= d.threshold ? d.scale : 0.f;
 }
 
+// the four-words-per-call stream (element e = word e % 4 of block e / 4, as the flat-table
+// masks): dropout_factor4 for one element, dropout_factors4 for the 4-aligned group from e4
+__device__ __forceinline__ float dropout_factor4(const Dropout& d, uint64_t idx) {
+  if (!d.active) return 1.f;
+  const uint4 w = philox4(d.seed, dropout_offset(d, d.offset), idx >> 2);
+  const uint32_t x = (idx & 3) == 0 ? w.x : (idx & 3) == 1 ? w.y : (idx & 3) == 2 ? w.z : w.w;
+  return x >= d.threshold ? d.scale : 0.f;
+}
+__device__ __forceinline__ float4 dropout_factors4(const Dropout& d, uint64_t e4) {
+  if (!d.active) return make_float4(1.f, 1.f, 1.f, 1.f);
+  const uint4 w = philox4(d.seed, dropout_offset(d, d.offset), e4 >> 2);
+  return make_float4(w.x >= d.threshold ? d.scale : 0.f, w.y >= d.threshold ? d.scale : 0.f,
+                     w.z >= d.threshold ? d.scale : 0.f, w.w >= d.threshold ? d.scale : 0.f);
+}
+
 // skinny.hip: resident-W projection and whole-tile weight gradient (1 = launched,
 // 0 = shape not covered: the caller runs its tiled GEMM)
 template <typename T>

@@ -294,7 +294,7 @@ __device__ __forceinline__ void head_row_fwd(const HeadArgs& a, const HeadShared
 #pragma unroll 8
     for (int f = 0; f < F; ++f) c = fmaf(uh[f], vh[f * M], c);
     if (cp != nullptr) cp[k] = c;
-    xs[k] = elu1(c) * dropout_factor(a.dx, (uint64_t)i * KX + k);
+    xs[k] = elu1(c) * dropout_factor4(a.dx, (uint64_t)i * KX + k);
   }
   wave_sync();
   const float inv = deg > 0 ? 1.f / (float)deg : 0.f;
@@ -308,7 +308,7 @@ __device__ __forceinline__ void head_row_fwd(const HeadArgs& a, const HeadShared
       float hg = 0.f;
 #pragma unroll 8
       for (int k = 0; k < KX; ++k) hg = fmaf(xs[k], s.W[k * M + j], hg);
-      const float at = (fl[j] ? inv : 0.f) * dropout_factor(a.dg, (uint64_t)i * M + j);
+      const float at = (fl[j] ? inv : 0.f) * dropout_factor4(a.dg, (uint64_t)i * M + j);
       hgv[q] = hg;
       av[q] = at;
       y[q] = elu1(elu1(at * hg));
@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_fwd_reg_kernel(HeadArgs a,
           c = fmaf(q.z, vreg[4 * f4 + 2], c);
           c = fmaf(q.w, vreg[4 * f4 + 3], c);
         }
-        xs[r * KXV + lane] = elu1(c) * dropout_factor(a.dx, (uint64_t)(r0 + r) * KXV + lane);
+        xs[r * KXV + lane] = elu1(c) * dropout_factor4(a.dx, (uint64_t)(r0 + r) * KXV + lane);
       }
     }
     wave_sync();
@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(kHeadThreads) head_fwd_reg_kernel(HeadArgs a,
         }
         const int deg = rps[r + 1] - rps[r];
         const float at = (fl[r * 64 + jl] ? (deg > 0 ? 1.f / (float)deg : 0.f) : 0.f) *
-                         dropout_factor(a.dg, (uint64_t)(r0 + r) * M + jl);
+                         dropout_factor4(a.dg, (uint64_t)(r0 + r) * M + jl);
         y = elu1(elu1(at * hg));
       }
       float mx = y;
@@ -593,14 +593,17 @@ __global__ void __launch_bounds__(kHeadThreads) head_fwd_mfma_kernel(HeadArgs a,
     }
     // x^T = dropout(elu(C^T)); element (row r0 + r16, k = h M + 16 jb + 4 g + q)
     const uint64_t row = (uint64_t)(r0 + r16);
+    // (the 4 consecutive elements q of a lane are one 4-aligned group of the mask stream:
+    // one generator call for all four)
 #pragma unroll
     for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int jb = 0; jb < MB; ++jb)
+      for (int jb = 0; jb < MB; ++jb) {
+        const float4 kf = dropout_factors4(a.dx, row * KX + h * M + 16 * jb + 4 * g);
+        const float kq[4] = {kf.x, kf.y, kf.z, kf.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          xc[h][jb][q] = elu1(xc[h][jb][q]) *
-                         dropout_factor(a.dx, row * KX + h * M + 16 * jb + 4 * g + q);
+        for (int q = 0; q < 4; ++q) xc[h][jb][q] = elu1(xc[h][jb][q]) * kq[q];
+      }
     // hg^T = W^T @ x^T, k in the accumulators' order
     f32x4 hg[MB];
 #pragma unroll
@@ -620,15 +623,17 @@ __global__ void __launch_bounds__(kHeadThreads) head_fwd_mfma_kernel(HeadArgs a,
     float y[MB][4];
     float mx = -INFINITY;
 #pragma unroll
-    for (int jb = 0; jb < MB; ++jb)
+    for (int jb = 0; jb < MB; ++jb) {
+      const float4 kf = dropout_factors4(a.dg, row * M + 16 * jb + 4 * g);
+      const float kq[4] = {kf.x, kf.y, kf.z, kf.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = 16 * jb + 4 * g + q;
-        const float at = (rv && fl[r16 * M + j] ? inv : 0.f) *
-                         dropout_factor(a.dg, row * M + j);
+        const float at = (rv && fl[r16 * M + j] ? inv : 0.f) * kq[q];
         y[jb][q] = elu1(elu1(at * hg[jb][q]));
         mx = fmaxf(mx, y[jb][q]);
       }
+    }
     mx = fmaxf(mx, xor_shfl(mx, 16));
     mx = fmaxf(mx, xor_shfl(mx, 32));
     float sm = 0.f;
@@ -803,7 +808,7 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
       }
       float dck = 0.f;
       if (lane < KX) {
-        const float keep = dropout_factor(a.dx, (uint64_t)i * KX + lane);
+        const float keep = dropout_factor4(a.dx, (uint64_t)i * KX + lane);
         dck = dx * keep * delu1(cp[lane]);
       }
       // lanes c, c + 64 < HF (head h = c / F, uniform per half): d u_out[c], its BN input
@@ -855,7 +860,7 @@ __global__ void __launch_bounds__(64) head_bwd_rows_kernel(HeadArgs a, const T* 
         dx = fmaf(d, s.W[k * M + j], dx);
         PW[k * M + j] = fmaf(xk, d, PW[k * M + j]);
       }
-      const float keep = dropout_factor(a.dx, (uint64_t)i * KX + k);
+      const float keep = dropout_factor4(a.dx, (uint64_t)i * KX + k);
       dcv[k] = dx * keep * delu1(cp[k]);
     }
     wave_sync();
@@ -1093,6 +1098,8 @@ __global__ void __launch_bounds__(256) head_bwd_rows2_kernel(HeadArgs a, const T
     // the row's forward up to the log-softmax inputs (head_row_fwd, QM = 1, on the
     // prefetched inputs)
     const float dov = cur.dov;
+    // this lane's x dropout factor (element i KX + lane), used forward and backward
+    const float kx = lane < KX ? dropout_factor4(a.dx, (uint64_t)i * KX + lane) : 0.f;
     float y[1], hg[1], at[1];
     {
       const int deg = cur.hi - cur.lo;
@@ -1115,7 +1122,7 @@ __global__ void __launch_bounds__(256) head_bwd_rows2_kernel(HeadArgs a, const T
 #pragma unroll 8
         for (int f = 0; f < F; ++f) c = fmaf(uh[f], vh[f * M], c);
         cp[lane] = c;
-        xs[lane] = elu1(c) * dropout_factor(a.dx, (uint64_t)i * KX + lane);
+        xs[lane] = elu1(c) * kx;
       }
       wave_sync();
       const float inv = deg > 0 ? 1.f / (float)deg : 0.f;
@@ -1126,7 +1133,7 @@ __global__ void __launch_bounds__(256) head_bwd_rows2_kernel(HeadArgs a, const T
         float hv = 0.f;
 #pragma unroll 8
         for (int kk = 0; kk < KX; ++kk) hv = fmaf(xs[kk], s.W[kk * M + lane], hv);
-        const float av = (fl[lane] ? inv : 0.f) * dropout_factor(a.dg, (uint64_t)i * M + lane);
+        const float av = (fl[lane] ? inv : 0.f) * dropout_factor4(a.dg, (uint64_t)i * M + lane);
         hg[0] = hv;
         at[0] = av;
         y[0] = elu1(elu1(av * hv));
@@ -1153,10 +1160,7 @@ __global__ void __launch_bounds__(256) head_bwd_rows2_kernel(HeadArgs a, const T
       rPW[j] = fmaf(xk, d, rPW[j]);
     }
     float dck = 0.f;
-    if (lane < KX) {
-      const float keep = dropout_factor(a.dx, (uint64_t)i * KX + lane);
-      dck = dx * keep * delu1(cp[lane]);
-    }
+    if (lane < KX) dck = dx * kx * delu1(cp[lane]);
     // lanes c, c + 64 < HF (head h = c / F, uniform per half): d u_out[c], its BN input
     // gradient and the v_out / BatchNorm partials
 #pragma unroll

@@ -113,8 +113,8 @@ def _run(cuda, n, m, H, F_, p, training, dtype=torch.float32, sparse=True, seed=
     with torch.set_grad_enabled(training):
         out = MF._ModelHead.apply(u_, v_, W_, g, bns, training, 1e-5, 0.1, 0.2, pp, sx, pp, sa,
                                   *params)
-    keep_x = MF.dropout_keep_mask(n * H * m, pp, sx, cuda).cpu().bool() if pp > 0 else None
-    keep_g = MF.dropout_keep_mask(n * m, pp, sa, cuda).cpu().bool() if pp > 0 else None
+    keep_x = MF.dropout_keep_mask(n * H * m, pp, sx, cuda, flat4=True).cpu().bool() if pp > 0 else None
+    keep_g = MF.dropout_keep_mask(n * m, pp, sa, cuda, flat4=True).cpu().bool() if pp > 0 else None
     dout = None
     if training:
         dout = torch.zeros(n, m)
