@@ -205,3 +205,25 @@ def test_bench_line_is_small_strict_json():
         assert k in legs, k
     assert legs["bip1m_f32"]["frac"] is None  # the planted infinity
     assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
+
+
+def test_bip_kernel_patterns_match_rocprof_names():
+    """The bipartite rooflines' PMC lookup names both kernel families (the mask kernels of
+    edge_bip2.hip and the CSR walk of edge_bip.hip) as rocprofv3 reports them: fp32
+    demangled, bf16 mangled (DF16b) or demangled with the type as "bool _Accum"."""
+    import re
+
+    fwd, bwd = bench.bip_kernel_patterns(2, 64, False, True)
+    names_f = ["void msha::bip2::bip2_fwd_kernel<float, true, false>(unsigned int const*)",
+               "void msha::bip::bip_fwd_kernel<2, 64, float, true, false, 2>(int const*)"]
+    names_b = ["void msha::bip2::bip2_bwd_kernel<float, true, false, false>(unsigned int const*)",
+               "void msha::bip::bip_bwd_kernel<2, 64, float, true, true, 2>(int const*)"]
+    assert all(re.search(fwd, n) for n in names_f) and not any(re.search(fwd, n) for n in names_b)
+    assert all(re.search(bwd, n) for n in names_b) and not any(re.search(bwd, n) for n in names_f)
+    # the v branch (HS) is pinned: a u-only forward is another instantiation
+    assert not re.search(fwd, "void msha::bip2::bip2_fwd_kernel<float, false, false>(unsigned")
+    fwd16, bwd16 = bench.bip_kernel_patterns(2, 64, True, True)
+    assert re.search(fwd16, "_ZN4msha4bip215bip2_fwd_kernelIDF16bLb1ELb0EEEvPKjPKiPKh")
+    assert re.search(fwd16, "void msha::bip2::bip2_fwd_kernel<bool _Accum, bool, E, false>")
+    assert re.search(bwd16, "_ZN4msha4bip215bip2_bwd_kernelIDF16bLb1ELb0ELb0EEEv")
+    assert not re.search(fwd16, "void msha::bip2::bip2_fwd_kernel<float, true, false>(")
