@@ -67,6 +67,7 @@ __global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
   // comes through LDS a chunk at a time (a serial loop over global loads cost ~0.5 us per
   // entry in every block)
   __shared__ int32_t br[kLossThreads], bc[kLossThreads];
+  __shared__ uint64_t whit[kLossThreads / 64];
   const float v = B > 0 ? -gloss[0] / (float)B : 0.f;
   for (int64_t b0 = 0; b0 < B; b0 += kLossThreads) {
     __syncthreads();  // (the fill above / the previous chunk's reads)
@@ -81,13 +82,19 @@ __global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
     }
     br[threadIdx.x] = rr;
     bc[threadIdx.x] = cc;
+    // which of the chunk's entries fall in this block's rows (one mask per wave): the lane
+    // then visits those alone, in batch order (its scan over every entry was ~2 us a block)
+    const uint64_t hit = __ballot(rr >= 0);
+    if ((threadIdx.x & 63) == 0) whit[threadIdx.x >> 6] = hit;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int nb = (int)min((int64_t)kLossThreads, B - b0);
-      for (int q = 0; q < nb; ++q) {
-        if (br[q] < 0) continue;
-        T* p = base + (int64_t)br[q] * ld + bc[q];
-        *p = from_f32<T>(to_f32(*p) + v);
+#pragma unroll
+      for (int w = 0; w < kLossThreads / 64; ++w) {
+        for (uint64_t m = whit[w]; m != 0ull; m &= m - 1ull) {
+          const int q = w * 64 + __builtin_ctzll(m);
+          T* p = base + (int64_t)br[q] * ld + bc[q];
+          *p = from_f32<T>(to_f32(*p) + v);
+        }
       }
     }
   }
