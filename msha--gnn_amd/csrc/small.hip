@@ -44,12 +44,12 @@ __global__ void __launch_bounds__(kSmallThreads) small_fwd_kernel(SmallArgs a) {
   if (t < N) {
     float acc = 0.f;
     int k = 0;
-    for (; k + 8 <= K; k += 8) {
-      float w[8];
+    for (; k + 32 <= K; k += 32) {  // 32 loads in flight (8 a round left K = 128 at 16 L2 round trips)
+      float w[32];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) w[q] = a.W[(int64_t)(k + q) * N + t];
+      for (int q = 0; q < 32; ++q) w[q] = a.W[(int64_t)(k + q) * N + t];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc = fmaf(xr[k + q], w[q], acc);
+      for (int q = 0; q < 32; ++q) acc = fmaf(xr[k + q], w[q], acc);
     }
     for (; k < K; ++k) acc = fmaf(xr[k], a.W[(int64_t)k * N + t], acc);
     hr[t] = acc;
@@ -105,12 +105,12 @@ __global__ void __launch_bounds__(kSmallThreads) small_bwd_kernel(SmallArgs a, i
       const float* wk = a.W + (int64_t)t * N;
       float acc = 0.f;
       int n = 0;
-      for (; n + 8 <= N; n += 8) {
-        float w[8];
+      for (; n + 32 <= N; n += 32) {  // 32 loads in flight
+        float w[32];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) w[q] = wk[n + q];
+        for (int q = 0; q < 32; ++q) w[q] = wk[n + q];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc = fmaf(dr[n + q], w[q], acc);
+        for (int q = 0; q < 32; ++q) acc = fmaf(dr[n + q], w[q], acc);
       }
       for (; n < N; ++n) acc = fmaf(dr[n], wk[n], acc);
       a.dX[(int64_t)b * K + t] = acc;
@@ -123,7 +123,18 @@ __global__ void __launch_bounds__(kSmallThreads) small_bwd_kernel(SmallArgs a, i
     if (e >= K * N) return;
     const int k = e / N, n = e - k * N;
     float acc = 0.f;
-    for (int i = 0; i < M; ++i) acc = fmaf(a.X[(int64_t)i * K + k], small_d(a, i, n), acc);
+    int i = 0;
+    for (; i + 8 <= M; i += 8) {  // 8 rows' loads in flight, added in row order
+      float x[8], d[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        x[q] = a.X[(int64_t)(i + q) * K + k];
+        d[q] = small_d(a, i + q, n);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc = fmaf(x[q], d[q], acc);
+    }
+    for (; i < M; ++i) acc = fmaf(a.X[(int64_t)i * K + k], small_d(a, i, n), acc);
     a.dW[e] = acc;
     return;
   }
@@ -134,7 +145,18 @@ __global__ void __launch_bounds__(kSmallThreads) small_bwd_kernel(SmallArgs a, i
     if (d == nullptr || o == nullptr) continue;
     const int hh = r / F;
     float sc = 0.f;
-    for (int i = 0; i < M; ++i) sc = fmaf(d[i * H + hh], a.h[(int64_t)i * N + r], sc);
+    int i = 0;
+    for (; i + 8 <= M; i += 8) {
+      float dv[8], hv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        dv[q] = d[(i + q) * H + hh];
+        hv[q] = a.h[(int64_t)(i + q) * N + r];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sc = fmaf(dv[q], hv[q], sc);
+    }
+    for (; i < M; ++i) sc = fmaf(d[i * H + hh], a.h[(int64_t)i * N + r], sc);
     o[r] = sc;
   }
 }
