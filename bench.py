@@ -647,9 +647,10 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, group_ok, steps=16, wa
         def score(h, s_, d_):  # alternate output buffers (the pipelined scorer keeps two)
             o = outs[mode][calls[0] % 2]
             calls[0] += 1
+            # the pair batch is index-checked once below (the same arrays every batch)
             if mode == "mlp":
-                return MF.score_pairs(h, s_, d_, "mlp", W, b, out=o)
-            return MF.score_pairs(h, s_, d_, "inner", out=o)
+                return MF.score_pairs(h, s_, d_, "mlp", W, b, out=o, check=False)
+            return MF.score_pairs(h, s_, d_, "inner", out=o, check=False)
         return score
 
     def sync_all():
@@ -657,6 +658,7 @@ def link_score_bench(dev, rowptr, col, n, F, world, rank, group_ok, steps=16, wa
             tdist.barrier()
         torch.cuda.synchronize(dev)
 
+    MF.check_pair_indices(t_src, t_dst, n)  # torch's h[idx] rule, once per pair batch
     res = {}
     s = 2 if dtype == torch.bfloat16 else 4
     for mode in ("mlp", "inner"):

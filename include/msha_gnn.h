@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 13
+#define MSHA_ABI_VERSION 14
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -258,6 +258,10 @@ MSHA_API int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_t 
                                     uint64_t offset, float* d_el, float* d_er, void* d_hc,
                                     void* d_hs, void* ws, size_t ws_bytes,
                                     msha_stream_t stream);
+/* The source-row count from which msha_bip_attention_bwd takes the row-mask kernel
+ * (graphs with msha_graph.rowmask; default 131072, or MSHA_BIP2_BWD_MIN_ROWS): rows >= 0
+ * sets it for the process and returns the previous value, rows < 0 only returns it. */
+MSHA_API int64_t msha_bip2_bwd_min_rows(int64_t rows);
 
 /* Column-side (transposed) aggregate over the CSC view:
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
@@ -506,6 +510,23 @@ MSHA_API int msha_pair_linear(int64_t n_pairs, int64_t K, int64_t N, const float
 MSHA_API int msha_pair_inner_fwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
                                  const int64_t* gi, const float* G2, int64_t ldg2,
                                  const int64_t* gj, float* out, msha_stream_t stream);
+/* 'inner' with the gathered tables' row counts (ABI 14): a pair whose gi / gj index lies
+ * outside [0, g_rows) / [0, g2_rows) scores NaN and sets *err = 1 (err nullable) instead
+ * of reading past the table.  dtype MSHA_DTYPE_F32 (feat in [4, 256]) or
+ * MSHA_DTYPE_BF16 (feat in [8, 512]); replaces the gather of LLP.py:233 + LLP.py:112-115. */
+MSHA_API int msha_pair_inner_fwd_ex(int64_t n_pairs, int32_t feat, int32_t dtype, const void* G,
+                                    int64_t ldg, const int64_t* gi, int64_t g_rows,
+                                    const void* G2, int64_t ldg2, const int64_t* gj,
+                                    int64_t g2_rows, int32_t* err, float* out,
+                                    msha_stream_t stream);
+/* Index validation of a pair batch before a fused gather (LLP.py:233: torch's h[idx]
+ * raises for idx outside [-rows, rows) and wraps a negative idx to rows + idx): flags[0]
+ * is set to 1 when any gi (gj) lies outside [-g_rows, g_rows) ([-g2_rows, g2_rows)),
+ * flags[1] when any is negative.  flags (2 x int32, device) are OR-ed into, never
+ * cleared: the caller zeroes them.  gi / gj nullable. */
+MSHA_API int msha_pair_index_check(int64_t n_pairs, const int64_t* gi, int64_t g_rows,
+                                   const int64_t* gj, int64_t g2_rows, int32_t* flags,
+                                   msha_stream_t stream);
 /* backward of 'inner' given its output s: dx_i = dout*s*(1-s)*x_j, dx_j = ...*x_i */
 MSHA_API int msha_pair_inner_bwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
                                  const int64_t* gi, const float* G2, int64_t ldg2,

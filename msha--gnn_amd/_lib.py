@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 13  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 14  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -161,6 +161,10 @@ SIGNATURES = {
                                    U64, U64, P, P]),
     "msha_pair_inner_fwd": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
     "msha_pair_inner_fwd_bf16": (C.c_int, [I64, I32, P, I64, P, P, I64, P, P, P]),
+    "msha_pair_inner_fwd_ex": (C.c_int, [I64, I32, I32, P, I64, P, I64, P, I64, P, I64, P, P,
+                                         P]),
+    "msha_bip2_bwd_min_rows": (I64, [I64]),
+    "msha_pair_index_check": (C.c_int, [I64, P, I64, P, I64, P, P]),
     "msha_pair_linear_bf16": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32, U64,
                                         U64, P, P]),
     "msha_pair_linear_bf16_ex": (C.c_int, [I64, I64, I64, P, I64, P, P, I64, P, P, P, I32, F32,

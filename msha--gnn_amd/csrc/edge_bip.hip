@@ -29,6 +29,8 @@
 //     d_er_j is one LDS float add per slot.
 // Reference: Ablation.py:266-274 (OursLayer3 scores, masked softmax, dropout,
 // u = att @ h1, v = att.T @ h2), Ours.py:84-86 (the backward's row coefficients).
+#include <atomic>
+
 #include "edge_geo.h"
 
 namespace msha {
@@ -881,6 +883,13 @@ int bip2_bwd(const msha_graph* g, int dtype, const float* el, const float* er, c
 int bip2_fwd(const msha_graph* g, int dtype, const float* el, const float* er, const void* hc,
              const void* hs, float slope, const Dropout& dp, void* u, float* lse, float* attd,
              void* v, float* part, int nb, hipStream_t s);
+int bip3_bwd(const msha_graph* g, int dtype, const float* el, const float* er, const void* hc,
+             const float* lse, const void* dU, const void* hs, const void* dV,
+             const float* row_coef, float slope, const Dropout& dp, float* d_el, float* d_er,
+             void* d_hc, void* d_hs, float* part, int nb, hipStream_t s);
+int bip3_fwd(const msha_graph* g, int dtype, const float* el, const float* er, const void* hc,
+             const void* hs, float slope, const Dropout& dp, void* u, float* lse, float* attd,
+             void* v, float* part, int nb, hipStream_t s);
 
 namespace bip {
 
@@ -1045,7 +1054,8 @@ extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
   if (u_lo == nullptr && bip2_ok(g, heads, feat, neg_slope) &&
-      bip2_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s))
+      (bip3_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s) ||
+       bip2_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s)))
     return check_launch("bip_attention_fwd");
   bool done = false;
 #define X(h, f)                                                                                  \
@@ -1064,6 +1074,18 @@ extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_
 #undef X
   if (!done) return fail(MSHA_ERR_UNSUPPORTED, "bip_attention_fwd: unsupported (heads, feat)");
   return check_launch("bip_attention_fwd");
+}
+
+static std::atomic<int64_t>& bip2_bwd_cut() {
+  static std::atomic<int64_t> cut{[] {
+    const char* v = getenv("MSHA_BIP2_BWD_MIN_ROWS");
+    return v != nullptr && *v ? (int64_t)atoll(v) : (int64_t)131072;
+  }()};
+  return cut;
+}
+
+extern "C" int64_t msha_bip2_bwd_min_rows(int64_t rows) {
+  return rows >= 0 ? bip2_bwd_cut().exchange(rows) : bip2_bwd_cut().load();
 }
 
 extern "C" int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_t feat,
@@ -1091,13 +1113,13 @@ extern "C" int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_
   // the mask backward wins on large graphs (bip1m: 450 -> 380-416 us) but not on the shipped
   // ones (R15: 36.6 vs 31.7 us, rocprof, profiles/round5_step_r15_v1): rows per wave too few
   // to amortise its per-wave d_er and slab epilogue.  MSHA_BIP2_BWD_MIN_ROWS moves the cut.
-  static const int64_t min_rows = [] {
-    const char* v = getenv("MSHA_BIP2_BWD_MIN_ROWS");
-    return v != nullptr && *v ? (int64_t)atoll(v) : (int64_t)131072;
-  }();
-  if (g->n_rows >= min_rows && bip2_ok(g, heads, feat, neg_slope) &&
-      bip2_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
-               d_hs, (float*)ws, nb, s))
+  // msha_bip2_bwd_min_rows sets it per process (tests run small graphs through both).
+  if (bip2_ok(g, heads, feat, neg_slope) &&
+      (bip3_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
+                d_hs, (float*)ws, nb, s) ||
+       (g->n_rows >= msha_bip2_bwd_min_rows(-1) &&
+        bip2_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
+                 d_hs, (float*)ws, nb, s))))
     return check_launch("bip_attention_bwd");
   bool done = false;
 #define X(h, f)                                                                                  \

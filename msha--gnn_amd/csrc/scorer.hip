@@ -14,11 +14,41 @@ namespace msha {
 
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
 
+// One pass over a pair batch's row indices (LLP.py:233, h[source_index]): flags[0] = 1
+// when an index lies outside [-rows, rows) (torch's h[idx] raises), flags[1] = 1 when
+// one is negative inside it (torch wraps it to rows + idx).  One global OR per wave.
+__global__ void __launch_bounds__(256) pair_index_check_kernel(
+    int64_t n, const int64_t* __restrict__ gi, int64_t rows_i, const int64_t* __restrict__ gj,
+    int64_t rows_j, int32_t* __restrict__ flags) {
+  bool oob = false, neg = false;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    if (gi != nullptr) {
+      const int64_t v = gi[t];
+      oob |= v >= rows_i || v < -rows_i;
+      neg |= v < 0;
+    }
+    if (gj != nullptr) {
+      const int64_t v = gj[t];
+      oob |= v >= rows_j || v < -rows_j;
+      neg |= v < 0;
+    }
+  }
+  const uint64_t bo = __ballot(oob), bn = __ballot(neg);
+  if (lane_id() == 0) {
+    if (bo) atomicOr(flags, 1);
+    if (bn) atomicOr(flags + 1, 1);
+  }
+}
+
+// rows_i / rows_j bound the gathered rows (INT64_MAX: unchecked); a pair with an index
+// outside [0, rows) scores NaN and sets *err (nullable) instead of reading past the table.
 template <typename T>
 __global__ void __launch_bounds__(256) pair_inner_kernel(
     int64_t n_pairs, int F, const T* __restrict__ G, int64_t ldg,
     const int64_t* __restrict__ gi, const T* __restrict__ G2, int64_t ldg2,
-    const int64_t* __restrict__ gj, float* __restrict__ out) {
+    const int64_t* __restrict__ gj, int64_t rows_i, int64_t rows_j, int32_t* __restrict__ err,
+    float* __restrict__ out) {
   constexpr int V = Pk<T>::V;          // elements per 16-byte lane chunk
   const int lane = lane_id();
   const int QP = F / V;                // lanes per pair
@@ -36,7 +66,12 @@ __global__ void __launch_bounds__(256) pair_inner_kernel(
       if (b < n_pairs && slot < PPW) {
         const int64_t i = gi ? gi[b] : b;
         const int64_t j = gj ? gj[b] : b;
-        acc[u] = pk_dot(pk_load(G + i * ldg + V * q), pk_load(G2 + j * ldg2 + V * q));
+        if ((uint64_t)i < (uint64_t)rows_i && (uint64_t)j < (uint64_t)rows_j) {
+          acc[u] = pk_dot(pk_load(G + i * ldg + V * q), pk_load(G2 + j * ldg2 + V * q));
+        } else {
+          acc[u] = __builtin_nanf("");
+          if (err != nullptr && q == 0) atomicOr(err, 1);
+        }
       }
     }
 #pragma unroll
@@ -152,40 +187,69 @@ extern "C" int msha_pair_hadamard_sigmoid(int64_t n_pairs, int32_t feat, const f
   return check_launch("pair_hadamard_sigmoid");
 }
 
+extern "C" int msha_pair_index_check(int64_t n_pairs, const int64_t* gi, int64_t g_rows,
+                                     const int64_t* gj, int64_t g2_rows, int32_t* flags,
+                                     msha_stream_t stream) {
+  MSHA_ARG_CHECK(n_pairs >= 0 && flags != nullptr, "pair_index_check: bad arguments");
+  MSHA_ARG_CHECK((gi == nullptr || g_rows >= 0) && (gj == nullptr || g2_rows >= 0),
+                 "pair_index_check: negative row count");
+  if (n_pairs == 0 || (gi == nullptr && gj == nullptr)) return MSHA_OK;
+  hipLaunchKernelGGL(pair_index_check_kernel, dim3(grid_for(n_pairs, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, n_pairs, gi, g_rows, gj, g2_rows, flags);
+  return check_launch("pair_index_check");
+}
+
+template <typename T>
+static int pair_inner_launch(const char* name, int vmax, int64_t n_pairs, int32_t feat,
+                             const void* G, int64_t ldg, const int64_t* gi, const void* G2,
+                             int64_t ldg2, const int64_t* gj, int64_t g_rows, int64_t g2_rows,
+                             int32_t* err, float* out, msha_stream_t stream) {
+  constexpr int V = Pk<T>::V;
+  MSHA_ARG_CHECK(n_pairs >= 0 && feat >= V && feat <= vmax && (feat & (feat - 1)) == 0,
+                 "pair_inner_fwd: feat must be a power of two in [16 B, 64 lanes x 16 B]");
+  MSHA_ARG_CHECK(G && G2 && out, "pair_inner_fwd: null pointer");
+  MSHA_ARG_CHECK(ldg % V == 0 && ldg2 % V == 0 && ((uintptr_t)G % 16) == 0 &&
+                     ((uintptr_t)G2 % 16) == 0,
+                 "pair_inner_fwd: tables must be 16-byte aligned with 16-byte rows pitch");
+  if (n_pairs == 0) return MSHA_OK;
+  if (gi == nullptr) g_rows = INT64_MAX;  // row b of the table itself: the caller's count
+  if (gj == nullptr) g2_rows = INT64_MAX;
+  const int ppw = 64 / (feat / V) * 4;
+  hipLaunchKernelGGL(pair_inner_kernel<T>, dim3(grid_for((n_pairs + ppw - 1) / ppw, 4, 1 << 20)),
+                     dim3(256), 0, (hipStream_t)stream, n_pairs, (int)feat, (const T*)G, ldg, gi,
+                     (const T*)G2, ldg2, gj, g_rows, g2_rows, err, out);
+  return check_launch(name);
+}
+
 extern "C" int msha_pair_inner_fwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,
                                    const int64_t* gi, const float* G2, int64_t ldg2,
                                    const int64_t* gj, float* out, msha_stream_t stream) {
-  MSHA_ARG_CHECK(n_pairs >= 0 && feat >= 4 && feat <= 256 && (feat & (feat - 1)) == 0,
-                 "pair_inner_fwd: feat must be a power of two in [4, 256]");
-  MSHA_ARG_CHECK(G && G2 && out, "pair_inner_fwd: null pointer");
-  MSHA_ARG_CHECK(ldg % 4 == 0 && ldg2 % 4 == 0 && ((uintptr_t)G % 16) == 0 &&
-                     ((uintptr_t)G2 % 16) == 0,
-                 "pair_inner_fwd: tables must be 16-byte aligned with ld % 4 == 0");
-  if (n_pairs == 0) return MSHA_OK;
-  const int ppw = 64 / (feat / 4) * 4;
-  hipLaunchKernelGGL(pair_inner_kernel<float>,
-                     dim3(grid_for((n_pairs + ppw - 1) / ppw, 4, 1 << 20)), dim3(256), 0,
-                     (hipStream_t)stream, n_pairs, (int)feat, G, ldg, gi, G2, ldg2, gj, out);
-  return check_launch("pair_inner_fwd");
+  return pair_inner_launch<float>("pair_inner_fwd", 256, n_pairs, feat, G, ldg, gi, G2, ldg2, gj,
+                                  INT64_MAX, INT64_MAX, nullptr, out, stream);
 }
 
 extern "C" int msha_pair_inner_fwd_bf16(int64_t n_pairs, int32_t feat, const void* G,
                                         int64_t ldg, const int64_t* gi, const void* G2,
                                         int64_t ldg2, const int64_t* gj, float* out,
                                         msha_stream_t stream) {
-  MSHA_ARG_CHECK(n_pairs >= 0 && feat >= 8 && feat <= 512 && (feat & (feat - 1)) == 0,
-                 "pair_inner_fwd_bf16: feat must be a power of two in [8, 512]");
-  MSHA_ARG_CHECK(G && G2 && out, "pair_inner_fwd_bf16: null pointer");
-  MSHA_ARG_CHECK(ldg % 8 == 0 && ldg2 % 8 == 0 && ((uintptr_t)G % 16) == 0 &&
-                     ((uintptr_t)G2 % 16) == 0,
-                 "pair_inner_fwd_bf16: tables must be 16-byte aligned with ld % 8 == 0");
-  if (n_pairs == 0) return MSHA_OK;
-  const int ppw = 64 / (feat / 8) * 4;
-  hipLaunchKernelGGL(pair_inner_kernel<bf16_t>,
-                     dim3(grid_for((n_pairs + ppw - 1) / ppw, 4, 1 << 20)), dim3(256), 0,
-                     (hipStream_t)stream, n_pairs, (int)feat, (const bf16_t*)G, ldg, gi,
-                     (const bf16_t*)G2, ldg2, gj, out);
-  return check_launch("pair_inner_fwd_bf16");
+  return pair_inner_launch<bf16_t>("pair_inner_fwd_bf16", 512, n_pairs, feat, G, ldg, gi, G2,
+                                   ldg2, gj, INT64_MAX, INT64_MAX, nullptr, out, stream);
+}
+
+extern "C" int msha_pair_inner_fwd_ex(int64_t n_pairs, int32_t feat, int32_t dtype, const void* G,
+                                      int64_t ldg, const int64_t* gi, int64_t g_rows,
+                                      const void* G2, int64_t ldg2, const int64_t* gj,
+                                      int64_t g2_rows, int32_t* err, float* out,
+                                      msha_stream_t stream) {
+  MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16,
+                 "pair_inner_fwd_ex: dtype must be MSHA_DTYPE_F32 or MSHA_DTYPE_BF16");
+  MSHA_ARG_CHECK((gi == nullptr || g_rows >= 0) && (gj == nullptr || g2_rows >= 0),
+                 "pair_inner_fwd_ex: negative row count");
+  if (dtype == MSHA_DTYPE_BF16)
+    return pair_inner_launch<bf16_t>("pair_inner_fwd_ex", 512, n_pairs, feat, G, ldg, gi, G2, ldg2,
+                                     gj, g_rows, g2_rows, err, out, stream);
+  return pair_inner_launch<float>("pair_inner_fwd_ex", 256, n_pairs, feat, G, ldg, gi, G2, ldg2,
+                                  gj, g_rows, g2_rows, err, out, stream);
 }
 
 extern "C" int msha_pair_inner_bwd(int64_t n_pairs, int32_t feat, const float* G, int64_t ldg,

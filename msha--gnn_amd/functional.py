@@ -992,25 +992,59 @@ def pair_layer(x_i, x_j, W, b, p=0.0, training=False, sigmoid=False, seed=None):
     return _PairLayer.apply(x_i, x_j, W, b, p, seed, sigmoid)
 
 
-def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None, out_dtype=None):
+def check_pair_indices(src, dst, rows: int, rows2: int | None = None):
+    """torch's ``h[idx]`` index rule for a fused pair gather (LLP.py:233): an index
+    outside [-rows, rows) raises IndexError; negative ones inside are wrapped to
+    rows + idx.  One device pass (``msha_pair_index_check``) and one flag read (a
+    stream sync).  Returns the (possibly wrapped) int64 index tensors."""
+    rows2 = rows if rows2 is None else rows2
+    src = src.to(torch.int64).contiguous()
+    dst = dst.to(torch.int64).contiguous()
+    if src.numel() != dst.numel():
+        raise ValueError(f"pair indices differ in length: {src.numel()} vs {dst.numel()}")
+    flags = torch.zeros(2, dtype=torch.int32, device=src.device)
+    _lib.call("msha_pair_index_check", src.numel(), src.data_ptr(), int(rows), dst.data_ptr(),
+              int(rows2), flags.data_ptr(), _stream(src))
+    oob, neg = flags.tolist()
+    if oob:
+        for idx, n in ((src, rows), (dst, rows2)):
+            bad = idx[(idx >= n) | (idx < -n)]
+            if bad.numel():
+                raise IndexError(f"index {int(bad[0])} is out of bounds for dimension 0 "
+                                 f"with size {n}")
+    if neg:
+        src = torch.where(src < 0, src + rows, src)
+        dst = torch.where(dst < 0, dst + rows2, dst)
+    return src, dst
+
+
+def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None, out_dtype=None,
+                check=True):
     """Fused caller gather + predictor (LLP.py:233 + LLP.py:104-115), inference:
     ``predictor(h[src], h[dst])`` without materialising the gathered rows.
     'inner' -> (P,), 'mlp' (one used Linear W (hidden, F), b) -> (P, hidden).
     A bf16 ``h`` runs the bf16 kernels (bf16 MFMA for 'mlp'; fp32 scores, or bf16
-    'mlp' scores with ``out_dtype=torch.bfloat16``, as a bf16 LinkPredictor returns)."""
+    'mlp' scores with ``out_dtype=torch.bfloat16``, as a bf16 LinkPredictor returns).
+    ``check`` (default) applies torch's ``h[idx]`` rule first (``check_pair_indices``:
+    IndexError outside [-n, n), negative indices wrapped; one stream sync).  With
+    ``check=False`` the caller vouches for indices in [0, n) (a pipelined scorer whose
+    batch was checked once); the 'inner' kernel still bounds every row and scores a
+    stray pair NaN, the fp32 'mlp' gather reads zeros for it."""
     _lib.require_cuda(h, src, dst)
     dt = _table_dtype(h)
     h = _tc(h, dt)
     bf = dt == BF16
+    if check:
+        src, dst = check_pair_indices(src, dst, h.shape[0])
     src = src.to(torch.int64).contiguous()
     dst = dst.to(torch.int64).contiguous()
     P, Fd = src.numel(), h.shape[1]
     s = _stream(h)
     if mode == "inner":
         out = torch.empty(P, device=h.device, dtype=torch.float32) if out is None else out
-        _lib.call("msha_pair_inner_fwd_bf16" if bf else "msha_pair_inner_fwd", P, Fd,
-                  h.data_ptr(), h.stride(0), src.data_ptr(), h.data_ptr(), h.stride(0),
-                  dst.data_ptr(), out.data_ptr(), s)
+        _lib.call("msha_pair_inner_fwd_ex", P, Fd, _code(dt), h.data_ptr(),
+                  h.stride(0), src.data_ptr(), h.shape[0], h.data_ptr(), h.stride(0),
+                  dst.data_ptr(), h.shape[0], None, out.data_ptr(), s)
         return out
     W, b = _tc(W, dt), _f32c(b)
     N = W.shape[0]

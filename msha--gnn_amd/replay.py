@@ -23,11 +23,21 @@ statements (the loss, ``.item()``, torch's Adam) run unchanged around it.
   ``.grad`` by the node's backward itself: with ``zero_grad()`` setting ``.grad`` to None
   (torch's default, train.py:226) ``.grad`` becomes an alias of the static buffer, as the
   AccumulateGrad nodes of ``torch.cuda.make_graphed_callables`` adopt theirs; an existing
-  ``.grad`` is added to (one that already aliases the buffer, zeroed in place, holds the
-  new gradient after the replay).  The parameters are not inputs of the node, so the
-  engine runs no AccumulateGrad node per parameter (~20 per model: ~0.1 ms of host time
-  per backward); one anchor leaf makes the output require grad.  Parameter hooks
-  (``register_hook`` / post-accumulate hooks) do not fire on this path.
+  ``.grad`` is added to.  Accumulation keeps torch's semantics: a ``.grad`` that still
+  aliases the static buffer when the next forward or backward replays (two ``backward()``
+  calls without ``zero_grad()``, or ``zero_grad(set_to_none=False)``) is first moved to a
+  fresh tensor -- the forward graph shares the backward graph's memory pool, so its
+  replay would overwrite the buffer -- and the replayed gradient is added to it.  With
+  ``zero_grad()`` (set to None) before each forward, as train.py does, no copy is made.  The parameters are not inputs of the
+  node, so the engine runs no AccumulateGrad node per parameter (~20 per model: ~0.1 ms
+  of host time per backward); one anchor leaf makes the output require grad.  Parameter
+  hooks (``register_hook`` / post-accumulate hooks) do not fire on this path.
+* The forward hands back a fresh copy of the graph's static output, so an output held
+  across iterations keeps its values.  The graph's saved activations serve one pending
+  backward at a time: a forward whose graph still has a live, un-run backward (two
+  forwards before one ``backward()``) runs the eager path instead, and a backward of an
+  output whose graph has replayed a newer forward since raises instead of replaying on
+  the newer activations.
 * Not replayed (the eager path runs): eval mode, no grad mode, record mode, an outer
   graph capture (``step.GraphedStep``), a parameter registered with
   ``optim.Adam.fuse_dropout_grad``, or ``MSHA_MODEL_REPLAY=0``.
@@ -35,6 +45,7 @@ statements (the loss, ``.item()``, torch's Adam) run unchanged around it.
 from __future__ import annotations
 
 import os
+import weakref
 from collections import OrderedDict
 
 import torch
@@ -60,6 +71,8 @@ class _ModelGraphs:
     def __init__(self, fwd, params, buffers, src, keep):
         dev = src.device
         self.params = params
+        self.gen = 0  # forward replays so far; a backward replays only the newest
+        self.pending = None  # weakref to the newest forward's autograd node until its backward
         self.keep = keep  # the adjacencies the captured launches read: kept alive
         self.src = src.detach().clone()
         self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -94,23 +107,44 @@ class _ModelGraphs:
 class _Replay(torch.autograd.Function):
     @staticmethod
     def forward(ctx, graphs, src, anchor):
+        # the forward graph reuses the pool the backward graph's gradient buffers live in:
+        # a .grad still aliasing one of them (kept across iterations, no zero_grad) is
+        # moved out first, or the replay would overwrite it
+        for p, gr in zip(graphs.params, graphs.grads):
+            cur = p.grad
+            if gr is not None and cur is not None and cur.data_ptr() == gr.data_ptr():
+                p.grad = cur.clone()
         graphs.src.copy_(src)
         graphs.fwd.replay()
-        ctx.graphs = graphs
-        return graphs.out.detach()
+        graphs.gen += 1
+        graphs.pending = weakref.ref(ctx)
+        ctx.graphs, ctx.gen = graphs, graphs.gen
+        return graphs.out.clone()
 
     @staticmethod
     def backward(ctx, dout):
         g = ctx.graphs
+        if ctx.gen != g.gen:
+            raise RuntimeError(
+                "msha replay: backward of a model output whose captured graph has replayed a "
+                "newer forward since; run the backward before the next training forward, or "
+                "set MSHA_MODEL_REPLAY=0")
+        # a .grad still aliasing its static buffer holds an earlier gradient that the
+        # replay would overwrite: move it out, then accumulate as torch would
+        for p, gr in zip(g.params, g.grads):
+            cur = p.grad
+            if gr is not None and cur is not None and cur.data_ptr() == gr.data_ptr():
+                p.grad = cur.clone()
         g.dout.copy_(dout)
         g.bwd.replay()
+        g.pending = None
         for p, gr in zip(g.params, g.grads):
             if gr is None:
                 continue
             cur = p.grad
             if cur is None:
                 p.grad = gr.detach()
-            elif cur.data_ptr() != gr.data_ptr():
+            else:
                 cur.add_(gr)
         return None, None, None
 
@@ -123,12 +157,10 @@ def run(model, fwd, consts, source_index):
     cache = d.get("_msha_graphs")
     if cache is None:
         cache = d["_msha_graphs"] = OrderedDict()
-    params = d.get("_msha_params")
-    if params is None or len(params) != sum(1 for _ in model.parameters()):
-        params = d["_msha_params"] = [p for p in model.parameters() if p.requires_grad]
+    params = [p for p in model.parameters() if p.requires_grad]  # current objects
     key = (tuple((id(c), getattr(c, "_version", None)) for c in consts),
            source_index.shape, source_index.dtype, model.dropout,
-           tuple([p.data_ptr() for p in params]))
+           tuple([(id(p), p.data_ptr()) for p in params]))
     g = cache.get(key)
     if g is None:
         if any(getattr(p, "_msha_fused_adam", None) is not None for p in params):
@@ -138,6 +170,8 @@ def run(model, fwd, consts, source_index):
         while len(cache) > MAX_GRAPHS:
             cache.popitem(last=False)
     else:
+        if g.pending is not None and g.pending() is not None:
+            return fwd(source_index)  # its previous output's backward is still to run: eager
         cache.move_to_end(key)
     anchor = d.get("_msha_anchor")
     if anchor is None or anchor.device != source_index.device:

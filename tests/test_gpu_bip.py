@@ -210,3 +210,35 @@ def test_shipped_graph_models_run_on_the_bipartite_kernels(cuda, msha):
     assert {"bip_attention_fwd", "bip_attention_bwd"} <= names, names
     assert not names & {"edge_attention_fwd", "edge_attention_bwd_rows", "csc_aggregate"}, names
     assert torch.allclose(out.detach().exp().sum(1), torch.ones(n, device=cuda), atol=1e-4)
+
+
+@pytest.fixture
+def mask_bwd_everywhere(msha):
+    """Route every M <= 32, 2 x 64 graph through the row-mask backward (bip2_bwd), not
+    only those above the 131,072-row cut (msha_bip2_bwd_min_rows)."""
+    from msha_gnn_amd import _lib
+
+    prev = _lib.fn("msha_bip2_bwd_min_rows")(0)
+    yield
+    _lib.fn("msha_bip2_bwd_min_rows")(prev)
+
+
+MASK_CASES = [c for c in CASES if c[1] <= 32 and c[2] == 2 and c[3] == 64]
+
+
+@pytest.mark.parametrize("case", MASK_CASES, ids=lambda c: f"n{c[0]}m{c[1]}d{c[4]}")
+@pytest.mark.parametrize("p", [0.0, 0.5])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_bip_mask_backward_small_graphs(cuda, msha, mask_bwd_everywhere, case, p, dtype):
+    """The row-mask backward's template variants (dropout keep-bit regeneration, bf16)
+    on the small graphs, every output against the fp64 oracle and the general kernels."""
+    test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.4])
+def test_ours_attention_mask_backward(cuda, msha, mask_bwd_everywhere, p):
+    """Ours (row_coef, with and without dropout) through the row-mask backward: the
+    COEF / DROP variants of bip2_bwd_kernel against the dense fp64 restatement."""
+    from test_gpu_ours import check_ours_attention_vs_dense
+
+    check_ours_attention_vs_dense(cuda, p)

@@ -237,3 +237,138 @@ def test_model_replay_matches_eager(cuda, msha, kind):
     outs = [model(inter, city, prov, src).detach().clone() for _ in range(3)]
     assert model.__dict__.get("_msha_graphs")
     assert not torch.equal(outs[1], outs[2]) and torch.isfinite(outs[2]).all()
+
+
+def _ours_small(cuda, msha, kind="Ours", p=0.0):
+    from msha_gnn_amd import layers
+    from msha_gnn_amd.data import GroupAdjacency
+
+    z = golden("ours_small.npz")
+    inter = msha.normalize_adjacency_matrix(t(z["counts"], cuda))
+    city = GroupAdjacency(torch.as_tensor(z["city"], device=cuda))
+    prov = GroupAdjacency(torch.as_tensor(z["prov"], device=cuda))
+    src = torch.as_tensor(z["source_index"], device=cuda)
+    tgt = torch.as_tensor(np.arange(src.numel()) % z["counts"].shape[1], device=cuda)
+    n, m = z["counts"].shape
+    cls = layers.Ours if kind == "Ours" else layers.ablation3
+    torch.manual_seed(0)
+    model = cls(16, 8, m, 2, p, {i: 0.1 * i for i in range(n)}, n, m).to(cuda)
+    model.train()
+    return model, (inter, city, prov), src, tgt
+
+
+def _grads(model):
+    return {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("kind", ["Ours", "ablation3"])
+def test_model_replay_accumulates_like_eager(cuda, msha, kind):
+    """replay.py keeps torch's gradient semantics: two backward() calls without
+    zero_grad() accumulate (the first .grad aliases the static buffer), and
+    zero_grad(set_to_none=False) followed by a backward gives the new gradient."""
+    from msha_gnn_amd import replay
+
+    res = {}
+    for rp in (False, True):
+        replay.REPLAY = rp
+        try:
+            model, consts, src, tgt = _ours_small(cuda, msha, kind)
+            for _ in range(2):  # settle the capture first (replay: warm-up + capture)
+                model.zero_grad()
+                F.nll_loss(model(*consts, src)[src], tgt).backward()
+            model.zero_grad()
+            F.nll_loss(model(*consts, src)[src], tgt).backward()
+            one = _grads(model)
+            F.nll_loss(model(*consts, src)[src], tgt).backward()  # no zero_grad: accumulate
+            two = _grads(model)
+            model.zero_grad(set_to_none=False)
+            F.nll_loss(model(*consts, src)[src], tgt).backward()
+            again = _grads(model)
+            if rp:
+                assert model.__dict__.get("_msha_graphs"), "replay path not taken"
+            res[rp] = (one, two, again)
+        finally:
+            replay.REPLAY = True
+    # (dropout 0, parameters unchanged: every backward adds the same gradient)
+    for rp in (False, True):
+        for k in res[rp][0]:
+            one, two, again = (r[k] for r in res[rp])
+            d2 = float((two - 2 * one).abs().max())
+            da = float((again - one).abs().max())
+            scale = float(one.abs().max())
+            assert d2 <= 1e-6 * scale and da <= 1e-6 * scale, (
+                f"replay={rp} {k}: |two - 2 one| {d2:.3g}, |again - one| {da:.3g}, max|one| {scale:.3g}")
+    for k in res[False][0]:
+        torch.testing.assert_close(res[True][0][k], res[False][0][k], rtol=1e-5, atol=1e-7, msg=k)
+
+
+def test_model_replay_pending_output_and_stale_backward(cuda, msha):
+    """Two forwards before one backward match eager (the second runs eagerly while the
+    first output's backward is pending); an output held across iterations keeps its
+    values; a backward of an output whose graph replayed a newer forward raises."""
+    from msha_gnn_amd import replay
+
+    res = {}
+    for rp in (False, True):
+        replay.REPLAY = rp
+        try:
+            model, consts, src, tgt = _ours_small(cuda, msha, "Ours")
+            for _ in range(2):
+                model.zero_grad()
+                F.nll_loss(model(*consts, src)[src], tgt).backward()
+            model.zero_grad()
+            o1 = model(*consts, src)
+            o2 = model(*consts, src)
+            (F.nll_loss(o1[src], tgt) + 0.5 * F.nll_loss(o2[src], tgt)).backward()
+            res[rp] = (o1.detach().clone(), o2.detach().clone(), _grads(model))
+            if rp:
+                held = o1.detach()
+                snap = held.clone()
+                model.zero_grad()
+                F.nll_loss(model(*consts, src)[src], tgt).backward()
+                assert torch.equal(held, snap), "held output changed by the next replay"
+                l1 = F.nll_loss(model(*consts, src)[src], tgt)
+                l1.backward(retain_graph=True)
+                F.nll_loss(model(*consts, src)[src], tgt).backward()
+                with pytest.raises(RuntimeError, match="newer forward"):
+                    l1.backward()
+        finally:
+            replay.REPLAY = True
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-6, atol=1e-6)
+    for k, v in res[False][2].items():
+        torch.testing.assert_close(res[True][2][k], v, rtol=1e-5, atol=1e-7, msg=k)
+
+
+def test_model_replay_follows_replaced_parameter(cuda, msha):
+    """A Parameter object replaced on the model is trained: the captured graphs are
+    keyed on the current parameter objects, not a cached list."""
+    from msha_gnn_amd import replay
+
+    model, consts, src, tgt = _ours_small(cuda, msha, "ablation3")
+    for _ in range(3):
+        model.zero_grad()
+        F.nll_loss(model(*consts, src)[src], tgt).backward()
+    name, old = next((k, p) for k, p in model.named_parameters() if p.dim() == 2)
+    mod = model
+    *path, leaf = name.split(".")
+    for a in path:
+        mod = getattr(mod, a)
+    old_grad = old.grad.detach().clone()
+    new = torch.nn.Parameter(old.detach().clone() * 1.5)
+    setattr(mod, leaf, new)
+    model.zero_grad()
+    F.nll_loss(model(*consts, src)[src], tgt).backward()
+    assert new.grad is not None and torch.isfinite(new.grad).all()
+    assert torch.equal(old.grad, old_grad), "the replaced parameter's gradient moved"
+    replay.REPLAY = False
+    try:
+        model.zero_grad()
+        ref = F.nll_loss(model(*consts, src)[src], tgt)
+        ref.backward()
+        want = new.grad.detach().clone()
+    finally:
+        replay.REPLAY = True
+    model.zero_grad()
+    F.nll_loss(model(*consts, src)[src], tgt).backward()
+    torch.testing.assert_close(new.grad, want, rtol=1e-5, atol=1e-7)

@@ -200,17 +200,20 @@ def test_head_bf16_vs_fp64(cuda, msha):
 
 
 def test_models_use_the_fused_head(cuda, msha):
-    """ablation3 / Ours route their tail through the model head in training and under
-    no_grad; eval with autograd takes the per-head launches."""
+    """ablation3 / Ours route their tail through the model head in training (eager and
+    inside the replay path's captured forward) and under no_grad; eval with autograd
+    takes the per-head launches."""
     from msha_gnn_amd import layers
 
     class Probe:
         calls = 0
+        captured = 0
 
     orig = layers.MF.model_head
 
     def probe(*a, **k):
         Probe.calls += 1
+        Probe.captured += int(torch.cuda.is_current_stream_capturing())
         return orig(*a, **k)
 
     from msha_gnn_amd import replay
@@ -220,17 +223,26 @@ def test_models_use_the_fused_head(cuda, msha):
     torch.manual_seed(0)
     model = layers.ablation3(128, 64, 32, 2, 0.5, gdp, 200, 32).to(cuda)
     layers.MF.model_head = probe
-    prev, replay.REPLAY = replay.REPLAY, False  # count the eager forward's calls
+    prev = replay.REPLAY
     try:
         model.train()
+        replay.REPLAY = False  # eager training forward: one head call
         model(g, None, None, torch.arange(4, device=cuda)).sum().backward()
-        assert Probe.calls == 1
+        assert Probe.calls == 1 and Probe.captured == 0
+        replay.REPLAY = True  # replay path: the head is inside the captured forward
+        src = torch.arange(4, device=cuda)
+        model(g, None, None, src).sum().backward()
+        assert model.__dict__.get("_msha_graphs"), "replay path not taken"
+        assert Probe.captured == 1, "captured forward did not route through the model head"
+        before = Probe.calls
+        model(g, None, None, src).sum().backward()  # pure replay: no Python head call
+        assert Probe.calls == before
         model.eval()
         with torch.no_grad():
             model(g, None, None, None)
-        assert Probe.calls == 2
+        assert Probe.calls == before + 1
         model(g, None, None, None)
-        assert Probe.calls == 2
+        assert Probe.calls == before + 1
     finally:
         replay.REPLAY = prev
         layers.MF.model_head = orig

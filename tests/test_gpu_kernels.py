@@ -663,6 +663,54 @@ def test_score_pairs_fused_gather(cuda, F):
     tol_close(mlp, O.score_pairs(h, src, dst, "mlp", [(W, b), (None, None)]), 1e-5, 1e-6)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_score_pairs_index_rule(cuda, dt):
+    """The fused gather follows torch's h[idx] (LLP.py:233): an index n or -(n+1) raises
+    IndexError in both 'inner' and 'mlp'; -1 is row n-1; the 'inner' kernel given row
+    counts scores a stray pair NaN and sets its error flag instead of reading past h."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(3)
+    n, P, F, hid = 3000, 4096, 64, 64
+    h = t(rng.standard_normal((n, F)).astype(np.float32), cuda, dt)
+    W = t((rng.standard_normal((hid, F)) / 8).astype(np.float32), cuda, dt)
+    b = t(rng.standard_normal(hid).astype(np.float32), cuda)
+    src = torch.as_tensor(rng.integers(0, n, P), device=cuda)
+    dst = torch.as_tensor(rng.integers(0, n, P), device=cuda)
+    for mode in ("inner", "mlp"):
+        args = (W, b) if mode == "mlp" else ()
+        for bad in (n, -(n + 1), 10 * n):
+            for which in (0, 1):
+                s_, d_ = src.clone(), dst.clone()
+                (s_, d_)[which][P // 2] = bad
+                with pytest.raises(IndexError, match="out of bounds"):
+                    MF.score_pairs(h, s_, d_, mode, *args)
+        # negative indices wrap like torch's
+        s_, d_ = src.clone(), dst.clone()
+        s_[:7] = -1
+        d_[100:110] = -torch.arange(1, 11, device=cuda)
+        got = MF.score_pairs(h, s_, d_, mode, *args)
+        want = MF.score_pairs(h, torch.where(s_ < 0, s_ + n, s_), torch.where(d_ < 0, d_ + n, d_),
+                              mode, *args)
+        assert torch.equal(got, want)
+    # the kernel-side guard of the unchecked 'inner' path
+    s_ = src.clone()
+    s_[5], s_[77] = n, -1
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    out = torch.empty(P, device=cuda)
+    _lib.call("msha_pair_inner_fwd_ex", P, F, MF._code(dt), h.data_ptr(), h.stride(0),
+              s_.data_ptr(), n, h.data_ptr(), h.stride(0), dst.data_ptr(), n, err.data_ptr(),
+              out.data_ptr(), MF._stream(h))
+    assert int(err.item()) == 1
+    o = out.cpu()
+    assert torch.isnan(o[5]) and torch.isnan(o[77])
+    ok = torch.ones(P, dtype=torch.bool)
+    ok[[5, 77]] = False
+    ref = MF.score_pairs(h, src, dst, "inner").cpu()
+    assert torch.equal(o[ok], ref[ok])
+
+
 # ------------------------------------------------------- BatchNorm + LeakyReLU
 @pytest.mark.parametrize("R,C,dtype", [(32, 64, "f32"), (39179, 64, "f32"), (1000, 300, "f32"),
                                        (5000, 64, "bf16")])
