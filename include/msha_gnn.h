@@ -698,14 +698,16 @@ MSHA_API int msha_dropout_keep_mask_word(uint64_t seed, uint64_t offset, int64_t
  *   g  = grad (* keep * 1/(1-p) when drop_p > 0) + weight_decay * param
  *   m  = m + (1 - beta1) (g - m);  v = beta2 v + (1 - beta2) g^2
  *   t  = *step + 1;  param -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
- * with *step advanced first by a one-block launch (capturable: the step lives on the
- * device, as torch's capturable Adam keeps it).  param, grad, exp_avg, exp_avg_sq share `dtype` (bf16 state for bf16
+ * in one launch: every block reads *step and uses *step + 1, and the last block to finish
+ * advances *step (capturable: the step lives on the device, as torch's capturable Adam
+ * keeps it).  param, grad, exp_avg, exp_avg_sq share `dtype` (bf16 state for bf16
  * parameters, as torch keeps it), contiguous, n elements.  drop_p > 0 fuses a dropout
  * backward into the gradient read: grad is then the dropout's OUTPUT gradient and keep is
  * msha_segments' flat mask (element e: word e % 4 of the Philox4x32-10 block (drop_seed;
  * counter {e / 4, drop_offset})), so the parameter's own gradient never exists (the
  * feature dropout of Sfeatures, Ablation.py:296, Ours.py:161).  ws: device scratch of
- * msha_adam_workspace_size() bytes (the step's per-tensor scalars; stream-ordered reuse). */
+ * msha_adam_workspace_size() bytes, zero-filled before its first use (the launch's
+ * completion ticket, left at zero by every launch; stream-ordered reuse). */
 #define MSHA_MAX_ADAM 64
 typedef struct msha_adam_tensor {
   void* param;

@@ -123,6 +123,29 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
   static constexpr uint32_t RB = kD * sizeof(T);     // bytes per table row
 };
 
+// LDS staging image of a 32-row x 64-feature tile: rows padded by 16 bytes, so the 8 rows
+// a B-fragment read walks (one feature each, ds_read2 pairs 1 row apart) sit on
+// different banks
+#ifndef BIP3_PAD
+#define BIP3_PAD 1
+#endif
+#ifndef BIP3_HSLATE
+#define BIP3_HSLATE 0  // 1 (hs pieces issued after d_hs) failed the 120k-row d_hs check with the padded staging; not understood, off
+#endif
+template <typename T>
+struct Stg {
+  static constexpr int P = kF + (BIP3_PAD ? 16 / (int)sizeof(T) : 0);  // row pitch in elements
+  static constexpr int N = 32 * P;                    // elements per image
+};
+
+// att^T image [term][row 32][col 32] bf16: the 8-byte block cb (columns 4 cb .. 4 cb + 3)
+// of row r sits at block cb ^ ((r >> 1) & 7), so the 32 rows' writes of one block spread
+// over 16 bank pairs (unswizzled, 64-byte rows put them on 2) and each transposed read of
+// 4 rows x 8 blocks still covers 64 distinct banks
+__device__ __forceinline__ int img_off(int q, int r, int cb) {
+  return (q * 32 + r) * 32 + 4 * (cb ^ ((r >> 1) & 7));
+}
+
 // one 8-row x 1-feature fragment of a streamed table, raw (rows along k)
 template <typename T>
 struct Chunk {
@@ -169,7 +192,7 @@ __device__ __forceinline__ void chunk_terms(const Chunk<T>& c, bf16x8 (&b)[Tab<T
 template <typename T>
 __device__ __forceinline__ void st_frag(T* st, const f32x16& acc, int n, int t, int c) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) st[((i & 3) + 8 * (i >> 2) + 4 * c) * kF + 32 * n + t] = (T)acc[i];
+  for (int i = 0; i < 16; ++i) st[((i & 3) + 8 * (i >> 2) + 4 * c) * Stg<T>::P + 32 * n + t] = (T)acc[i];
 }
 template <typename T>
 __device__ __forceinline__ void flush_rows(const T* st, rsrc_t rs, int32_t r0, int h, int lane) {
@@ -178,7 +201,7 @@ __device__ __forceinline__ void flush_rows(const T* st, rsrc_t rs, int32_t r0, i
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int q = lane + 64 * k, row = q / CPR, pc = q % CPR;
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(st + row * kF + pc * (16 / (int)sizeof(T)));
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(st + row * Stg<T>::P + pc * (16 / (int)sizeof(T)));
     __builtin_amdgcn_raw_buffer_store_b128(
         v, rs, (uint32_t)row * Tab<T>::RB + (uint32_t)(h * kF) * sizeof(T) + (uint32_t)pc * 16u,
         (uint32_t)r0 * Tab<T>::RB, 0);
@@ -207,7 +230,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
   __shared__ float ert[64];
   __shared__ __attribute__((aligned(16))) bf16_t trb[HS ? (kWaves * TRW > 16384 ? kWaves * TRW : 16384) : 8];  // >= the 32 KB reduce
   __shared__ uint64_t kw[DROP ? kWaves : 1][32];
-  __shared__ __attribute__((aligned(16))) T ust[BIP3_UST ? kWaves : 1][32 * kF];
+  __shared__ __attribute__((aligned(16))) T ust[BIP3_UST ? kWaves : 1][Stg<T>::N];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = wv & 1;
@@ -406,7 +429,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
           for (int m = 0; m < 4; ++m) {
             const int s = m >> 1, o = 4 * (m & 1);
             bf16x4 v4 = {A[s][q][o], A[s][q][o + 1], A[s][q][o + 2], A[s][q][o + 3]};
-            *reinterpret_cast<bf16x4*>(img + (q * 32 + t) * 32 + 4 * c + 8 * m) = v4;
+            *reinterpret_cast<bf16x4*>(img + img_off(q, t, c + 2 * m)) = v4;
           }
       }
 
@@ -449,7 +472,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < NPc; ++k) {
           const int q = lane + 64 * k, row = q / CPR, pc = q % CPR;
-          *reinterpret_cast<u32x4_t*>(hsi + row * kF + pc * (16 / (int)sizeof(T))) = ring.p[k];
+          *reinterpret_cast<u32x4_t*>(hsi + row * Stg<T>::P + pc * (16 / (int)sizeof(T))) = ring.p[k];
         }
         load_ring(r0 + kPf * kTile, ring);
 #endif
@@ -462,13 +485,13 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
             Chunk<T> chk;
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              chk.w[j] = __float_as_uint(hsi[(16 * s + 8 * c + j) * kF + 32 * n + t]);
+              chk.w[j] = __float_as_uint(hsi[(16 * s + 8 * c + j) * Stg<T>::P + 32 * n + t]);
             chunk_terms<T>(chk, B);
           } else {
-            const bf16_t* p = reinterpret_cast<const bf16_t*>(hsi) + (16 * s + 8 * c + qq) * kF +
+            const bf16_t* p = reinterpret_cast<const bf16_t*>(hsi) + (16 * s + 8 * c + qq) * Stg<T>::P +
                               32 * n + 16 * (g & 1) + 4 * pp;
             const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)p);
-            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(p + 4 * kF));
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(p + 4 * Stg<T>::P));
             B[0] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
 #else
@@ -480,9 +503,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
           for (int q = 0; q < NA; ++q) {
             // block rows 16 s + 8 c + {0..3 | 4..7}, columns 16 (g & 1) + 4 pp; the lane
             // gets column 16 (g & 1) + i16 = lane & 31
-            const bf16_t* p = img + (q * 32 + 16 * s + 8 * c + qq) * 32 + 16 * (g & 1) + 4 * pp;
-            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)p);
-            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(p + 4 * 32));
+            const int rr = 16 * s + 8 * c + qq, cb = 4 * (g & 1) + pp;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + img_off(q, rr, cb)));
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + img_off(q, rr + 4, cb)));
             At[q] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
           vacc[n] = prod<NA, NT>(At, B, vacc[n]);
@@ -535,17 +558,19 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
 //   ds_ij = att_ij (keep_ij g_ij - D_i),  de_ij = ds_ij lrelu'(pre_ij),
 //   d_el_i = sum_j de_ij,  d_er_j = sum_i de_ij,  d_hs_i = sum_j attd_ij dV_j,
 //   d_hc_j = sum_i attd_ij dU_i.
-// Per 32-row tile and head (one head per wave, as the forward):
+// A block takes one head (blockIdx.x & 1), its 8 waves their own row ranges.  Per 32-row
+// tile:
 //   phase A (lane (t, c)): att from lse on the lane's 16 columns, the keep bits;
-//   G^T = [hc | dV] [dU | hs]^T on the matrix cores (K = 128): A = a per-block LDS image
-//     of [hc | dV] fragments (column on the lane), B = the rows' dU / hs pieces with the
-//     features along k (two 16-byte loads per lane and k-step).  The accumulator tile
-//     has the row on the lane and the columns col(c, r) in its registers: exactly phase
-//     A's layout, so phase C needs no lane movement;
+//   G^T = [hc | dV] [dU | hs]^T on the matrix cores (K = 128): A = the block's LDS image of
+//     [hc | dV] fragments (column on the lane), B = the rows' dU / hs pieces with the
+//     features along k (16-byte loads, one tile ahead).  The accumulator tile has the row
+//     on the lane and the columns col(c, r) in its registers: phase A's layout, so phase C
+//     needs no lane movement.  The dU pieces also go to the wave's staging image;
 //   phase C (lane (t, c)): D, ds, de, d_el (one permlane32 swap per sum), d_er summed over
 //     the tile's rows by a recursive-halving exchange into one register per lane;
-//   d_hs = attd dV (A = attd as it stands, B = dV fragments from LDS), d_hc += attd^T dU
-//     (A = the attd^T image, B = dU with the rows along k, reloaded from L2).
+//   d_hc += attd^T dU (A = the attd^T image, B = dU with the rows along k, read from the
+//     staging image), then d_hs = attd dV (A = attd as it stands, B = dV fragments) leaves
+//     through the same staging image as 16-byte row pieces.
 template <typename T, bool HS, bool COEF, bool DROP>
 __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
     const uint32_t* __restrict__ rowmask, const int32_t* __restrict__ rowptr,
@@ -558,64 +583,66 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
   constexpr uint32_t RB = Tab<T>::RB;
   constexpr int TRW = NA * 32 * 32;
   constexpr int KS = HS ? 8 : 4;  // k-steps of G (16 features each: dU, then hs)
-  constexpr int kPairs = kWaves / 2;
-  __shared__ bf16x8 afr[2 * KS * NT * 64];           // [h][k-step][term][lane]
-  __shared__ bf16x8 bdv[HS ? 8 * NT * 64 : 1];       // [h][n][s][term][lane]
+  constexpr int SGW = Stg<T>::N * (int)sizeof(T) / 2;  // staging image per wave, in bf16 units
+  // the end-of-kernel reduce reuses the per-wave images: 4 x 32 x 64 floats
+  constexpr int IMG = kWaves * (TRW + SGW) > 16384 ? kWaves * (TRW + SGW) : 16384;
+  __shared__ bf16x8 afr[KS * NT * 64];           // [k-step][term][lane]
+  __shared__ bf16x8 bdv[HS ? 4 * NT * 64 : 1];   // [n][s][term][lane]
   __shared__ float ert[64];
-  __shared__ __attribute__((aligned(16))) bf16_t trb[kWaves * TRW > 16384 ? kWaves * TRW : 16384];
+  __shared__ __attribute__((aligned(16))) bf16_t trb[IMG];
   __shared__ uint64_t kw[DROP ? kWaves : 1][16];
   __shared__ float sder[kWaves][32];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = wv & 1;
+  const int h = blockIdx.x & 1;
   const int t = lane & 31, c = lane >> 5;
 
-  // A fragments of [hc | dV]: item (h, k-step) x lane (j, c) holds the 8 features
-  // 16 k' + 8 c .. + 7 of head h of hc[j] (k' = k-step < 4) or dV[j] (k-step - 4)
-  for (int it = tid; it < 2 * KS * 64; it += kWaves * 64) {
-    const int l = it & 63, hk = it >> 6, ks = hk % KS, hh = hk / KS;
+  // A fragments of [hc | dV] of head h: k-step x lane (j, c) holds the 8 features
+  // 16 k' + 8 c .. + 7 of hc[j] (k' = k-step < 4) or dV[j] (k-step - 4)
+  for (int it = tid; it < KS * 64; it += kWaves * 64) {
+    const int l = it & 63, ks = it >> 6;
     const int j = l & 31, cc = l >> 5;
     const T* src = ks < 4 ? hc : dV;
-    const int f0 = hh * kF + 16 * (ks & 3) + 8 * cc;
+    const int f0 = h * kF + 16 * (ks & 3) + 8 * cc;
     float x[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) x[q] = j < M ? to_f32(src[j * kD + f0 + q]) : 0.f;
     const Terms<NT> tt = split<NT>(x);
 #pragma unroll
-    for (int q = 0; q < NT; ++q) afr[(hk * NT + q) * 64 + l] = tt.t[q];
+    for (int q = 0; q < NT; ++q) afr[(ks * NT + q) * 64 + l] = tt.t[q];
   }
   if (HS) {  // B fragments of dV for d_hs: as the forward's hc image
-    for (int it = tid; it < 8 * 64; it += kWaves * 64) {
-      const int l = it & 63, hns = it >> 6, s = hns & 1, n = (hns >> 1) & 1, hh = hns >> 2;
+    for (int it = tid; it < 4 * 64; it += kWaves * 64) {
+      const int l = it & 63, ns = it >> 6, s = ns & 1, n = ns >> 1;
       const int f = l & 31, cc = l >> 5;
       float x[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int col = col_of(cc, 8 * s + j);
-        x[j] = col < M ? to_f32(dV[col * kD + hh * kF + 32 * n + f]) : 0.f;
+        x[j] = col < M ? to_f32(dV[col * kD + h * kF + 32 * n + f]) : 0.f;
       }
       const Terms<NT> tt = split<NT>(x);
 #pragma unroll
-      for (int q = 0; q < NT; ++q) bdv[(hns * NT + q) * 64 + l] = tt.t[q];
+      for (int q = 0; q < NT; ++q) bdv[(ns * NT + q) * 64 + l] = tt.t[q];
     }
   }
   if (tid < 64) ert[tid] = (tid >> 1) < M ? er[tid] : 0.f;
   __syncthreads();
 
   const uint64_t doff = DROP ? dropout_offset(dp, dp.offset) : 0;
-  const int64_t Pt = (int64_t)gridDim.x * kPairs, pw = (int64_t)blockIdx.x * kPairs + (wv >> 1);
+  const int64_t Wt = (int64_t)(gridDim.x >> 1) * kWaves, w = (int64_t)(blockIdx.x >> 1) * kWaves + wv;
   const int32_t n_tiles = (n_rows + kTile - 1) / kTile;
-  const int32_t tb = (int32_t)(pw * n_tiles / Pt), te = (int32_t)((pw + 1) * n_tiles / Pt);
+  const int32_t tb = (int32_t)(w * n_tiles / Wt), te = (int32_t)((w + 1) * n_tiles / Wt);
   const int32_t rb = tb * kTile, re = min(n_rows, te * kTile);
-  // the column whose d_er this lane accumulates (recursive halving over t's bits 4..1)
-  const int rown = ((t >> 1) & 1) | (((t >> 2) & 1) << 1) | (((t >> 3) & 1) << 2) | (((t >> 4) & 1) << 3);
 
   f32x16 hacc[2];  // d_hc of head h: [n] C[col][feature]
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
     for (int i = 0; i < 16; ++i) hacc[n][i] = 0.f;
-  float derv = 0.f;
+  float derv[16];  // d_er of the lane's columns col(c, r) over its rows
+#pragma unroll
+  for (int r = 0; r < 16; ++r) derv[r] = 0.f;
 
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
@@ -629,6 +656,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
     const rsrc_t r_hs = make_rsrc(HS ? hs : nullptr, (uint32_t)re * RB);
     const rsrc_t r_dhs = make_rsrc(HS ? d_hs : nullptr, (uint32_t)re * RB);
     bf16_t* const img = trb + wv * TRW;
+    T* const stg = reinterpret_cast<T*>(trb + kWaves * TRW + wv * SGW);
     const uint32_t v_eh = (uint32_t)(2 * t + h) * 4u;
 
     struct In {
@@ -675,11 +703,6 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         u32x4v v4 = {p.w[0], p.w[1], p.w[2], p.w[3]};
         b[0] = __builtin_bit_cast(bf16x8, v4);
       }
-    };
-    // dU rows along k for d_hc: fragment (n, s) of lane (f, c) = rows 16 s + 8 c + j
-    auto du_voff = [&](int k) -> uint32_t {
-      const int s = k & 1, n = k >> 1;
-      return (uint32_t)(16 * s + 8 * c) * RB + (uint32_t)(h * kF + 32 * n + t) * sizeof(T);
     };
 
     Piece ring[KS];
@@ -733,7 +756,8 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         return DROP ? (((keep >> r) & 1u) ? a[r] * dp.scale : 0.f) : a[r];
       };
 
-      // ---- G^T = [hc | dV] [dU | hs]^T: lane (t, c), register r = g of column col(c, r)
+      // ---- G^T = [hc | dV] [dU | hs]^T: lane (t, c), register r = g of column col(c, r);
+      // the dU pieces stay in the staging image [row][feature] for d_hc
       f32x16 G;
 #pragma unroll
       for (int i = 0; i < 16; ++i) G[i] = 0.f;
@@ -742,11 +766,20 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         if (ks & 1) asm volatile("" ::: "memory");  // two k-steps' fragments at a time
         bf16x8 B[NT], Af[NT];
         piece_terms(ring[ks], B);
-        load_piece(ks, r0 + kTile, ring[ks]);
+        if (ks < 4) {
+          uint32_t* q = reinterpret_cast<uint32_t*>(stg + t * Stg<T>::P + 16 * ks + 8 * c);
+          *reinterpret_cast<u32x4_t*>(q) = u32x4_t{ring[ks].w[0], ring[ks].w[1], ring[ks].w[2], ring[ks].w[3]};
+          if constexpr (PW == 8)
+            *reinterpret_cast<u32x4_t*>(q + 4) = u32x4_t{ring[ks].w[4], ring[ks].w[5], ring[ks].w[6], ring[ks].w[7]};
+        }
+        // the next tile's dU pieces now; its hs pieces after this tile's d_hs (their
+        // registers are free through the d_hc / d_hs peak)
+        if (ks < 4 || !BIP3_HSLATE) load_piece(ks, r0 + kTile, ring[ks]);
 #pragma unroll
-        for (int q = 0; q < NT; ++q) Af[q] = afr[((h * KS + ks) * NT + q) * 64 + lane];
+        for (int q = 0; q < NT; ++q) Af[q] = afr[(ks * NT + q) * 64 + lane];
         G = prod<NT, NT>(Af, B, G);
       }
+
       // ---- phase C: D, ds, de, d_el, d_er
       float dsum = 0.f;
 #pragma unroll
@@ -783,21 +816,10 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         if (c == 0)
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(del), r_del, v_eh, (uint32_t)r0 * 8u, 0);
       }
-      // d_er: the 16 columns' sums over the 32 rows, one per lane pair (t, t ^ 1)
-      {
+      // d_er: per lane (row t of every tile, the lane's 16 columns), summed over the lanes
+      // once at the end
 #pragma unroll
-        for (int lvl = 3; lvl >= 0; --lvl) {  // xor 16, 8, 4, 2 (keep the half of bit t)
-          const int half = 1 << lvl, o = 2 << lvl;
-          const bool up = (t & o) != 0;
-#pragma unroll
-          for (int k = 0; k < half; ++k) {
-            const float send = up ? de[k] : de[k + half];
-            const float keepv = up ? de[k + half] : de[k];
-            de[k] = keepv + xor_shfl(send, o);
-          }
-        }
-        derv += de[0] + xor_shfl(de[0], 1);
-      }
+      for (int r = 0; r < 16; ++r) derv[r] += de[r];
 
       // ---- attd: A operand of d_hs, and the attd^T image for d_hc
       bf16x8 A[2][NA];
@@ -816,10 +838,42 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         for (int m = 0; m < 4; ++m) {
           const int s = m >> 1, o = 4 * (m & 1);
           bf16x4 v4 = {A[s][q][o], A[s][q][o + 1], A[s][q][o + 2], A[s][q][o + 3]};
-          *reinterpret_cast<bf16x4*>(img + (q * 32 + t) * 32 + 4 * c + 8 * m) = v4;
+          *reinterpret_cast<bf16x4*>(img + img_off(q, t, c + 2 * m)) = v4;
         }
 
-      // ---- d_hs = attd dV (C[row][feature])
+      // ---- d_hc += attd^T dU; B = dU with the rows along k, from the staging image
+      {
+        const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int s = k & 1, n = k >> 1;
+          bf16x8 B[NT];
+          if constexpr (sizeof(T) == 4) {
+            Chunk<T> chk;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              chk.w[j] = __float_as_uint(stg[(16 * s + 8 * c + j) * Stg<T>::P + 32 * n + t]);
+            chunk_terms<T>(chk, B);
+          } else {
+            const bf16_t* p = reinterpret_cast<const bf16_t*>(stg) + (16 * s + 8 * c + qq) * Stg<T>::P +
+                              32 * n + 16 * (g & 1) + 4 * pp;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)p);
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(p + 4 * Stg<T>::P));
+            B[0] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+          bf16x8 At[NA];
+#pragma unroll
+          for (int q = 0; q < NA; ++q) {
+            const int rr = 16 * s + 8 * c + qq, cb = 4 * (g & 1) + pp;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + img_off(q, rr, cb)));
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(img + img_off(q, rr + 4, cb)));
+            At[q] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+          hacc[n] = prod<NA, NT>(At, B, hacc[n]);
+        }
+      }
+
+      // ---- d_hs = attd dV (C[row][feature]), out through the staging image
       if (HS) {
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
@@ -831,51 +885,35 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
           for (int s = 0; s < 2; ++s) {
             bf16x8 B[NT];
 #pragma unroll
-            for (int q = 0; q < NT; ++q) B[q] = bdv[((((h * 2 + n) * 2 + s) * NT) + q) * 64 + lane];
+            for (int q = 0; q < NT; ++q) B[q] = bdv[(((n * 2 + s) * NT) + q) * 64 + lane];
             acc = prod<NA, NT>(A[s], B, acc);
           }
-          const uint32_t vo = (uint32_t)(h * kF + 32 * n + t) * sizeof(T) + (uint32_t)(4 * c) * RB;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const uint32_t so = (uint32_t)(r0 + (i & 3) + 8 * (i >> 2)) * RB;
-            if constexpr (sizeof(T) == 4)
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i]), r_dhs, vo, so, 0);
-            else
-              __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, (bf16_t)acc[i]), r_dhs,
-                                                    vo, so, 0);
-          }
+          st_frag<T>(stg, acc, n, t, c);
         }
-      }
-
-      // ---- d_hc += attd^T dU; B = dU with the rows along k (this tile's rows, fetched by
-      // G's pieces: L2 hits)
-      {
-        Chunk<T> duc[4];
+        flush_rows<T>(stg, r_dhs, r0, h, lane);
+        if (BIP3_HSLATE) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) load_chunk<T>(r_du, du_voff(k), (uint32_t)r0 * RB, duc[k]);
-        const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int s = k & 1, n = k >> 1;
-          bf16x8 B[NT];
-          chunk_terms<T>(duc[k], B);
-          bf16x8 At[NA];
-#pragma unroll
-          for (int q = 0; q < NA; ++q) {
-            const bf16_t* p = img + (q * 32 + 16 * s + 8 * c + qq) * 32 + 16 * (g & 1) + 4 * pp;
-            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)p);
-            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(p + 4 * 32));
-            At[q] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          }
-          hacc[n] = prod<NA, NT>(At, B, hacc[n]);
+          for (int ks = 4; ks < KS; ++ks) load_piece(ks, r0 + kTile, ring[ks]);
         }
       }
     }
   }
-  // block partial [d_hc (M x 128)][d_er (M x 2)]: waves w and w + 4 (same head) first,
-  // then head h = R[h] + R[h + 2]; d_er over the head's four waves in order
+  // block partial [d_hc (M x 128)][d_er (M x 2)] of head h (the other head's slices 0):
+  // waves w and w + 4 first, then R0 + R1 + R2 + R3; d_er over the waves in order
   static_assert(kWaves == 8, "the reduce below pairs waves w and w + 4");
-  if ((t & 1) == 0) sder[wv][col_of(c, rown)] = derv;
+  // d_er over the wave's 32 row lanes of each half: xor-butterfly within the 32-lane
+  // halves (every lane ends with the sums; lanes 0 / 32 write their half's 16 columns)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = derv[r];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += xor_shfl(v, o);
+    derv[r] = v;
+  }
+  if (t == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sder[wv][col_of(c, r)] = derv[r];
+  }
   float* red = reinterpret_cast<float*>(trb);  // 4 x 32 x 64 floats
   __syncthreads();
   auto slot = [&](int n, int i) -> int { return ((i & 3) + 8 * (i >> 2) + 4 * c) * kF + 32 * n + t; };
@@ -900,11 +938,18 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
   float* dst = part + (int64_t)blockIdx.x * (((MD + MH) + 3) & ~3);
   for (int i = tid; i < MD; i += kWaves * 64) {
     const int j = i / kD, hh = (i / kF) & 1, f = i % kF;
-    dst[i] = red[hh * 32 * kF + j * kF + f] + red[(hh + 2) * 32 * kF + j * kF + f];
+    const int o = j * kF + f;
+    dst[i] = hh != h ? 0.f
+                     : ((red[o] + red[32 * kF + o]) + red[2 * 32 * kF + o]) + red[3 * 32 * kF + o];
   }
   for (int i = tid; i < MH; i += kWaves * 64) {
     const int j = i >> 1, hh = i & 1;
-    dst[MD + i] = ((sder[hh][j] + sder[hh + 2][j]) + sder[hh + 4][j]) + sder[hh + 6][j];
+    float a = 0.f;
+    if (hh == h) {
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) a += sder[q][j];
+    }
+    dst[MD + i] = a;
   }
 }
 
@@ -963,7 +1008,9 @@ int bip3_bwd(const msha_graph* g, int dtype, const float* el, const float* er, c
              void* d_hc, void* d_hs, float* part, int nb, hipStream_t s) {
   if (!bip3_enabled()) return 0;
   const int32_t n_tiles = (int32_t)((g->n_rows + bip3::kTile - 1) / bip3::kTile);
-  const int nbk = (int)std::max<int64_t>(1, std::min<int64_t>(nb, (n_tiles + 3) / 4));
+  // blocks in head pairs (blockIdx.x & 1 = head), each wave at least one tile
+  const int64_t pairs = std::max<int64_t>(1, std::min<int64_t>(nb / 2, (n_tiles + bip3::kWaves - 1) / bip3::kWaves));
+  const int nbk = (int)(2 * pairs);
   const dim3 grid(nbk), block(bip3::kWaves * 64);
   auto go = [&](auto kern, auto tag) {
     using T = decltype(tag);

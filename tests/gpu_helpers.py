@@ -99,6 +99,65 @@ def rel_close(got, ref, rtol, floor, name=""):
     return worst
 
 
+def _row_rms(x):
+    """RMS over each row (leading index) of x, broadcast back to x's shape; a 1-D or 0-D x
+    is one row."""
+    x = np.asarray(x, np.float64)
+    if x.ndim <= 1 or x.size == x.shape[0]:  # a vector (also (n, 1)): one row
+        return np.full(x.shape, np.sqrt(np.mean(x * x)) if x.size else 0.0)
+    r = np.sqrt(np.mean(x.reshape(x.shape[0], -1) ** 2, axis=1))
+    return np.broadcast_to(r.reshape((-1,) + (1,) * (x.ndim - 1)), x.shape)
+
+
+def _row_max(x):
+    """max |x| over each row (leading index), broadcast back; a vector: one row."""
+    x = np.abs(np.asarray(x, np.float64))
+    if x.ndim <= 1 or x.size == x.shape[0]:  # a vector (also (n, 1)): one row
+        return np.full(x.shape, x.max() if x.size else 0.0)
+    r = x.reshape(x.shape[0], -1).max(axis=1)
+    return np.broadcast_to(r.reshape((-1,) + (1,) * (x.ndim - 1)), x.shape)
+
+
+def ref32_close(got, ref64, ref32, rtol, name="", k=4.0):
+    """Against the reference's fp64 run, EVERY element:
+
+        |got - ref64| <= rtol |ref64| + k e_row,
+
+    e_row = the largest |ref32 - ref64| on the element's row: the worst error the
+    reference's own fp32 run (the north_star's CPU path, same formulation, parameters
+    and LeakyReLU branches) makes on that row.  A cancelled element is held to a few times
+    the accuracy fp32 arithmetic reaches on its row, never to a fraction of the tensor's
+    largest element (no max|ref| floor, no fraction clause)."""
+    got = np.asarray(got, np.float64)
+    ref64 = np.asarray(ref64, np.float64)
+    e = _row_max(np.asarray(ref32, np.float64) - ref64)
+    err = np.abs(got - ref64)
+    bound = rtol * np.abs(ref64) + k * e + 1e-300
+    worst = float((err / bound).max()) if err.size else 0.0
+    print(f"{name}: worst err / bound {worst:.3g} (rtol {rtol}, {k} x the row's largest "
+          f"fp32-reference error)")
+    assert np.all(err <= bound), (
+        f"{name}: {int((err > bound).sum())} of {err.size} elements beyond rtol |ref| + "
+        f"{k} x the reference's fp32 row error (worst {worst:.3g}x the bound)")
+    return worst
+
+
+def rms_close(got, ref, rtol, name=""):
+    """EVERY element within rtol max(|ref|, RMS of its row of ref): relative above the
+    row's typical magnitude, absolute at that magnitude below it (a cancelled element's
+    error is set by the size of its terms, of the order of its row's typical element);
+    no max|ref| floor."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    bound = rtol * np.maximum(np.abs(ref), _row_rms(ref)) + 1e-300
+    worst = float((err / bound).max()) if err.size else 0.0
+    print(f"{name}: worst err / bound {worst:.3g} (rtol {rtol} of max(|ref|, row RMS))")
+    assert np.all(err <= bound), (f"{name}: {int((err > bound).sum())} of {err.size} elements "
+                                  f"beyond {rtol} max(|ref|, row RMS) (worst {worst:.3g}x)")
+    return worst
+
+
 def _seg_sum(x, ptr):
     """Sums of x over the contiguous segments [ptr[k], ptr[k+1]) of axis 0 (empty ones 0),
     via a running sum (the terms here are non-negative)."""

@@ -15,7 +15,14 @@
   references on the bf16-rounded values, 1e-2.
 
 C4 and bip1m: every element within rtol |ref| + 4 sqrt(n) 2^-24 A, A the absolute terms of
-its own sum (gpu_helpers.bounded_close).  configs[1]/[2] module checks: tol_close.
+its own sum (gpu_helpers.bounded_close; bf16-stored results add their own 2^-9 storage
+rounding, the accumulation is fp32 on both paths).  configs[1] module checks: every
+element within 1e-5 |ref64| + 4x the largest error of the reference's own fp32 run on its row (the same
+dense formulation run in fp32 on the same parameters and branches; gpu_helpers.
+ref32_close).  configs[2] outputs: every element within 1e-2 max(|ref|, row RMS)
+(gpu_helpers.rms_close); bf16 gradients: 1e-2 on 99 % of the elements or no worse than
+the reference's own bf16 run, the worst error printed per tensor.  No tolerance here is
+a fraction of a tensor's largest element.
 """
 import os
 import sys
@@ -26,7 +33,8 @@ import torch
 import torch.nn.functional as F
 
 import dense_ref as D
-from gpu_helpers import BF16_STORE, U32, bounded_close, edge_abs_terms, rel_close, tol_close
+from gpu_helpers import (BF16_STORE, U32, bounded_close, edge_abs_terms, ref32_close, rms_close,
+                         tol_close)
 from oracle import cpu_oracle
 from oracle import gnn_oracle as O
 
@@ -487,47 +495,55 @@ def test_ours_layer_full_graph(cuda, msha, year):
     src = _batch(yg, seed=int(year))
     city_adj, prov_adj = _groups(yg, cuda)
     p64 = D.layer_params(layer)
+    p32 = D.layer_params(layer, dtype=torch.float32)  # the reference's own fp32 arithmetic
     layer = layer.to(cuda)
     St, Rt = S.to(cuda).requires_grad_(True), R.to(cuda).requires_grad_(True)
     src_t = torch.as_tensor(src, device=cuda)
+    args = (torch.as_tensor(yg["mask"]), torch.as_tensor(yg["city"]), torch.as_tensor(yg["prov"]),
+            torch.as_tensor(src))
 
     layer.eval()
     with torch.no_grad():
         y_eval = layer(St, Rt, yg["adj"], city_adj, prov_adj, src_t, False)
+        y32e = D.ours_layer(S, R, p32, *args, False)
     ref = O.ours_layer_fwd(S.double().numpy(), R.double().numpy(), _oracle_params(p64),
                            yg["rowptr"], yg["col"], yg["city"], yg["prov"], src, False)
-    tol_close(y_eval.cpu().numpy(), ref["out"], F32_TOL, F32_TOL)
+    ref32_close(y_eval.cpu().numpy(), ref["out"], y32e.numpy(), F32_TOL, "eval out")
 
     layer.train()
     with _Branches() as rec:
         y = layer(St, Rt, yg["adj"], city_adj, prov_adj, src_t, False)
+    br = rec.heads(1)[0]
     ref = O.ours_layer_fwd(S.double().numpy(), R.double().numpy(), _oracle_params(p64),
                            yg["rowptr"], yg["col"], yg["city"], yg["prov"], src, True)
-    tol_close(y.detach().cpu().numpy(), ref["out"], F32_TOL, F32_TOL)
+    S32, R32 = S.clone().requires_grad_(True), R.clone().requires_grad_(True)
+    y32 = D.ours_layer(S32, R32, p32, *args, True, br)
+    ref32_close(y.detach().cpu().numpy(), ref["out"], y32.detach().numpy(), F32_TOL, "train out")
 
     y.backward(dout.to(cuda))
     S64 = S.double().requires_grad_(True)
     R64 = R.double().requires_grad_(True)
     # gradients: the fp64 reference on the LeakyReLU branches the GPU took (dense_ref)
-    y64 = D.ours_layer(S64, R64, p64, torch.as_tensor(yg["mask"]),
-                       torch.as_tensor(yg["city"]), torch.as_tensor(yg["prov"]),
-                       torch.as_tensor(src), True, rec.heads(1)[0])
-    tol_close(y.detach().cpu().numpy(), y64.detach().numpy(), F32_TOL, F32_TOL)
+    y64 = D.ours_layer(S64, R64, p64, *args, True, br)
+    ref32_close(y.detach().cpu().numpy(), y64.detach().numpy(), y32.detach().numpy(), F32_TOL,
+                "train out (dense)")
     (y64 * dout.double()).sum().backward()
-    tol_close(St.grad.cpu().numpy(), S64.grad.numpy(), F32_TOL, F32_TOL)
-    tol_close(Rt.grad.cpu().numpy(), R64.grad.numpy(), F32_TOL, F32_TOL)
+    (y32 * dout).sum().backward()
+    ref32_close(St.grad.cpu().numpy(), S64.grad.numpy(), S32.grad.numpy(), F32_TOL, "S")
+    ref32_close(Rt.grad.cpu().numpy(), R64.grad.numpy(), R32.grad.numpy(), F32_TOL, "R")
     for k, name in D.GRAD_KEYS.items():
         got = dict(layer.named_parameters())[name].grad
-        tol_close(got.cpu().numpy(), p64[k].grad.numpy(), F32_TOL, F32_TOL)
+        ref32_close(got.cpu().numpy(), p64[k].grad.numpy(), p32[k].grad.numpy(), F32_TOL, name)
 
 
-def _model_grads_vs_dense(model, yg, src_t, tgt, ours, brs, training=True):
-    """fp32 model forward + nll(out[src], tgt) backward on the GPU vs the dense fp64
-    restatement of the same model (same parameters)."""
-    heads = [D.layer_params(a) for a in model.attentions]
-    Sf = model.Sfeatures.detach().cpu().double().requires_grad_(True)
-    Rf = model.Rfeatures.detach().cpu().double().requires_grad_(True)
-    oW = model.out_att.W.detach().cpu().double().requires_grad_(True)
+def _model_grads_vs_dense(model, yg, src_t, tgt, ours, brs, training=True, dtype=torch.float64):
+    """fp32 model forward + nll(out[src], tgt) backward on the GPU vs the dense
+    restatement of the same model (same parameters) in ``dtype`` on the CPU: fp64 (the
+    reference) or fp32 (the reference's own arithmetic, the error scale of ref32_close)."""
+    heads = [D.layer_params(a, dtype=dtype) for a in model.attentions]
+    Sf = model.Sfeatures.detach().cpu().to(dtype).requires_grad_(True)
+    Rf = model.Rfeatures.detach().cpu().to(dtype).requires_grad_(True)
+    oW = model.out_att.W.detach().cpu().to(dtype).requires_grad_(True)
     kw = {}
     if ours:
         kw = dict(city=torch.as_tensor(yg["city"]), prov=torch.as_tensor(yg["prov"]),
@@ -561,20 +577,30 @@ def test_model_train_step_full_2015(cuda, msha, kind):
         out = model(yg["adj"], city_adj, prov_adj, src_t)
     loss = F.nll_loss(out[src_t], tgt)
     loss.backward()
+    brs = rec.heads(2)
     out64, loss64, Sf, Rf, oW, heads = _model_grads_vs_dense(model, yg, src_t, tgt,
-                                                             kind == "Ours", rec.heads(2))
-    tol_close(out.detach().cpu().numpy(), out64.detach().numpy(), F32_TOL, F32_TOL)
+                                                             kind == "Ours", brs)
+    # the reference's own fp32 arithmetic on the same parameters and branches: the error
+    # scale of every elementwise bound below (gpu_helpers.ref32_close)
+    out32, _, Sf32, Rf32, oW32, heads32 = _model_grads_vs_dense(
+        model, yg, src_t, tgt, kind == "Ours", brs, dtype=torch.float32)
+    ref32_close(out.detach().cpu().numpy(), out64.detach().numpy(), out32.detach().numpy(),
+                F32_TOL, "log-probabilities")
     assert abs(float(loss.detach()) - float(loss64.detach())) <= F32_TOL * abs(float(loss64.detach()))
-    tol_close(model.Sfeatures.grad.cpu().numpy(), Sf.grad.numpy(), F32_TOL, F32_TOL)
-    tol_close(model.Rfeatures.grad.cpu().numpy(), Rf.grad.numpy(), F32_TOL, F32_TOL)
-    tol_close(model.out_att.W.grad.cpu().numpy(), oW.grad.numpy(), F32_TOL, F32_TOL)
-    for att, p64 in zip(model.attentions, heads):
+    ref32_close(model.Sfeatures.grad.cpu().numpy(), Sf.grad.numpy(), Sf32.grad.numpy(), F32_TOL,
+                "Sfeatures")
+    ref32_close(model.Rfeatures.grad.cpu().numpy(), Rf.grad.numpy(), Rf32.grad.numpy(), F32_TOL,
+                "Rfeatures")
+    ref32_close(model.out_att.W.grad.cpu().numpy(), oW.grad.numpy(), oW32.grad.numpy(), F32_TOL,
+                "out_att.W")
+    for i, (att, p64, p32) in enumerate(zip(model.attentions, heads, heads32)):
         params = dict(att.named_parameters())
         for k, name in D.GRAD_KEYS.items():
             if kind == "ablation3" and k in ("a3", "a4"):
                 assert params[name].grad is None
                 continue
-            tol_close(params[name].grad.cpu().numpy(), p64[k].grad.numpy(), F32_TOL, F32_TOL)
+            ref32_close(params[name].grad.cpu().numpy(), p64[k].grad.numpy(), p32[k].grad.numpy(),
+                        F32_TOL, f"attention_{i}.{name}")
 
 
 def test_ablation3_bf16_model_vs_fp64(cuda, msha):
@@ -603,7 +629,8 @@ def test_ablation3_bf16_model_vs_fp64(cuda, msha):
     loss.backward()
     out64, loss64, Sf, Rf, oW, heads = _model_grads_vs_dense(model, yg, src_t, tgt, False,
                                                              rec.heads(2))
-    tol_close(out.detach().float().cpu().numpy(), out64.detach().numpy(), BF16_TOL, BF16_TOL)
+    rms_close(out.detach().float().cpu().numpy(), out64.detach().numpy(), BF16_TOL,
+              "log-probabilities (bf16)")
     assert abs(float(loss.detach()) - float(loss64.detach())) <= BF16_TOL * abs(float(loss64.detach()))
     # the reference's own arithmetic in bf16 (dense_ref in torch bf16, same parameters and
     # branches): the bound a bf16 run of the reference itself meets
@@ -671,13 +698,13 @@ def test_ours_layer_bf16_vs_oracle(cuda, msha, year):
     assert y_eval.dtype == torch.bfloat16
     ref = O.ours_layer_fwd(S.double().numpy(), R.double().numpy(), _oracle_params(p64),
                            yg["rowptr"], yg["col"], yg["city"], yg["prov"], src, False)
-    tol_close(y_eval.float().cpu().numpy(), ref["out"], BF16_TOL, BF16_TOL)
+    rms_close(y_eval.float().cpu().numpy(), ref["out"], BF16_TOL, "eval out (bf16)")
     layer.train()
     with _Branches() as rec:
         y = layer(St, Rt, yg["adj"], city_adj, prov_adj, src_t, False)
     ref = O.ours_layer_fwd(S.double().numpy(), R.double().numpy(), _oracle_params(p64),
                            yg["rowptr"], yg["col"], yg["city"], yg["prov"], src, True)
-    tol_close(y.detach().float().cpu().numpy(), ref["out"], BF16_TOL, BF16_TOL)
+    rms_close(y.detach().float().cpu().numpy(), ref["out"], BF16_TOL, "train out (bf16)")
     y.backward(dout.to(cuda))
     args = (torch.as_tensor(yg["mask"]), torch.as_tensor(yg["city"]),
             torch.as_tensor(yg["prov"]), torch.as_tensor(src), True)
