@@ -258,9 +258,10 @@ MSHA_API int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_t 
                                     uint64_t offset, float* d_el, float* d_er, void* d_hc,
                                     void* d_hs, void* ws, size_t ws_bytes,
                                     msha_stream_t stream);
-/* The source-row count from which msha_bip_attention_bwd takes the row-mask kernel
- * (graphs with msha_graph.rowmask; default 131072, or MSHA_BIP2_BWD_MIN_ROWS): rows >= 0
- * sets it for the process and returns the previous value, rows < 0 only returns it. */
+/* The source-row count from which msha_bip_attention_fwd / _bwd take the MFMA row-mask
+ * kernels (graphs with msha_graph.rowmask, 2 heads x 64; below it the mask forward and the
+ * CSR-walk backward; default 131072, or MSHA_BIP2_BWD_MIN_ROWS): rows >= 0 sets it for
+ * the process and returns the previous value, rows < 0 only returns it. */
 MSHA_API int64_t msha_bip2_bwd_min_rows(int64_t rows);
 
 /* Column-side (transposed) aggregate over the CSC view:
@@ -698,16 +699,14 @@ MSHA_API int msha_dropout_keep_mask_word(uint64_t seed, uint64_t offset, int64_t
  *   g  = grad (* keep * 1/(1-p) when drop_p > 0) + weight_decay * param
  *   m  = m + (1 - beta1) (g - m);  v = beta2 v + (1 - beta2) g^2
  *   t  = *step + 1;  param -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
- * in one launch: every block reads *step and uses *step + 1, and the last block to finish
- * advances *step (capturable: the step lives on the device, as torch's capturable Adam
- * keeps it).  param, grad, exp_avg, exp_avg_sq share `dtype` (bf16 state for bf16
+ * with *step advanced first by a one-block launch (capturable: the step lives on the
+ * device, as torch's capturable Adam keeps it).  param, grad, exp_avg, exp_avg_sq share `dtype` (bf16 state for bf16
  * parameters, as torch keeps it), contiguous, n elements.  drop_p > 0 fuses a dropout
  * backward into the gradient read: grad is then the dropout's OUTPUT gradient and keep is
  * msha_segments' flat mask (element e: word e % 4 of the Philox4x32-10 block (drop_seed;
  * counter {e / 4, drop_offset})), so the parameter's own gradient never exists (the
  * feature dropout of Sfeatures, Ablation.py:296, Ours.py:161).  ws: device scratch of
- * msha_adam_workspace_size() bytes, zero-filled before its first use (the launch's
- * completion ticket, left at zero by every launch; stream-ordered reuse). */
+ * msha_adam_workspace_size() bytes (the step's per-tensor scalars; stream-ordered reuse). */
 #define MSHA_MAX_ADAM 64
 typedef struct msha_adam_tensor {
   void* param;

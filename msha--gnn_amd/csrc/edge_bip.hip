@@ -1053,8 +1053,11 @@ extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_
                    "bip_attention_fwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
+  // the MFMA kernels (edge_bip3.hip) from msha_bip2_bwd_min_rows rows up; below it (the
+  // shipped graphs: < 1 tile per wave) the mask forward of edge_bip2.hip
   if (u_lo == nullptr && bip2_ok(g, heads, feat, neg_slope) &&
-      (bip3_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s) ||
+      ((g->n_rows >= msha_bip2_bwd_min_rows(-1) &&
+        bip3_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s)) ||
        bip2_fwd(g, dtype, el, er, hc, hs, neg_slope, dp, u, lse, attd, v, (float*)ws, nb, s)))
     return check_launch("bip_attention_fwd");
   bool done = false;
@@ -1110,16 +1113,17 @@ extern "C" int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_
   const int nb = bip::cu_count();
   hipStream_t s = (hipStream_t)stream;
   const Dropout dp = make_dropout(drop_p, seed, offset, s);
-  // the mask backward wins on large graphs (bip1m: 450 -> 380-416 us) but not on the shipped
-  // ones (R15: 36.6 vs 31.7 us, rocprof, profiles/round5_step_r15_v1): rows per wave too few
-  // to amortise its per-wave d_er and slab epilogue.  MSHA_BIP2_BWD_MIN_ROWS moves the cut.
-  // msha_bip2_bwd_min_rows sets it per process (tests run small graphs through both).
-  if (bip2_ok(g, heads, feat, neg_slope) &&
+  // the MFMA backward (edge_bip3.hip; mask backward edge_bip2.hip with MSHA_BIP3=0) wins on
+  // large graphs (bip1m fp32: CSR walk 450 us, mask 380-416, MFMA ~400; bf16 MFMA 204) but
+  // not on the shipped ones (R15: MFMA 36.1, mask 36.6, CSR walk 31.6 us; rows per wave too
+  // few to amortise the per-block setup and partial epilogue).  MSHA_BIP2_BWD_MIN_ROWS /
+  // msha_bip2_bwd_min_rows (per process: tests run small graphs through both) move the
+  // cut, for the forward's choice as well.
+  if (g->n_rows >= msha_bip2_bwd_min_rows(-1) && bip2_ok(g, heads, feat, neg_slope) &&
       (bip3_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
                 d_hs, (float*)ws, nb, s) ||
-       (g->n_rows >= msha_bip2_bwd_min_rows(-1) &&
-        bip2_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
-                 d_hs, (float*)ws, nb, s))))
+       bip2_bwd(g, dtype, el, er, hc, lse, dU, hs, dV, row_coef, neg_slope, dp, d_el, d_er, d_hc,
+                d_hs, (float*)ws, nb, s)))
     return check_launch("bip_attention_bwd");
   bool done = false;
 #define X(h, f)                                                                                  \

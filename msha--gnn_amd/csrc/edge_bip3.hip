@@ -1007,6 +1007,13 @@ int bip3_bwd(const msha_graph* g, int dtype, const float* el, const float* er, c
              const float* row_coef, float slope, const Dropout& dp, float* d_el, float* d_er,
              void* d_hc, void* d_hs, float* part, int nb, hipStream_t s) {
   if (!bip3_enabled()) return 0;
+  // fp32: the mask backward of edge_bip2.hip measured faster at bip1m (390 vs 406-432 us:
+  // the six-product split of G's 128-deep operands and of dU's second layout is VALU-heavy);
+  // MSHA_BIP3_BWD32=1 (read per call) takes this kernel for fp32 as well
+  if (dtype != MSHA_DTYPE_BF16) {
+    const char* v = getenv("MSHA_BIP3_BWD32");
+    if (v == nullptr || atoi(v) == 0) return 0;
+  }
   const int32_t n_tiles = (int32_t)((g->n_rows + bip3::kTile - 1) / bip3::kTile);
   // blocks in head pairs (blockIdx.x & 1 = head), each wave at least one tile
   const int64_t pairs = std::max<int64_t>(1, std::min<int64_t>(nb / 2, (n_tiles + bip3::kWaves - 1) / bip3::kWaves));

@@ -19,7 +19,7 @@ struct AdamBatch {
   double lr, b1, b2, eps, wd;  // torch's Python-float hyperparameters
   int n;
   int first[MSHA_MAX_ADAM + 1];  // blocks [first[i], first[i+1]) update tensor i (1-D grid)
-  unsigned int* ticket;  // completion ticket (workspace, zero between launches)
+  float2* scal;         // per tensor: (step_size, sqrt(bias_correction2)) of this step
   const uint64_t* ctr;  // device replay counter (dropout offsets)
 };
 
@@ -63,9 +63,16 @@ __device__ __forceinline__ void adam_elem(const AdamScalars& a, float g, float& 
   p = p - a.step_size * (m / denom);     // param.addcdiv_(exp_avg, denom, -step_size)
 }
 
-// bias corrections of step t (exact integer t) in double, as torch computes them on the
-// host: beta ** t by squaring (<= 2 log2 t double multiplies, a few ulps)
-__device__ __forceinline__ float2 adam_scalars(const AdamBatch& b, float t) {
+// The step counts advance in a one-block launch ahead of the update (as torch's
+// capturable Adam adds 1 to its device steps first): every block of the update then reads
+// finished scalars -- no completion counter, no per-block double-precision pow.
+__global__ void __launch_bounds__(64) adam_prep_kernel(AdamBatch b) {
+  const int i = threadIdx.x;
+  if (i >= b.n) return;
+  const float t = *b.t[i].step + 1.f;
+  *b.t[i].step = t;
+  // bias corrections from the step count in double (torch: 1 - beta ** step on the host);
+  // beta ** t by squaring (exact integer t: <= 2 log2 t double multiplies, a few ulps)
   double p1 = 1.0, p2 = 1.0, s1 = b.b1, s2 = b.b2;
   for (uint32_t e = (uint32_t)t; e != 0; e >>= 1) {
     if (e & 1u) {
@@ -75,13 +82,11 @@ __device__ __forceinline__ float2 adam_scalars(const AdamBatch& b, float t) {
     s1 *= s1;
     s2 *= s2;
   }
-  return make_float2((float)(b.lr / (1.0 - p1)), (float)sqrt(1.0 - p2));
+  const double bc1 = 1.0 - p1;
+  const double bc2 = 1.0 - p2;
+  b.scal[i] = make_float2((float)(b.lr / bc1), (float)sqrt(bc2));
 }
 
-// One launch: every block reads its tensor's step count t - 1 and uses t (as torch's
-// capturable Adam adds 1 first), and the last block to finish -- a completion ticket in
-// the workspace, zero between launches -- advances every step count.  (Round 5 ran a
-// one-block launch ahead of the update for the scalars: one more graph node, ~4 us.)
 __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
   // the tensor of this block: first[ti] <= blockIdx.x < first[ti + 1] (binary search over
   // the <= 64 boundaries; every block works -- a 2-D grid sized by the largest tensor left
@@ -95,10 +100,7 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
   const int ti = lo;
   const msha_adam_tensor& T = b.t[ti];
   const int dt = T.dtype;
-  __shared__ float2 sc_sh;
-  if (threadIdx.x == 0) sc_sh = adam_scalars(b, *T.step + 1.f);
-  __syncthreads();
-  const float2 sc = sc_sh;
+  const float2 sc = b.scal[ti];
   AdamScalars a;  // the scalars torch hands its fp32 kernels
   a.b1c = (float)(1.0 - b.b1);
   a.b2c = (float)(1.0 - b.b2);
@@ -153,16 +155,6 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
     ad_st(T.exp_avg, dt, e, m);
     ad_st(T.exp_avg_sq, dt, e, v);
   }
-  // every block has read its step count before it takes a ticket: the last one advances them
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(b.ticket, 1u) == gridDim.x - 1) {
-      for (int i = 0; i < b.n; ++i) *b.t[i].step += 1.f;
-      *b.ticket = 0u;
-      __threadfence();
-    }
-  }
 }
 
 }  // namespace msha
@@ -204,9 +196,10 @@ extern "C" int msha_adam_step(int32_t n, const msha_adam_tensor* tensors, double
   b.n = n;
   hipStream_t s = (hipStream_t)stream;
   b.ctr = rng_counter(s);
-  b.ticket = (unsigned int*)ws;
+  b.scal = (float2*)ws;
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(64), 0, s, b);
   hipLaunchKernelGGL(adam_kernel, dim3(nblocks), dim3(256), 0, s, b);
   return check_launch("adam_step");
 }
 
-extern "C" size_t msha_adam_workspace_size(void) { return 256; }
+extern "C" size_t msha_adam_workspace_size(void) { return sizeof(float2) * MSHA_MAX_ADAM; }

@@ -14,6 +14,22 @@ from test_gpu_kernels import _keep_mask
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(params=["default", "mfma", "mfma_bwd32"])
+def bip_path(request, msha, monkeypatch):
+    """The library's size-based choice ("default": below 131,072 rows the mask forward and
+    the CSR-walk backward) and the large-graph choice forced on every 2 x 64, M <= 32 graph
+    ("mfma": msha_bip2_bwd_min_rows(0): the MFMA kernels of edge_bip3.hip, but the fp32
+    backward on edge_bip2.hip's mask kernel; "mfma_bwd32": MSHA_BIP3_BWD32=1, the MFMA
+    backward for fp32 too)."""
+    from msha_gnn_amd import _lib
+
+    if request.param == "mfma_bwd32":
+        monkeypatch.setenv("MSHA_BIP3_BWD32", "1")
+    prev = _lib.fn("msha_bip2_bwd_min_rows")(-1 if request.param == "default" else 0)
+    yield request.param
+    _lib.fn("msha_bip2_bwd_min_rows")(prev)
+
 CASES = [
     # (n, m, H, F, max_deg, extra); M * H <= 64 (one row's slots fit one group)
     (3000, 32, 2, 64, 6, dict(empty_rows=(3, 7, 2999), hot_col=4)),   # R15 shape
@@ -45,7 +61,7 @@ def _run(MF, graph, el, er, hc, hs, dU, dV, p, seed, dev, dtype, bip):
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}m{c[1]}H{c[2]}F{c[3]}d{c[4]}")
 @pytest.mark.parametrize("p", [0.0, 0.5])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-def test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype):
+def test_bip_vs_oracle_and_general(cuda, msha, bip_path, case, p, dtype):
     from msha_gnn_amd import _lib
     from msha_gnn_amd import functional as MF
     from msha_gnn_amd.graph import Graph
@@ -85,7 +101,7 @@ def test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype):
         bounded_close(b.float().cpu().numpy(), r, A[name], A[per[name]], tol, name + " (general)")
 
 
-def test_bip_raw_abi_lse_attd_deterministic(cuda, msha):
+def test_bip_raw_abi_lse_attd_deterministic(cuda, msha, bip_path):
     """The C ABI directly: lse and the attention export against the oracle, u-only
     (no hs) forward, and bitwise-identical repeats (wave- and block-ordered sums)."""
     from msha_gnn_amd import _lib
@@ -145,7 +161,7 @@ def test_bip_raw_abi_lse_attd_deterministic(cuda, msha):
 
 
 @pytest.mark.parametrize("p", [0.0, 0.5])
-def test_bip_many_groups_per_wave_vs_general(cuda, msha, p):
+def test_bip_many_groups_per_wave_vs_general(cuda, msha, bip_path, p):
     """120k rows: every wave walks many 8-row groups, with sub-groups and the next
     group's loads in flight (the small cases above give each wave one or two rows).
     Every output against the general kernels (functional.BIP = False)."""
@@ -213,32 +229,21 @@ def test_shipped_graph_models_run_on_the_bipartite_kernels(cuda, msha):
 
 
 @pytest.fixture
-def mask_bwd_everywhere(msha):
-    """Route every M <= 32, 2 x 64 graph through the row-mask backward (bip2_bwd), not
-    only those above the 131,072-row cut (msha_bip2_bwd_min_rows)."""
+def mask_bwd_everywhere(msha, monkeypatch):
+    """Route every M <= 32, 2 x 64 graph through the MFMA kernels (edge_bip3.hip, the fp32
+    backward included), not only those above the 131,072-row cut (msha_bip2_bwd_min_rows)."""
     from msha_gnn_amd import _lib
 
+    monkeypatch.setenv("MSHA_BIP3_BWD32", "1")
     prev = _lib.fn("msha_bip2_bwd_min_rows")(0)
     yield
     _lib.fn("msha_bip2_bwd_min_rows")(prev)
 
 
-MASK_CASES = [c for c in CASES if c[1] <= 32 and c[2] == 2 and c[3] == 64]
-
-
-@pytest.mark.parametrize("case", MASK_CASES, ids=lambda c: f"n{c[0]}m{c[1]}d{c[4]}")
-@pytest.mark.parametrize("p", [0.0, 0.5])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-def test_bip_mask_backward_small_graphs(cuda, msha, mask_bwd_everywhere, case, p, dtype):
-    """The row-mask backward's template variants (dropout keep-bit regeneration, bf16)
-    on the small graphs, every output against the fp64 oracle and the general kernels."""
-    test_bip_vs_oracle_and_general(cuda, msha, case, p, dtype)
-
-
 @pytest.mark.parametrize("p", [0.0, 0.4])
 def test_ours_attention_mask_backward(cuda, msha, mask_bwd_everywhere, p):
-    """Ours (row_coef, with and without dropout) through the row-mask backward: the
-    COEF / DROP variants of bip2_bwd_kernel against the dense fp64 restatement."""
+    """Ours (row_coef, with and without dropout) through the MFMA kernels: the COEF / DROP
+    variants of bip3_bwd_kernel against the dense fp64 restatement."""
     from test_gpu_ours import check_ours_attention_vs_dense
 
     check_ours_attention_vs_dense(cuda, p)
