@@ -894,8 +894,8 @@ def train_step_leg(dev, year="2015", model_kind="Ours", steps=20, warmup=5,
             gs = GraphedStep(body, dev, warmup=warmup)
 
             def one(k):
-                feed(k)
-                return gs.replay()
+                # the batch copy and the dropout replay counter's increment: one launch
+                return gs.replay(feed=(sr_s, batches[k % len(batches)]))
 
             # untimed replays: a graph's first launches carry one-time setup (an occasional
             # ~25 ms first-replay stall put one year's step at 1.9 ms instead of 0.5)

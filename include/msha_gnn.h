@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 14
+#define MSHA_ABI_VERSION 15
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -128,6 +128,12 @@ MSHA_API int msha_debug_head_timeline(void* buf);
 MSHA_API int msha_set_rng_counter(int32_t device, const uint64_t* counter);
 /* the counter installed for `device` (< 0: current device), NULL if none */
 MSHA_API const uint64_t* msha_get_rng_counter(int32_t device);
+/* (ABI 15) A replayed step's feed: copies `bytes` from src to dst (device memory) and adds 1
+ * to *counter (NULL: no counter) in ONE stream-ordered launch, so a graph whose counter
+ * increment is left to its feed (msha_gnn_amd.step.GraphedStep.replay(feed=...)) starts
+ * with its first kernel instead of an add node. */
+MSHA_API int msha_feed_step(void* dst, const void* src, int64_t bytes, uint64_t* counter,
+                            msha_stream_t stream);
 
 /* keep[i] = 1 iff element i survives F.dropout(p) under (seed, offset).  The
  * kernels below draw exactly these masks (stream-ordered Philox4x32-10), which
@@ -263,6 +269,11 @@ MSHA_API int msha_bip_attention_bwd(const msha_graph* g, int32_t heads, int32_t 
  * CSR-walk backward; default 131072, or MSHA_BIP2_BWD_MIN_ROWS): rows >= 0 sets it for
  * the process and returns the previous value, rows < 0 only returns it. */
 MSHA_API int64_t msha_bip2_bwd_min_rows(int64_t rows);
+/* (ABI 15) The Ours intra forward's dropout draws: mode 1 packs the matched (batch entry,
+ * node) pairs of consecutive nodes into one Philox draw per <= 64 pairs (default), mode 0
+ * draws per node for the whole batch (MSHA_OURS_PACK_DRAWS=0 starts with it); both give
+ * the same bits.  Returns the previous mode; mode < 0 only queries. */
+MSHA_API int32_t msha_ours_pack_draws(int32_t mode);
 
 /* Column-side (transposed) aggregate over the CSC view:
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
@@ -699,14 +710,15 @@ MSHA_API int msha_dropout_keep_mask_word(uint64_t seed, uint64_t offset, int64_t
  *   g  = grad (* keep * 1/(1-p) when drop_p > 0) + weight_decay * param
  *   m  = m + (1 - beta1) (g - m);  v = beta2 v + (1 - beta2) g^2
  *   t  = *step + 1;  param -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
- * with *step advanced first by a one-block launch (capturable: the step lives on the
+ * in one launch whose last block advances *step (capturable: the step lives on the
  * device, as torch's capturable Adam keeps it).  param, grad, exp_avg, exp_avg_sq share `dtype` (bf16 state for bf16
  * parameters, as torch keeps it), contiguous, n elements.  drop_p > 0 fuses a dropout
  * backward into the gradient read: grad is then the dropout's OUTPUT gradient and keep is
  * msha_segments' flat mask (element e: word e % 4 of the Philox4x32-10 block (drop_seed;
  * counter {e / 4, drop_offset})), so the parameter's own gradient never exists (the
  * feature dropout of Sfeatures, Ablation.py:296, Ours.py:161).  ws: device scratch of
- * msha_adam_workspace_size() bytes (the step's per-tensor scalars; stream-ordered reuse). */
+ * msha_adam_workspace_size() bytes, ZERO-FILLED before its first use (the launch's
+ * completion ticket, back at zero when the launch ends; stream-ordered reuse). */
 #define MSHA_MAX_ADAM 64
 typedef struct msha_adam_tensor {
   void* param;

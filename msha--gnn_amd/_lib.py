@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 14  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 15  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -95,6 +95,8 @@ class MshaSegment(C.Structure):
 SIGNATURES = {
     "msha_abi_version": (C.c_int, []),
     "msha_set_rng_counter": (C.c_int, [I32, P]),
+    "msha_feed_step": (C.c_int, [P, P, I64, P, P]),
+    "msha_ours_pack_draws": (I32, [I32]),
     "msha_get_rng_counter": (P, [I32]),
     "msha_last_error": (C.c_char_p, []),
     "msha_debug_timeline": (C.c_int, [P, I64]),

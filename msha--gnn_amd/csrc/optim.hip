@@ -14,12 +14,15 @@
 
 namespace msha {
 
+constexpr int kAdamLeaves = 64;  // completion-ticket leaves (see adam_kernel's end)
+constexpr int kAdamLine = 64;    // uint32 words per ticket counter: one 256-B line each
+
 struct AdamBatch {
   msha_adam_tensor t[MSHA_MAX_ADAM];
   double lr, b1, b2, eps, wd;  // torch's Python-float hyperparameters
   int n;
   int first[MSHA_MAX_ADAM + 1];  // blocks [first[i], first[i+1]) update tensor i (1-D grid)
-  float2* scal;         // per tensor: (step_size, sqrt(bias_correction2)) of this step
+  uint32_t* ticket;     // completion ticket: top counter, then the leaves (workspace, zero between launches)
   const uint64_t* ctr;  // device replay counter (dropout offsets)
 };
 
@@ -63,16 +66,9 @@ __device__ __forceinline__ void adam_elem(const AdamScalars& a, float g, float& 
   p = p - a.step_size * (m / denom);     // param.addcdiv_(exp_avg, denom, -step_size)
 }
 
-// The step counts advance in a one-block launch ahead of the update (as torch's
-// capturable Adam adds 1 to its device steps first): every block of the update then reads
-// finished scalars -- no completion counter, no per-block double-precision pow.
-__global__ void __launch_bounds__(64) adam_prep_kernel(AdamBatch b) {
-  const int i = threadIdx.x;
-  if (i >= b.n) return;
-  const float t = *b.t[i].step + 1.f;
-  *b.t[i].step = t;
-  // bias corrections from the step count in double (torch: 1 - beta ** step on the host);
-  // beta ** t by squaring (exact integer t: <= 2 log2 t double multiplies, a few ulps)
+// bias corrections of step t (exact integer t) in double, as torch computes them on the
+// host: beta ** t by squaring (<= 2 log2 t double multiplies, a few ulps)
+__device__ __forceinline__ float2 adam_scalars(const AdamBatch& b, float t) {
   double p1 = 1.0, p2 = 1.0, s1 = b.b1, s2 = b.b2;
   for (uint32_t e = (uint32_t)t; e != 0; e >>= 1) {
     if (e & 1u) {
@@ -82,11 +78,16 @@ __global__ void __launch_bounds__(64) adam_prep_kernel(AdamBatch b) {
     s1 *= s1;
     s2 *= s2;
   }
-  const double bc1 = 1.0 - p1;
-  const double bc2 = 1.0 - p2;
-  b.scal[i] = make_float2((float)(b.lr / bc1), (float)sqrt(bc2));
+  return make_float2((float)(b.lr / (1.0 - p1)), (float)sqrt(1.0 - p2));
 }
 
+// One launch (round 5 ran a one-block launch ahead of the update for the scalars: one more
+// graph node, ~4 us).  Every thread reads its tensor's step count t - 1 and derives step t's
+// scalars itself (as torch's capturable Adam adds 1 first); the last block to finish -- a
+// completion ticket in the workspace, zero between launches -- advances every step count.
+// The ticket is a relaxed atomic with no fence: each block's step read was consumed by its
+// whole update before the block takes its ticket, and nothing else is published through
+// it (a device-scope fence per block writes back L2: that form measured 102 us vs 25).
 __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
   // the tensor of this block: first[ti] <= blockIdx.x < first[ti + 1] (binary search over
   // the <= 64 boundaries; every block works -- a 2-D grid sized by the largest tensor left
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
   const int ti = lo;
   const msha_adam_tensor& T = b.t[ti];
   const int dt = T.dtype;
-  const float2 sc = b.scal[ti];
+  const float2 sc = adam_scalars(b, *T.step + 1.f);
   AdamScalars a;  // the scalars torch hands its fp32 kernels
   a.b1c = (float)(1.0 - b.b1);
   a.b2c = (float)(1.0 - b.b2);
@@ -155,6 +156,32 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamBatch b) {
     ad_st(T.exp_avg, dt, e, m);
     ad_st(T.exp_avg_sq, dt, e, v);
   }
+  // two-level completion ticket: 64 leaf counters (a 256-B line each) and one top
+  // counter -- same-address atomics serialise at the memory side, so 2048 blocks on one
+  // counter added ~18 us; here no counter sees more than 64
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t leaf = blockIdx.x & (kAdamLeaves - 1);
+    const uint32_t in_leaf = (gridDim.x - leaf + kAdamLeaves - 1) / kAdamLeaves;
+    const uint32_t leaves = min(gridDim.x, (uint32_t)kAdamLeaves);
+    uint32_t* lc = b.ticket + (1 + leaf) * kAdamLine;
+    int last = 0;
+    if (__hip_atomic_fetch_add(lc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_leaf - 1) {
+      *lc = 0u;  // every block of this leaf has counted
+      last = __hip_atomic_fetch_add(b.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             leaves - 1;
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (s_last) {
+    const bool own = (int)threadIdx.x < b.n;
+    const float t = own ? *b.t[threadIdx.x].step + 1.f : 0.f;
+    __syncthreads();  // every count read before any is written (tensors may share one)
+    if (own) *b.t[threadIdx.x].step = t;
+    if (threadIdx.x == 0) *b.ticket = 0u;
+  }
 }
 
 }  // namespace msha
@@ -196,10 +223,11 @@ extern "C" int msha_adam_step(int32_t n, const msha_adam_tensor* tensors, double
   b.n = n;
   hipStream_t s = (hipStream_t)stream;
   b.ctr = rng_counter(s);
-  b.scal = (float2*)ws;
-  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(64), 0, s, b);
+  b.ticket = (uint32_t*)ws;
   hipLaunchKernelGGL(adam_kernel, dim3(nblocks), dim3(256), 0, s, b);
   return check_launch("adam_step");
 }
 
-extern "C" size_t msha_adam_workspace_size(void) { return sizeof(float2) * MSHA_MAX_ADAM; }
+extern "C" size_t msha_adam_workspace_size(void) {
+  return sizeof(uint32_t) * kAdamLine * (1 + kAdamLeaves);
+}

@@ -18,6 +18,9 @@
 //                gather-aggregate the matching h2 rows (dropout per (b, n))
 //           bwd_gather (wave per (b, kind)): G_b = sum_{n in group} drop * dU_n
 //           bwd_finish (one workgroup): scalar chain, deterministic per-row sums
+#include <atomic>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace msha {
@@ -284,8 +287,9 @@ __global__ void __launch_bounds__(256) ours_fwd_kernel(OursArgs a, const float* 
 // (2 blocks of 4 waves per CU left each wave ~19 dependent node steps: 60 us vs 43 us
 // for the global-gather form).
 constexpr int kOursFwdWaves = 8;
-template <typename T, int KD>
-__global__ void __launch_bounds__(64 * kOursFwdWaves) ours_fwd_lds_kernel(OursArgs a,
+template <typename T, int KD, bool PACK>
+__global__ void __launch_bounds__(64 * kOursFwdWaves)
+__attribute__((amdgpu_waves_per_eu(KD >= 4 ? 4 : 8))) ours_fwd_lds_kernel(OursArgs a,
                                                            const float* __restrict__ bstat,
                                                            const T* __restrict__ u_in,
                                                            T* __restrict__ u_out) {
@@ -335,6 +339,121 @@ __global__ void __launch_bounds__(64 * kOursFwdWaves) ours_fwd_lds_kernel(OursAr
   int hk[KD];
 #pragma unroll
   for (int k = 0; k < KD; ++k) hk[k] = min(lane + 64 * k, D - 1) / a.F;
+  if (PACK && a.dp.active) {
+    // Intra dropout: the keep bits of a (batch entry, node) pair are needed only where the
+    // entry's group matches the node's (~3 of 64 entries per node at the 2015 graph), but a
+    // per-node draw costs the whole wave one Philox block per head pair.  So the matched
+    // pairs of consecutive nodes are packed into groups of <= 64 (one lane each, in node
+    // then entry order), one draw covers a group, and each node's matches read their
+    // words from LDS at (group base + rank of the entry among the node's matches).  Same
+    // draws, same sums in the same order as the per-node form below.
+    uint16_t* pl = reinterpret_cast<uint16_t*>(w4s + B * H) + wv * 64;
+    uint2* kw = reinterpret_cast<uint2*>(
+                    reinterpret_cast<uint16_t*>(w4s + B * H) + kOursFwdWaves * 64 +
+                    ((B * D) & 1) * 2) + wv * 64;  // 8-B aligned: sx + w3s + w4s is 4 (B D + 2 B H) B
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int64_t c0 = n; c0 < a.N; c0 += 64 * nwaves) {
+      // this wave's next <= 64 nodes c0 + k nwaves: group ids one per lane
+      const int kc = (int)min<int64_t>(64, (a.N - c0 + nwaves - 1) / nwaves);
+      const int64_t nl = c0 + (int64_t)lane * nwaves;
+      const int32_t cg3 = lane < kc ? a.gid3[nl] : -1, cg4 = lane < kc ? a.gid4[nl] : -1;
+      float uin[KD];
+#pragma unroll
+      for (int k = 0; k < KD; ++k) {
+        const int d = lane + 64 * k;
+        uin[k] = d < D ? to_f32(u_in[c0 * D + d]) : 0.f;
+      }
+      int k0 = 0;
+      while (k0 < kc) {
+        int cnt = 0, k1 = k0;
+        for (; k1 < kc; ++k1) {
+          const int32_t g3 = __builtin_amdgcn_readlane(cg3, k1);
+          const int32_t g4 = __builtin_amdgcn_readlane(cg4, k1);
+          const uint64_t bal = __ballot(bvalid && (bg3 == g3 || bg4 == g4));
+          const int c = __popcll(bal);
+          if (k1 > k0 && cnt + c > 64) break;
+          if ((bal >> lane) & 1ull) pl[cnt + __popcll(bal & lt)] = (uint16_t)(((k1 - k0) << 6) | lane);
+          cnt += c;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < cnt) {
+          const int q = pl[lane];
+          const int64_t node = c0 + (int64_t)(k0 + (q >> 6)) * nwaves;
+          uint32_t kb3, kb4;
+          intra_keep_bits(a.dp, H, (uint64_t)(q & 63) * a.N + node, kb3, kb4);
+          kw[lane] = make_uint2(kb3, kb4);
+        }
+        __builtin_amdgcn_wave_barrier();
+        int base = 0;
+        for (int kk = k0; kk < k1; ++kk) {
+          const int64_t nd = c0 + (int64_t)kk * nwaves;
+          const bool has_next = kk + 1 < kc;
+          float nuin[KD];
+#pragma unroll
+          for (int k = 0; k < KD; ++k) {
+            const int d = lane + 64 * k;
+            nuin[k] = has_next && d < D ? to_f32(u_in[(nd + nwaves) * D + d]) : 0.f;
+          }
+          const int32_t g3 = __builtin_amdgcn_readlane(cg3, kk);
+          const int32_t g4 = __builtin_amdgcn_readlane(cg4, kk);
+          const uint64_t bal3 = __ballot(bvalid && bg3 == g3);
+          const uint64_t bal4 = __ballot(bvalid && bg4 == g4);
+          const uint64_t ball = bal3 | bal4;
+          float acc3[KD], acc4[KD];
+#pragma unroll
+          for (int k = 0; k < KD; ++k) acc3[k] = acc4[k] = 0.f;
+          for (int kind = 0; kind < 2; ++kind) {
+            uint64_t bal = kind == 0 ? bal3 : bal4;
+            const float* ws = kind == 0 ? w3s : w4s;
+            while (bal) {
+              const int bit0 = __ffsll((long long)bal) - 1;
+              bal &= bal - 1;
+              const bool two = bal != 0;
+              const int bit1 = two ? __ffsll((long long)bal) - 1 : bit0;
+              if (two) bal &= bal - 1;
+              const int bits[2] = {bit0, bit1};
+              float wv2[2][KD], xv2[2][KD];
+#pragma unroll
+              for (int q = 0; q < 2; ++q) {
+                const int bit = bits[q];
+                const uint2 kwd = kw[base + __popcll(ball & ((1ull << bit) - 1ull))];
+                const uint32_t kbits = kind == 0 ? kwd.x : kwd.y;
+#pragma unroll
+                for (int k = 0; k < KD; ++k) {
+                  const int d = min(lane + 64 * k, D - 1);
+                  const int h = hk[k];
+                  const float drop = h < 32 ? (((kbits >> h) & 1u) ? a.dp.scale : 0.f)
+                                            : intra_drop(a.dp, kind, h, (uint64_t)bit * a.N + nd);
+                  wv2[q][k] = ws[bit * H + h] * drop;
+                  xv2[q][k] = sx[bit * D + d];
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < 2; ++q) {
+                if (q == 1 && !two) break;
+#pragma unroll
+                for (int k = 0; k < KD; ++k) {
+                  if (kind == 0) acc3[k] = fmaf(wv2[q][k], xv2[q][k], acc3[k]);
+                  else acc4[k] = fmaf(wv2[q][k], xv2[q][k], acc4[k]);
+                }
+              }
+            }
+          }
+          base += __popcll(ball);
+#pragma unroll
+          for (int k = 0; k < KD; ++k) {
+            const int d = lane + 64 * k;
+            if (d < D) u_out[nd * D + d] = from_f32<T>(uin[k] + (acc3[k] + acc4[k]));
+            uin[k] = nuin[k];
+          }
+        }
+        // the next group's pair list overwrites this one's: every lane is past its reads
+        __builtin_amdgcn_wave_barrier();
+        k0 = k1;
+      }
+    }
+    return;
+  }
   int32_t g3 = a.gid3[n], g4 = a.gid4[n];
   float uin[KD];
 #pragma unroll
@@ -816,6 +935,21 @@ static OursArgs make_args(const msha_graph* g, const msha_groups* grp, int64_t B
 
 using namespace msha;
 
+// the intra-dropout draw form of ours_fwd_lds_kernel: packed (default; MSHA_OURS_PACK_DRAWS=0
+// starts the process with the per-node form), switchable for A/B runs and the bitwise test
+static std::atomic<int>& ours_pack_flag() {
+  static std::atomic<int> f([] {
+    const char* v = getenv("MSHA_OURS_PACK_DRAWS");
+    return v == nullptr || atoi(v) != 0 ? 1 : 0;
+  }());
+  return f;
+}
+
+extern "C" int32_t msha_ours_pack_draws(int32_t mode) {
+  if (mode < 0) return ours_pack_flag().load();
+  return ours_pack_flag().exchange(mode != 0 ? 1 : 0);
+}
+
 template <typename T>
 static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const float* el,
                        const float* er, const float* lse, const void* u_inter, float* bstat,
@@ -826,10 +960,16 @@ static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const 
   const int D = a.H * a.F;
   if (B > 0 && B <= 64 && D <= 256) {
     // the batch staged in LDS (ours_fwd_lds_kernel): a persistent grid, four blocks per CU
-    const size_t lds = (size_t)B * (D + 2 * a.H) * sizeof(float);
+    // + the dropout path's per-wave pair list (64 x u16) and keep words (64 x uint2, 8-B
+    // aligned: see the kernel)
+    const size_t lds = (size_t)B * (D + 2 * a.H) * sizeof(float) + 4 +
+                       kOursFwdWaves * 64 * (sizeof(uint16_t) + sizeof(uint2));
     const dim3 grid(grid_for(g->n_rows, kOursFwdWaves, 4 * ours_cu_count()));
-#define FWDL(kd) hipLaunchKernelGGL((ours_fwd_lds_kernel<T, kd>), grid, dim3(64 * kOursFwdWaves), lds, s, a, \
-                                    (const float*)bstat, (const T*)u_inter, (T*)u_out)
+    const bool pk = a.dp.active && msha_ours_pack_draws(-1) != 0;
+#define FWDL(kd)                                                                                 \
+  hipLaunchKernelGGL((pk ? ours_fwd_lds_kernel<T, kd, true> : ours_fwd_lds_kernel<T, kd, false>), grid, \
+                     dim3(64 * kOursFwdWaves), lds, s, a, (const float*)bstat, (const T*)u_inter,     \
+                     (T*)u_out)
     if (D <= 64) FWDL(1);
     else if (D <= 128) FWDL(2);
     else FWDL(4);

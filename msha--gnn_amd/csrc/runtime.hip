@@ -50,7 +50,32 @@ __global__ void __launch_bounds__(256) dropout_mask_kernel(Dropout d, int64_t n,
   }
 }
 
+// a step's batch copy with the replay counter's increment folded in (msha_feed_step): one
+// launch ahead of a graph replay instead of a copy plus the graph's first (add) node
+__global__ void __launch_bounds__(256) feed_step_kernel(uint8_t* __restrict__ dst,
+                                                       const uint8_t* __restrict__ src,
+                                                       int64_t bytes, uint64_t* counter) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+  const bool v16 = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+  const int64_t n16 = v16 ? bytes / 16 : 0;
+  for (int64_t i = t; i < n16; i += nt)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (int64_t i = 16 * n16 + t; i < bytes; i += nt) dst[i] = src[i];
+  if (t == 0 && counter != nullptr) *counter += 1;
+}
+
 }  // namespace msha
+
+extern "C" int msha_feed_step(void* dst, const void* src, int64_t bytes, uint64_t* counter,
+                              msha_stream_t stream) {
+  MSHA_ARG_CHECK(bytes >= 0 && (bytes == 0 || (dst != nullptr && src != nullptr)),
+                 "feed_step: bad buffers");
+  const int64_t units = bytes / 16 + 1;
+  hipLaunchKernelGGL(msha::feed_step_kernel, dim3(msha::grid_for(units, 256, 1024)), dim3(256), 0,
+                     (hipStream_t)stream, (uint8_t*)dst, (const uint8_t*)src, bytes, counter);
+  return msha::check_launch("feed_step");
+}
 
 extern "C" int msha_abi_version(void) { return MSHA_ABI_VERSION; }
 

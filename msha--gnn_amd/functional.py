@@ -94,6 +94,20 @@ def rng_counter(device=None):
     return _RNG_COUNTERS.get(torch.cuda.current_device() if dev is None else dev)
 
 
+def feed_step(dst: torch.Tensor, src: torch.Tensor, counter: torch.Tensor | None = None):
+    """``dst.copy_(src)`` plus ``counter += 1`` in one launch (msha_feed_step): the feed of a
+    replayed step whose graph leaves its replay-counter increment to the feed
+    (``step.GraphedStep.replay(feed=...)``).  Same-size contiguous tensors on one device."""
+    _lib.require_cuda(dst)
+    if (src.device != dst.device or src.dtype != dst.dtype or src.numel() != dst.numel()
+            or not (src.is_contiguous() and dst.is_contiguous())):
+        raise ValueError("feed_step: same-shape contiguous tensors of one dtype and device")
+    if counter is not None and (counter.dtype != torch.int64 or counter.device != dst.device):
+        raise ValueError("feed_step: the counter is an int64 tensor on the feed's device")
+    _lib.call("msha_feed_step", dst.data_ptr(), src.data_ptr(), dst.numel() * dst.element_size(),
+              None if counter is None else counter.data_ptr(), _lib.stream_handle(dst.device))
+
+
 def _stream(t):
     return _lib.stream_handle(t.device)
 

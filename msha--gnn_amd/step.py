@@ -9,9 +9,10 @@ dropout, the loss, the capturable Adam) all become graph nodes.
 
 Dropout stays fresh across replays: the library's Philox draws take their seeds as
 kernel arguments (frozen at capture), so a device replay counter is installed with
-``functional.set_rng_counter`` and incremented as the first node of the graph
-(include/msha_gnn.h, msha_set_rng_counter); torch's own dropout uses its
-generator's graph-safe offsets.
+``functional.set_rng_counter`` and incremented ahead of every replay
+(include/msha_gnn.h, msha_set_rng_counter): by ``replay(feed=(dst, src))``'s batch copy
+itself (msha_feed_step, one launch for both), else by a separate add; torch's own dropout
+uses its generator's graph-safe offsets.
 """
 from __future__ import annotations
 
@@ -46,10 +47,15 @@ class GraphedStep:
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.counter.add_(1)
             self.out = body()
 
-    def replay(self) -> torch.Tensor:
+    def replay(self, feed=None) -> torch.Tensor:
+        """Advance the replay counter and replay.  ``feed=(dst, src)``: copy the next batch
+        into the static input ``dst`` in the same launch that advances the counter."""
+        if feed is not None:
+            MF.feed_step(feed[0], feed[1], self.counter)
+        else:
+            self.counter.add_(1)
         self.graph.replay()
         return self.out
 

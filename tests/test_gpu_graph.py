@@ -101,6 +101,73 @@ def test_graphed_train_step_matches_eager(cuda, msha):
         torch.testing.assert_close(runs[True][1][k], p, rtol=1e-5, atol=1e-6, msg=k)
 
 
+@pytest.mark.parametrize("nbytes", [0, 1, 17, 512, 4099])
+def test_feed_step_copies_and_counts(cuda, msha, nbytes):
+    """msha_feed_step: dst.copy_(src) and counter += 1 in one launch, any size and
+    alignment (uint8 views offset by one byte take the byte path)."""
+    from msha_gnn_amd import functional as MF
+
+    for off in (0, 1):
+        src = torch.randint(0, 256, (nbytes + off,), dtype=torch.uint8, device=cuda)[off:]
+        dst = torch.zeros(nbytes + off, dtype=torch.uint8, device=cuda)[off:]
+        ctr = torch.full((1,), 41, dtype=torch.int64, device=cuda)
+        MF.feed_step(dst, src, ctr)
+        torch.testing.assert_close(dst, src, rtol=0, atol=0)
+        assert int(ctr) == 42
+        MF.feed_step(dst, src)  # no counter
+    with pytest.raises(ValueError):
+        MF.feed_step(torch.zeros(4, device=cuda), torch.zeros(5, device=cuda))
+
+
+def test_graphed_step_feed_matches_separate_copy(cuda, msha):
+    """GraphedStep.replay(feed=(dst, src)) (batch copy and replay-counter increment in one
+    launch) replays the same steps as a separate copy + replay(): dropout 0.5, so every
+    replay's masks depend on the counter."""
+    from msha_gnn_amd.data import GroupAdjacency
+    from msha_gnn_amd.step import GraphedStep
+
+    z = golden("ours_small.npz")
+    inter = msha.normalize_adjacency_matrix(t(z["counts"], cuda))
+    city = GroupAdjacency(torch.as_tensor(z["city"], device=cuda))
+    prov = GroupAdjacency(torch.as_tensor(z["prov"], device=cuda))
+    src0 = torch.as_tensor(z["source_index"], device=cuda)
+    n, m = z["counts"].shape
+    g = torch.Generator().manual_seed(1)
+    batches = [torch.randint(0, n, (src0.numel(),), generator=g).to(cuda) for _ in range(3)]
+    tgt = torch.as_tensor(np.arange(src0.numel()) % m, device=cuda)
+    runs = {}
+    for fused in (False, True):
+        model = _ours_model(z, cuda, 0.5)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
+        model.train()
+        src_s = batches[0].clone()
+
+        def body():
+            opt.zero_grad(set_to_none=True)
+            loss = F.nll_loss(model(inter, city, prov, src_s)[src_s], tgt)
+            loss.backward()
+            opt.step()
+            return loss
+
+        torch.manual_seed(0)
+        gs = GraphedStep(body, cuda, warmup=1)
+        losses = []
+        for k in range(4):
+            b = batches[k % len(batches)]
+            if fused:
+                out = gs.replay(feed=(src_s, b))
+            else:
+                src_s.copy_(b)
+                out = gs.replay()
+            losses.append(float(out.detach()))
+        assert int(gs.counter) == 5
+        gs.close()
+        runs[fused] = (losses, {k: p.detach().clone() for k, p in model.named_parameters()})
+    assert runs[True][0] == runs[False][0]
+    for k, p in runs[False][1].items():
+        torch.testing.assert_close(runs[True][1][k], p, rtol=0, atol=0, msg=k)
+
+
 def test_two_graphed_steps_keep_their_counters(cuda, msha):
     """Two live GraphedSteps on one device: each replays fresh masks from its own
     counter; closing the newer one reinstalls the older one's counter (the library keeps

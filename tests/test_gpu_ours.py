@@ -236,3 +236,39 @@ def test_ours_record_dump_matches_reference(cuda, msha):
     assert bool((C12 == -1).all())
     tol_close(C3.cpu().numpy(), r["rec.coeff3"], 1e-5, 1e-6)
     tol_close(C4.cpu().numpy(), r["rec.coeff4"], 1e-5, 1e-6)
+
+
+@pytest.mark.parametrize("n", [3000, 200_000])
+def test_ours_packed_intra_draws_bitwise(cuda, msha, n):
+    """The intra forward's packed dropout draws (msha_ours_pack_draws 1: matched (entry,
+    node) pairs of consecutive nodes share one Philox draw per <= 64 pairs) give the
+    per-node form's bits.  n = 200k puts ~24 nodes on every wave; half the batch sits in
+    one province, so its nodes carry 32+ matches and the 64-pair groups split."""
+    from msha_gnn_amd import _lib
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph, Groups
+
+    rng = np.random.default_rng(3)
+    m, H, Fd, B = 32, 2, 64, 64
+    counts = np.zeros((n, m), np.float32)
+    counts[np.arange(n), rng.integers(0, m, n)] = 1
+    city = rng.integers(0, 400, n)
+    prov = city // 40
+    src = rng.integers(0, n, B)
+    src[: B // 2] = rng.choice(np.flatnonzero(prov == 0), B // 2)
+    graph = Graph.from_dense(t(counts, cuda))
+    groups = Groups(city, prov, cuda)
+    ins = [t(rng.standard_normal(s) * 0.3, cuda) for s in ((n, H), (m, H), (m, H, Fd),
+                                                           (n, H, Fd), (H, Fd), (H, Fd))]
+    lib = _lib.load()
+    outs = []
+    try:
+        for mode in (1, 0):
+            lib.msha_ours_pack_draws(mode)
+            u, _ = MF.ours_attention(graph, groups, torch.as_tensor(src, device=cuda), *ins,
+                                     p=0.5, training=True, seed=11)
+            outs.append(u.detach().clone())
+    finally:
+        lib.msha_ours_pack_draws(1)
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0] != 0).any()
