@@ -274,6 +274,13 @@ MSHA_API int64_t msha_bip2_bwd_min_rows(int64_t rows);
  * draws per node for the whole batch (MSHA_OURS_PACK_DRAWS=0 starts with it); both give
  * the same bits.  Returns the previous mode; mode < 0 only queries. */
 MSHA_API int32_t msha_ours_pack_draws(int32_t mode);
+/* (ABI 15) The fp32 weight gradient's kernel (projection backward, dW = X^T D'): mode 0 =
+ * auto (default: from 131,072 rows -- MSHA_WGRAD_S3_MIN_ROWS -- the operands split into
+ * three bf16 terms in registers, six products on the bf16 MFMA; the exact-fp32 MFMA below),
+ * 1 = exact-fp32 MFMA, 2 = split-bf16 through LDS images, 3 = the register split at any
+ * size (MSHA_WGRAD=fp32 / x3 / s3 start the process with 1 / 2 / 3).  Returns the previous
+ * mode; mode < 0 only queries. */
+MSHA_API int32_t msha_wgrad_kernel(int32_t mode);
 
 /* Column-side (transposed) aggregate over the CSC view:
  *   out[j]   = sum_{e in col j} w[e] * table[row(e)]   (per head; table (n_rows,heads,feat))
@@ -403,6 +410,17 @@ MSHA_API int msha_gemm_f32_head_outer_colsum(
     int32_t heads, int32_t feat, const float* de, const float* a, const float* de2,
     const float* a2, const float* T, float* cs1, float* cs2, void* cs_ws, size_t cs_ws_bytes,
     msha_stream_t stream);
+/* (ABI 15) The same, where T is the projection's own output X W (Ablation.py:262, h = X @ W;
+ * A = X^T): cs1[n] = sum_a W[a, n] G[n / feat, a] with G = de^T X accumulated from the rows
+ * the weight gradient already reads, so T is never read.  Equal in real arithmetic; in fp32
+ * it differs from the T form by T's own rounding.  heads == 2 and the split-bf16
+ * weight-gradient kernel (msha_wgrad_kernel mode 0) only; MSHA_ERR_UNSUPPORTED otherwise. */
+MSHA_API int msha_gemm_f32_head_outer_colsum_w(
+    int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk, const float* B,
+    int64_t sBk, int64_t sBn, float* C, int64_t ldc, int32_t splits, void* ws, size_t ws_bytes,
+    int32_t heads, int32_t feat, const float* de, const float* a, const float* de2,
+    const float* a2, const float* W, int64_t ldw, float* cs1, float* cs2, void* cs_ws,
+    size_t cs_ws_bytes, msha_stream_t stream);
 
 /* Projection with the attention-score halves fused into its epilogue:
  *   h = X @ W  (M x heads*feat),  el[m,h] = h[m,h,:] . al[h,:],  er[m,h] = h[m,h,:] . ar[h,:]

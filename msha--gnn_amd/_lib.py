@@ -97,6 +97,7 @@ SIGNATURES = {
     "msha_set_rng_counter": (C.c_int, [I32, P]),
     "msha_feed_step": (C.c_int, [P, P, I64, P, P]),
     "msha_ours_pack_draws": (I32, [I32]),
+    "msha_wgrad_kernel": (I32, [I32]),
     "msha_get_rng_counter": (P, [I32]),
     "msha_last_error": (C.c_char_p, []),
     "msha_debug_timeline": (C.c_int, [P, I64]),
@@ -148,6 +149,9 @@ SIGNATURES = {
     "msha_gemm_f32_head_outer_colsum": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P,
                                                   I64, I32, P, SZ, I32, I32, P, P, P, P, P, P,
                                                   P, P, SZ, P]),
+    "msha_gemm_f32_head_outer_colsum_w": (C.c_int, [I64, I64, I64, P, I64, I64, P, I64, I64, P,
+                                                    I64, I32, P, SZ, I32, I32, P, P, P, P, P,
+                                                    I64, P, P, P, SZ, P]),
     "msha_add_head_outer": (C.c_int, [I64, I32, I32, P, P, P, P, P, P, P]),
     "msha_head_colsum_workspace_size": (SZ, [I64, I32, I32]),
     "msha_head_colsum": (C.c_int, [I64, I32, I32, I32, P, P, P, P, P, P, SZ, P]),

@@ -352,13 +352,16 @@ int skinny_dx(int64_t M, int64_t N, int64_t K, const float* Dh, const float* W, 
               int hH, int hF, const float* d1, const float* a1, const float* d2, const float* a2,
               hipStream_t s);
 // cs_tab (optional): also cs_out1[n] = sum_r de[r, n / hF] cs_tab[r, n] (cs_out2 with de2)
-// through the per-block partials in cs_part (2 x N x 256 floats); cs_tab has B's row pitch
+// through the per-block partials in cs_part (2 x N x 256 floats); cs_tab has B's row pitch.
+// cs_w (optional, instead of cs_tab, where cs_tab = A^T-rows x cs_w): the same sums as
+// (de^T X) cs_w from the rows already loaded (two heads; partials 4 x 128 x 256 floats)
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
                  const float* a, const float* de2, const float* a2, hipStream_t s,
                  const float* cs_tab = nullptr, float* cs_part = nullptr,
-                 float* cs_out1 = nullptr, float* cs_out2 = nullptr);
+                 float* cs_out1 = nullptr, float* cs_out2 = nullptr,
+                 const float* cs_w = nullptr, int64_t ldw = 0);
 
 // Welford triple (count, mean, M2) and Chan's combination (bn.hip, head.hip)
 struct Wf {

@@ -770,7 +770,8 @@ extern "C" int msha_gemm_f32_head_outer(int64_t M, int64_t N, int64_t K, const f
 }
 
 extern "C" size_t msha_head_outer_colsum_workspace_size(int64_t N) {
-  return N > 0 ? (size_t)2 * (size_t)N * 256 * sizeof(float) : 0;
+  // (T form: 2 x N x 256 block partials; W form: 4 x 128 x 256 -- the larger of the two)
+  return N > 0 ? (size_t)4 * (size_t)(N > 128 ? N : 128) * 256 * sizeof(float) : 0;
 }
 
 // The projection's weight gradient and score-vector gradients in one pass over the rows
@@ -802,6 +803,36 @@ extern "C" int msha_gemm_f32_head_outer_colsum(
                     feat, de, a, de2, a2, s, T, (float*)cs_ws, cs1, cs2))
     return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum: shape outside the fused kernel");
   return check_launch("gemm_f32_head_outer_colsum");
+}
+
+// (ABI 15) The same outputs where T = X W is the projection's own output (Ablation.py:262,
+// h = X @ W): cs1[n] = sum_k de[k, n / feat] (X W)[k, n] = sum_a W[a, n] G[n / feat, a] with
+// G = de^T X accumulated from the X rows the weight gradient already streams, so h is never
+// read (a third of the pass's bytes).  The sums are the same in real arithmetic; in fp32
+// they differ from the T form by h's own rounding.  Two heads, split-bf16 weight-gradient
+// kernel only; MSHA_ERR_UNSUPPORTED otherwise (the caller runs the T form).
+extern "C" int msha_gemm_f32_head_outer_colsum_w(
+    int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk, const float* B,
+    int64_t sBk, int64_t sBn, float* C, int64_t ldc, int32_t splits, void* ws, size_t ws_bytes,
+    int32_t heads, int32_t feat, const float* de, const float* a, const float* de2,
+    const float* a2, const float* W, int64_t ldw, float* cs1, float* cs2, void* cs_ws,
+    size_t cs_ws_bytes, msha_stream_t stream) {
+  MSHA_ARG_CHECK(M > 0 && N > 0 && K > 0, "gemm_f32_head_outer_colsum_w: bad sizes");
+  MSHA_ARG_CHECK(A && B && C && de && a && W && cs1 && ((de2 == nullptr) == (a2 == nullptr)) &&
+                     ((de2 == nullptr) == (cs2 == nullptr)),
+                 "gemm_f32_head_outer_colsum_w: null pointer");
+  MSHA_ARG_CHECK(heads > 0 && feat > 0 && feat % 4 == 0 && N == (int64_t)heads * feat && ldw >= N,
+                 "gemm_f32_head_outer_colsum_w: N must be heads*feat, feat a multiple of 4, ldw >= N");
+  MSHA_ARG_CHECK(splits >= 1 && splits <= 65535, "gemm_f32_head_outer_colsum_w: splits out of range");
+  MSHA_ARG_CHECK(cs_ws && cs_ws_bytes >= msha_head_outer_colsum_workspace_size(N),
+                 "gemm_f32_head_outer_colsum_w: colsum workspace too small");
+  if (!aligned16(a) || (a2 != nullptr && !aligned16(a2)))
+    return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum_w: 16-byte aligned a, a2");
+  hipStream_t s = (hipStream_t)stream;
+  if (!skinny_wgrad(M, N, K, A, sAm, sAk, B, sBk, sBn, C, ldc, 0.f, splits, ws, ws_bytes, heads,
+                    feat, de, a, de2, a2, s, nullptr, (float*)cs_ws, cs1, cs2, W, ldw))
+    return fail(MSHA_ERR_UNSUPPORTED, "gemm_f32_head_outer_colsum_w: shape outside the fused kernel");
+  return check_launch("gemm_f32_head_outer_colsum_w");
 }
 
 // every projection path computes its score dots in the row-score order (skinny.hip

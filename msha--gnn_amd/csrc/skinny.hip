@@ -24,6 +24,8 @@
 //
 // Both are deterministic (fixed summation orders); numerics are the fp32 MFMA's exact
 // fma chain (fp32) or fp32 accumulation of bf16 products (bf16).
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -1616,6 +1618,372 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+
+// ------------------------------------------- weight gradient, split-bf16 in registers ---
+// The same dW as wgrad_kernel on the bf16 matrix pipe.  Every fp32 operand is split into
+// three bf16 terms x = x_h + x_m + x_l (|x - sum| <= 2^-27 |x|) and the six products whose
+// weight reaches fp32's 2^-24 (lh, hl, mm, mh, hm, hh, small first) run as
+// v_mfma_f32_32x32x16_bf16: 16x the exact-fp32 MFMA's rate, so the six cost 3/8 of one
+// exact product.  Unlike wgrad_x3.hip (both operands staged as bf16 LDS images and read
+// back with transposed LDS reads, one block of six 18 KB images per CU) no operand is
+// transposed: a 16-row step's k index is (row group q = lane >> 5, j < 8), so lane
+// (i = lane & 31, q) loads float4 X[r + 8q + j][4i .. 4i + 3] and D[r + 8q + j][4i .. 4i + 3]
+// for j < 8, and component t of its eight X float4s IS its A fragment of the 32 x 32 tile
+// of dW rows {4i + t}, component u of its D' float4s its B fragment of dW columns {4i + u}.
+// One wave per SIMD owns the whole 128 x 128 dW of its row range (16 tiles, 256
+// accumulator registers, so X is read once).  X is double-buffered a step ahead; D, e and
+// h (CS) are reloaded for the next step as soon as this step's B terms and column sums
+// have consumed them, and the B terms (split once per step) wait in LDS, each lane reading
+// back its own 16 B, so their registers go to the loads in flight.  The four waves of a
+// block add their tiles through four 32-row LDS images per pass ((w0 + w2) + (w1 + w3),
+// wgrad_kernel's order) into the same slab / partials.
+constexpr int kWsWaves = 4;
+constexpr int kWsImg = 32 * kWgPitch;  // floats of one 32-row LDS image of the block sum
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two fp32 -> their three packed bf16 terms: v_cvt_pk_bf16_f32 (RNE) + v_pk_add_f32 for the
+// exact residuals, 9 instructions a pair
+__device__ __forceinline__ uint32_t pk_bf16(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ f32x2 unpk_bf16(uint32_t b) {
+  return f32x2{__uint_as_float(b << 16), __uint_as_float(b & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3x8(const f32x2 (&v)[4], bf16x8& h, bf16x8& m, bf16x8& l) {
+  uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    hw[p] = pk_bf16(v[p]);
+    const f32x2 r = v[p] - unpk_bf16(hw[p]);
+    mw[p] = pk_bf16(r);
+    lw[p] = pk_bf16(r - unpk_bf16(mw[p]));
+  }
+  h = __builtin_bit_cast(bf16x8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+  m = __builtin_bit_cast(bf16x8, make_uint4(mw[0], mw[1], mw[2], mw[3]));
+  l = __builtin_bit_cast(bf16x8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+}
+
+template <bool HO, int CSM>
+__global__ void __launch_bounds__(64 * kWsWaves) __attribute__((amdgpu_waves_per_eu(1, 1)))
+wgrad_s3_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __restrict__ D,
+                int64_t ldd, const float* __restrict__ d1, const float* __restrict__ a1,
+                const float* __restrict__ d2, const float* __restrict__ a2, int hH, int hF,
+                float* __restrict__ slab, const float* __restrict__ hs, float* __restrict__ cpart) {
+  // CSM: the score-vector gradients' column sums -- 0 none; 1 cs[n] = sum_r e[r, n / hF]
+  // T[r, n] from a table T (= h); 2 (two heads) G[head][a] = sum_r e[r, head] X[r, a] from
+  // the X rows already in registers (dal = G W: wgrad_gw_kernel), so h is never read
+  constexpr bool CS = CSM == 1, GS = CSM == 2;
+  static_assert(CSM == 0 || HO, "the score-vector gradients need the head terms");
+  // the B terms [wave][u][term][lane] (48 KB) during the loop; the block sum's four 32-row
+  // images (68 KB) after it
+  __shared__ __attribute__((aligned(16))) float red[kWsWaves * kWsImg];
+  __shared__ __attribute__((aligned(16))) float csred[CS ? kWsWaves * 2 * 128 : GS ? kWsWaves * 4 * 128 : 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i32 = lane & 31, q = lane >> 5;
+  const int nq = gridDim.x * kWsWaves;
+  const int gs = blockIdx.x * kWsWaves + w;
+  const int r0 = __builtin_amdgcn_readfirstlane((int)(((int64_t)gs * M) / nq));
+  const int r1 = __builtin_amdgcn_readfirstlane((int)(((int64_t)(gs + 1) * M) / nq));
+  const int c4 = 4 * i32;  // this lane's four dW columns (and X columns)
+  const int hh = HO ? c4 / hF : 0;
+  TL_OPEN(3);  // marks: entry, row loop start, row loop done, block sum done, exit
+  float av1[4] = {0.f, 0.f, 0.f, 0.f}, av2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (HO) {
+    const float4 v1 = *reinterpret_cast<const float4*>(a1 + c4);
+    av1[0] = v1.x, av1[1] = v1.y, av1[2] = v1.z, av1[3] = v1.w;
+    if (d2 != nullptr) {
+      const float4 v2 = *reinterpret_cast<const float4*>(a2 + c4);
+      av2[0] = v2.x, av2[1] = v2.y, av2[2] = v2.z, av2[3] = v2.w;
+    }
+  }
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[t][u][v] = 0.f;
+  // descriptors end at the wave's last row: rows past r1 read 0 and add nothing, with no
+  // per-lane mask (the offsets are one VGPR per stream + a scalar row term)
+  const uint32_t sx = (uint32_t)ldx * 4u, sd = (uint32_t)ldd * 4u, se = (uint32_t)hH * 4u;
+  const rsrc_t r_x = make_rsrc(X, (uint32_t)r1 * sx);
+  const rsrc_t r_d = make_rsrc(D, (uint32_t)r1 * sd);
+  const rsrc_t r_e1 = make_rsrc(HO ? d1 : nullptr, HO ? (uint32_t)r1 * se : 0u);
+  const rsrc_t r_e2 = make_rsrc(HO ? d2 : nullptr, HO && d2 ? (uint32_t)r1 * se : 0u);
+  const rsrc_t r_h = make_rsrc(CS ? hs : nullptr, CS ? (uint32_t)r1 * sd : 0u);
+  const uint32_t vx = 8u * q * sx + 16u * i32, vd = 8u * q * sd + 16u * i32, ve = 8u * q * se + 4u * hh;
+  auto roff = [&](int rb, int j, uint32_t stride, uint32_t v) -> uint32_t {
+    return v + (uint32_t)(rb + j) * stride;
+  };
+  u32x4_t xa[8], xb[8], dv[8], hv[CS ? 8 : 1];
+  float e1[8], e2[8];             // this lane's head's e of the step's rows
+  f32x2 eg1[GS ? 8 : 1], eg2[GS ? 8 : 1];  // GS: both heads' e of the rows
+  float g1[GS ? 2 : 1][4], g2[GS ? 2 : 1][4];
+  if (GS)
+#pragma unroll
+    for (int hd = 0; hd < 2; ++hd)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) g1[hd][t] = g2[hd][t] = 0.f;
+  const uint32_t veg = 8u * q * se;
+  auto load_x = [&](int rb, u32x4_t(&x)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = buf_b128(r_x, roff(rb, j, sx, vx));
+  };
+  auto load_d = [&](int rb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dv[j] = buf_b128(r_d, roff(rb, j, sd, vd));
+      if (GS) {  // (se = 8: both heads of a row in one load)
+        const auto a = __builtin_amdgcn_raw_buffer_load_b64(r_e1, roff(rb, j, se, veg), 0, 0);
+        const auto b = __builtin_amdgcn_raw_buffer_load_b64(r_e2, roff(rb, j, se, veg), 0, 0);
+        eg1[j] = f32x2{__uint_as_float(a[0]), __uint_as_float(a[1])};
+        eg2[j] = f32x2{__uint_as_float(b[0]), __uint_as_float(b[1])};
+      } else if (HO) {
+        e1[j] = buf_f32(r_e1, roff(rb, j, se, ve));
+        e2[j] = buf_f32(r_e2, roff(rb, j, se, ve));
+      }
+      if (CS) hv[j] = buf_b128(r_h, roff(rb, j, sd, vd));
+    }
+  };
+  float cs1[4] = {0.f, 0.f, 0.f, 0.f}, cs2[4] = {0.f, 0.f, 0.f, 0.f};
+  // this wave's B terms of the step, [u][term][lane] (16 B each): parked in LDS so their 48
+  // registers go to the loads in flight; each lane reads back its own
+  bf16x8* bst = reinterpret_cast<bf16x8*>(red) + w * (4 * 3 * 64) + lane;
+  auto step = [&](const u32x4_t(&x)[8], int rb_next) {
+    if (GS)  // G += e^T X over this step's rows (before load_d replaces e)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float xv = __uint_as_float(x[j][t]);
+          g1[0][t] = fmaf(eg1[j].x, xv, g1[0][t]);
+          g1[1][t] = fmaf(eg1[j].y, xv, g1[1][t]);
+          g2[0][t] = fmaf(eg2[j].x, xv, g2[0][t]);
+          g2[1][t] = fmaf(eg2[j].y, xv, g2[1][t]);
+        }
+    if (CS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float h = __uint_as_float(hv[j][u]);
+          cs1[u] = fmaf(e1[j], h, cs1[u]);
+          cs2[u] = fmaf(e2[j], h, cs2[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      f32x2 dd[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        f32x2 d = {__uint_as_float(dv[2 * p][u]), __uint_as_float(dv[2 * p + 1][u])};
+        if (HO) {
+          const f32x2 e1p = GS ? f32x2{hh ? eg1[2 * p].y : eg1[2 * p].x, hh ? eg1[2 * p + 1].y : eg1[2 * p + 1].x}
+                               : f32x2{e1[2 * p], e1[2 * p + 1]};
+          const f32x2 e2p = GS ? f32x2{hh ? eg2[2 * p].y : eg2[2 * p].x, hh ? eg2[2 * p + 1].y : eg2[2 * p + 1].x}
+                               : f32x2{e2[2 * p], e2[2 * p + 1]};
+          d = e2p * av2[u] + (e1p * av1[u] + d);  // wgrad_kernel's order, two rows at once
+        }
+        dd[p] = d;
+      }
+      bf16x8 th, tm, tl;
+      split3x8(dd, th, tm, tl);
+      bst[(u * 3 + 0) * 64] = th;
+      bst[(u * 3 + 1) * 64] = tm;
+      bst[(u * 3 + 2) * 64] = tl;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    load_d(rb_next);  // the next step's D', e, h: in flight under this step's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    // the next tile's B terms are read from LDS under the current tile's six MFMAs
+    bf16x8 bh = bst[0], bm = bst[64], bl = bst[128];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      __builtin_amdgcn_sched_barrier(0);  // one tile row's A terms live at a time
+      f32x2 xs[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) xs[p] = f32x2{__uint_as_float(x[2 * p][t]), __uint_as_float(x[2 * p + 1][t])};
+      bf16x8 ah, am, al;
+      split3x8(xs, ah, am, al);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bf16x8 ch = bh, cm = bm, cl = bl;
+        if (t < 3 || u < 3) {
+          const int nu = (u + 1) & 3;
+          bh = bst[(nu * 3 + 0) * 64];
+          bm = bst[(nu * 3 + 1) * 64];
+          bl = bst[(nu * 3 + 2) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the reads leave before these MFMAs
+        // one accumulation chain per tile (32x32x16 bf16 issues back to back on one
+        // accumulator): lh, hl, mm, mh, hm, hh -- the small products first
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, cm, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, ch, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cm, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch, acc[t][u], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  load_x(r0, xa);
+  load_d(r0);
+  TL_MARK();
+  for (int rb = r0; rb < r1; rb += 32) {
+    load_x(rb + 16, xb);  // past r1: reads 0
+    __builtin_amdgcn_sched_barrier(0);
+    step(xa, rb + 16);
+    __builtin_amdgcn_sched_barrier(0);
+    load_x(rb + 32, xa);
+    __builtin_amdgcn_sched_barrier(0);
+    step(xb, rb + 32);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  TL_MARK();
+  if (CS) {  // the two row groups of the lane pair, then the waves via LDS
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      cs1[u] += __shfl_xor(cs1[u], 32);
+      cs2[u] += __shfl_xor(cs2[u], 32);
+    }
+    if (q == 0) {
+      *reinterpret_cast<float4*>(csred + (w * 2 + 0) * 128 + c4) = make_float4(cs1[0], cs1[1], cs1[2], cs1[3]);
+      *reinterpret_cast<float4*>(csred + (w * 2 + 1) * 128 + c4) = make_float4(cs2[0], cs2[1], cs2[2], cs2[3]);
+    }
+  }
+  if (GS) {  // the two row groups of the lane pair, then the waves via LDS: [w][which][head][a]
+#pragma unroll
+    for (int hd = 0; hd < 2; ++hd)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        g1[hd][t] += __shfl_xor(g1[hd][t], 32);
+        g2[hd][t] += __shfl_xor(g2[hd][t], 32);
+      }
+    if (q == 0)
+#pragma unroll
+      for (int hd = 0; hd < 2; ++hd) {
+        *reinterpret_cast<float4*>(csred + ((w * 2 + 0) * 2 + hd) * 128 + c4) =
+            make_float4(g1[hd][0], g1[hd][1], g1[hd][2], g1[hd][3]);
+        *reinterpret_cast<float4*>(csred + ((w * 2 + 1) * 2 + hd) * 128 + c4) =
+            make_float4(g2[hd][0], g2[hd][1], g2[hd][2], g2[hd][3]);
+      }
+  }
+  // ---- block sum, 32 dW rows a pass: every wave parks its slice in its own image, then
+  // all four store (w0 + w2) + (w1 + w3) (wgrad_kernel's order), 512 contiguous bytes a
+  // row.  C layout: reg v of lane l is tile row 8 (v / 4) + 4 (l >> 5) + (v % 4), column
+  // l & 31 -> dW row 4 m + t (pass v / 4), columns 4 (l & 31) + u
+  float* out = slab + (int64_t)blockIdx.x * (128 * 128);
+  float* img = red + w * kWsImg;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    __syncthreads();  // the B slots (pass 0) / the previous pass's images are free
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int vv = 0; vv < 4; ++vv) {
+        const int v = 4 * pass + vv;
+        const int row = 4 * (4 * q + vv) + t;  // row within the pass's 32
+        *reinterpret_cast<float4*>(img + row * kWgPitch + c4) =
+            make_float4(acc[t][0][v], acc[t][1][v], acc[t][2][v], acc[t][3][v]);
+      }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32 * 32 / (64 * kWsWaves); ++k) {
+      const int f = tid + k * 64 * kWsWaves;
+      const int row = f >> 5, col = (f & 31) * 4;
+      const float4 x0 = *reinterpret_cast<const float4*>(red + 0 * kWsImg + row * kWgPitch + col);
+      const float4 x1 = *reinterpret_cast<const float4*>(red + 1 * kWsImg + row * kWgPitch + col);
+      const float4 x2 = *reinterpret_cast<const float4*>(red + 2 * kWsImg + row * kWgPitch + col);
+      const float4 x3 = *reinterpret_cast<const float4*>(red + 3 * kWsImg + row * kWgPitch + col);
+      // row r of the pass is dW row 4 (8 pass + r / 4 ... ): rows 32 pass .. 32 pass + 31
+      *reinterpret_cast<float4*>(out + (32 * pass + row) * 128 + col) =
+          make_float4((x0.x + x2.x) + (x1.x + x3.x), (x0.y + x2.y) + (x1.y + x3.y),
+                      (x0.z + x2.z) + (x1.z + x3.z), (x0.w + x2.w) + (x1.w + x3.w));
+    }
+  }
+  TL_MARK();
+  if (GS && w == 0 && q == 0) {  // waves in order; part[which][head][a][block]
+    const int nb = gridDim.x;
+#pragma unroll
+    for (int wh = 0; wh < 4; ++wh)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < kWsWaves; ++k) v += csred[(k * 4 + wh) * 128 + c4 + t];
+        cpart[((int64_t)wh * 128 + c4 + t) * nb + blockIdx.x] = v;
+      }
+  }
+  if (CS && w == 0 && q == 0) {  // waves in order; part[which][n][block]
+    const int nb = gridDim.x;
+#pragma unroll
+    for (int which = 0; which < 2; ++which)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < kWsWaves; ++k) v += csred[(k * 2 + which) * 128 + c4 + u];
+        cpart[((int64_t)which * 128 + c4 + u) * nb + blockIdx.x] = v;
+      }
+  }
+  TL_MARK();
+}
+
+// The G-based column sums (wgrad_s3_kernel CSM 2): block (which, head) sums its G[a] over
+// the row blocks (nb <= 256; a wave per 32 a, lane l takes blocks l, l + 64, .. in order,
+// then a fixed xor tree), then
+// cs_which[head * hF + f] = sum_a W[a][head * hF + f] G[a]: a wave per 16 a, lanes over f
+// (coalesced W rows), the four waves' partials added in wave order.
+__global__ void __launch_bounds__(256) wgrad_gw_kernel(const float* __restrict__ cpart, int nb,
+                                                       const float* __restrict__ W, int64_t ldw,
+                                                       int hF, float* __restrict__ cs1,
+                                                       float* __restrict__ cs2) {
+  __shared__ float G[128];
+  __shared__ float part[4][256];
+  const int which = blockIdx.x >> 1, hd = blockIdx.x & 1;
+  float* out = which == 0 ? cs1 : cs2;
+  if (out == nullptr) return;  // (block-uniform)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float* src = cpart + (int64_t)(which * 2 + hd) * 128 * nb;
+  {  // wave wv: a in [32 wv, 32 wv + 32); every load in flight at once (nb <= 256)
+    float v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const float* r = src + (int64_t)(32 * wv + k) * nb;
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int b = lane + 64 * c;
+        s += b < nb ? r[b] : 0.f;
+      }
+      v[k] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v[k] += __shfl_xor(v[k], o);
+      if (lane == 0) G[32 * wv + k] = v[k];
+    }
+  }
+  __syncthreads();
+  for (int f0 = 0; f0 < hF; f0 += 256) {
+    for (int f = f0 + lane; f < f0 + 256 && f < hF; f += 64) {
+      const int n = hd * hF + f;
+      float v = 0.f;
+#pragma unroll 8
+      for (int a = 32 * wv; a < 32 * wv + 32; ++a) v = fmaf(W[(int64_t)a * ldw + n], G[a], v);
+      part[wv][f - f0] = v;
+    }
+    __syncthreads();
+    for (int f = f0 + (int)threadIdx.x; f < f0 + 256 && f < hF; f += 256)
+      out[hd * hF + f] = ((part[0][f - f0] + part[1][f - f0]) + part[2][f - f0]) + part[3][f - f0];
+    __syncthreads();
+  }
+}
+
 }  // namespace sk
 
 // ------------------------------------------------------------------ dispatch ---
@@ -1779,11 +2147,25 @@ int wgrad_x3(int64_t K, const float* X, int64_t ldx, const float* D, int64_t ldd
              const float* de, const float* a, const float* de2, const float* a2, float* slab,
              int nb, const float* cs_tab, float* cs_part, hipStream_t s);
 
+// The fp32 weight gradient's kernel: MSHA_WGRAD=s3 (split-bf16, register operands, at any
+// size), x3 (split-bf16 through LDS images, wgrad_x3.hip) or fp32 (exact-fp32 MFMA,
+// wgrad_kernel); unset: s3 from MSHA_WGRAD_S3_MIN_ROWS (131,072) rows, fp32 below.
+// Switchable at run time (msha_wgrad_kernel) for A/B runs and tests.
+static std::atomic<int>& wgrad_mode() {
+  static std::atomic<int> m([] {
+    const char* v = getenv("MSHA_WGRAD");
+    if (v == nullptr || !*v) return 0;
+    return strcmp(v, "x3") == 0 ? 2 : strcmp(v, "fp32") == 0 ? 1 : strcmp(v, "s3") == 0 ? 3 : 0;
+  }());
+  return m;
+}
+
 int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, int64_t sAk,
                  const float* B, int64_t sBk, int64_t sBn, float* C, int64_t ldc, float beta,
                  int32_t splits, void* ws, size_t ws_bytes, int hH, int hF, const float* de,
                  const float* a, const float* de2, const float* a2, hipStream_t s,
-                 const float* cs_tab, float* cs_part, float* cs_out1, float* cs_out2) {
+                 const float* cs_tab, float* cs_part, float* cs_out1, float* cs_out2,
+                 const float* cs_w, int64_t ldw) {
   if (!skinny_enabled() || M != 128 || N != 128 || sAm != 1 || sBn != 1) return 0;
   if (K < 4096 || K >= (1ll << 31) || splits < 16) return 0;
   if (sAk % 4 || sBk % 4 || ((uintptr_t)A | (uintptr_t)B) & 15) return 0;
@@ -1797,7 +2179,43 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
                           (de2 != nullptr) != (cs_out2 != nullptr) || ((uintptr_t)cs_tab & 7)))
     return 0;
   float* slab = (float*)ws;
-  if (wgrad_x3(K, A, sAk, B, sBk, hH, hF, de, a, de2, a2, slab, (int)nb, cs_tab, cs_part, s)) {
+  // below ~128k rows a wave of the split kernel has too few 16-row steps to repay its
+  // fixed costs (C4 100k rows: 46 vs 43 us): the exact-fp32 kernel runs there
+  static const int64_t s3_min = [] {
+    const char* v = getenv("MSHA_WGRAD_S3_MIN_ROWS");
+    return v != nullptr && *v ? (int64_t)atoll(v) : (int64_t)131072;
+  }();
+  const int req = wgrad_mode().load();  // 3: the split kernel whatever the rows
+  const int mode = req == 3 ? 0 : req == 0 && K < s3_min ? 1 : req;
+  const bool small = K * sAk * 4 < (1ll << 31) && K * sBk * 4 < (1ll << 31);
+  if (cs_w != nullptr) {
+    // the column sums from G = e^T X and W (two heads, split-bf16 kernel only)
+    if (mode != 0 || !small || hH != 2 || de == nullptr || cs_part == nullptr || cs_out1 == nullptr ||
+        (de2 != nullptr) != (cs_out2 != nullptr) || ldw < 128)
+      return 0;
+    hipLaunchKernelGGL((sk::wgrad_s3_kernel<true, 2>), dim3((unsigned)nb), dim3(64 * sk::kWsWaves), 0, s,
+                       (int)K, A, sAk, B, sBk, de, a, de2, a2, hH, hF, slab, nullptr, cs_part);
+    hipLaunchKernelGGL(sk::wgrad_reduce_kernel<float>, dim3(128 * 128 / (4 * sk::kWrCols)), dim3(256), 0,
+                       s, (const float*)slab, (int)nb, C, ldc, beta, (const float*)nullptr,
+                       (float*)nullptr, (float*)nullptr);
+    hipLaunchKernelGGL(sk::wgrad_gw_kernel, dim3(de2 != nullptr ? 4 : 2), dim3(256), 0, s,
+                       (const float*)cs_part, (int)nb, cs_w, ldw, hF, cs_out1, cs_out2);
+    return 1;
+  }
+  if (mode == 0 && small) {
+    // split-bf16, register operands (wgrad_s3_kernel): same slab / partial layout
+    if (cs_tab != nullptr)
+      hipLaunchKernelGGL((sk::wgrad_s3_kernel<true, 1>), dim3((unsigned)nb), dim3(64 * sk::kWsWaves), 0,
+                         s, (int)K, A, sAk, B, sBk, de, a, de2, a2, hH, hF, slab, cs_tab, cs_part);
+    else if (de != nullptr)
+      hipLaunchKernelGGL((sk::wgrad_s3_kernel<true, 0>), dim3((unsigned)nb), dim3(64 * sk::kWsWaves), 0,
+                         s, (int)K, A, sAk, B, sBk, de, a, de2, a2, hH, hF, slab, nullptr, nullptr);
+    else
+      hipLaunchKernelGGL((sk::wgrad_s3_kernel<false, 0>), dim3((unsigned)nb), dim3(64 * sk::kWsWaves),
+                         0, s, (int)K, A, sAk, B, sBk, nullptr, nullptr, nullptr, nullptr, 1, 4, slab,
+                         nullptr, nullptr);
+  } else if (mode == 2 &&
+             wgrad_x3(K, A, sAk, B, sBk, hH, hF, de, a, de2, a2, slab, (int)nb, cs_tab, cs_part, s)) {
     // split-bf16 (wgrad_x3.hip): same slab / partial layout
   } else if (cs_tab != nullptr)
     hipLaunchKernelGGL((sk::wgrad_kernel<true, true>), dim3((unsigned)nb), dim3(64 * sk::kWgWaves), 0, s,
@@ -1822,6 +2240,14 @@ int skinny_wgrad(int64_t M, int64_t N, int64_t K, const float* A, int64_t sAm, i
 // Diagnostic: install (buf != NULL) or remove the per-wave timeline buffer of the skinny
 // kernels (slots x 64 uint64 words, device memory); MSHA_ERR_UNSUPPORTED unless the library
 // was built with -DSK_TIMELINE (build.py --variant timeline).
+// (ABI 15) the fp32 weight-gradient kernel: 0 auto (split-bf16 registers from 131,072 rows,
+// exact fp32 below), 1 exact fp32, 2 split-bf16 LDS images, 3 split-bf16 registers at any
+// size; returns the previous mode, mode < 0 only queries
+extern "C" int32_t msha_wgrad_kernel(int32_t mode) {
+  if (mode < 0 || mode > 3) return msha::wgrad_mode().load();
+  return msha::wgrad_mode().exchange(mode);
+}
+
 extern "C" int msha_debug_timeline(void* buf, int64_t slots) {
 #ifdef SK_TIMELINE
   uint64_t* p = (uint64_t*)buf;

@@ -209,16 +209,13 @@ wgrad_x3_kernel(int M, const float* __restrict__ X, int64_t ldx, const float* __
 }  // namespace wx3
 
 // dW block partials into slab (nb x 128 x 128) for skinny.hip's wgrad_reduce_kernel; 1 =
-// launched.  Opt-in (MSHA_WGRAD_X3=1): measured slower than the exact-fp32 wgrad_kernel at
-// bip1m (421 vs 382 us) and R15 (27.5 vs 21 us), profiles/round5_bench_v1/README.md.
+// launched.  Opt-in (MSHA_WGRAD=x3): measured slower than the exact-fp32 wgrad_kernel at
+// bip1m (421 vs 382 us) and R15 (27.5 vs 21 us), profiles/round5_bench_v1/README.md; the
+// register-operand split (skinny.hip wgrad_s3_kernel) replaced both.
 int wgrad_x3(int64_t K, const float* X, int64_t ldx, const float* D, int64_t ldd, int hH, int hF,
              const float* de, const float* a, const float* de2, const float* a2, float* slab,
              int nb, const float* cs_tab, float* cs_part, hipStream_t s) {
-  static const int env = [] {
-    const char* v = getenv("MSHA_WGRAD_X3");
-    return v != nullptr && *v ? atoi(v) : 0;
-  }();
-  if (env == 0 || K * ldx * 4 >= (1ll << 31) || K * ldd * 4 >= (1ll << 31)) return 0;
+  if (K * ldx * 4 >= (1ll << 31) || K * ldd * 4 >= (1ll << 31)) return 0;
   const dim3 grid(nb), block(wx3::kThreads);
   if (cs_tab != nullptr)
     hipLaunchKernelGGL((wx3::wgrad_x3_kernel<true, true>), grid, block, 0, s, (int)K, X, ldx, D,

@@ -662,7 +662,7 @@ class _ProjectScores(torch.autograd.Function):
                 kw["out_dtype"] = wdt if dt == BF16 else None
                 if dt == torch.float32 and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
                     # dW, dal, dar in one pass over the rows where the shape allows
-                    fused = _wgrad_colsum(X, dh, outer, h)
+                    fused = _wgrad_colsum(X, dh, outer, h, W)
                     if fused is not None:
                         dW, o1, o2 = fused
                         dal, dar = _score_grads(d_el, d_er, o1, o2, al, ar, aldt, ardt)
@@ -701,10 +701,13 @@ def _score_grads(d_el, d_er, o1, o2, al, ar, aldt, ardt):
     return dal, dar
 
 
-def _wgrad_colsum(X, dh, outer, h):
+def _wgrad_colsum(X, dh, outer, h, W=None):
     """dW = X^T (dh + d1 (x) a1 [+ d2 (x) a2]) and the column sums of d1 (x) h, d2 (x) h
     (msha_gemm_f32_head_outer_colsum: one pass over the rows), or None where the fused
-    kernel does not cover the shape (the caller runs the two ops)."""
+    kernel does not cover the shape (the caller runs the two ops).  With W (h = X @ W, the
+    projection's own output) the sums come as (d^T X) W from the rows the weight gradient
+    already reads (msha_gemm_f32_head_outer_colsum_w: h is not read) where that kernel
+    covers the shape."""
     H, Fd, d1, a1, d2, a2 = outer
     M, K = X.shape
     N = dh.shape[1]
@@ -720,6 +723,16 @@ def _wgrad_colsum(X, dh, outer, h):
     o1 = torch.empty(H, Fd, device=dev, dtype=torch.float32)
     o2 = torch.empty(H, Fd, device=dev, dtype=torch.float32) if d2 is not None else None
     A = X.t()
+    if W is not None and W.dtype == torch.float32 and W.shape == (K, N) and W.stride(1) == 1:
+        rc = _lib.fn("msha_gemm_f32_head_outer_colsum_w")(
+            K, N, M, A.data_ptr(), A.stride(0), A.stride(1), dh.data_ptr(), dh.stride(0),
+            dh.stride(1), dW.data_ptr(), dW.stride(0), splits, buf.data_ptr(), wsb, H, Fd,
+            d1.data_ptr(), a1.data_ptr(), _lib.ptr(d2), _lib.ptr(a2), W.data_ptr(), W.stride(0),
+            o1.data_ptr(), _lib.ptr(o2), buf.data_ptr() + wsb, cwsb, _stream(X))
+        if rc == 0:
+            return dW, o1, o2
+        if rc != _lib.MSHA_ERR_UNSUPPORTED:
+            _lib.raise_for(rc, "msha_gemm_f32_head_outer_colsum_w")
     rc = _lib.fn("msha_gemm_f32_head_outer_colsum")(
         K, N, M, A.data_ptr(), A.stride(0), A.stride(1), dh.data_ptr(), dh.stride(0),
         dh.stride(1), dW.data_ptr(), dW.stride(0), splits, buf.data_ptr(), wsb, H, Fd,

@@ -128,11 +128,11 @@ def summarize(waves, kind):
     return s
 
 
-def main(out):
+def main(out, n=100_000, H=8, F=16, kinds=("proj", "wgrad")):
     os.makedirs(out, exist_ok=True)
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
-    n, K, H, F = 100_000, 128, 8, 16
+    K = 128
     X = torch.rand(n, K, generator=g).to(dev)
     W = (torch.randn(K, H * F, generator=g) * K ** -0.5).to(dev)
     al = torch.randn(H, F, generator=g).to(dev)
@@ -142,10 +142,15 @@ def main(out):
     d2 = torch.randn(n, H, generator=g).to(dev)
     buf = torch.zeros(SLOTS * STRIDE, dtype=torch.int64, device=dev)
     res = {}
-    for kind, fn in (("proj", lambda: MF.project_scores(X, W, al, ar, heads=H)),
-                     ("wgrad", lambda: MF.gemm_head_outer(X.t(), dh, 1, (H, F, d1, al, d2, ar)))):
+    T = torch.randn(n, H * F, generator=g).to(dev)
+    legs = {"proj": lambda: MF.project_scores(X, W, al, ar, heads=H),
+            "wgrad": lambda: MF.gemm_head_outer(X.t(), dh, 1, (H, F, d1, al, d2, ar)),
+            # the score-vector column sums fused in (bip1m's and C4's form)
+            "wgrad_cs": lambda: MF._wgrad_colsum(X, dh, (H, F, d1, al, d2, ar), T)}
+    for kind in kinds:
+        fn = legs[kind]
         waves = decode(capture(fn, buf), 0)
-        summ = summarize(waves, kind)
+        summ = summarize(waves, "wgrad" if kind.startswith("wgrad") else kind)
         res[kind] = summ
         json.dump({"summary": summ,
                    "waves": [{k: (v.tolist() if isinstance(v, np.ndarray) else v)
@@ -156,4 +161,8 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "timeline"))
+    # OUT [rows heads feat kind,kind]: e.g. OUT 1000000 2 64 wgrad_cs (the bip1m shape)
+    a = sys.argv[1:]
+    main(a[0] if a else os.path.join(ROOT, "gpurun_out", "timeline"),
+         *([int(a[1]), int(a[2]), int(a[3])] if len(a) > 3 else []),
+         *([tuple(a[4].split(","))] if len(a) > 4 else []))

@@ -493,6 +493,26 @@ def test_project_scores_fwd_bwd(cuda, M, K, H, F):
         tol_close(got.grad.cpu().numpy(), want.grad.numpy(), 1e-4, 1e-5)
 
 
+@pytest.fixture(params=["s3", "fp32"])
+def wgrad_kernel(request, msha):
+    """Run under each fp32 weight-gradient kernel: split-bf16 in registers (the default)
+    and the exact-fp32 MFMA (msha_wgrad_kernel)."""
+    from msha_gnn_amd import _lib
+
+    lib = _lib.load()
+    prev = lib.msha_wgrad_kernel({"s3": 3, "fp32": 1}[request.param])
+    yield request.param
+    lib.msha_wgrad_kernel(prev)
+
+
+def _wgrad_bound(got, X, tot, name):
+    """Every dW element within 4 sqrt(n) u sum_r |X[r, a]| |tot[r, n]| (n = rows + the
+    split's six products and the block / slab reduce levels) of the fp64 product."""
+    A = np.abs(X.astype(np.float64)).T @ np.abs(tot)
+    ref = X.T.astype(np.float64) @ tot
+    bounded_close(got, ref, A, X.shape[0] + 64, 0.0, name)
+
+
 @pytest.mark.parametrize("operand,M,H,F,K,two", [(1, 100000, 8, 16, 128, True),
                                                  (1, 5000, 2, 64, 96, False),
                                                  (1, 50015, 2, 64, 128, True),
@@ -501,7 +521,7 @@ def test_project_scores_fwd_bwd(cuda, M, K, H, F):
                                                  (0, 4096, 4, 32, 64, False),
                                                  (0, 2048, 1, 64, 64, True),
                                                  (0, 517, 1, 8, 40, False)])
-def test_gemm_head_outer(cuda, operand, M, H, F, K, two):
+def test_gemm_head_outer(cuda, wgrad_kernel, operand, M, H, F, K, two):
     """dX = (dh + de (x) a) W^T (operand 0) and dW = X^T (dh + de (x) a) (operand 1)
     with the sum folded into the operand loads, vs torch fp64.  Operand 0 with M >= 1024,
     D and the output width in {64, 128} runs the resident-W kernel (skinny.hip
@@ -530,6 +550,7 @@ def test_gemm_head_outer(cuda, operand, M, H, F, K, two):
         again = MF.gemm_head_outer(t(X, cuda).t(), t(dh, cuda), 1, outer).cpu().numpy()
         assert np.array_equal(got, again)  # block partials added in a fixed order
         ref = X.T.astype(np.float64) @ tot
+        _wgrad_bound(got, X, tot, f"dW[{wgrad_kernel}]")
     tol_close(got, ref, 1e-5, 1e-5)
 
 
@@ -867,7 +888,7 @@ def test_pair_linear_resident_w(cuda, msha, K, N):
 
 @pytest.mark.parametrize("M,H,F,two", [(100000, 8, 16, True), (50015, 2, 64, True),
                                        (4096, 8, 16, False), (8191, 1, 128, True)])
-def test_gemm_head_outer_colsum(cuda, M, H, F, two):
+def test_gemm_head_outer_colsum(cuda, wgrad_kernel, M, H, F, two):
     """msha_gemm_f32_head_outer_colsum: dW = X^T (dh + de (x) a [+ de2 (x) a2]) and the
     score-vector gradients sum_r de[r,h] T[r,h*F+f] from one pass over the rows, vs
     torch fp64 (1e-5), deterministic across calls; a shape outside the fused kernel
@@ -895,6 +916,7 @@ def test_gemm_head_outer_colsum(cuda, M, H, F, two):
         tot += np.repeat(de2, F, 1) * a2.reshape(-1)
     dW, o1, o2 = runs[0]
     tol_close(dW.cpu().numpy(), X.T.astype(np.float64) @ tot, 1e-5, 1e-5)
+    _wgrad_bound(dW.cpu().numpy(), X, tot, f"dW[{wgrad_kernel}]")
     T3 = T.astype(np.float64).reshape(M, H, F)
     tol_close(o1.cpu().numpy(), np.einsum("mh,mhf->hf", de.astype(np.float64), T3), 1e-5, 1e-5)
     if two:
@@ -904,3 +926,50 @@ def test_gemm_head_outer_colsum(cuda, M, H, F, two):
         assert o2 is None
     # K = 64 columns of X: not the fused kernel's shape
     assert MF._wgrad_colsum(t(X[:, :64], cuda), t(dh, cuda), outer, t(T, cuda)) is None
+
+
+@pytest.mark.parametrize("M,F", [(1_000_000, 64), (50015, 64), (4096, 64), (50015, 32)])
+def test_gemm_head_outer_colsum_w(cuda, msha, M, F):
+    """msha_gemm_f32_head_outer_colsum_w: the score-vector gradients as (de^T X) W from the
+    rows the weight gradient streams (h = X W never read), two heads: dW and both column
+    sums elementwise within the fp32 bound of the fp64 sums over h = X W; deterministic.  Four
+    heads (F = 32) are outside the W form: the same call takes the T form over h."""
+    from msha_gnn_amd import _lib
+
+    lib = _lib.load()
+    prev = lib.msha_wgrad_kernel(3)  # the split kernel at every size (the W form's home)
+    try:
+        _colsum_w_case(cuda, M, F)
+    finally:
+        lib.msha_wgrad_kernel(prev)
+
+
+def _colsum_w_case(cuda, M, F):
+    from msha_gnn_amd import functional as MF
+
+    rng = np.random.default_rng(M + 7)
+    H, K = 128 // F, 128
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((K, H * F)) / np.sqrt(K)).astype(np.float32)
+    dh = rng.standard_normal((M, H * F)).astype(np.float32)
+    de = rng.standard_normal((M, H)).astype(np.float32)
+    de2 = rng.standard_normal((M, H)).astype(np.float32)
+    a = rng.standard_normal((H, F)).astype(np.float32)
+    a2 = rng.standard_normal((H, F)).astype(np.float32)
+    outer = (H, F, t(de, cuda), t(a, cuda), t(de2, cuda), t(a2, cuda))
+    Xt, Wt = t(X, cuda), t(W, cuda)
+    h = Xt @ Wt  # the forward's h (the W form never reads it)
+    runs = [MF._wgrad_colsum(Xt, t(dh, cuda), outer, h, Wt) for _ in range(2)]
+    for x, y in zip(runs[0], runs[1]):
+        assert torch.equal(x, y)
+    dW, o1, o2 = (r.cpu().numpy() for r in runs[0])
+    tot = dh.astype(np.float64) + np.repeat(de, F, 1) * a.reshape(-1) + np.repeat(de2, F, 1) * a2.reshape(-1)
+    _wgrad_bound(dW, X, tot, "dW")
+    X64, W64 = X.astype(np.float64), W.astype(np.float64)
+    h64 = (X64 @ W64).reshape(M, H, F)
+    for e, o, nm in ((de, o1, "dal"), (de2, o2, "dar")):
+        ref = np.einsum("mh,mhf->hf", e.astype(np.float64), h64)
+        # |terms|: sum_r |e| sum_a |X| |W| (the rearranged sum's own magnitudes)
+        A = np.einsum("mh,mhf->hf", np.abs(e).astype(np.float64),
+                      (np.abs(X64) @ np.abs(W64)).reshape(M, H, F))
+        bounded_close(o.reshape(H, F), ref, A, M + 2 * K, 0.0, nm)
