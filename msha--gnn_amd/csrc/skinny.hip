@@ -1955,9 +1955,10 @@ __global__ void __launch_bounds__(256) wgrad_gw_kernel(const float* __restrict__
       const float* r = src + (int64_t)(32 * wv + k) * nb;
       float s = 0.f;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < 4; ++c) {  // unconditional loads (clamped), masked adds
         const int b = lane + 64 * c;
-        s += b < nb ? r[b] : 0.f;
+        const float x = r[b < nb ? b : nb - 1];
+        s += b < nb ? x : 0.f;
       }
       v[k] = s;
     }

@@ -49,9 +49,11 @@ STAT_C = 4.0  # standard deviations of the rounding-error random walk allowed
 
 BF16_U = 2.0 ** -8  # bf16 unit roundoff with one extra bit of slack (stored bf16 values)
 BF16_STORE = 2.0 ** -9  # one round-to-nearest bf16 storage rounding, relative
+# an fp32 value carried as hi + mid bf16 terms (RNE each): |x - hi - mid| <= 2^-18 |x|
+BF16_SPLIT2 = 2.0 ** -18
 
 
-def bounded_close(got, ref, absterms, nterms, rtol, name="", u=U32, store_u=0.0):
+def bounded_close(got, ref, absterms, nterms, rtol, name="", u=U32, store_u=0.0, split_u=0.0):
     """Sums against an fp64 reference, EVERY element (no fraction clause):
 
         |got - ref| <= rtol |ref| + store_u |ref| + 4 sqrt(n) u A
@@ -65,7 +67,9 @@ def bounded_close(got, ref, absterms, nterms, rtol, name="", u=U32, store_u=0.0)
     element is held to its own terms, never to the tensor's largest.  ``u``: the unit
     roundoff of the accumulation (fp32 2^-24, also on the bf16 paths: their operands are
     exact bf16 values, fed to the reference as such, and they accumulate in fp32);
-    ``store_u``: the result's own storage rounding (a bf16 output: 2^-9, BF16_STORE).
+    ``store_u``: the result's own storage rounding (a bf16 output: 2^-9, BF16_STORE);
+    ``split_u``: a deterministic per-term operand error, bound + split_u A (an fp32 operand
+    carried as two bf16 terms on the matrix cores: 2^-18, BF16_SPLIT2).
     Returns (max err / bound, fraction within rtol |ref| alone) for reporting."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
@@ -75,7 +79,7 @@ def bounded_close(got, ref, absterms, nterms, rtol, name="", u=U32, store_u=0.0)
         n = n.reshape((-1,) + (1,) * (ref.ndim - 1))
     n = np.broadcast_to(n, ref.shape)
     err = np.abs(got - ref)
-    bound = (rtol + store_u) * np.abs(ref) + STAT_C * np.sqrt(n) * u * A + 1e-300
+    bound = (rtol + store_u) * np.abs(ref) + (STAT_C * np.sqrt(n) * u + split_u) * A + 1e-300
     worst = float((err / bound).max()) if err.size else 0.0
     assert np.all(err <= bound), (
         f"{name}: {int((err > bound).sum())} of {err.size} elements beyond "
