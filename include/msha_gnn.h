@@ -115,6 +115,10 @@ MSHA_API int msha_debug_timeline(void* buf, int64_t slots);
  * marks into buf (>= 2048 x 64 uint64, device memory; NULL removes it).  Same build
  * condition as msha_debug_timeline. */
 MSHA_API int msha_debug_head_timeline(void* buf);
+/* Diagnostic: the MFMA bipartite kernels (edge_bip3.hip) stamp per-wave marks into buf
+ * (slots x 64 uint64 words, device memory: forward waves in the first half of the slots,
+ * backward waves in the second; NULL removes it).  Same build condition. */
+MSHA_API int msha_debug_bip_timeline(void* buf, int64_t slots);
 
 /* ---------------------------------------------------------------- dropout --- */
 /* Dropout under HIP-graph replay.  Every dropout draw of the library is Philox4x32-10

@@ -102,6 +102,7 @@ SIGNATURES = {
     "msha_last_error": (C.c_char_p, []),
     "msha_debug_timeline": (C.c_int, [P, I64]),
     "msha_debug_head_timeline": (C.c_int, [P]),
+    "msha_debug_bip_timeline": (C.c_int, [P, I64]),
     "msha_dropout_keep_mask": (C.c_int, [U64, U64, I64, F32, P, P]),
     "msha_inter_adjacency": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
     "msha_normalize_adjacency": (C.c_int, [P, I64, I64, P, P, P]),

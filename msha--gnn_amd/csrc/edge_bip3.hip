@@ -41,6 +41,52 @@ int bip_reduce(const float* part, int32_t nb, int32_t stride, int32_t n, int32_t
 
 namespace bip3 {
 
+// ---- per-wave timeline (diagnostic build, -DSK_TIMELINE; scripts/bip_timeline.py) ------
+// Lane 0 of every wave stamps (wall clock at 100 MHz, shader clock) pairs at fixed mark
+// indices into its slot of the buffer msha_debug_bip_timeline installs: the forward's
+// waves use the first half of the slots, the backward's the second; words 0 / 1 = XCC id
+// << 32 | HW_ID and the kernel tag, mark k at words 2 + 2k.  In the shipped build every
+// mark compiles to nothing.
+constexpr int kTlStride = 64;  // 64-bit words per wave slot
+#ifdef SK_TIMELINE
+__device__ uint64_t* g_tl = nullptr;
+__device__ int64_t g_tl_slots = 0;
+struct Tl {
+  uint64_t* p;
+};
+__device__ __forceinline__ Tl tl_open(int bwd, int tag) {
+  const int64_t half = g_tl_slots / 2;
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  Tl r{nullptr};
+  if (g_tl != nullptr && w < half) r.p = g_tl + (bwd * half + w) * kTlStride;
+  if (r.p != nullptr && (threadIdx.x & 63) == 0) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    r.p[0] = ((uint64_t)xcc << 32) | hw;
+    r.p[1] = (uint64_t)tag;
+  }
+  return r;
+}
+__device__ __forceinline__ void tl_mark(const Tl& r, int k) {
+  if (r.p != nullptr && (threadIdx.x & 63) == 0 && 2 * k + 3 < kTlStride) {
+    r.p[2 + 2 * k] = __builtin_amdgcn_s_memrealtime();
+    r.p[3 + 2 * k] = __builtin_amdgcn_s_memtime();
+  }
+}
+#define B3TL_OPEN(bwd, tag) const ::msha::bip3::Tl tl_ = ::msha::bip3::tl_open(bwd, tag)
+#define B3TL_MARK(k) ::msha::bip3::tl_mark(tl_, (k))
+#else
+#define B3TL_OPEN(bwd, tag) \
+  do {                      \
+  } while (0)
+#define B3TL_MARK(k) \
+  do {               \
+  } while (0)
+#endif
+// marks: 0 entry, 1 tables staged, per tile it < kTlTiles kTlPer marks from 2 + kTlPer it,
+// then loop end and exit
+constexpr int kTlTiles = 4;
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -235,6 +281,10 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = wv & 1;
   const int t = lane & 31, c = lane >> 5;
+  // forward marks per tile: start, softmax done, attention images written, u out, v issued
+  constexpr int kTlPer = 5;
+  B3TL_OPEN(0, (int)sizeof(T) + 16 * HS + 32 * ATTD + 64 * DROP);
+  B3TL_MARK(0);
 
   // B fragments of hc: item (h, n, s) x lane (f, c) holds hc[col(s, 8c + j)][h 64 + 32 n + f]
   for (int it = tid; it < 8 * 64; it += kWaves * 64) {
@@ -252,6 +302,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
   }
   if (tid < 64) ert[tid] = (tid >> 1) < M ? er[tid] : 0.f;  // ert[2 j + h] = er[j][h]
   __syncthreads();
+  B3TL_MARK(1);
 
   const uint64_t doff = DROP ? dropout_offset(dp, dp.offset) : 0;
   const int64_t Pt = (int64_t)gridDim.x * kPairs, pw = (int64_t)blockIdx.x * kPairs + (wv >> 1);
@@ -336,6 +387,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       // (a compiler barrier: the loop-invariant LDS reads of er and of hc's fragments stay
       // inside the loop instead of being hoisted into registers for the whole range)
       asm volatile("" ::: "memory");
+      const int it = (r0 - rb) / kTile;
+      const bool tlm = it < kTlTiles;
+      if (tlm) B3TL_MARK(2 + kTlPer * it);
       const In cu = nx;
       load_a(r0 + kTile, nx);
 
@@ -409,6 +463,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
                                                   0, 0);
         }
       }
+      if (tlm) B3TL_MARK(3 + kTlPer * it);
 
       // ---- att as the A operand (rows on the lanes) and the att^T image
       bf16x8 A[2][NA];  // [s][term]
@@ -432,6 +487,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
             *reinterpret_cast<bf16x4*>(img + img_off(q, t, c + 2 * m)) = v4;
           }
       }
+      if (tlm) B3TL_MARK(4 + kTlPer * it);
 
       // ---- u = att hc: C[row][feature], lane = feature, 16 rows per lane
 #pragma unroll
@@ -463,6 +519,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
         }
       }
       if (BIP3_UST) flush_rows<T>(ust[BIP3_UST ? wv : 0], r_u, r0, h, lane);
+      if (tlm) B3TL_MARK(5 + kTlPer * it);
 
       // ---- v += att^T hs: A = att^T (transposed image reads), B = hs rows along k
       if (HS) {
@@ -510,7 +567,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
           }
           vacc[n] = prod<NA, NT>(At, B, vacc[n]);
         }
-      }    };
+      }
+      if (tlm) B3TL_MARK(6 + kTlPer * it);
+    };
     if (kPf > 1) {
       for (int32_t r0 = rb; r0 < re; r0 += 2 * kTile) {
         tile(r0, ringA);
@@ -520,6 +579,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       for (int32_t r0 = rb; r0 < re; r0 += kTile) tile(r0, ringA);
     }
   }
+  B3TL_MARK(2 + kTlPer * kTlTiles);
   if (HS) {
     // block sum of the waves' v (fixed order): waves 4-7 park theirs in R[w - 4], waves
     // 0-3 add theirs (same head: w and w + 4), then head h = R[h] + R[h + 2]
@@ -550,6 +610,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       dst[i] = red[hh * 32 * kF + j * kF + f] + red[(hh + 2) * 32 * kF + j * kF + f];
     }
   }
+  B3TL_MARK(3 + kTlPer * kTlTiles);
 }
 
 // ----------------------------------------------------------------------- backward ---
@@ -596,6 +657,11 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = blockIdx.x & 1;
   const int t = lane & 31, c = lane >> 5;
+  // backward marks per tile: start, phase A done, G issued, phase C done, d_hc issued,
+  // d_hs out
+  constexpr int kTlPer = 6;
+  B3TL_OPEN(1, 128 + (int)sizeof(T) + 16 * HS + 32 * COEF + 64 * DROP);
+  B3TL_MARK(0);
 
   // A fragments of [hc | dV] of head h: k-step x lane (j, c) holds the 8 features
   // 16 k' + 8 c .. + 7 of hc[j] (k' = k-step < 4) or dV[j] (k-step - 4)
@@ -628,6 +694,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
   }
   if (tid < 64) ert[tid] = (tid >> 1) < M ? er[tid] : 0.f;
   __syncthreads();
+  B3TL_MARK(1);
 
   const uint64_t doff = DROP ? dropout_offset(dp, dp.offset) : 0;
   const int64_t Wt = (int64_t)(gridDim.x >> 1) * kWaves, w = (int64_t)(blockIdx.x >> 1) * kWaves + wv;
@@ -713,6 +780,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
 
     for (int32_t r0 = rb; r0 < re; r0 += kTile) {
       asm volatile("" ::: "memory");
+      const int it = (r0 - rb) / kTile;
+      const bool tlm = it < kTlTiles;
+      if (tlm) B3TL_MARK(2 + kTlPer * it);
       const In cu = nx;
       load_a(r0 + kTile, nx);
       const bool virt = cu.fl != 0;
@@ -755,6 +825,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       auto attd_of = [&](int r) -> float {
         return DROP ? (((keep >> r) & 1u) ? a[r] * dp.scale : 0.f) : a[r];
       };
+      if (tlm) B3TL_MARK(3 + kTlPer * it);
 
       // ---- G^T = [hc | dV] [dU | hs]^T: lane (t, c), register r = g of column col(c, r);
       // the dU pieces stay in the staging image [row][feature] for d_hc
@@ -779,6 +850,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         for (int q = 0; q < NT; ++q) Af[q] = afr[(ks * NT + q) * 64 + lane];
         G = prod<NT, NT>(Af, B, G);
       }
+      if (tlm) B3TL_MARK(4 + kTlPer * it);
 
       // ---- phase C: D, ds, de, d_el, d_er
       float dsum = 0.f;
@@ -820,6 +892,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       // once at the end
 #pragma unroll
       for (int r = 0; r < 16; ++r) derv[r] += de[r];
+      if (tlm) B3TL_MARK(5 + kTlPer * it);
 
       // ---- attd: A operand of d_hs, and the attd^T image for d_hc
       bf16x8 A[2][NA];
@@ -872,6 +945,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
           hacc[n] = prod<NA, NT>(At, B, hacc[n]);
         }
       }
+      if (tlm) B3TL_MARK(6 + kTlPer * it);
 
       // ---- d_hs = attd dV (C[row][feature]), out through the staging image
       if (HS) {
@@ -896,8 +970,10 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
           for (int ks = 4; ks < KS; ++ks) load_piece(ks, r0 + kTile, ring[ks]);
         }
       }
+      if (tlm) B3TL_MARK(7 + kTlPer * it);
     }
   }
+  B3TL_MARK(2 + kTlPer * kTlTiles);
   // block partial [d_hc (M x 128)][d_er (M x 2)] of head h (the other head's slices 0):
   // waves w and w + 4 first, then R0 + R1 + R2 + R3; d_er over the waves in order
   static_assert(kWaves == 8, "the reduce below pairs waves w and w + 4");
@@ -951,6 +1027,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
     }
     dst[MD + i] = a;
   }
+  B3TL_MARK(3 + kTlPer * kTlTiles);
 }
 
 }  // namespace bip3
@@ -1047,3 +1124,22 @@ int bip3_bwd(const msha_graph* g, int dtype, const float* el, const float* er, c
 }
 
 }  // namespace msha
+
+// Diagnostic: install (buf != NULL: slots x 64 uint64 words, device memory; the forward's
+// waves take slots [0, slots / 2), the backward's the rest) or remove the per-wave timeline
+// of the MFMA bipartite kernels; MSHA_ERR_UNSUPPORTED unless the library was built with
+// -DSK_TIMELINE (build.py --variant timeline).
+extern "C" int msha_debug_bip_timeline(void* buf, int64_t slots) {
+#ifdef SK_TIMELINE
+  uint64_t* p = (uint64_t*)buf;
+  const int64_t n = buf != nullptr ? slots : 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::bip3::g_tl), &p, sizeof(p)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(msha::bip3::g_tl_slots), &n, sizeof(n)) != hipSuccess)
+    return msha::fail(MSHA_ERR_HIP, "debug_bip_timeline: hipMemcpyToSymbol failed");
+  return MSHA_OK;
+#else
+  (void)buf;
+  (void)slots;
+  return msha::fail(MSHA_ERR_UNSUPPORTED, "debug_bip_timeline: library built without SK_TIMELINE");
+#endif
+}
