@@ -175,6 +175,15 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
 #ifndef BIP3_PAD
 #define BIP3_PAD 1
 #endif
+#ifndef BIP3_PRIO
+#define BIP3_PRIO 0  // 1: waves 4-7 (the second wave of each SIMD) at s_setprio 1 (A/B knob)
+#endif
+#ifndef BIP3_APF
+#define BIP3_APF 1  // tiles ahead the per-row inputs (mask, el, lse, flag, rowptr) are loaded
+#endif
+#ifndef BIP3_CLATE
+#define BIP3_CLATE 0  // backward: the softmax backward after d_hc / d_hs (A/B knob)
+#endif
 #ifndef BIP3_HSLATE
 #define BIP3_HSLATE 0  // 1 (hs pieces issued after d_hs) failed the 120k-row d_hs check with the padded staging; not understood, off
 #endif
@@ -316,6 +325,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) vacc[n][i] = 0.f;
 
+  if (BIP3_PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
     const rsrc_t r_rp = make_rsrc((ATTD || DROP) ? rowptr : nullptr, (uint32_t)(re + 1) * 4u);
@@ -380,8 +390,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       load_ring(rb, ringA);
       if (kPf > 1) load_ring(rb + kTile, ringB);
     }
-    In nx;
+    In nx, nx2;
     load_a(rb, nx);
+    if (BIP3_APF > 1) load_a(rb + kTile, nx2);
 
     auto tile = [&](int32_t r0, Ring& ring) {
       // (a compiler barrier: the loop-invariant LDS reads of er and of hc's fragments stay
@@ -391,7 +402,12 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       const bool tlm = it < kTlTiles;
       if (tlm) B3TL_MARK(2 + kTlPer * it);
       const In cu = nx;
-      load_a(r0 + kTile, nx);
+      if (BIP3_APF > 1) {
+        nx = nx2;
+        load_a(r0 + 2 * kTile, nx2);
+      } else {
+        load_a(r0 + kTile, nx);
+      }
 
       // ---- phase A: softmax of (row t, head h) over the lane's 16 columns
       const bool virt = cu.fl != 0;
@@ -711,6 +727,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) derv[r] = 0.f;
 
+  if (BIP3_PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
     const rsrc_t r_rp = make_rsrc(DROP ? rowptr : nullptr, (uint32_t)(re + 1) * 4u);
@@ -775,8 +792,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
     Piece ring[KS];
 #pragma unroll
     for (int k = 0; k < KS; ++k) load_piece(k, rb, ring[k]);
-    In nx;
+    In nx, nx2;
     load_a(rb, nx);
+    if (BIP3_APF > 1) load_a(rb + kTile, nx2);
 
     for (int32_t r0 = rb; r0 < re; r0 += kTile) {
       asm volatile("" ::: "memory");
@@ -784,7 +802,12 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       const bool tlm = it < kTlTiles;
       if (tlm) B3TL_MARK(2 + kTlPer * it);
       const In cu = nx;
-      load_a(r0 + kTile, nx);
+      if (BIP3_APF > 1) {
+        nx = nx2;
+        load_a(r0 + 2 * kTile, nx2);
+      } else {
+        load_a(r0 + kTile, nx);
+      }
       const bool virt = cu.fl != 0;
 
       // ---- phase A: att (pre-dropout) on the mask, the keep bits of the lane's columns
@@ -852,7 +875,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       }
       if (tlm) B3TL_MARK(4 + kTlPer * it);
 
-      // ---- phase C: D, ds, de, d_el, d_er
+      // ---- phase C: D, ds, de, d_el, d_er (BIP3_CLATE: after d_hc / d_hs, which need only
+      // attd, so G's MFMAs complete under them instead of in front of the softmax backward)
+      auto phase_c = [&]() {
       float dsum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -892,6 +917,8 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       // once at the end
 #pragma unroll
       for (int r = 0; r < 16; ++r) derv[r] += de[r];
+      };
+      if (!BIP3_CLATE) phase_c();
       if (tlm) B3TL_MARK(5 + kTlPer * it);
 
       // ---- attd: A operand of d_hs, and the attd^T image for d_hc
@@ -970,6 +997,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
           for (int ks = 4; ks < KS; ++ks) load_piece(ks, r0 + kTile, ring[ks]);
         }
       }
+      if (BIP3_CLATE) phase_c();
       if (tlm) B3TL_MARK(7 + kTlPer * it);
     }
   }
