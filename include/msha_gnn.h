@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 15
+#define MSHA_ABI_VERSION 16
 
 #if defined(__GNUC__) || defined(__clang__)
 #define MSHA_API __attribute__((visibility("default")))
@@ -675,6 +675,16 @@ MSHA_API int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int3
                            uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
                            const void* dout, void* du, void* dv, float* dW, float* dzero,
                            int64_t n_zero, void* ws, size_t ws_bytes, msha_stream_t stream);
+/* (ABI 16) msha_head_bwd with dout's row flags already computed by its producer
+ * (msha_nll_rows_bwd_flags: rflag[i] = row i of dout has a nonzero, wmask[w] bit k = rflag[64w
+ * + k]): the backward's own row scan is skipped.  Same outputs, bit for bit. */
+MSHA_API int msha_head_bwd_flagged(const msha_graph* g, const msha_head_params* hp,
+                                   int32_t dtype, const void* u, const void* v, const float* W,
+                                   float p_x, uint64_t seed_x, float p_att, uint64_t seed_att,
+                                   const float* stats, const void* dout, const uint8_t* rflag,
+                                   const uint64_t* wmask, void* du, void* dv, float* dW,
+                                   float* dzero, int64_t n_zero, void* ws, size_t ws_bytes,
+                                   msha_stream_t stream);
 
 
 /* ---- Training loss on gathered rows (train.py:227-229): F.nll_loss(logp[rows], cols),
@@ -692,6 +702,19 @@ MSHA_API int msha_nll_rows_fwd(int64_t N, int64_t M, int64_t B, const int64_t* r
 MSHA_API int msha_nll_rows_bwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
                                const int64_t* cols, const float* gloss, int32_t dtype,
                                void* dlogp, int64_t ld, msha_stream_t stream);
+/* (ABI 16) the backward that also flags dlogp's nonzero rows for the model head's backward
+ * (msha_head_bwd_flagged): rflag (N bytes), wmask (ceil(N / 64) words), both or neither. */
+/* (ABI 16) on = 1: the block-partial reduce of the next msha_bip_attention_fwd / _bwd on this
+ * host thread is handed to the next msha_ours_intra_fwd / stage 1 of msha_ours_intra_bwd on
+ * the same stream, which runs it as extra blocks of its own launch (one graph node fewer each
+ * way).  on = 0: separate launches again; a reduce still pending is launched now.  The
+ * outputs (v; d_hc, d_er) are complete once the taking launch (or the on = 0 call) is
+ * enqueued. */
+MSHA_API int msha_bip_defer_reduce(int32_t on);
+MSHA_API int msha_nll_rows_bwd_flags(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                                     const int64_t* cols, const float* gloss, int32_t dtype,
+                                     void* dlogp, int64_t ld, uint8_t* rflag, uint64_t* wmask,
+                                     msha_stream_t stream);
 
 /* ---- Batched segment copies: the models' per-head parameter packing (Ablation.py:262-267,
  * Ours.py:58-75 read W1/W2/a/a3/a4 of every head; one launch stacks them, one scatters

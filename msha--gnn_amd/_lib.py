@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first: the library binds t
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSHA_GNN_LIB", os.path.join(_PKG, "lib", "libmsha_gnn.so"))
 
-ABI_VERSION = 15  # MSHA_ABI_VERSION of include/msha_gnn.h
+ABI_VERSION = 16  # MSHA_ABI_VERSION of include/msha_gnn.h
 MSHA_OK, MSHA_ERR_ARG, MSHA_ERR_UNSUPPORTED, MSHA_ERR_HIP = 0, -1, -2, -3
 
 
@@ -202,6 +202,10 @@ SIGNATURES = {
     "msha_head_fwd": (C.c_int, [GP, HPP, I32, P, P, P, I32, F32, U64, F32, U64, P, P, P, SZ, P]),
     "msha_head_bwd": (C.c_int, [GP, HPP, I32, P, P, P, F32, U64, F32, U64, P, P, P, P, P, P, I64,
                                 P, SZ, P]),
+    "msha_bip_defer_reduce": (C.c_int, [I32]),
+    "msha_nll_rows_bwd_flags": (C.c_int, [I64, I64, I64, P, P, P, I32, P, I64, P, P, P]),
+    "msha_head_bwd_flagged": (C.c_int, [GP, HPP, I32, P, P, P, F32, U64, F32, U64, P, P, P, P, P,
+                                        P, P, P, I64, P, SZ, P]),
 }
 
 _lib = None

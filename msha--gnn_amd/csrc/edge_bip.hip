@@ -31,6 +31,7 @@
 // u = att @ h1, v = att.T @ h2), Ours.py:84-86 (the backward's row coefficients).
 #include <atomic>
 
+#include "bip_reduce.h"
 #include "edge_geo.h"
 
 namespace msha {
@@ -825,54 +826,66 @@ __global__ void __launch_bounds__((bwd_waves<H, HT, T, HS>() * 64)) bip_bwd_kern
   }
 }
 
-// out[i] = sum_b part[b][i] in block order (i < n_t -> out_t as T, else out_f fp32).
-// A block owns 16 consecutive entries; its 64 streams (lane / 16 of each wave, wave-major)
-// sum contiguous block ranges (every load of a stream in flight at once), then the
-// stream sums add in stream order.  256 blocks at M x H x F = 4096: the whole chip reads
-// the partials (64 blocks of one 64-entry slice each ran latency-bound, 6.6 us).
+// out[i] = sum_b part[b][i] in block order: bip_reduce.h (bip_reduce_block).  256 blocks at
+// M x H x F = 4096: the whole chip reads the partials (64 blocks of one 64-entry slice each
+// ran latency-bound, 6.6 us).
 template <typename T>
-__global__ void __launch_bounds__(1024) bip_reduce_kernel(const float* __restrict__ part,
-                                                          int32_t nb, int32_t stride, int32_t n,
-                                                          int32_t n_t, T* __restrict__ out_t,
-                                                          float* __restrict__ out_f,
-                                                          int32_t seg, int32_t seg_stride,
-                                                          int32_t blk, int32_t blk_off,
-                                                          int32_t fblk, int32_t fstride) {
+__global__ void __launch_bounds__(1024) bip_reduce_kernel(BipReduce r) {
   __shared__ float red[64][17];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = lane & 15, st = wv * 4 + (lane >> 4);  // entry in the slice, stream
-  const int i = blockIdx.x * 16 + c;
-  const int per = (nb + 63) / 64;
-  const int b0 = st * per, b1 = min(nb, b0 + per);
-  float a = 0.f;
-  if (i < n)
-    for (int b = b0; b < b1; ++b) a += part[(int64_t)b * stride + i];
-  red[st][c] = a;
-  __syncthreads();
-  if (threadIdx.x < 16 && i < n) {
-    float sum = red[0][c];
-#pragma unroll 8
-    for (int q = 1; q < 64; ++q) sum += red[q][c];
-    // (a head-split launch's partials are [head blk][column seg]: entry i lands at column
-    // (i % blk) / seg, head i / blk of the HT-head table)
-    if (i < n_t)
-      out_t[((i % blk) / seg) * seg_stride + (i / blk) * blk_off + i % seg] = from_f32<T>(sum);
-    else out_f[((i - n_t) % fblk) * fstride + (i - n_t) / fblk] = sum;
-  }
+  bip_reduce_block<T, 1024>(r, blockIdx.x, red);
 }
 
 }  // namespace bip
 
+// ---- the reduce launch, or its hand-over to the next Ours-layer launch (bip_reduce.h) ----
+namespace {
+thread_local int t_defer = 0;         // msha_bip_defer_reduce
+thread_local bool t_has = false;      // a reduce is pending
+thread_local BipReduce t_pending;
+thread_local hipStream_t t_pending_s = nullptr;
+}  // namespace
+
+static void bip_reduce_launch(const BipReduce& r, hipStream_t s) {
+  if (r.bf16)
+    hipLaunchKernelGGL(bip::bip_reduce_kernel<bf16_t>, dim3(r.blocks()), dim3(1024), 0, s, r);
+  else
+    hipLaunchKernelGGL(bip::bip_reduce_kernel<float>, dim3(r.blocks()), dim3(1024), 0, s, r);
+}
+
+void bip_reduce_run(const BipReduce& r, hipStream_t s) { bip_reduce_launch(r, s); }
+
+bool bip_reduce_submit(const BipReduce& r, hipStream_t s) {
+  if (t_has) {  // (one at a time: an earlier one not taken runs now)
+    bip_reduce_launch(t_pending, t_pending_s);
+    t_has = false;
+  }
+  if (!t_defer) {
+    bip_reduce_launch(r, s);
+    return false;
+  }
+  t_pending = r;
+  t_pending_s = s;
+  t_has = true;
+  return true;
+}
+
+bool bip_reduce_take(BipReduce& r, hipStream_t s) {
+  if (!t_has) return false;
+  if (t_pending_s != s) {  // another stream: not fused, run it where it was submitted
+    bip_reduce_launch(t_pending, t_pending_s);
+    t_has = false;
+    return false;
+  }
+  r = t_pending;
+  t_has = false;
+  return true;
+}
+
 // (edge_bip2.hip) block partials -> v or d_hc + d_er, un-split layout
 int bip_reduce(const float* part, int32_t nb, int32_t stride, int32_t n, int32_t n_t, void* out_t,
                bool bf16, float* out_f, int32_t fblk, hipStream_t s) {
-  const dim3 grid((n + 15) / 16), block(1024);
-  if (bf16)
-    hipLaunchKernelGGL(bip::bip_reduce_kernel<bf16_t>, grid, block, 0, s, part, nb, stride, n, n_t,
-                       (bf16_t*)out_t, out_f, n_t, 0, n_t, 0, fblk, 1);
-  else
-    hipLaunchKernelGGL(bip::bip_reduce_kernel<float>, grid, block, 0, s, part, nb, stride, n, n_t,
-                       (float*)out_t, out_f, n_t, 0, n_t, 0, fblk, 1);
+  BipReduce r{part, out_t, out_f, nb, stride, n, n_t, n_t, 0, n_t, 0, fblk, 1, bf16 ? 1 : 0};
+  bip_reduce_submit(r, s);
   return 1;
 }
 bool bip2_ok(const msha_graph* g, int heads, int feat, float slope);
@@ -980,9 +993,9 @@ static void bip_launch_fwd(const msha_graph* g, const float* el, const float* er
     else go(bip::bip_fwd_kernel<H, F, T, true, false>, g1, w1);
     const int32_t MD = (int32_t)(g->n_cols * H * F), MDh = (int32_t)(g->n_cols * F);
     // partials [block][head][column][F] (split) or [block][column][H F]
-    hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + 15) / 16), dim3(1024), 0, s, part,
-                       nb, MD, MD, MD, (T*)v, (float*)nullptr, split ? F : MD,
-                       split ? H * F : 0, split ? MDh : MD, split ? F : 0, 1, 1);
+    const BipReduce r{part, v, nullptr, nb, MD, MD, MD, split ? F : MD, split ? H * F : 0,
+                      split ? MDh : MD, split ? F : 0, 1, 1, sizeof(T) == 2 ? 1 : 0};
+    bip_reduce_submit(r, s);
   } else if (split) {
     if constexpr (kSplit) {
       if (attd != nullptr) go(bip::bip_fwd_kernel<1, F, T, false, true, H>, gs, ws);
@@ -1028,10 +1041,10 @@ static void bip_launch_bwd(const msha_graph* g, const float* el, const float* er
   const int32_t MD = (int32_t)(g->n_cols * H * F), MH = (int32_t)(g->n_cols * H);
   const int32_t MDh = (int32_t)(g->n_cols * F), M = (int32_t)g->n_cols;
   // partials [block][d_hc (split: [head][column][F])][d_er (split: [head][column])]
-  hipLaunchKernelGGL(bip::bip_reduce_kernel<T>, dim3((MD + MH + 15) / 16), dim3(1024), 0, s, part,
-                     nb, bip::part_stride(MD + MH), MD + MH, MD, (T*)d_hc, d_er,
-                     split ? F : MD, split ? H * F : 0, split ? MDh : MD, split ? F : 0,
-                     split ? M : MH, split ? H : 1);
+  const BipReduce r{part, d_hc, d_er, nb, bip::part_stride(MD + MH), MD + MH, MD,
+                    split ? F : MD, split ? H * F : 0, split ? MDh : MD, split ? F : 0,
+                    split ? M : MH, split ? H : 1, sizeof(T) == 2 ? 1 : 0};
+  bip_reduce_submit(r, s);
 }
 
 extern "C" int msha_bip_attention_fwd(const msha_graph* g, int32_t heads, int32_t feat,
@@ -1085,6 +1098,20 @@ static std::atomic<int64_t>& bip2_bwd_cut() {
     return v != nullptr && *v ? (int64_t)atoll(v) : (int64_t)131072;
   }()};
   return cut;
+}
+
+// (ABI 16) 1: the block-partial reduce of the next bipartite forward / backward is handed to
+// the next Ours-layer launch on the same stream (msha_ours_intra_fwd / stage 1 of
+// msha_ours_intra_bwd run it as extra blocks: one graph node fewer each way); 0: back to
+// separate launches, and a reduce still pending is launched now
+extern "C" int msha_bip_defer_reduce(int32_t on) {
+  t_defer = on != 0;
+  if (!t_defer && t_has) {
+    bip_reduce_launch(t_pending, t_pending_s);
+    t_has = false;
+    return check_launch("bip_defer_reduce");
+  }
+  return MSHA_OK;
 }
 
 extern "C" int64_t msha_bip2_bwd_min_rows(int64_t rows) {

@@ -101,6 +101,17 @@ constexpr float kLog2e = 1.4426950408889634f;
 #endif
 constexpr int kPf = BIP3_PF;  // forward: tiles of hs fragments in flight ahead (1 or 2)
 
+// Static tile split of a block's range [b0, b1) over its n parts (wave pairs forward, waves
+// backward): the first half of the parts are the first-dispatched wave of each SIMD, which
+// wins the SIMD's issue arbitration by age (bip1m timelines: the second wave's loop runs
+// 7-12 % longer on the same tiles), so it takes 1 + skew/1000 shares, the second half
+// 1 - skew/1000.  Part k starts at the cumulative weight of parts < k.
+__device__ __forceinline__ int32_t skew_split(int32_t b0, int32_t b1, int k, int n, int skew) {
+  const int64_t wo = 1000 + skew, wy = 1000 - skew, h = n / 2;
+  const int64_t cum = k <= h ? k * wo : h * wo + (k - h) * wy;
+  return b0 + (int32_t)((int64_t)(b1 - b0) * cum / (h * (wo + wy)));
+}
+
 // column of the lane's r-th attention value (half c)
 __device__ __forceinline__ constexpr int col_of(int c, int r) { return 4 * c + (r & 3) + 8 * (r >> 2); }
 
@@ -176,10 +187,19 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
 #define BIP3_PAD 1
 #endif
 #ifndef BIP3_PRIO
-#define BIP3_PRIO 0  // 1: waves 4-7 (the second wave of each SIMD) at s_setprio 1 (A/B knob)
+#define BIP3_PRIO 0  // 1: waves 4-7 (the second wave of each SIMD) at s_setprio 1; 2: turns (A/B)
 #endif
 #ifndef BIP3_APF
 #define BIP3_APF 1  // tiles ahead the per-row inputs (mask, el, lse, flag, rowptr) are loaded
+#endif
+#ifndef BIP3_SKEW_F
+#define BIP3_SKEW_F 0  // forward: per-mille extra tiles of the first-dispatched wave pairs
+#endif
+#ifndef BIP3_SKEW_B
+#define BIP3_SKEW_B 0  // backward: per-mille extra tiles of the first-dispatched waves
+#endif
+#ifndef BIP3_APF_B
+#define BIP3_APF_B BIP3_APF  // the same for the backward
 #endif
 #ifndef BIP3_CLATE
 #define BIP3_CLATE 0  // backward: the softmax backward after d_hc / d_hs (A/B knob)
@@ -316,7 +336,13 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
   const uint64_t doff = DROP ? dropout_offset(dp, dp.offset) : 0;
   const int64_t Pt = (int64_t)gridDim.x * kPairs, pw = (int64_t)blockIdx.x * kPairs + (wv >> 1);
   const int32_t n_tiles = (n_rows + kTile - 1) / kTile;
-  const int32_t tb = (int32_t)(pw * n_tiles / Pt), te = (int32_t)((pw + 1) * n_tiles / Pt);
+  int32_t tb = (int32_t)(pw * n_tiles / Pt), te = (int32_t)((pw + 1) * n_tiles / Pt);
+  if (BIP3_SKEW_F != 0) {  // the block's tiles, the first-dispatched pairs (waves 0-3) more
+    const int32_t b0 = (int32_t)((int64_t)blockIdx.x * n_tiles / gridDim.x);
+    const int32_t b1 = (int32_t)((int64_t)(blockIdx.x + 1) * n_tiles / gridDim.x);
+    tb = skew_split(b0, b1, wv >> 1, kPairs, BIP3_SKEW_F);
+    te = skew_split(b0, b1, (wv >> 1) + 1, kPairs, BIP3_SKEW_F);
+  }
   const int32_t rb = tb * kTile, re = min(n_rows, te * kTile);
 
   f32x16 vacc[2];
@@ -325,7 +351,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) vacc[n][i] = 0.f;
 
-  if (BIP3_PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
+  if (BIP3_PRIO == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
     const rsrc_t r_rp = make_rsrc((ATTD || DROP) ? rowptr : nullptr, (uint32_t)(re + 1) * 4u);
@@ -401,6 +427,12 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       const int it = (r0 - rb) / kTile;
       const bool tlm = it < kTlTiles;
       if (tlm) B3TL_MARK(2 + kTlPer * it);
+      if (BIP3_PRIO == 2) {  // the two waves of a SIMD take turns at priority, a tile each
+        if (((it + (wv >= 4 ? 1 : 0)) & 1) != 0)
+          __builtin_amdgcn_s_setprio(1);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
       const In cu = nx;
       if (BIP3_APF > 1) {
         nx = nx2;
@@ -715,7 +747,13 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
   const uint64_t doff = DROP ? dropout_offset(dp, dp.offset) : 0;
   const int64_t Wt = (int64_t)(gridDim.x >> 1) * kWaves, w = (int64_t)(blockIdx.x >> 1) * kWaves + wv;
   const int32_t n_tiles = (n_rows + kTile - 1) / kTile;
-  const int32_t tb = (int32_t)(w * n_tiles / Wt), te = (int32_t)((w + 1) * n_tiles / Wt);
+  int32_t tb = (int32_t)(w * n_tiles / Wt), te = (int32_t)((w + 1) * n_tiles / Wt);
+  if (BIP3_SKEW_B != 0) {  // the block's tiles, the first-dispatched waves 0-3 more
+    const int64_t nbh = gridDim.x >> 1, bh = blockIdx.x >> 1;
+    const int32_t b0 = (int32_t)(bh * n_tiles / nbh), b1 = (int32_t)((bh + 1) * n_tiles / nbh);
+    tb = skew_split(b0, b1, wv, kWaves, BIP3_SKEW_B);
+    te = skew_split(b0, b1, wv + 1, kWaves, BIP3_SKEW_B);
+  }
   const int32_t rb = tb * kTile, re = min(n_rows, te * kTile);
 
   f32x16 hacc[2];  // d_hc of head h: [n] C[col][feature]
@@ -727,7 +765,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) derv[r] = 0.f;
 
-  if (BIP3_PRIO && wv >= 4) __builtin_amdgcn_s_setprio(1);
+  if (BIP3_PRIO == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
     const rsrc_t r_rp = make_rsrc(DROP ? rowptr : nullptr, (uint32_t)(re + 1) * 4u);
@@ -794,15 +832,21 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
     for (int k = 0; k < KS; ++k) load_piece(k, rb, ring[k]);
     In nx, nx2;
     load_a(rb, nx);
-    if (BIP3_APF > 1) load_a(rb + kTile, nx2);
+    if (BIP3_APF_B > 1) load_a(rb + kTile, nx2);
 
     for (int32_t r0 = rb; r0 < re; r0 += kTile) {
       asm volatile("" ::: "memory");
       const int it = (r0 - rb) / kTile;
       const bool tlm = it < kTlTiles;
       if (tlm) B3TL_MARK(2 + kTlPer * it);
+      if (BIP3_PRIO == 2) {  // the two waves of a SIMD take turns at priority, a tile each
+        if (((it + (wv >= 4 ? 1 : 0)) & 1) != 0)
+          __builtin_amdgcn_s_setprio(1);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
       const In cu = nx;
-      if (BIP3_APF > 1) {
+      if (BIP3_APF_B > 1) {
         nx = nx2;
         load_a(r0 + 2 * kTile, nx2);
       } else {

@@ -1683,11 +1683,14 @@ extern "C" int msha_head_fwd(const msha_graph* g, const msha_head_params* hp, in
   return check_launch("head_fwd");
 }
 
-extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
-                             const void* u, const void* v, const float* W, float p_x,
-                             uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
-                             const void* dout, void* du, void* dv, float* dW, float* dzero,
-                             int64_t n_zero, void* ws, size_t ws_bytes, msha_stream_t stream) {
+// rflag / wmask (nullable, together): the row flags of dout already computed by its producer
+// (msha_nll_rows_bwd_flags) -- the split row pass then launches no scan of its own
+static int head_bwd_impl(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
+                         const void* u, const void* v, const float* W, float p_x,
+                         uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
+                         const void* dout, void* du, void* dv, float* dW, float* dzero,
+                         int64_t n_zero, void* ws, size_t ws_bytes, const uint8_t* rflag,
+                         const uint64_t* wmask, msha_stream_t stream) {
   if (int rc = head_check(g, hp, dtype)) return rc;
   MSHA_ARG_CHECK(u && v && W && stats && dout && du && dv && dW, "head_bwd: null pointer");
   const HeadLayout L = head_layout(g->n_rows, (int)g->n_cols, hp->heads, hp->feat);
@@ -1731,14 +1734,21 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
     const size_t lds2 = sizeof(float) * ((size_t)a.HF * a.M + (size_t)a.KX * a.M + 4 * (size_t)a.HF +
                                          32 * 192 + 4 * ((size_t)a.HF + 3 * (size_t)a.KX + 2 * (size_t)a.M));
     const dim3 gs((unsigned)((a.N + 255) / 256));
+    const bool scan = wmask == nullptr;
+    if (!scan) {
+      w.rflag = const_cast<uint8_t*>(rflag);
+      w.wmask = const_cast<uint64_t*>(wmask);
+    }
     if (bf) {
-      hipLaunchKernelGGL(head_bwd_scan_kernel<bf16_t>, gs, dim3(256), 0, s, (const bf16_t*)dout,
-                         a.N, a.M, w.rflag, w.wmask);
+      if (scan)
+        hipLaunchKernelGGL(head_bwd_scan_kernel<bf16_t>, gs, dim3(256), 0, s, (const bf16_t*)dout,
+                           a.N, a.M, w.rflag, w.wmask);
       hipLaunchKernelGGL(head_bwd_rows2_kernel<bf16_t>, dim3(g2), dim3(256), lds2, s, a,
                          (const bf16_t*)u, (const bf16_t*)dout, w, (int)nwords);
     } else {
-      hipLaunchKernelGGL(head_bwd_scan_kernel<float>, gs, dim3(256), 0, s, (const float*)dout,
-                         a.N, a.M, w.rflag, w.wmask);
+      if (scan)
+        hipLaunchKernelGGL(head_bwd_scan_kernel<float>, gs, dim3(256), 0, s, (const float*)dout,
+                           a.N, a.M, w.rflag, w.wmask);
       hipLaunchKernelGGL(head_bwd_rows2_kernel<float>, dim3(g2), dim3(256), lds2, s, a,
                          (const float*)u, (const float*)dout, w, (int)nwords);
     }
@@ -1764,6 +1774,27 @@ extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, in
     hipLaunchKernelGGL(head_bwd_apply_kernel<float>, ga, dim3(256), 0, s, a, (const float*)u,
                        (const float*)v, w, (float*)du, (float*)dv);
   return check_launch("head_bwd");
+}
+
+extern "C" int msha_head_bwd(const msha_graph* g, const msha_head_params* hp, int32_t dtype,
+                             const void* u, const void* v, const float* W, float p_x,
+                             uint64_t seed_x, float p_att, uint64_t seed_att, const float* stats,
+                             const void* dout, void* du, void* dv, float* dW, float* dzero,
+                             int64_t n_zero, void* ws, size_t ws_bytes, msha_stream_t stream) {
+  return head_bwd_impl(g, hp, dtype, u, v, W, p_x, seed_x, p_att, seed_att, stats, dout, du, dv,
+                       dW, dzero, n_zero, ws, ws_bytes, nullptr, nullptr, stream);
+}
+
+extern "C" int msha_head_bwd_flagged(const msha_graph* g, const msha_head_params* hp,
+                                     int32_t dtype, const void* u, const void* v, const float* W,
+                                     float p_x, uint64_t seed_x, float p_att, uint64_t seed_att,
+                                     const float* stats, const void* dout, const uint8_t* rflag,
+                                     const uint64_t* wmask, void* du, void* dv, float* dW,
+                                     float* dzero, int64_t n_zero, void* ws, size_t ws_bytes,
+                                     msha_stream_t stream) {
+  MSHA_ARG_CHECK(rflag != nullptr && wmask != nullptr, "head_bwd_flagged: null row flags");
+  return head_bwd_impl(g, hp, dtype, u, v, W, p_x, seed_x, p_att, seed_att, stats, dout, du, dv,
+                       dW, dzero, n_zero, ws, ws_bytes, rflag, wmask, stream);
 }
 
 // Diagnostic: install (buf != NULL: >= 256 slots x 64 uint64 words, device memory) or

@@ -41,11 +41,16 @@ __global__ void __launch_bounds__(kLossThreads) nll_rows_fwd_kernel(
   if (threadIdx.x == 0) loss[0] = B > 0 ? -part[0] / (float)B : __builtin_nanf("");
 }
 
+// With rflag / wmask (msha_nll_rows_bwd_flags) each block also flags its rows whose gradient
+// is nonzero -- one byte a row and one 64-row bit mask a word (a block's 64 rows are one
+// word) -- the row scan the model head's backward would otherwise launch over the same
+// gradient (head.hip head_bwd_scan_kernel: same test, value != 0 after the adds).
+static_assert(kLossRowsPerBlock == 64, "one wmask word per block");
 template <typename T>
 __global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
     int64_t N, int64_t M, int64_t B, const int64_t* __restrict__ rows,
     const int64_t* __restrict__ cols, const float* __restrict__ gloss, T* __restrict__ dlogp,
-    int64_t ld) {
+    int64_t ld, uint8_t* __restrict__ rflag, uint64_t* __restrict__ wmask) {
   const int64_t r0 = (int64_t)blockIdx.x * kLossRowsPerBlock;
   const int64_t r1 = min(N, r0 + kLossRowsPerBlock);
   T* base = dlogp + r0 * ld;
@@ -98,6 +103,20 @@ __global__ void __launch_bounds__(kLossThreads) nll_rows_bwd_kernel(
       }
     }
   }
+  if (wmask != nullptr) {
+    __syncthreads();  // (lane 0's adds)
+    if (threadIdx.x < 64) {
+      const int64_t i = r0 + threadIdx.x;
+      int nz = 0;
+      if (i < r1) {
+        const T* dr = dlogp + i * ld;
+        for (int j = 0; j < (int)M; ++j) nz |= to_f32(dr[j]) != 0.f;
+        rflag[i] = nz ? 1 : 0;
+      }
+      const uint64_t bits = __ballot(nz != 0);
+      if (threadIdx.x == 0) wmask[blockIdx.x] = bits;
+    }
+  }
 }
 
 }  // namespace msha
@@ -121,19 +140,28 @@ extern "C" int msha_nll_rows_fwd(int64_t N, int64_t M, int64_t B, const int64_t*
   return check_launch("nll_rows_fwd");
 }
 
-extern "C" int msha_nll_rows_bwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
-                                 const int64_t* cols, const float* gloss, int32_t dtype,
-                                 void* dlogp, int64_t ld, msha_stream_t stream) {
+extern "C" int msha_nll_rows_bwd_flags(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                                       const int64_t* cols, const float* gloss, int32_t dtype,
+                                       void* dlogp, int64_t ld, uint8_t* rflag, uint64_t* wmask,
+                                       msha_stream_t stream) {
   MSHA_ARG_CHECK(N > 0 && M > 0 && B >= 0 && ld >= M, "nll_rows_bwd: bad sizes");
   MSHA_ARG_CHECK(dlogp && gloss && (B == 0 || (rows && cols)), "nll_rows_bwd: null pointer");
   MSHA_ARG_CHECK(dtype == MSHA_DTYPE_F32 || dtype == MSHA_DTYPE_BF16, "nll_rows_bwd: bad dtype");
+  MSHA_ARG_CHECK((rflag == nullptr) == (wmask == nullptr), "nll_rows_bwd: rflag and wmask go together");
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)((N + kLossRowsPerBlock - 1) / kLossRowsPerBlock));
   if (dtype == MSHA_DTYPE_BF16)
     hipLaunchKernelGGL(nll_rows_bwd_kernel<bf16_t>, grid, dim3(kLossThreads), 0, s, N, M, B,
-                       rows, cols, gloss, (bf16_t*)dlogp, ld);
+                       rows, cols, gloss, (bf16_t*)dlogp, ld, rflag, wmask);
   else
     hipLaunchKernelGGL(nll_rows_bwd_kernel<float>, grid, dim3(kLossThreads), 0, s, N, M, B, rows,
-                       cols, gloss, (float*)dlogp, ld);
+                       cols, gloss, (float*)dlogp, ld, rflag, wmask);
   return check_launch("nll_rows_bwd");
+}
+
+extern "C" int msha_nll_rows_bwd(int64_t N, int64_t M, int64_t B, const int64_t* rows,
+                                 const int64_t* cols, const float* gloss, int32_t dtype,
+                                 void* dlogp, int64_t ld, msha_stream_t stream) {
+  return msha_nll_rows_bwd_flags(N, M, B, rows, cols, gloss, dtype, dlogp, ld, nullptr, nullptr,
+                                 stream);
 }

@@ -21,6 +21,7 @@
 #include <atomic>
 #include <cstdlib>
 
+#include "bip_reduce.h"
 #include "common.h"
 
 namespace msha {
@@ -82,11 +83,20 @@ __device__ __forceinline__ void intra_keep_bits(const Dropout& d, int H, uint64_
 }
 
 // ---------------------------------------------------------------------- prep ---
+// Blocks from nprep on run the bipartite forward's block-partial reduce of v (handed over by
+// msha_bip_defer_reduce; bip_reduce.h), which needs nothing prep computes: one launch
+// instead of two.
 template <typename T>
 __global__ void __launch_bounds__(256) ours_prep_kernel(
     OursArgs a, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const uint8_t* __restrict__ rowflag, const float* __restrict__ el,
-    const float* __restrict__ er, const float* __restrict__ lse, float* __restrict__ bstat) {
+    const float* __restrict__ er, const float* __restrict__ lse, float* __restrict__ bstat,
+    BipReduce rd, int nprep) {
+  if ((int)blockIdx.x >= nprep) {
+    __shared__ float red[64][17];
+    bip_reduce_block<T, 256>(rd, (int)blockIdx.x - nprep, red);
+    return;
+  }
   const int lane = lane_id();
   const int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (b >= a.B) return;
@@ -672,11 +682,19 @@ constexpr int kFinishLds = 2048;
 constexpr int kFinishKB = 8;  // items per wave whose loads are issued together
 constexpr int kFinishBg = 4096;  // floats of bgrad staged in LDS between the mode-0 phases
 
+// Mode 1's blocks from nwork on run the bipartite backward's block-partial reduce of d_hc /
+// d_er (handed over by msha_bip_defer_reduce; bip_reduce.h; independent of d_hs): one
+// launch instead of two.
 template <typename T>
 __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
     OursArgs a, int mode, const float* __restrict__ bstat, const float* __restrict__ G,
     float* __restrict__ bgrad, float* __restrict__ row_coef, float* __restrict__ da3s,
-    float* __restrict__ da4s, T* __restrict__ d_hs) {
+    float* __restrict__ da4s, T* __restrict__ d_hs, BipReduce rd, int nwork) {
+  if ((int)blockIdx.x >= nwork) {
+    __shared__ float red[64][17];
+    bip_reduce_block<T, 1024>(rd, (int)blockIdx.x - nwork, red);
+    return;
+  }
   __shared__ int64_t s_src[kFinishLds];
   __shared__ int32_t s_next[kFinishLds];  // next batch entry with the same source, -1 = none
   __shared__ int32_t s_first[kFinishLds];  // first batch entry of its source
@@ -872,9 +890,9 @@ __global__ void __launch_bounds__(1024) ours_bwd_finish_kernel(
       }
     }
   } else {
-    // mode 1 runs on a grid: block k takes items [k, k + gridDim.x, ...) * blockDim.x
+    // mode 1 runs on a grid: block k takes items [k, k + nwork, ...) * blockDim.x
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < B * D;
-         t += (int64_t)gridDim.x * blockDim.x) {
+         t += (int64_t)nwork * blockDim.x) {
       const int64_t b = t / D;
       const int d = (int)(t % D);
       const int h = d / F;
@@ -954,9 +972,18 @@ template <typename T>
 static void launch_fwd(const OursArgs& a, const msha_graph* g, int64_t B, const float* el,
                        const float* er, const float* lse, const void* u_inter, float* bstat,
                        void* u_out, hipStream_t s) {
-  if (B > 0)
-    hipLaunchKernelGGL(ours_prep_kernel<T>, dim3(grid_for(B, 4)), dim3(256), 0, s, a, g->rowptr,
-                       g->col, g->rowflag, el, er, lse, bstat);
+  // the bipartite forward's v reduce, when it was handed over, rides along as extra blocks
+  BipReduce rd{};
+  const bool fuse = bip_reduce_take(rd, s);
+  const int nprep = B > 0 ? (int)grid_for(B, 4) : 0;
+  if (fuse && rd.bf16 != (sizeof(T) == 2 ? 1 : 0)) {  // (not this launch's table type)
+    bip_reduce_run(rd, s);
+    rd = BipReduce{};
+  }
+  const int nred = fuse && rd.part != nullptr ? rd.blocks() : 0;
+  if (nprep + nred > 0)
+    hipLaunchKernelGGL(ours_prep_kernel<T>, dim3(nprep + nred), dim3(256), 0, s, a, g->rowptr,
+                       g->col, g->rowflag, el, er, lse, bstat, rd, nprep);
   const int D = a.H * a.F;
   if (B > 0 && B <= 64 && D <= 256) {
     // the batch staged in LDS (ours_fwd_lds_kernel): a persistent grid, four blocks per CU
@@ -1036,14 +1063,22 @@ static void launch_bwd(const OursArgs& a, int stage, int64_t B, int nck, int hea
                        dim3(grid_for(2 * B * heads * feat, 256, 4096)), dim3(256), 0, s, B,
                        heads * feat, nck, (const float*)Gp, G, row_coef, a.N * heads);
     hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(1), dim3(1024), 0, s, a, 0, bstat,
-                       (const float*)G, bgrad, row_coef, da3s, da4s, (T*)nullptr);
+                       (const float*)G, bgrad, row_coef, da3s, da4s, (T*)nullptr, BipReduce{}, 1);
   } else {
     // mode 1 (d_hs of the batch rows) is independent per (b, d): one thread per item
     // on a grid (single workgroup: ~20 us, grid: 13 us at B = 64, D = 128)
-    hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(grid_for(B * heads * feat, 1024, 256)),
-                       dim3(1024), 0, s, a, 1, bstat,
+    // + the bipartite backward's d_hc / d_er reduce, when it was handed over
+    BipReduce rd{};
+    const bool fuse = bip_reduce_take(rd, s);
+    const int nwork = (int)grid_for(B * heads * feat, 1024, 256);
+    if (fuse && rd.bf16 != (sizeof(T) == 2 ? 1 : 0)) {  // (not this launch's table type)
+      bip_reduce_run(rd, s);
+      rd = BipReduce{};
+    }
+    const int nred = fuse && rd.part != nullptr ? rd.blocks() : 0;
+    hipLaunchKernelGGL(ours_bwd_finish_kernel<T>, dim3(nwork + nred), dim3(1024), 0, s, a, 1, bstat,
                        (const float*)G, bgrad, (float*)nullptr, (float*)nullptr,
-                       (float*)nullptr, (T*)d_hs);
+                       (float*)nullptr, (T*)d_hs, rd, nwork);
   }
 }
 

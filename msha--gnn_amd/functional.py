@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import functools
+import os
 import struct
 
 import torch
@@ -1092,6 +1093,12 @@ def score_pairs(h, src, dst, mode="inner", W=None, b=None, out=None, out_dtype=N
 
 
 # --------------------------------------------------------- full MSHA layer (Ours) ---
+# the bipartite kernels' block-partial reduce rides in the Ours layer's prep / finish
+# launches (msha_bip_defer_reduce; one graph node fewer each way); MSHA_BIP_DEFER=0: separate
+# reduce launches (A/B)
+BIP_DEFER_REDUCE = os.environ.get("MSHA_BIP_DEFER", "1") != "0"
+
+
 class _OursAttention(torch.autograd.Function):
     """Ours.py:54-101 core: inter attention (u, v) + batch intra attention added to u."""
 
@@ -1115,25 +1122,33 @@ class _OursAttention(torch.autograd.Function):
         lse = torch.empty(n, H, device=dev, dtype=torch.float32)
         attd = torch.empty(max(graph.n_edges, 1), H, device=dev, dtype=torch.float32)
         v = torch.empty(m, H, Fd, device=dev, dtype=dt)
-        if bip:
-            # u, v and the attention export in one pass (msha_bip_attention_fwd)
-            ws = _bip_ws(graph, H, Fd, dev)
-            _lib.call("msha_bip_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
-                      er.data_ptr(), h1.data_ptr(), h2.data_ptr(), slope, p, seed, 0,
-                      u_inter.data_ptr(), None, lse.data_ptr(), attd.data_ptr(), v.data_ptr(),
-                      ws.data_ptr(), ws.numel(), s)
-        else:
-            _lib.call("msha_edge_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
-                      er.data_ptr(), h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(),
-                      _lib.ptr(u_lo), lse.data_ptr(), attd.data_ptr(), s)
-            _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
-        ctx.bip = bip
         bstat = torch.empty(max(B, 1), H, 8, device=dev, dtype=torch.float32)
         u = torch.empty_like(u_inter)
-        _lib.call("msha_ours_intra_fwd", g, groups.desc, B, src.data_ptr(), H, Fd, _code(dt),
-                  h2.data_ptr(),
-                  a3s.data_ptr(), a4s.data_ptr(), el.data_ptr(), er.data_ptr(), lse.data_ptr(),
-                  u_inter.data_ptr(), slope, p, seed, 0, bstat.data_ptr(), u.data_ptr(), s)
+        defer = bip and BIP_DEFER_REDUCE
+        try:
+            if bip:
+                # u, v and the attention export in one pass (msha_bip_attention_fwd); its v
+                # reduce runs inside the intra launch below (msha_bip_defer_reduce)
+                ws = _bip_ws(graph, H, Fd, dev)
+                if defer:
+                    _lib.call("msha_bip_defer_reduce", 1)
+                _lib.call("msha_bip_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
+                          er.data_ptr(), h1.data_ptr(), h2.data_ptr(), slope, p, seed, 0,
+                          u_inter.data_ptr(), None, lse.data_ptr(), attd.data_ptr(),
+                          v.data_ptr(), ws.data_ptr(), ws.numel(), s)
+            else:
+                _lib.call("msha_edge_attention_fwd", g, H, Fd, _code(dt), el.data_ptr(),
+                          er.data_ptr(), h1.data_ptr(), slope, p, seed, 0, u_inter.data_ptr(),
+                          _lib.ptr(u_lo), lse.data_ptr(), attd.data_ptr(), s)
+                _csc_aggregate(graph, H, Fd, attd, None, h2, v, None, s)
+            _lib.call("msha_ours_intra_fwd", g, groups.desc, B, src.data_ptr(), H, Fd,
+                      _code(dt), h2.data_ptr(), a3s.data_ptr(), a4s.data_ptr(), el.data_ptr(),
+                      er.data_ptr(), lse.data_ptr(), u_inter.data_ptr(), slope, p, seed, 0,
+                      bstat.data_ptr(), u.data_ptr(), s)
+        finally:
+            if defer:
+                _lib.call("msha_bip_defer_reduce", 0)  # (launches it if still pending)
+        ctx.bip = bip
         ctx.graph, ctx.groups, ctx.p, ctx.seed, ctx.slope = graph, groups, p, seed, slope
         ctx.save_for_backward(el, er, h1, h2, a3s, a4s, lse, u_inter, bstat, src,
                               u_lo if u_lo is not None else el.new_empty(0))
@@ -1175,16 +1190,24 @@ class _OursAttention(torch.autograd.Function):
         d_hc = torch.empty(m, H, Fd, device=dev, dtype=dt)
         d_er = torch.empty(m, H, device=dev, dtype=torch.float32)
         if ctx.bip:
-            # row and column gradients of the inter attention in one pass
+            # row and column gradients of the inter attention in one pass; its d_hc / d_er
+            # reduce runs inside the intra stage-1 launch (msha_bip_defer_reduce)
             ws = _bip_ws(graph, H, Fd, dev)
-            _lib.call("msha_bip_attention_bwd", g, H, Fd, _code(dt), el.data_ptr(),
-                      er.data_ptr(), h1.data_ptr(), lse.data_ptr(), dU.data_ptr(),
-                      h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p,
-                      ctx.seed, 0, d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
-                      d_hs.data_ptr(), ws.data_ptr(), ws.numel(), s)
-            _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0,
-                      G.data_ptr(), bgrad.data_ptr(), None, None, None, d_hs.data_ptr(), None,
-                      0, s)
+            defer = BIP_DEFER_REDUCE
+            try:
+                if defer:
+                    _lib.call("msha_bip_defer_reduce", 1)
+                _lib.call("msha_bip_attention_bwd", g, H, Fd, _code(dt), el.data_ptr(),
+                          er.data_ptr(), h1.data_ptr(), lse.data_ptr(), dU.data_ptr(),
+                          h2.data_ptr(), dV.data_ptr(), row_coef.data_ptr(), ctx.slope, ctx.p,
+                          ctx.seed, 0, d_el.data_ptr(), d_er.data_ptr(), d_hc.data_ptr(),
+                          d_hs.data_ptr(), ws.data_ptr(), ws.numel(), s)
+                _lib.call("msha_ours_intra_bwd", *args, 1, ctx.slope, ctx.p, ctx.seed, 0,
+                          G.data_ptr(), bgrad.data_ptr(), None, None, None, d_hs.data_ptr(),
+                          None, 0, s)
+            finally:
+                if defer:
+                    _lib.call("msha_bip_defer_reduce", 0)
             return d_el, d_er, d_hc, d_hs, da3s, da4s, None, None, None, None, None, None
         rec = torch.empty(E, 2, H, device=dev, dtype=torch.float32)  # (de, attd) per edge
         de, attd = rec[:, 0], rec[:, 1]
@@ -1249,6 +1272,14 @@ def _head_params(H, F, eps, momentum, slope, ptrs, dyn=None):
         for h, v in enumerate(lst):
             arr[h] = v
     return hp
+
+
+# the loss backward flags its gradient's nonzero rows for the model head's backward
+# (msha_nll_rows_bwd_flags -> msha_head_bwd_flagged: one launch fewer per step);
+# MSHA_NLL_FLAGS=0 keeps the head's own row scan (A/B).  HEAD_BWD_FLAGGED counts the head
+# backwards that took the flags (tests).
+NLL_FLAGS = os.environ.get("MSHA_NLL_FLAGS", "1") != "0"
+HEAD_BWD_FLAGGED = [0]
 
 
 class _ModelHead(torch.autograd.Function):
@@ -1342,6 +1373,9 @@ class _ModelHead(torch.autograd.Function):
         dev = u.device
         dt = u.dtype
         dout = _tc(dout, dt)
+        flags = getattr(dout, "_msha_rowflags", None)  # from _NllRows.backward, if dout is its d
+        if flags is not None and (flags[1] != dout.shape[0] or not dout.is_contiguous()):
+            flags = None
         du = torch.empty_like(u)
         dv = torch.empty_like(v)
         dW = torch.empty_like(W32)
@@ -1361,10 +1395,20 @@ class _ModelHead(torch.autograd.Function):
             _lib.fn("msha_head_workspace_size")(g, H, F))))
         shape, adt, adev = ctx.a_meta
         da = torch.empty(shape, dtype=torch.float32, device=adev)  # zeroed by the reduce
-        _lib.call("msha_head_bwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
-                  W32.data_ptr(), px, sx, pa, sa, stats.data_ptr(), dout.data_ptr(),
-                  du.data_ptr(), dv.data_ptr(), dW.data_ptr(), da.data_ptr(), da.numel(),
-                  ws.data_ptr(), ws.numel(), _stream(u))
+        if flags is not None:
+            fl, n = flags
+            nw = (n + 63) // 64
+            HEAD_BWD_FLAGGED[0] += 1
+            _lib.call("msha_head_bwd_flagged", g, C_byref(hp), _code(dt), u.data_ptr(),
+                      v.data_ptr(), W32.data_ptr(), px, sx, pa, sa, stats.data_ptr(),
+                      dout.data_ptr(), fl.data_ptr() + 8 * nw, fl.data_ptr(), du.data_ptr(),
+                      dv.data_ptr(), dW.data_ptr(), da.data_ptr(), da.numel(), ws.data_ptr(),
+                      ws.numel(), _stream(u))
+        else:
+            _lib.call("msha_head_bwd", g, C_byref(hp), _code(dt), u.data_ptr(), v.data_ptr(),
+                      W32.data_ptr(), px, sx, pa, sa, stats.data_ptr(), dout.data_ptr(),
+                      du.data_ptr(), dv.data_ptr(), dW.data_ptr(), da.data_ptr(), da.numel(),
+                      ws.data_ptr(), ws.numel(), _stream(u))
         # gradients in the parameters' dtypes: one cast launch for every non-fp32 one
         casts = []
 
@@ -1718,8 +1762,18 @@ class _NllRows(torch.autograd.Function):
         N, M = ctx.shape
         g = _f32c(gloss.reshape(1))
         d = torch.empty(N, M, device=rows.device, dtype=ctx.dt)
-        _lib.call("msha_nll_rows_bwd", N, M, rows.numel(), rows.data_ptr(), cols.data_ptr(),
-                  g.data_ptr(), _code(ctx.dt), d.data_ptr(), M, _stream(d))
+        if NLL_FLAGS:
+            # the rows of d with a nonzero, flagged here for the model head's backward (its
+            # consumer in every model): msha_head_bwd_flagged then skips its own row scan
+            nw = (N + 63) // 64
+            fl = torch.empty(8 * nw + N, device=rows.device, dtype=torch.uint8)
+            _lib.call("msha_nll_rows_bwd_flags", N, M, rows.numel(), rows.data_ptr(),
+                      cols.data_ptr(), g.data_ptr(), _code(ctx.dt), d.data_ptr(), M,
+                      fl.data_ptr() + 8 * nw, fl.data_ptr(), _stream(d))
+            d._msha_rowflags = (fl, N)
+        else:
+            _lib.call("msha_nll_rows_bwd", N, M, rows.numel(), rows.data_ptr(), cols.data_ptr(),
+                      g.data_ptr(), _code(ctx.dt), d.data_ptr(), M, _stream(d))
         return d, None, None
 
 

@@ -47,13 +47,13 @@ def decode(raw, bwd):
     per = len(PHASES[bwd]) + 1
     nm = 2 + per * 4 + 2
     waves = []
-    for row in rows:
+    for slot, row in enumerate(rows):
         if row[1] == 0:
             continue
         m = row[2:2 + 2 * nm].reshape(nm, 2).astype(np.int64)
         hw = int(row[0]) & 0xFFFFFFFF
         waves.append(dict(tag=int(row[1]), simd=(hw >> 4) & 3, cu=(hw >> 8) & 15,
-                          rt=m[:, 0], mt=m[:, 1]))
+                          xcc=int(row[0]) >> 32, wv=slot % 8, rt=m[:, 0], mt=m[:, 1]))
     if not waves:
         return None
     t0 = min(int(w["rt"][0]) for w in waves)
@@ -82,6 +82,12 @@ def decode(raw, bwd):
     out["loop_cyc"] = pct([cyc(w, 1, lend) for w in waves])
     out["epilogue_cyc"] = pct([cyc(w, lend, lend + 1) for w in waves])
     out["wave_cyc"] = pct([cyc(w, 0, lend + 1) for w in waves])
+    # where the spread comes from: the loop by wave of the block (waves w and w + 4 share a
+    # SIMD, w + 4 dispatched second) and by XCD
+    out["loop_cyc_by_wave"] = {k: pct([cyc(w, 1, lend) for w in waves if w["wv"] == k], (50,))["p50"]
+                               for k in range(8)}
+    out["loop_cyc_by_xcc"] = {k: pct([cyc(w, 1, lend) for w in waves if w["xcc"] == k], (50,))["p50"]
+                              for k in sorted({w["xcc"] for w in waves})}
     out["window_us"] = round(max(ex), 2)
     return out
 

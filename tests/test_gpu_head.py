@@ -429,3 +429,81 @@ def test_nll_loss_rows_matches_torch(cuda, msha, dtype):
     assert torch.isfinite(c.grad.float()).all()
     e = torch.empty(0, dtype=torch.int64, device=cuda)
     assert torch.isnan(MF.nll_loss_rows(logp, e, e)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_nll_bwd_row_flags_match_scan(cuda, msha, dtype):
+    """msha_nll_rows_bwd_flags: the gradient is the plain backward's, bit for bit, and the
+    row flags are the head backward's scan of it (rflag[i] = row i has a nonzero, wmask
+    word w bit k = rflag[64 w + k]); a row whose entries cancel to zero is not flagged."""
+    from msha_gnn_amd import _lib
+
+    gen = torch.Generator(device=cuda).manual_seed(7)
+    N, M, B = 39179, 32, 64
+    rows = torch.randint(0, N, (B,), device=cuda, generator=gen)
+    cols = torch.randint(0, M, (B,), device=cuda, generator=gen)
+    rows[-1] = N - 1  # the last, partial word
+    g = torch.tensor([2.5], device=cuda)
+    code = 1 if dtype == torch.bfloat16 else 0
+    d0 = torch.empty(N, M, device=cuda, dtype=dtype)
+    d1 = torch.empty(N, M, device=cuda, dtype=dtype)
+    nw = (N + 63) // 64
+    rflag = torch.full((N,), 7, device=cuda, dtype=torch.uint8)
+    wmask = torch.zeros(nw, device=cuda, dtype=torch.int64)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("msha_nll_rows_bwd", N, M, B, rows.data_ptr(), cols.data_ptr(), g.data_ptr(), code,
+              d0.data_ptr(), M, s)
+    _lib.call("msha_nll_rows_bwd_flags", N, M, B, rows.data_ptr(), cols.data_ptr(), g.data_ptr(),
+              code, d1.data_ptr(), M, rflag.data_ptr(), wmask.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(d0, d1)
+    want = (d1.float() != 0).any(1)
+    assert torch.equal(rflag.bool(), want)
+    bits = want.cpu().numpy()
+    words = np.zeros(nw, np.uint64)
+    for i in np.nonzero(bits)[0]:
+        words[i // 64] |= np.uint64(1) << np.uint64(i % 64)
+    assert np.array_equal(wmask.cpu().numpy().view(np.uint64), words)
+    # gloss 0: every row zero, nothing flagged
+    z = torch.zeros(1, device=cuda)
+    _lib.call("msha_nll_rows_bwd_flags", N, M, B, rows.data_ptr(), cols.data_ptr(), z.data_ptr(),
+              code, d1.data_ptr(), M, rflag.data_ptr(), wmask.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert int(rflag.sum()) == 0 and int(wmask.abs().sum()) == 0
+
+
+def test_head_bwd_takes_the_loss_row_flags(cuda, msha):
+    """loss = nll_loss_rows(model head): the head backward takes the loss backward's row flags
+    (msha_head_bwd_flagged, no scan launch) and every gradient equals the scanning path's
+    bit for bit (MSHA_NLL_FLAGS=0 form)."""
+    from msha_gnn_amd import functional as MF
+
+    n, m, H, F_ = 3000, 32, 2, 64
+    g, _ = _graph(n, m, 11, cuda)
+    gen = torch.Generator().manual_seed(12)
+    u0 = torch.randn(n, H, F_, generator=gen).to(cuda)
+    v0 = torch.randn(m, H, F_, generator=gen).to(cuda)
+    W0 = (torch.randn(H * m, m, generator=gen) * (H * m) ** -0.5).to(cuda)
+    rows = torch.randint(0, n, (64,), generator=gen).to(cuda)
+    cols = torch.randint(0, m, (64,), generator=gen).to(cuda)
+    res = []
+    for flags in (True, False):
+        MF.NLL_FLAGS = flags
+        try:
+            bns = _bns(H, F_, cuda, 13)
+            a = torch.zeros(2 * m, 1, device=cuda, requires_grad=True)
+            u, v, W = (t.clone().requires_grad_(True) for t in (u0, v0, W0))
+            params = ([b[0].weight for b in bns] + [b[0].bias for b in bns]
+                      + [b[1].weight for b in bns] + [b[1].bias for b in bns] + [a])
+            out = MF._ModelHead.apply(u, v, W, g, bns, True, 1e-5, 0.1, 0.2, 0.3, 21, 0.3, 22,
+                                      *params)
+            before = MF.HEAD_BWD_FLAGGED[0]
+            MF.nll_loss_rows(out, rows, cols).backward()
+            took = MF.HEAD_BWD_FLAGGED[0] - before
+            res.append((took, [t.grad.clone() for t in (u, v, W)] +
+                        [p.grad.clone() for p in params[:-1]]))
+        finally:
+            MF.NLL_FLAGS = True
+    assert res[0][0] == 1 and res[1][0] == 0
+    for x, y in zip(res[0][1], res[1][1]):
+        assert torch.equal(x, y)

@@ -272,3 +272,44 @@ def test_ours_packed_intra_draws_bitwise(cuda, msha, n):
         lib.msha_ours_pack_draws(1)
     assert torch.equal(outs[0], outs[1])
     assert (outs[0] != 0).any()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("n", [3000, 140_000])
+def test_ours_deferred_reduce_bitwise(cuda, msha, n, dtype):
+    """The bipartite forward's v reduce and backward's d_hc / d_er reduce run as extra blocks
+    of the intra prep / stage-1 finish launches (msha_bip_defer_reduce): u, v and every
+    gradient equal the separate-launch form's bits.  n = 140k takes the MFMA / mask kernels
+    (>= 131,072 rows), n = 3000 the CSR walk; with dropout and the Ours row coefficients."""
+    from msha_gnn_amd import functional as MF
+    from msha_gnn_amd.graph import Graph, Groups
+
+    rng = np.random.default_rng(5)
+    m, H, Fd, B = 32, 2, 64, 64
+    counts = np.zeros((n, m), np.float32)
+    for k in range(3):
+        counts[np.arange(n), rng.integers(0, m, n)] = 1
+    city = rng.integers(0, 300, n)
+    prov = city // 30
+    src = torch.as_tensor(rng.integers(0, n, B), device=cuda)
+    graph = Graph.from_dense(t(counts, cuda))
+    groups = Groups(city, prov, cuda)
+    base = [t(rng.standard_normal(s) * 0.3, cuda) for s in ((n, H), (m, H), (m, H, Fd),
+                                                            (n, H, Fd), (H, Fd), (H, Fd))]
+    base[2], base[3] = base[2].to(dtype), base[3].to(dtype)
+    dU = t(rng.standard_normal((n, H, Fd)), cuda).to(dtype)
+    dV = t(rng.standard_normal((m, H, Fd)), cuda).to(dtype)
+    res = []
+    try:
+        for defer in (True, False):
+            MF.BIP_DEFER_REDUCE = defer
+            ins = [x.detach().clone().requires_grad_(True) for x in base]
+            u, v = MF.ours_attention(graph, groups, src, *ins, p=0.3, training=True, seed=5)
+            torch.autograd.backward([u, v], [dU, dV])
+            torch.cuda.synchronize()
+            res.append([u.detach().clone(), v.detach().clone()] + [x.grad.clone() for x in ins])
+    finally:
+        MF.BIP_DEFER_REDUCE = True
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert (res[0][1] != 0).any() and (res[0][4] != 0).any()

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol(msha):
     from msha_gnn_amd import _lib
 
     lib = _lib.load()  # loads without touching the GPU
-    assert lib.msha_abi_version() == _lib.ABI_VERSION == 15
+    assert lib.msha_abi_version() == _lib.ABI_VERSION == 16
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (msha_\w+)", out))
