@@ -186,14 +186,26 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
 #ifndef BIP3_PAD
 #define BIP3_PAD 1
 #endif
+// The second-dispatched wave of each SIMD (waves 4-7) loses the SIMD's issue arbitration by
+// age: on the same tiles its loop runs 7-12 % longer (profiles/round6_bip_timeline), and the
+// kernel ends with it.  Measured (bip1m, HIP events, scripts/r6/fold.sh): the forward gives
+// waves 0-3 5 % more tiles (BIP3_SKEW_F 50: bf16 116.5 -> 112.7 us); the backward lets the
+// two waves take turns at priority, a tile each (BIP3_PRIO_B 2: bf16 205.8 -> 198.0 us).
+// 1: waves 4-7 at s_setprio 1 throughout (measured no better: the roles just swap).
 #ifndef BIP3_PRIO
-#define BIP3_PRIO 0  // 1: waves 4-7 (the second wave of each SIMD) at s_setprio 1; 2: turns (A/B)
+#define BIP3_PRIO 0
+#endif
+#ifndef BIP3_PRIO_F
+#define BIP3_PRIO_F BIP3_PRIO  // forward
+#endif
+#ifndef BIP3_PRIO_B
+#define BIP3_PRIO_B 2  // backward
 #endif
 #ifndef BIP3_APF
 #define BIP3_APF 1  // tiles ahead the per-row inputs (mask, el, lse, flag, rowptr) are loaded
 #endif
 #ifndef BIP3_SKEW_F
-#define BIP3_SKEW_F 0  // forward: per-mille extra tiles of the first-dispatched wave pairs
+#define BIP3_SKEW_F 50  // forward: per-mille extra tiles of the first-dispatched wave pairs
 #endif
 #ifndef BIP3_SKEW_B
 #define BIP3_SKEW_B 0  // backward: per-mille extra tiles of the first-dispatched waves
@@ -351,7 +363,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) vacc[n][i] = 0.f;
 
-  if (BIP3_PRIO == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
+  if (BIP3_PRIO_F == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
     const rsrc_t r_rp = make_rsrc((ATTD || DROP) ? rowptr : nullptr, (uint32_t)(re + 1) * 4u);
@@ -427,7 +439,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_fwd_kernel(
       const int it = (r0 - rb) / kTile;
       const bool tlm = it < kTlTiles;
       if (tlm) B3TL_MARK(2 + kTlPer * it);
-      if (BIP3_PRIO == 2) {  // the two waves of a SIMD take turns at priority, a tile each
+      if (BIP3_PRIO_F == 2) {  // the two waves of a SIMD take turns at priority, a tile each
         if (((it + (wv >= 4 ? 1 : 0)) & 1) != 0)
           __builtin_amdgcn_s_setprio(1);
         else
@@ -765,7 +777,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) derv[r] = 0.f;
 
-  if (BIP3_PRIO == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
+  if (BIP3_PRIO_B == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
   if (rb < re) {
     const rsrc_t r_mask = make_rsrc(rowmask, (uint32_t)re * 4u);
     const rsrc_t r_rp = make_rsrc(DROP ? rowptr : nullptr, (uint32_t)(re + 1) * 4u);
@@ -839,7 +851,7 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       const int it = (r0 - rb) / kTile;
       const bool tlm = it < kTlTiles;
       if (tlm) B3TL_MARK(2 + kTlPer * it);
-      if (BIP3_PRIO == 2) {  // the two waves of a SIMD take turns at priority, a tile each
+      if (BIP3_PRIO_B == 2) {  // the two waves of a SIMD take turns at priority, a tile each
         if (((it + (wv >= 4 ? 1 : 0)) & 1) != 0)
           __builtin_amdgcn_s_setprio(1);
         else
