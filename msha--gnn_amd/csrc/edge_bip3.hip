@@ -188,9 +188,10 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
 #endif
 // The second-dispatched wave of each SIMD (waves 4-7) loses the SIMD's issue arbitration by
 // age: on the same tiles its loop runs 7-12 % longer (profiles/round6_bip_timeline), and the
-// kernel ends with it.  Measured (bip1m, HIP events, scripts/r6/fold.sh): the forward gives
-// waves 0-3 5 % more tiles (BIP3_SKEW_F 50: bf16 116.5 -> 112.7 us); the backward lets the
-// two waves take turns at priority, a tile each (BIP3_PRIO_B 2: bf16 205.8 -> 198.0 us).
+// kernel ends with it.  Measured (bip1m, HIP events, scripts/r6/fold.sh, profiles/
+// round6_fold_ab): the backward lets the two waves take turns at priority, a tile each
+// (BIP3_PRIO_B 2: bf16 205.0 -> 197.4 us over two A/B pairs); giving the forward's waves 0-3
+// 5 % more tiles (BIP3_SKEW_F 50) measured within noise over three runs, so it is off.
 // 1: waves 4-7 at s_setprio 1 throughout (measured no better: the roles just swap).
 #ifndef BIP3_PRIO
 #define BIP3_PRIO 0
@@ -205,7 +206,7 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
 #define BIP3_APF 1  // tiles ahead the per-row inputs (mask, el, lse, flag, rowptr) are loaded
 #endif
 #ifndef BIP3_SKEW_F
-#define BIP3_SKEW_F 50  // forward: per-mille extra tiles of the first-dispatched wave pairs
+#define BIP3_SKEW_F 0  // forward: per-mille extra tiles of the first-dispatched wave pairs
 #endif
 #ifndef BIP3_SKEW_B
 #define BIP3_SKEW_B 0  // backward: per-mille extra tiles of the first-dispatched waves
