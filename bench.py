@@ -469,20 +469,21 @@ class Clock:
 
 
 def bip_kernel_patterns(H, F, bf, hs):
-    """rocprofv3 names of the bipartite forward / backward kernels: the mask kernels
+    """rocprofv3 names of the bipartite forward / backward kernels: the MFMA kernels
+    (edge_bip3.hip, <T, HS, ATTD, DROP> / <T, HS, COEF, DROP>), the mask kernels
     (edge_bip2.hip, <T, HS, ATTD> / <T, HS, COEF, DROP>) or the CSR-walk ones (edge_bip.hip,
     <H, F, T, HS, ATTD, HT> / <H, F, T, ...>), whichever the library chose; bf16
     instances stay mangled (DF16b) or demangle the type as "bool _Accum"."""
     h = str(bool(hs)).lower()
     if bf:
         fwd = (rf"(bip_fwd_kernel(ILi{H}ELi{F}EDF16bLb{int(hs)}E|<{H}, {F}, bool _Accum, "
-               rf"bool, E, false(, \d+)?>)|bip2_fwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum|<__bf16, {h}))")
+               rf"bool, E, false(, \d+)?>)|bip[23]_fwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum|<__bf16, {h}))")
         bwd = (rf"(bip_bwd_kernel(ILi{H}ELi{F}EDF16b|<{H}, {F}, bool _Accum)"
-               rf"|bip2_bwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum|<__bf16, {h}))")
+               rf"|bip[23]_bwd_kernel(IDF16bLb{int(hs)}E|<bool _Accum|<__bf16, {h}))")
     else:
         fwd = (rf"(bip_fwd_kernel<{H}, {F}, float, {h}, false(, \d+)?>"
-               rf"|bip2_fwd_kernel<float, {h}, (true|false)>)")
-        bwd = rf"(bip_bwd_kernel<{H}, {F}, float|bip2_bwd_kernel<float, {h},)"
+               rf"|bip[23]_fwd_kernel<float, {h}, (true|false)(, false)?>)")
+        bwd = rf"(bip_bwd_kernel<{H}, {F}, float|bip[23]_bwd_kernel<float, {h},)"
     return fwd, bwd
 
 
