@@ -214,6 +214,9 @@ struct Tab {  // table storage: fp32 -> 3 terms, bf16 -> exact
 #ifndef BIP3_APF_B
 #define BIP3_APF_B BIP3_APF  // the same for the backward
 #endif
+#ifndef BIP3_HSSYNC
+#define BIP3_HSSYNC 1  // fp32 backward: hs pieces loaded in their own tile (0: a tile ahead)
+#endif
 #ifndef BIP3_CLATE
 #define BIP3_CLATE 0  // backward: the softmax backward after d_hc / d_hs (A/B knob)
 #endif
@@ -840,9 +843,12 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       }
     };
 
-    Piece ring[KS];
+    // fp32 with BIP3_HSSYNC: only the dU pieces ride one tile ahead; the hs pieces are
+    // loaded at the top of their own tile (32 registers fewer through the d_hc / d_hs peak)
+    constexpr int KR = (HS && sizeof(T) == 4 && BIP3_HSSYNC) ? 4 : KS;
+    Piece ring[KR];
 #pragma unroll
-    for (int k = 0; k < KS; ++k) load_piece(k, rb, ring[k]);
+    for (int k = 0; k < KR; ++k) load_piece(k, rb, ring[k]);
     In nx, nx2;
     load_a(rb, nx);
     if (BIP3_APF_B > 1) load_a(rb + kTile, nx2);
@@ -866,6 +872,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
         load_a(r0 + kTile, nx);
       }
       const bool virt = cu.fl != 0;
+      Piece hsp[KS - KR > 0 ? KS - KR : 1];
+#pragma unroll
+      for (int k = 0; k < KS - KR; ++k) load_piece(KR + k, r0, hsp[k]);
 
       // ---- phase A: att (pre-dropout) on the mask, the keep bits of the lane's columns
       float a[16];
@@ -916,16 +925,17 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
       for (int ks = 0; ks < KS; ++ks) {
         if (ks & 1) asm volatile("" ::: "memory");  // two k-steps' fragments at a time
         bf16x8 B[NT], Af[NT];
-        piece_terms(ring[ks], B);
+        const Piece& pc = ks < KR ? ring[ks < KR ? ks : 0] : hsp[ks >= KR ? ks - KR : 0];
+        piece_terms(pc, B);
         if (ks < 4) {
           uint32_t* q = reinterpret_cast<uint32_t*>(stg + t * Stg<T>::P + 16 * ks + 8 * c);
-          *reinterpret_cast<u32x4_t*>(q) = u32x4_t{ring[ks].w[0], ring[ks].w[1], ring[ks].w[2], ring[ks].w[3]};
+          *reinterpret_cast<u32x4_t*>(q) = u32x4_t{pc.w[0], pc.w[1], pc.w[2], pc.w[3]};
           if constexpr (PW == 8)
-            *reinterpret_cast<u32x4_t*>(q + 4) = u32x4_t{ring[ks].w[4], ring[ks].w[5], ring[ks].w[6], ring[ks].w[7]};
+            *reinterpret_cast<u32x4_t*>(q + 4) = u32x4_t{pc.w[4], pc.w[5], pc.w[6], pc.w[7]};
         }
         // the next tile's dU pieces now; its hs pieces after this tile's d_hs (their
         // registers are free through the d_hc / d_hs peak)
-        if (ks < 4 || !BIP3_HSLATE) load_piece(ks, r0 + kTile, ring[ks]);
+        if (ks < KR && (ks < 4 || !BIP3_HSLATE)) load_piece(ks, r0 + kTile, ring[ks < KR ? ks : 0]);
 #pragma unroll
         for (int q = 0; q < NT; ++q) Af[q] = afr[(ks * NT + q) * 64 + lane];
         G = prod<NT, NT>(Af, B, G);
@@ -1049,9 +1059,9 @@ __global__ void __launch_bounds__(kWaves * 64) bip3_bwd_kernel(
           st_frag<T>(stg, acc, n, t, c);
         }
         flush_rows<T>(stg, r_dhs, r0, h, lane);
-        if (BIP3_HSLATE) {
+        if (BIP3_HSLATE && KR == KS) {
 #pragma unroll
-          for (int ks = 4; ks < KS; ++ks) load_piece(ks, r0 + kTile, ring[ks]);
+          for (int ks = 4; ks < KS; ++ks) load_piece(ks, r0 + kTile, ring[ks < KR ? ks : 0]);
         }
       }
       if (BIP3_CLATE) phase_c();
@@ -1169,12 +1179,15 @@ int bip3_bwd(const msha_graph* g, int dtype, const float* el, const float* er, c
              const float* row_coef, float slope, const Dropout& dp, float* d_el, float* d_er,
              void* d_hc, void* d_hs, float* part, int nb, hipStream_t s) {
   if (!bip3_enabled()) return 0;
-  // fp32: the mask backward of edge_bip2.hip measured faster at bip1m (390 vs 406-432 us:
-  // the six-product split of G's 128-deep operands and of dU's second layout is VALU-heavy);
-  // MSHA_BIP3_BWD32=1 (read per call) takes this kernel for fp32 as well
+  // fp32: with the hs pieces loaded in their own tile (BIP3_HSSYNC) the loop no longer
+  // spills and this kernel beats the mask backward of edge_bip2.hip at bip1m (370-377 vs
+  // 393-400 us, profiles/round6_bwd32_ab; the spilled form's scratch reloads waited for every
+  // outstanding load).  Its dropout variants still spill (the keep words): with dropout the
+  // mask kernel runs.  MSHA_BIP3_BWD32 (read per call): 1 forces this kernel, 0 the mask one.
   if (dtype != MSHA_DTYPE_BF16) {
     const char* v = getenv("MSHA_BIP3_BWD32");
-    if (v == nullptr || atoi(v) == 0) return 0;
+    const int force = v != nullptr && *v ? atoi(v) : -1;
+    if (force == 0 || (force < 0 && dp.active)) return 0;
   }
   const int32_t n_tiles = (int32_t)((g->n_rows + bip3::kTile - 1) / bip3::kTile);
   // blocks in head pairs (blockIdx.x & 1 = head), each wave at least one tile

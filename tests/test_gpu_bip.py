@@ -19,13 +19,12 @@ pytestmark = pytest.mark.gpu
 def bip_path(request, msha, monkeypatch):
     """The library's size-based choice ("default": below 131,072 rows the mask forward and
     the CSR-walk backward) and the large-graph choice forced on every 2 x 64, M <= 32 graph
-    ("mfma": msha_bip2_bwd_min_rows(0): the MFMA kernels of edge_bip3.hip, but the fp32
-    backward on edge_bip2.hip's mask kernel; "mfma_bwd32": MSHA_BIP3_BWD32=1, the MFMA
-    backward for fp32 too)."""
+    ("mfma": msha_bip2_bwd_min_rows(0) with MSHA_BIP3_BWD32=0: the MFMA kernels of
+    edge_bip3.hip, but the fp32 backward on edge_bip2.hip's mask kernel; "mfma_bwd32": the
+    MFMA backward for fp32 too, the library's large-graph default since round 6)."""
     from msha_gnn_amd import _lib
 
-    if request.param == "mfma_bwd32":
-        monkeypatch.setenv("MSHA_BIP3_BWD32", "1")
+    monkeypatch.setenv("MSHA_BIP3_BWD32", "1" if request.param == "mfma_bwd32" else "0")
     prev = _lib.fn("msha_bip2_bwd_min_rows")(-1 if request.param == "default" else 0)
     yield request.param
     _lib.fn("msha_bip2_bwd_min_rows")(prev)
