@@ -208,16 +208,19 @@ def test_bench_line_is_small_strict_json():
 
 
 def test_bip_kernel_patterns_match_rocprof_names():
-    """The bipartite rooflines' PMC lookup names both kernel families (the mask kernels of
-    edge_bip2.hip and the CSR walk of edge_bip.hip) as rocprofv3 reports them: fp32
+    """The bipartite rooflines' PMC lookup names every kernel family (the MFMA kernels of
+    edge_bip3.hip, the mask kernels of edge_bip2.hip and the CSR walk of edge_bip.hip) as
+    rocprofv3 reports them: fp32
     demangled, bf16 mangled (DF16b) or demangled with the type as "bool _Accum"."""
     import re
 
     fwd, bwd = bench.bip_kernel_patterns(2, 64, False, True)
     names_f = ["void msha::bip2::bip2_fwd_kernel<float, true, false>(unsigned int const*)",
-               "void msha::bip::bip_fwd_kernel<2, 64, float, true, false, 2>(int const*)"]
+               "void msha::bip::bip_fwd_kernel<2, 64, float, true, false, 2>(int const*)",
+               "void msha::bip3::bip3_fwd_kernel<float, true, false, false>(unsigned int const*)"]
     names_b = ["void msha::bip2::bip2_bwd_kernel<float, true, false, false>(unsigned int const*)",
-               "void msha::bip::bip_bwd_kernel<2, 64, float, true, true, 2>(int const*)"]
+               "void msha::bip::bip_bwd_kernel<2, 64, float, true, true, 2>(int const*)",
+               "void msha::bip3::bip3_bwd_kernel<float, true, false, false>(unsigned int const*)"]
     assert all(re.search(fwd, n) for n in names_f) and not any(re.search(fwd, n) for n in names_b)
     assert all(re.search(bwd, n) for n in names_b) and not any(re.search(bwd, n) for n in names_f)
     # the v branch (HS) is pinned: a u-only forward is another instantiation
@@ -226,4 +229,8 @@ def test_bip_kernel_patterns_match_rocprof_names():
     assert re.search(fwd16, "_ZN4msha4bip215bip2_fwd_kernelIDF16bLb1ELb0EEEvPKjPKiPKh")
     assert re.search(fwd16, "void msha::bip2::bip2_fwd_kernel<bool _Accum, bool, E, false>")
     assert re.search(bwd16, "_ZN4msha4bip215bip2_bwd_kernelIDF16bLb1ELb0ELb0EEEv")
+    # the MFMA kernels (edge_bip3.hip), as rocprofv3 printed them in profiles/round6_bip_sq
+    assert re.search(fwd16, "void msha::bip3::bip3_fwd_kernel<bool _Accum, bool, E, false, false>(")
+    assert re.search(bwd16, "void msha::bip3::bip3_bwd_kernel<bool _Accum, bool, E, false, false>(")
+    assert not re.search(bwd16, "void msha::bip3::bip3_fwd_kernel<bool _Accum, bool, E, false, false>(")
     assert not re.search(fwd16, "void msha::bip2::bip2_fwd_kernel<float, true, false>(")
